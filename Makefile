@@ -1,0 +1,30 @@
+# Build liborleans_route.so (HIP, gfx950) and the CPU oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+SRC = orleans_amd/csrc/route_kernels.hip orleans_amd/csrc/orl_api.cpp
+HDR = include/orleans_route.h orleans_amd/csrc/orl_internal.h
+LIB = orleans_amd/liborleans_route.so
+OBJ = build/route_kernels.o build/orl_api.o
+
+all: $(LIB) oracle
+
+$(LIB): $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
+
+build/route_kernels.o: orleans_amd/csrc/route_kernels.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/orl_api.o: orleans_amd/csrc/orl_api.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,228 @@
+/*
+ * orleans_route.h — C ABI of liborleans_route.so, the MI355X batched grain-message routing engine.
+ *
+ * The engine replaces the per-message routing work of an Orleans 1.1 silo
+ * (randa1/orleans; paths below are relative to that checkout) with a batched HIP pipeline:
+ *   stage 1  GrainId uniform hash      JenkinsHash.ComputeHash(TCD,N0,N1)  src/Orleans/IDs/JenkinsHash.cs:126-144
+ *   stage 2  directory ring owner      LocalGrainDirectory.CalculateTargetSilo
+ *                                       src/OrleansRuntime/GrainDirectory/LocalGrainDirectory.cs:439-497
+ *   stage 3  directory partition probe GrainDirectoryPartition.LookUpGrain + IsValidSilo
+ *                                       src/OrleansRuntime/GrainDirectory/GrainDirectoryPartition.cs:326-344
+ *            + placement of misses     PlacementDirectorsManager.SelectOrAddActivation
+ *                                       src/OrleansRuntime/Placement/PlacementDirectorsManager.cs:70-91
+ *   stage 4  stable per-activation FIFO ActivationData.EnqueueMessage  src/OrleansRuntime/Catalog/ActivationData.cs:483-514
+ *   stage 5  multicast fan-out          ChirperAccount.PublishMessage   Samples/Chirper/ChirperGrains/ChirperAccount.cs:154-157
+ *
+ * The reference path has no FFI of its own (it is C#, internal interfaces only).  These entry
+ * points are what a C# `NativeMethods` class ([DllImport("orleans_route")], the pattern of
+ * src/Orleans/Statistics/ThreadCycleStopWatch.cs:120-128) would bind from inside
+ * LocalGrainDirectory / Dispatcher / MessageCenter; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every function returns an int status (ORL_OK = 0, < 0 = API error; orl_last_error(ctx) explains).
+ *    Nothing throws or aborts across the ABI.  Per-message outcomes are status bytes in the route word.
+ *  - Caller owns every host array; the library owns all device state (ring, directory table, scratch).
+ *  - `*_device` entry points take device pointers already resident in HBM and a hipStream_t (as void*);
+ *    they enqueue work and return without synchronising.
+ *  - A context is bound to one HIP device.  Calls on one context must not race (one submitting thread
+ *    per silo context, as SURVEY §8(b) recommends); ring/table updates take effect between batches.
+ *  - Silos are identified by a dense index 0..n_silos-1 (< 255); 0xFF means "null SiloAddress".
+ */
+#ifndef ORLEANS_ROUTE_H
+#define ORLEANS_ROUTE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORL_ABI_VERSION 1u
+#define ORL_MAX_SILOS 255u
+#define ORL_NULL_SILO 0xFFu
+#define ORL_NO_ACT 0xFFFFFFFFu
+#define ORL_MAX_RING 256u
+
+/* ---- API status codes ------------------------------------------------------------------- */
+#define ORL_OK 0
+#define ORL_E_INVALID (-1)   /* bad argument / unsupported key (ArgumentException analogues) */
+#define ORL_E_NOMEM (-2)     /* host or device allocation failed */
+#define ORL_E_DEVICE (-3)    /* HIP runtime error (message in orl_last_error) */
+#define ORL_E_CAPACITY (-4)  /* batch larger than orl_config.max_batch, or directory full */
+#define ORL_E_STATE (-5)     /* call not valid in the context's current state */
+#define ORL_E_OVERFLOW (-6)  /* Math.Abs(int.MinValue) analogue (OutboundMessageQueue.cs:141) */
+
+/* ---- UniqueKey categories (src/Orleans/IDs/UniqueKey.cs:41-49) ---------------------------- */
+#define ORL_CAT_NONE 0u
+#define ORL_CAT_SYSTEM_TARGET 1u
+#define ORL_CAT_SYSTEM_GRAIN 2u
+#define ORL_CAT_GRAIN 3u
+#define ORL_CAT_CLIENT 4u
+#define ORL_CAT_KEYEXT_GRAIN 6u
+
+/* GrainId identity = UniqueKey {N0, N1, TypeCodeData} (UniqueKey.cs:51-54).  24 bytes.
+ * Category lives in the top byte of type_code_data (UniqueKey.cs:141). */
+typedef struct orl_grain_key {
+    uint64_t type_code_data;
+    uint64_t n0;
+    uint64_t n1;
+} orl_grain_key;
+
+/* Header flags (orl_msg_hdr.flags) */
+#define ORL_HDR_ADDRESS_COMPLETE 0x01u /* Message.TargetAddress.IsComplete: skip routing (Dispatcher.cs:557-558) */
+#define ORL_HDR_HASH_VALID 0x02u       /* aux holds the precomputed uniform hash (KeyExt slow path, UniqueKey.cs:288-294) */
+
+/* One message header as the routing path reads it (Message.cs:199-291): 32 bytes, SoA-friendly AoS.
+ * Message order in a batch = arrival order. */
+typedef struct orl_msg_hdr {
+    orl_grain_key target;   /* TargetGrain */
+    uint8_t sending_silo;   /* SendingSilo index == "MyAddress" of the routing silo */
+    uint8_t category;       /* Message.Categories (Ping 0 / System 1 / Application 2), carried through */
+    uint8_t flags;          /* ORL_HDR_* */
+    uint8_t target_silo;    /* TargetSilo when ORL_HDR_ADDRESS_COMPLETE, else ignored */
+    uint32_t aux;           /* precomputed uniform hash when ORL_HDR_HASH_VALID */
+} orl_msg_hdr;
+
+/* ---- Per-message route word ---------------------------------------------------------------
+ * bits 0-7 directory owner silo, 8-15 target (host) silo, 16-23 ORL_ST_*, 24-31 ORL_RF_*      */
+#define ORL_ST_HIT 0u                  /* single activation found on a functional silo */
+#define ORL_ST_NEW_PLACEMENT 1u        /* miss: OnAddActivation chose the host silo (IsNewPlacement) */
+#define ORL_ST_SYSTEM_TARGET 2u        /* SystemTarget: owner = routing silo (LocalGrainDirectory.cs:442-447) */
+#define ORL_ST_ADDRESS_COMPLETE 3u     /* header already addressed; passed through */
+#define ORL_ST_OWNER_NULL 4u           /* owner null: "Grain directory is stopping" (:471-475, :483-493) */
+#define ORL_ST_NO_SEED 5u              /* membership-table grain without seed (ArgumentException :449-460) */
+#define ORL_ST_CLIENT_UNREGISTERED 6u  /* client grain miss (KeyNotFoundException, PlacementDirectorsManager.cs:75-81) */
+#define ORL_ST_KEYEXT_UNRESOLVED 7u    /* KeyExt grain: owner computed, partition lookup left to host */
+#define ORL_ST_REMOTE_OWNER 8u         /* owner's partition not held by this context (cache/FullLookup path) */
+
+#define ORL_RF_NEW_PLACEMENT 0x01u
+#define ORL_RF_LOOPBACK 0x02u          /* target silo == sending silo (OutboundMessageQueue.cs:113-119) */
+#define ORL_RF_OWNER_IS_SEED 0x04u
+
+#define ORL_ROUTE_OWNER(r) ((uint32_t)(r) & 0xFFu)
+#define ORL_ROUTE_HOST(r) (((uint32_t)(r) >> 8) & 0xFFu)
+#define ORL_ROUTE_STATUS(r) (((uint32_t)(r) >> 16) & 0xFFu)
+#define ORL_ROUTE_FLAGS(r) (((uint32_t)(r) >> 24) & 0xFFu)
+
+/* Placement policy for misses (deterministic subset of the reference directors) */
+#define ORL_POLICY_PREFER_LOCAL 0u  /* PreferLocalPlacementDirector.cs:38-44: the sending silo */
+#define ORL_POLICY_HASH_SPREAD 1u   /* RandomPlacementDirector.cs:59-66 with hash % |active| instead of SafeRandom */
+
+/* Route options (bit set) */
+#define ORL_OPT_EXCLUDE_IF_STOPPING 0x1u /* CalculateTargetSilo(grain, excludeThisSiloIfStopping=true) */
+#define ORL_OPT_NO_BUCKETS 0x2u          /* skip stage 4 (order/offsets not written) */
+
+/* Directory insert outcome (orl_dir_insert_single status[]) */
+#define ORL_INS_INSERTED 0u
+#define ORL_INS_EXISTING 1u      /* first writer wins: winner returned (GrainInfo.AddSingleActivation :100-114) */
+#define ORL_INS_INVALID_SILO 2u  /* !IsValidSilo(silo): AddSingleActivation returns null (:277-279) */
+#define ORL_INS_REMOTE_OWNER 3u  /* owner partition not local: caller must forward (LocalGrainDirectory.cs:529-541) */
+#define ORL_INS_OWNER_NULL 4u    /* owner null (directory stopping) */
+#define ORL_INS_UNSUPPORTED 5u   /* KeyExt / SystemTarget keys are not held in the device partition */
+
+typedef struct orl_config {
+    uint32_t abi_version;      /* must be ORL_ABI_VERSION */
+    int32_t device;            /* HIP device ordinal */
+    uint64_t dir_capacity;     /* max directory entries; table = next_pow2(2*dir_capacity) 32-B slots */
+    uint32_t n_act;            /* activation-handle space [0, n_act); buckets = n_act + 1 (last = unresolved) */
+    uint32_t placement_policy; /* ORL_POLICY_* */
+    uint64_t max_batch;        /* largest batch (messages, incl. fan-out output) the scratch is sized for */
+} orl_config;
+
+typedef struct orl_ctx orl_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+int orl_ctx_create(const orl_config* cfg, orl_ctx** out);
+int orl_ctx_destroy(orl_ctx* ctx);
+const char* orl_last_error(const orl_ctx* ctx);
+uint32_t orl_abi_version(void);
+
+/* ---- silo table + ring (LocalGrainDirectory membership events :243-304, :390-427) ---------
+ * running[i]: LocalGrainDirectory.Running of silo i (used for excludeMySelf, :478)
+ * functional[i]: Membership.IsFunctionalDirectory(i) (IsValidSilo, :421-427)
+ * local[i]: this context holds silo i's directory partition (its GPU hosts silo i)
+ * seed: index of the Seed silo (membership-table grain owner) or ORL_NULL_SILO */
+int orl_silos_set(orl_ctx* ctx, uint32_t n_silos, const uint8_t* running, const uint8_t* functional,
+                  const uint8_t* local, uint32_t seed);
+/* AddServer: sorted insert by signed consistent hash, before equal hashes (LocalGrainDirectory.cs:243-268) */
+int orl_ring_add_server(orl_ctx* ctx, uint32_t silo, int32_t consistent_hash);
+/* RemoveServer (LocalGrainDirectory.cs:270-304; list removal) */
+int orl_ring_remove_server(orl_ctx* ctx, uint32_t silo);
+int orl_ring_get(const orl_ctx* ctx, int32_t* hashes, uint8_t* silos, uint32_t cap, uint32_t* n_out);
+
+/* ---- host-side identity helpers (not per message) ----------------------------------------- */
+/* Utils.CalculateIdHash(text) (Utils.cs:201-220): SHA-256 of the UTF-16LE encoding of `utf8` text */
+int orl_calc_id_hash(const char* utf8, size_t len, int32_t* out);
+/* SiloAddress.GetConsistentHashCode (SiloAddress.cs:197-206): CalculateIdHash(endpoint + generation) */
+int orl_silo_consistent_hash(const char* endpoint_utf8, int32_t generation, int32_t* out);
+/* JenkinsHash.ComputeHash(byte[]) (JenkinsHash.cs:68-115) */
+uint32_t orl_jenkins_bytes(const uint8_t* data, size_t len);
+/* UniqueKey.GetUniformHashCode KeyExt branch (UniqueKey.cs:288-294; serialization BinaryTokenStreamWriter.cs:488-494) */
+uint32_t orl_keyext_uniform_hash(const orl_grain_key* key, const char* key_ext_utf8, size_t len);
+
+/* ---- directory partition (single activation) --------------------------------------------
+ * RegisterSingleActivation → GrainDirectoryPartition.AddSingleActivation (GrainDirectoryPartition.cs:270-287).
+ * Inserts are applied in array order: the first writer of a grain wins; later writers get the winner.
+ * The registering silo is the activation's silo (ActivationAddress.Silo): it computes the owner with
+ * CalculateTargetSilo(grain) (excludeThisSiloIfStopping = true).
+ * winner_act / winner_silo / status may be NULL.  acts[i] must be < n_act. */
+int orl_dir_insert_single(orl_ctx* ctx, const orl_grain_key* keys, const uint32_t* acts, const uint8_t* silos,
+                          size_t n, uint32_t* winner_act, uint8_t* winner_silo, uint8_t* status);
+/* RemoveGrain / RemoveActivation(force) of a single-activation grain (:290-318).  removed[i] = 1 if present. */
+int orl_dir_remove(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint8_t* removed);
+int orl_dir_count(const orl_ctx* ctx, uint64_t* n_out);
+/* Host lookup (LookUpGrain without the IsValidSilo filter): act/silo or ORL_NO_ACT/ORL_NULL_SILO */
+int orl_dir_lookup_host(const orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint32_t* act, uint8_t* silo);
+
+/* ---- stage 1 alone (tests) ---------------------------------------------------------------- */
+int orl_hash_batch(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint32_t* hashes_out);
+
+/* ---- the hot path --------------------------------------------------------------------------
+ * Stages 1-4 over n messages.  Outputs:
+ *   route[n]            route word (owner | host<<8 | status<<16 | flags<<24)
+ *   act[n]              activation handle or ORL_NO_ACT
+ *   order[n]            message indices grouped by bucket, arrival order kept inside a bucket
+ *   bucket_offsets[n_act+2]  bucket b holds order[offsets[b] .. offsets[b+1]); bucket n_act = unresolved
+ * Host-buffer form (P/Invoke): copies in/out over PCIe and synchronises. */
+int orl_route_batch(orl_ctx* ctx, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                    uint32_t* order, uint32_t* bucket_offsets);
+/* Device-resident form: all pointers in HBM; enqueued on `stream` (hipStream_t, NULL = default). */
+int orl_route_batch_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route,
+                           uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
+
+/* Stage 5 + 1-4: CSR multicast.  Publish p (account pubs[p] sending from silo pub_silo[p]) expands to
+ * one send per follower csr_tgt[csr_off[pubs[p]] .. csr_off[pubs[p]+1]) in CSR order; follower grain =
+ * GrainId(follower_tcd, long id) = key {follower_tcd, 0, id}.  Output message j (publisher-major) is
+ * routed as in orl_route_batch_device; pub_offsets[n_pub+1] (device) maps publishes to output ranges.
+ * *n_out (host) receives the number of emitted messages (this call synchronises `stream` once to read it). */
+int orl_fanout_route_device(orl_ctx* ctx, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                            const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
+                            uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
+                            uint32_t* d_order, uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
+
+/* ---- multi-GPU exchange support --------------------------------------------
+ * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is
+ * null / system target / complete stay on the sending rank (dest = my_rank).  Writes the partitioned
+ * headers to d_out (n entries, rank-major, arrival order kept), the source index of each to
+ * d_src_index, and per-rank counts to d_counts[nranks] (device, uint64). */
+int orl_partition_by_owner_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                                  const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank,
+                                  orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, void* stream);
+
+int orl_sync(orl_ctx* ctx);
+
+/* ---- introspection for benchmarks / profiling ------------------------------------------------ */
+/* With timing enabled, every orl_route_batch_device brackets its route kernel (stages 1-3), its bucketing
+ * kernels (stage 4) and the whole call with HIP events on the submission stream (no host sync per batch;
+ * up to ORL_TIMING_SLOTS batches are kept).  orl_set_timing(ctx, 1) clears the record.
+ * orl_timing_summary waits for the last recorded batch and returns the per-batch averages in ms. */
+#define ORL_TIMING_SLOTS 256u
+int orl_set_timing(orl_ctx* ctx, int enable);
+int orl_timing_summary(const orl_ctx* ctx, uint32_t* n_batches, float* route_kernel_ms, float* bucket_ms,
+                       float* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORLEANS_ROUTE_H */

@@ -1,0 +1,137 @@
+"""ctypes binding of liborleans_route.so (include/orleans_route.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``) and loaded from this package
+directory only.  There is deliberately no fallback: if the HIP library is missing, importing the
+engine raises, so a GPU run can never silently route through Python or the CPU oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+LIB_NAME = "liborleans_route.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# ---- constants mirrored from include/orleans_route.h -------------------------------------------------
+ABI_VERSION = 1
+NULL_SILO = 0xFF
+NO_ACT = 0xFFFFFFFF
+
+OK, E_INVALID, E_NOMEM, E_DEVICE, E_CAPACITY, E_STATE, E_OVERFLOW = 0, -1, -2, -3, -4, -5, -6
+
+CAT_NONE, CAT_SYSTEM_TARGET, CAT_SYSTEM_GRAIN, CAT_GRAIN, CAT_CLIENT, CAT_KEYEXT_GRAIN = 0, 1, 2, 3, 4, 6
+
+HDR_ADDRESS_COMPLETE = 0x01
+HDR_HASH_VALID = 0x02
+
+ST_HIT = 0
+ST_NEW_PLACEMENT = 1
+ST_SYSTEM_TARGET = 2
+ST_ADDRESS_COMPLETE = 3
+ST_OWNER_NULL = 4
+ST_NO_SEED = 5
+ST_CLIENT_UNREGISTERED = 6
+ST_KEYEXT_UNRESOLVED = 7
+ST_REMOTE_OWNER = 8
+
+RF_NEW_PLACEMENT = 0x01
+RF_LOOPBACK = 0x02
+RF_OWNER_IS_SEED = 0x04
+
+POLICY_PREFER_LOCAL = 0
+POLICY_HASH_SPREAD = 1
+
+OPT_EXCLUDE_IF_STOPPING = 0x1
+OPT_NO_BUCKETS = 0x2
+
+INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+
+# orl_grain_key / orl_msg_hdr as numpy structured dtypes (byte-identical to the C structs)
+KEY_DTYPE = np.dtype([("tcd", "<u8"), ("n0", "<u8"), ("n1", "<u8")])
+MSG_DTYPE = np.dtype([("tcd", "<u8"), ("n0", "<u8"), ("n1", "<u8"), ("sending_silo", "u1"), ("category", "u1"),
+                      ("flags", "u1"), ("target_silo", "u1"), ("aux", "<u4")])
+assert KEY_DTYPE.itemsize == 24 and MSG_DTYPE.itemsize == 32
+
+
+class orl_config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("dir_capacity", C.c_uint64),
+                ("n_act", C.c_uint32), ("placement_policy", C.c_uint32), ("max_batch", C.c_uint64)]
+
+
+# Every symbol include/orleans_route.h declares, with its ctypes signature.
+_P = C.c_void_p
+_u8p = C.POINTER(C.c_uint8)
+_SIGS = {
+    "orl_abi_version": (C.c_uint32, []),
+    "orl_ctx_create": (C.c_int, [C.POINTER(orl_config), C.POINTER(_P)]),
+    "orl_ctx_destroy": (C.c_int, [_P]),
+    "orl_last_error": (C.c_char_p, [_P]),
+    "orl_silos_set": (C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32]),
+    "orl_ring_add_server": (C.c_int, [_P, C.c_uint32, C.c_int32]),
+    "orl_ring_remove_server": (C.c_int, [_P, C.c_uint32]),
+    "orl_ring_get": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "orl_calc_id_hash": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int32)]),
+    "orl_silo_consistent_hash": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
+    "orl_jenkins_bytes": (C.c_uint32, [C.c_char_p, C.c_size_t]),
+    "orl_keyext_uniform_hash": (C.c_uint32, [_P, C.c_char_p, C.c_size_t]),
+    "orl_dir_insert_single": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P]),
+    "orl_dir_remove": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "orl_dir_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "orl_dir_lookup_host": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "orl_hash_batch": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "orl_route_batch": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
+    "orl_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
+    "orl_fanout_route_device": (C.c_int, [_P, _P, _P, _P, _P, C.c_size_t, C.c_uint64, C.c_uint32, _P, _P, _P, _P, _P,
+                                          C.POINTER(C.c_uint64), _P]),
+    "orl_partition_by_owner_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P, _P, _P,
+                                                _P]),
+    "orl_sync": (C.c_int, [_P]),
+    "orl_set_timing": (C.c_int, [_P, C.c_int]),
+    "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                     C.POINTER(C.c_float)]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+                           "the routing engine has no non-HIP fallback")
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.orl_abi_version() != ABI_VERSION:
+        raise RuntimeError("liborleans_route.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def ptr(a) -> C.c_void_p:
+    """Raw pointer of a numpy array (C-contiguous) or a torch tensor (data_ptr), or None."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+        return C.c_void_p(a.ctypes.data)
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    if isinstance(a, int):
+        return C.c_void_p(a)
+    raise TypeError(f"cannot take a pointer of {type(a)}")
+
+
+class OrleansRouteError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"orleans_route error {code}: {msg}")
+        self.code = code

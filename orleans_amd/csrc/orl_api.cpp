@@ -1,0 +1,704 @@
+// orl_api.cpp — host side of liborleans_route.so: context, silo table + ring (membership events),
+// directory partition mirror (registration), identity hashes, and the C ABI entry points.
+//
+// The host side is the control plane of the path: everything here runs once per membership change or
+// registration, never per message.  Per-message work is in route_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orl_internal.h"
+
+using namespace orl;
+
+namespace {
+
+// ---- SHA-256 (FIPS 180-4), for Utils.CalculateIdHash (Utils.cs:201-220) ---------------------------------
+struct Sha256 {
+    uint32_t h[8];
+    uint8_t buf[64];
+    uint64_t len = 0;
+    size_t fill = 0;
+    static constexpr uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+        0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+        0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+        0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+        0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+        0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+        0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+    Sha256() {
+        static const uint32_t H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+        std::memcpy(h, H0, sizeof h);
+    }
+    static uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+    void block(const uint8_t* p) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; ++i) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 64; ++i) {
+            const uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            const uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+        for (int i = 0; i < 64; ++i) {
+            const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+            const uint32_t ch = (e & f) ^ (~e & g);
+            const uint32_t t1 = hh + S1 + ch + K[i] + w[i];
+            const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+            const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+            const uint32_t t2 = S0 + mj;
+            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    }
+    void update(const uint8_t* p, size_t n) {
+        len += n;
+        while (n) {
+            const size_t take = std::min(n, 64 - fill);
+            std::memcpy(buf + fill, p, take);
+            fill += take; p += take; n -= take;
+            if (fill == 64) { block(buf); fill = 0; }
+        }
+    }
+    void final(uint8_t out[32]) {
+        const uint64_t bits = len * 8;
+        const uint8_t one = 0x80, zero = 0;
+        update(&one, 1);
+        while (fill != 56) update(&zero, 1);
+        uint8_t lb[8];
+        for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+        update(lb, 8);
+        for (int i = 0; i < 8; ++i) {
+            out[4 * i] = (uint8_t)(h[i] >> 24); out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+            out[4 * i + 2] = (uint8_t)(h[i] >> 8); out[4 * i + 3] = (uint8_t)h[i];
+        }
+    }
+};
+constexpr uint32_t Sha256::K[64];
+
+// UTF-8 → UTF-16LE (.NET Encoding.Unicode).  Returns false on malformed input.
+bool utf8_to_utf16le(const char* s, size_t n, std::vector<uint8_t>& out) {
+    out.clear();
+    size_t i = 0;
+    auto put = [&](uint32_t u) { out.push_back((uint8_t)u); out.push_back((uint8_t)(u >> 8)); };
+    while (i < n) {
+        const uint8_t c = (uint8_t)s[i];
+        uint32_t cp;
+        int extra;
+        if (c < 0x80) { cp = c; extra = 0; }
+        else if ((c >> 5) == 6) { cp = c & 0x1F; extra = 1; }
+        else if ((c >> 4) == 14) { cp = c & 0x0F; extra = 2; }
+        else if ((c >> 3) == 30) { cp = c & 0x07; extra = 3; }
+        else return false;
+        if (i + (size_t)extra >= n && extra) return false;  // truncated sequence
+        for (int k = 1; k <= extra; ++k) {
+            const uint8_t cc = (uint8_t)s[i + k];
+            if ((cc >> 6) != 2) return false;
+            cp = (cp << 6) | (cc & 0x3F);
+        }
+        i += 1 + extra;
+        if (cp >= 0x10000) {
+            cp -= 0x10000;
+            put(0xD800 + (cp >> 10));
+            put(0xDC00 + (cp & 0x3FF));
+        } else {
+            put(cp);
+        }
+    }
+    return true;
+}
+
+int32_t calc_id_hash_utf16(const std::vector<uint8_t>& u16) {
+    Sha256 sh;
+    sh.update(u16.data(), u16.size());
+    uint8_t d[32];
+    sh.final(d);
+    uint32_t h = 0;
+    for (int i = 0; i < 32; i += 4) h ^= (uint32_t)d[i] << 24 | (uint32_t)d[i + 1] << 16 | (uint32_t)d[i + 2] << 8 | d[i + 3];
+    return (int32_t)h;
+}
+
+// JenkinsHash.ComputeHash(byte[]) (JenkinsHash.cs:68-115)
+uint32_t jenkins_bytes(const uint8_t* d, size_t len) {
+    uint32_t a = 0x9e3779b9u, b = 0x9e3779b9u, c = 0;
+    size_t i = 0;
+    auto rd = [&](size_t k) { return (uint32_t)d[k] | (uint32_t)d[k + 1] << 8 | (uint32_t)d[k + 2] << 16 | (uint32_t)d[k + 3] << 24; };
+    while (i + 12 <= len) {
+        a += rd(i); b += rd(i + 4); c += rd(i + 8);
+        i += 12;
+        ORL_MIX(a, b, c);
+    }
+    c += (uint32_t)len;
+    const size_t rem = len - i;
+    for (size_t k = 0; k < rem; ++k) {
+        const uint32_t v = d[i + k];
+        if (k < 4) a += v << (8 * k);
+        else if (k < 8) b += v << (8 * (k - 4));
+        else c += v << (8 * (k - 7));
+    }
+    ORL_MIX(a, b, c);
+    return c;
+}
+
+uint64_t next_pow2(uint64_t v) {
+    uint64_t p = 16;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------
+struct orl_ctx {
+    orl_config cfg{};
+    bool device_mode = false;
+    std::string err;
+    // silos (LocalGrainDirectory membership view)
+    uint32_t n_silos = 0;
+    std::vector<uint8_t> running, functional, local;
+    uint32_t seed = ORL_NULL_SILO;
+    std::vector<std::pair<int32_t, uint8_t>> ring;  // membershipRingList (signed hash, silo)
+    // directory partition mirror
+    std::vector<DirSlot> table;
+    uint64_t mask = 0, count = 0, tombs = 0;
+    bool dir_dirty = true;
+    // device state
+    DirSlot* d_table = nullptr;
+    RouteParams hp{};
+    RouteParams* d_params = nullptr;
+    bool params_dirty = true;
+    uint8_t* d_rank_of_silo = nullptr;
+    Scratch s{};
+    hipStream_t stream = nullptr;
+    // host-buffer staging (orl_route_batch / orl_hash_batch)
+    void* st_in = nullptr; size_t st_in_cap = 0;
+    uint32_t* st_out = nullptr; size_t st_out_cap = 0;
+    uint32_t* st_off = nullptr;
+    // timing: 4 events per recorded batch (call begin, route begin, route end, call end)
+    bool timing = false;
+    std::vector<hipEvent_t> tev;
+    uint32_t tcount = 0;
+};
+
+namespace {
+
+int fail(orl_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char b[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(b, sizeof b, fmt, ap);
+        va_end(ap);
+        c->err = b;
+    }
+    return code;
+}
+
+int hipfail(orl_ctx* c, hipError_t e, const char* what) {
+    return fail(c, ORL_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define ORL_HIP(c, call)                                           \
+    do {                                                           \
+        hipError_t _e = (call);                                    \
+        if (_e != hipSuccess) return hipfail((c), _e, #call);      \
+    } while (0)
+
+bool silo_ok(const orl_ctx* c, uint32_t s) { return s < c->n_silos; }
+
+// CalculateTargetSilo on the host (LocalGrainDirectory.cs:439-497) for registrations.
+uint32_t host_owner(const orl_ctx* c, const orl_grain_key& k, uint32_t me, bool excl) {
+    const uint32_t cat = (uint32_t)(k.type_code_data >> 56);
+    if (cat == ORL_CAT_SYSTEM_TARGET) return me;
+    if (k.type_code_data == c->hp.mem_tcd && k.n0 == c->hp.mem_n0 && k.n1 == c->hp.mem_n1) return c->seed;
+    const int32_t h = (int32_t)jenkins3(k.type_code_data, k.n0, k.n1);
+    const bool running = me < c->n_silos && c->running[me];
+    const int n = (int)c->ring.size();
+    if (n == 0) return (excl && !running) ? ORL_NULL_SILO : me;
+    const bool ex = excl && !running;
+    int found = -1;
+    for (int i = 0; i < n; ++i)
+        if (c->ring[i].first <= h && !(c->ring[i].second == me && ex)) found = i;
+    if (found < 0) {
+        found = n - 1;
+        if (c->ring[found].second == me && ex) {
+            if (n > 1) found = n - 2; else return ORL_NULL_SILO;
+        }
+    }
+    return c->ring[found].second;
+}
+
+void rebuild_params(orl_ctx* c) {
+    RouteParams& P = c->hp;
+    const uint64_t mt = P.mem_tcd, m0 = P.mem_n0, m1 = P.mem_n1;
+    std::memset(&P, 0, sizeof P);
+    P.mem_tcd = mt; P.mem_n0 = m0; P.mem_n1 = m1;
+    P.ring_n = (uint32_t)c->ring.size();
+    for (size_t i = 0; i < c->ring.size(); ++i) {
+        P.ring_hash[i] = c->ring[i].first;
+        P.ring_silo[i] = c->ring[i].second;
+    }
+    uint32_t na = 0;
+    for (uint32_t s = 0; s < c->n_silos; ++s) {
+        if (c->running[s]) P.running[s >> 5] |= 1u << (s & 31);
+        if (c->functional[s]) { P.functional[s >> 5] |= 1u << (s & 31); P.active_list[na++] = (uint8_t)s; }
+        if (c->local[s]) P.local[s >> 5] |= 1u << (s & 31);
+    }
+    P.n_active = na;
+    P.seed = c->seed;
+    P.policy = c->cfg.placement_policy;
+    P.n_act = c->cfg.n_act;
+    c->params_dirty = true;
+}
+
+int sync_device_state(orl_ctx* c) {
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (c->params_dirty) {
+        ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
+        c->params_dirty = false;
+    }
+    if (c->dir_dirty) {
+        ORL_HIP(c, hipMemcpy(c->d_table, c->table.data(), c->table.size() * sizeof(DirSlot), hipMemcpyHostToDevice));
+        c->dir_dirty = false;
+    }
+    return ORL_OK;
+}
+
+bool keys_equal(const DirSlot& s, const orl_grain_key& k) {
+    return s.tcd == k.type_code_data && s.n0 == k.n0 && s.n1 == k.n1;
+}
+
+// Probe the mirror: returns slot index of the key, or -1; *free_slot = first reusable slot on the chain.
+int64_t dir_find(const orl_ctx* c, const orl_grain_key& k, int64_t* free_slot) {
+    const uint32_t h = jenkins3(k.type_code_data, k.n0, k.n1);
+    uint64_t i = fmix32(h) & c->mask;
+    int64_t fr = -1;
+    for (uint64_t step = 0; step <= c->mask; ++step) {
+        const DirSlot& s = c->table[i];
+        if (s.state == SLOT_EMPTY) { if (fr < 0) fr = (int64_t)i; break; }
+        if (s.state == SLOT_TOMB) { if (fr < 0) fr = (int64_t)i; }
+        else if (keys_equal(s, k)) { if (free_slot) *free_slot = fr; return (int64_t)i; }
+        i = (i + 1) & c->mask;
+    }
+    if (free_slot) *free_slot = fr;
+    return -1;
+}
+
+int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
+    if (in_bytes > c->st_in_cap) {
+        if (c->st_in) (void)hipFree(c->st_in);
+        c->st_in = nullptr; c->st_in_cap = 0;
+        ORL_HIP(c, hipMalloc(&c->st_in, in_bytes));
+        c->st_in_cap = in_bytes;
+    }
+    if (out_words > c->st_out_cap) {
+        if (c->st_out) (void)hipFree(c->st_out);
+        c->st_out = nullptr; c->st_out_cap = 0;
+        ORL_HIP(c, hipMalloc(&c->st_out, out_words * sizeof(uint32_t)));
+        c->st_out_cap = out_words;
+    }
+    return ORL_OK;
+}
+
+void free_device(orl_ctx* c) {
+    auto f = [](void* p) { if (p) (void)hipFree(p); };
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
+    f(c->s.keys_a); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits);
+    f(c->st_in); f(c->st_out); f(c->st_off);
+    for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+}  // namespace
+
+// =====================================================================================================
+extern "C" {
+
+uint32_t orl_abi_version(void) { return ORL_ABI_VERSION; }
+
+int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
+    if (!cfg || !out) return ORL_E_INVALID;
+    *out = nullptr;
+    if (cfg->abi_version != ORL_ABI_VERSION) return ORL_E_INVALID;
+    if (cfg->n_act == 0 || cfg->n_act >= 0x7FFFFFFFu) return ORL_E_INVALID;
+    if (cfg->placement_policy > ORL_POLICY_HASH_SPREAD) return ORL_E_INVALID;
+    if (cfg->max_batch >= (1ull << 31)) return ORL_E_INVALID;
+    orl_ctx* c = new (std::nothrow) orl_ctx();
+    if (!c) return ORL_E_NOMEM;
+    c->cfg = *cfg;
+    // Constants.SystemMembershipTableId = SystemGrain Guid 01145FEC-C21E-11E0-9105-D0FB4724019B (Constants.cs:66):
+    // Guid.ToByteArray = EC 5F 14 01 | 1E C2 | E0 11 | 91 05 D0 FB 47 24 01 9B
+    c->hp.mem_tcd = (uint64_t)ORL_CAT_SYSTEM_GRAIN << 56;
+    c->hp.mem_n0 = 0x11E0C21E01145FECull;
+    c->hp.mem_n1 = 0x9B012447FBD00591ull;
+    const uint64_t slots = next_pow2(std::max<uint64_t>(cfg->dir_capacity, 1) * 2);
+    try {
+        c->table.assign(slots, DirSlot{});
+    } catch (...) {
+        delete c;
+        return ORL_E_NOMEM;
+    }
+    c->mask = slots - 1;
+    rebuild_params(c);
+    if (cfg->device >= 0) {
+        c->device_mode = true;
+        auto bail = [&](hipError_t e, const char* what) {
+            int r = hipfail(c, e, what);
+            free_device(c);
+            delete c;
+            return r;
+        };
+        hipError_t e;
+        if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
+        if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
+        if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
+        if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
+        if ((e = hipMalloc((void**)&c->d_rank_of_silo, 256)) != hipSuccess) return bail(e, "hipMalloc(rank map)");
+        const uint64_t mb = std::max<uint64_t>(cfg->max_batch, kTile);
+        const uint64_t tiles = (mb + kTile - 1) / kTile;
+        c->s.max_batch = mb;
+        c->s.max_tiles = tiles;
+        const uint64_t hist_words = (1ull << kMaxDigitBits) * tiles;
+        if ((e = hipMalloc((void**)&c->s.keys_a, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(keys)");
+        if ((e = hipMalloc((void**)&c->s.idx_a, (mb + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(idx)");
+        if ((e = hipMalloc((void**)&c->s.sorted_keys, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(sorted)");
+        if ((e = hipMalloc((void**)&c->s.tile_hist, hist_words * 4)) != hipSuccess) return bail(e, "hipMalloc(tile_hist)");
+        if ((e = hipMalloc((void**)&c->s.scan_sums, ((hist_words + 4095) / 4096 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(scan)");
+        if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
+        if ((e = hipMalloc((void**)&c->st_off, ((size_t)cfg->n_act + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(offsets)");
+    }
+    *out = c;
+    return ORL_OK;
+}
+
+int orl_ctx_destroy(orl_ctx* c) {
+    if (!c) return ORL_E_INVALID;
+    if (c->device_mode) {
+        (void)hipSetDevice(c->cfg.device);
+        (void)hipStreamSynchronize(c->stream);
+        free_device(c);
+    }
+    delete c;
+    return ORL_OK;
+}
+
+const char* orl_last_error(const orl_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int orl_silos_set(orl_ctx* c, uint32_t n, const uint8_t* running, const uint8_t* functional, const uint8_t* local,
+                  uint32_t seed) {
+    if (!c) return ORL_E_INVALID;
+    if (n == 0 || n > ORL_MAX_SILOS) return fail(c, ORL_E_INVALID, "n_silos must be in [1, %u]", ORL_MAX_SILOS);
+    if (seed != ORL_NULL_SILO && seed >= n) return fail(c, ORL_E_INVALID, "seed %u out of range", seed);
+    for (auto& e : c->ring)
+        if (e.second >= n) return fail(c, ORL_E_STATE, "ring holds silo %u >= n_silos", e.second);
+    c->n_silos = n;
+    c->running.assign(n, 1); c->functional.assign(n, 1); c->local.assign(n, 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (running) c->running[i] = running[i] ? 1 : 0;
+        if (functional) c->functional[i] = functional[i] ? 1 : 0;
+        if (local) c->local[i] = local[i] ? 1 : 0;
+    }
+    c->seed = seed;
+    rebuild_params(c);
+    return ORL_OK;
+}
+
+int orl_ring_add_server(orl_ctx* c, uint32_t silo, int32_t hash) {
+    if (!c) return ORL_E_INVALID;
+    if (!silo_ok(c, silo)) return fail(c, ORL_E_INVALID, "silo %u not in the silo table (call orl_silos_set first)", silo);
+    for (auto& e : c->ring)
+        if (e.second == silo) return ORL_OK;  // membershipCache.Contains → already cached (:247-251)
+    if (c->ring.size() >= ORL_MAX_RING) return fail(c, ORL_E_CAPACITY, "ring full");
+    // FindLastIndex(s => s.hash < hash) + 1: before existing equal hashes (:259-261)
+    int idx = -1;
+    for (int i = 0; i < (int)c->ring.size(); ++i)
+        if (c->ring[i].first < hash) idx = i;
+    c->ring.insert(c->ring.begin() + (idx + 1), std::make_pair(hash, (uint8_t)silo));
+    rebuild_params(c);
+    return ORL_OK;
+}
+
+int orl_ring_remove_server(orl_ctx* c, uint32_t silo) {
+    if (!c) return ORL_E_INVALID;
+    auto it = std::find_if(c->ring.begin(), c->ring.end(), [&](const std::pair<int32_t, uint8_t>& e) { return e.second == silo; });
+    if (it != c->ring.end()) c->ring.erase(it);
+    rebuild_params(c);
+    return ORL_OK;
+}
+
+int orl_ring_get(const orl_ctx* c, int32_t* hashes, uint8_t* silos, uint32_t cap, uint32_t* n_out) {
+    if (!c || !n_out) return ORL_E_INVALID;
+    *n_out = (uint32_t)c->ring.size();
+    for (uint32_t i = 0; i < c->ring.size() && i < cap; ++i) {
+        if (hashes) hashes[i] = c->ring[i].first;
+        if (silos) silos[i] = c->ring[i].second;
+    }
+    return ORL_OK;
+}
+
+int orl_calc_id_hash(const char* utf8, size_t len, int32_t* out) {
+    if (!out || (!utf8 && len)) return ORL_E_INVALID;
+    std::vector<uint8_t> u16;
+    if (!utf8_to_utf16le(utf8, len, u16)) return ORL_E_INVALID;
+    *out = calc_id_hash_utf16(u16);
+    return ORL_OK;
+}
+
+int orl_silo_consistent_hash(const char* endpoint, int32_t generation, int32_t* out) {
+    if (!endpoint || !out) return ORL_E_INVALID;
+    std::string s(endpoint);
+    s += std::to_string(generation);  // Generation.ToString(CultureInfo.InvariantCulture)
+    return orl_calc_id_hash(s.data(), s.size(), out);
+}
+
+uint32_t orl_jenkins_bytes(const uint8_t* data, size_t len) { return jenkins_bytes(data, len); }
+
+uint32_t orl_keyext_uniform_hash(const orl_grain_key* k, const char* ext, size_t len) {
+    // BinaryTokenStreamWriter.Write(UniqueKey): N0, N1, TypeCodeData (LE8), Write(string) = int32 len + UTF-8
+    std::vector<uint8_t> b(28 + len);
+    auto put64 = [&](size_t o, uint64_t v) { for (int i = 0; i < 8; ++i) b[o + i] = (uint8_t)(v >> (8 * i)); };
+    put64(0, k->n0);
+    put64(8, k->n1);
+    put64(16, k->type_code_data);
+    const uint32_t l = (uint32_t)len;
+    for (int i = 0; i < 4; ++i) b[24 + i] = (uint8_t)(l >> (8 * i));
+    if (len) std::memcpy(b.data() + 28, ext, len);
+    return jenkins_bytes(b.data(), b.size());
+}
+
+int orl_dir_insert_single(orl_ctx* c, const orl_grain_key* keys, const uint32_t* acts, const uint8_t* silos, size_t n,
+                          uint32_t* wact, uint8_t* wsilo, uint8_t* status) {
+    if (!c || (n && (!keys || !acts || !silos))) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t st;
+        uint32_t a = ORL_NO_ACT;
+        uint8_t s = ORL_NULL_SILO;
+        const orl_grain_key& k = keys[i];
+        const uint32_t cat = (uint32_t)(k.type_code_data >> 56);
+        if (acts[i] >= c->cfg.n_act) return fail(c, ORL_E_INVALID, "act %u >= n_act %u at %zu", acts[i], c->cfg.n_act, i);
+        if (!silo_ok(c, silos[i])) return fail(c, ORL_E_INVALID, "silo %u out of range at %zu", silos[i], i);
+        if (cat == ORL_CAT_KEYEXT_GRAIN || cat == ORL_CAT_SYSTEM_TARGET) {
+            st = ORL_INS_UNSUPPORTED;
+        } else {
+            const uint32_t owner = host_owner(c, k, silos[i], true);
+            if (owner == ORL_NULL_SILO) st = ORL_INS_OWNER_NULL;
+            else if (!c->local[owner]) st = ORL_INS_REMOTE_OWNER;
+            else if (!c->functional[silos[i]]) st = ORL_INS_INVALID_SILO;  // AddSingleActivation :277-279
+            else {
+                int64_t fr = -1;
+                const int64_t at = dir_find(c, k, &fr);
+                if (at >= 0) {  // GrainInfo.AddSingleActivation: an instance exists → return it (:103-107)
+                    st = ORL_INS_EXISTING;
+                    a = c->table[at].act;
+                    s = c->table[at].silo;
+                } else {
+                    if (fr < 0 || (c->count + c->tombs + 1) * 2 > c->table.size())
+                        return fail(c, ORL_E_CAPACITY, "directory full (%llu entries)", (unsigned long long)c->count);
+                    DirSlot& d = c->table[fr];
+                    if (d.state == SLOT_TOMB) --c->tombs;
+                    d.tcd = k.type_code_data; d.n0 = k.n0; d.n1 = k.n1;
+                    d.act = acts[i]; d.silo = silos[i]; d.state = SLOT_FULL; d.pad = 0;
+                    ++c->count;
+                    c->dir_dirty = true;
+                    st = ORL_INS_INSERTED;
+                    a = acts[i];
+                    s = silos[i];
+                }
+            }
+        }
+        if (status) status[i] = st;
+        if (wact) wact[i] = a;
+        if (wsilo) wsilo[i] = s;
+    }
+    return ORL_OK;
+}
+
+int orl_dir_remove(orl_ctx* c, const orl_grain_key* keys, size_t n, uint8_t* removed) {
+    if (!c || (n && !keys)) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        const int64_t at = dir_find(c, keys[i], nullptr);
+        if (at >= 0) {
+            c->table[at].state = SLOT_TOMB;
+            --c->count;
+            ++c->tombs;
+            c->dir_dirty = true;
+        }
+        if (removed) removed[i] = at >= 0 ? 1 : 0;
+    }
+    return ORL_OK;
+}
+
+int orl_dir_count(const orl_ctx* c, uint64_t* n) {
+    if (!c || !n) return ORL_E_INVALID;
+    *n = c->count;
+    return ORL_OK;
+}
+
+int orl_dir_lookup_host(const orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* act, uint8_t* silo) {
+    if (!c || (n && !keys)) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        const int64_t at = dir_find(c, keys[i], nullptr);
+        if (act) act[i] = at >= 0 ? c->table[at].act : ORL_NO_ACT;
+        if (silo) silo[i] = at >= 0 ? c->table[at].silo : (uint8_t)ORL_NULL_SILO;
+    }
+    return ORL_OK;
+}
+
+int orl_hash_batch(orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* out) {
+    if (!c || (n && (!keys || !out))) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (n == 0) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    int r = ensure_staging(c, n * sizeof(orl_grain_key), n);
+    if (r) return r;
+    ORL_HIP(c, hipMemcpyAsync(c->st_in, keys, n * sizeof(orl_grain_key), hipMemcpyHostToDevice, c->stream));
+    int e = launch_hash((const orl_grain_key*)c->st_in, n, c->st_out, c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "k_hash");
+    ORL_HIP(c, hipMemcpyAsync(out, c->st_out, n * 4, hipMemcpyDeviceToHost, c->stream));
+    ORL_HIP(c, hipStreamSynchronize(c->stream));
+    return ORL_OK;
+}
+
+int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                           uint32_t* d_order, uint32_t* d_off, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_in || !d_route || !d_act)) return fail(c, ORL_E_INVALID, "null device buffer");
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    if (buckets && (!d_off || (n && !d_order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
+    int r = sync_device_state(c);
+    if (r) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipEvent_t* ev = nullptr;
+    if (c->timing && n > 0 && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
+    if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
+    int e = launch_route_bucket(c->d_params, c->d_table, c->mask, d_in, n, opts, c->cfg.n_act, d_route, d_act, d_order, d_off,
+                                c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
+    if (e) return hipfail(c, (hipError_t)e, "route launch");
+    if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
+    return ORL_OK;
+}
+
+int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                    uint32_t* order, uint32_t* offsets) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    if (n && (!in || !route || !act)) return fail(c, ORL_E_INVALID, "null host buffer");
+    if (buckets && (!offsets || (n && !order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    int r = ensure_staging(c, std::max<size_t>(n, 1) * sizeof(orl_msg_hdr), std::max<size_t>(n, 1) * 3);
+    if (r) return r;
+    uint32_t* d_route = c->st_out;
+    uint32_t* d_act = d_route + n;
+    uint32_t* d_order = d_act + n;
+    if (n) ORL_HIP(c, hipMemcpyAsync(c->st_in, in, n * sizeof(orl_msg_hdr), hipMemcpyHostToDevice, c->stream));
+    r = orl_route_batch_device(c, (const orl_msg_hdr*)c->st_in, n, opts, d_route, d_act, d_order, c->st_off, c->stream);
+    if (r) return r;
+    if (n) {
+        ORL_HIP(c, hipMemcpyAsync(route, d_route, n * 4, hipMemcpyDeviceToHost, c->stream));
+        ORL_HIP(c, hipMemcpyAsync(act, d_act, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (buckets) ORL_HIP(c, hipMemcpyAsync(order, d_order, n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (buckets) ORL_HIP(c, hipMemcpyAsync(offsets, c->st_off, ((size_t)c->cfg.n_act + 2) * 4, hipMemcpyDeviceToHost, c->stream));
+    ORL_HIP(c, hipStreamSynchronize(c->stream));
+    return ORL_OK;
+}
+
+int orl_fanout_route_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const uint32_t* d_pubs,
+                            const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                            uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                            uint32_t* d_off, uint64_t* n_out, void* stream) {
+    if (!c || !n_out) return ORL_E_INVALID;
+    if (!d_csr_off || !d_csr_tgt || !d_pub_offsets || !d_route || !d_act) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n_pub && (!d_pubs || !d_pub_silo)) return fail(c, ORL_E_INVALID, "null publisher buffer");
+    if (!(opts & ORL_OPT_NO_BUCKETS) && (!d_order || !d_off)) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
+    if (n_pub + 1 > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "too many publishers");
+    if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
+    int r = sync_device_state(c);
+    if (r) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_fanout_route_bucket(c->d_params, c->d_table, c->mask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, n_pub,
+                                       follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
+                                       c->s.max_batch, c->s, st);
+    if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > max_batch", (unsigned long long)*n_out);
+    if (e) return hipfail(c, (hipError_t)e, "fanout launch");
+    return ORL_OK;
+}
+
+int orl_partition_by_owner_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                  uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out, uint32_t* d_src, uint64_t* d_counts,
+                                  void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (nranks == 0 || nranks > 8 || my_rank >= nranks) return fail(c, ORL_E_INVALID, "nranks must be 1..8 and my_rank < nranks");
+    if (n && (!d_in || !d_out || !d_src)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (!d_counts) return fail(c, ORL_E_INVALID, "null counts buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch too large");
+    int r = sync_device_state(c);
+    if (r) return r;
+    uint8_t ros[256];
+    std::memset(ros, 0, sizeof ros);
+    for (uint32_t s = 0; s < c->n_silos; ++s) {
+        if (rank_of_silo[s] >= nranks) return fail(c, ORL_E_INVALID, "rank_of_silo[%u] = %u >= nranks", s, rank_of_silo[s]);
+        ros[s] = rank_of_silo[s];
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    ORL_HIP(c, hipMemcpyAsync(c->d_rank_of_silo, ros, 256, hipMemcpyHostToDevice, st));
+    ORL_HIP(c, hipStreamSynchronize(st));
+    int e = launch_partition_by_owner(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, d_out, d_src, d_counts,
+                                      c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "partition launch");
+    return ORL_OK;
+}
+
+int orl_sync(orl_ctx* c) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return ORL_OK;
+    ORL_HIP(c, hipStreamSynchronize(c->stream));
+    return ORL_OK;
+}
+
+int orl_set_timing(orl_ctx* c, int enable) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+    if (enable && c->tev.empty()) {
+        c->tev.assign(4 * (size_t)ORL_TIMING_SLOTS, nullptr);
+        for (auto& e : c->tev) ORL_HIP(c, hipEventCreate(&e));
+    }
+    c->timing = enable != 0;
+    c->tcount = 0;
+    return ORL_OK;
+}
+
+int orl_timing_summary(const orl_ctx* cc, uint32_t* n_batches, float* route_ms, float* bucket_ms, float* total_ms) {
+    orl_ctx* c = const_cast<orl_ctx*>(cc);
+    if (!c) return ORL_E_INVALID;
+    if (n_batches) *n_batches = c->tcount;
+    if (c->tcount == 0) return fail(c, ORL_E_STATE, "no timed batch");
+    ORL_HIP(c, hipEventSynchronize(c->tev[4 * (size_t)(c->tcount - 1) + 3]));
+    double a = 0, b = 0, t = 0;
+    for (uint32_t i = 0; i < c->tcount; ++i) {
+        const hipEvent_t* ev = &c->tev[4 * (size_t)i];
+        float x = 0, y = 0, z = 0;
+        ORL_HIP(c, hipEventElapsedTime(&x, ev[1], ev[2]));
+        ORL_HIP(c, hipEventElapsedTime(&y, ev[2], ev[3]));
+        ORL_HIP(c, hipEventElapsedTime(&z, ev[0], ev[3]));
+        a += x; b += y; t += z;
+    }
+    if (route_ms) *route_ms = (float)(a / c->tcount);
+    if (bucket_ms) *bucket_ms = (float)(b / c->tcount);
+    if (total_ms) *total_ms = (float)(t / c->tcount);
+    return ORL_OK;
+}
+
+}  // extern "C"

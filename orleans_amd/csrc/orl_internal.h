@@ -1,0 +1,147 @@
+// orl_internal.h — layouts shared by the host side (orl_api.cpp) and the CDNA4 kernels (route_kernels.hip).
+//
+// Nothing here is part of the public ABI (include/orleans_route.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/orleans_route.h"
+
+namespace orl {
+
+// ---- directory partition table (GrainDirectoryPartition, single-activation grains) -----------------
+// Open addressing, linear probing, power-of-two slot count, load <= 0.5.  One 32-B slot per grain:
+// the full 24-B GrainId key (UniqueKey.Equals compares N0,N1,TCD: UniqueKey.cs:248-255), the dense
+// activation handle, the activation's silo (ActivationInfo.SiloAddress) and a state byte.  Two slots
+// share a 64-B line, so a probe that steps once usually stays in the line it already fetched.
+enum : uint8_t { SLOT_EMPTY = 0, SLOT_FULL = 1, SLOT_TOMB = 2 };
+
+struct alignas(32) DirSlot {
+    uint64_t tcd;
+    uint64_t n0;
+    uint64_t n1;
+    uint32_t act;
+    uint8_t silo;
+    uint8_t state;
+    uint16_t pad;
+};
+static_assert(sizeof(DirSlot) == 32, "slot must be 32 bytes");
+
+// Probe start: murmur3 fmix32 of the Jenkins uniform hash.  The uniform hash alone would do for one
+// silo, but a GPU that holds only some ring ranges sees hashes confined to those ranges; fmix32 is a
+// bijection that spreads any range over the whole table.
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// ---- Jenkins lookup2, 24-byte form (JenkinsHash.cs:54-65, 126-144) ---------------------------------
+#define ORL_MIX(a, b, c)                 \
+    do {                                 \
+        a -= b; a -= c; a ^= (c >> 13);  \
+        b -= c; b -= a; b ^= (a << 8);   \
+        c -= a; c -= b; c ^= (b >> 13);  \
+        a -= b; a -= c; a ^= (c >> 12);  \
+        b -= c; b -= a; b ^= (a << 16);  \
+        c -= a; c -= b; c ^= (b >> 5);   \
+        a -= b; a -= c; a ^= (c >> 3);   \
+        b -= c; b -= a; b ^= (a << 10);  \
+        c -= a; c -= b; c ^= (b >> 15);  \
+    } while (0)
+
+__host__ __device__ inline uint32_t jenkins3(uint64_t u1, uint64_t u2, uint64_t u3) {
+    uint32_t a = 0x9e3779b9u, b = 0x9e3779b9u, c = 0u;
+    a += (uint32_t)u1;
+    b += (uint32_t)(u1 >> 32);
+    c += (uint32_t)u2;
+    ORL_MIX(a, b, c);
+    a += (uint32_t)(u2 >> 32);
+    b += (uint32_t)u3;
+    c += (uint32_t)(u3 >> 32);
+    ORL_MIX(a, b, c);
+    c += 24u;
+    ORL_MIX(a, b, c);
+    return c;
+}
+
+// ---- everything a route launch needs besides the messages (device copy, staged into LDS) ------------
+struct alignas(16) RouteParams {
+    int32_t ring_hash[ORL_MAX_RING];   // membershipRingList, ascending signed hash
+    uint8_t ring_silo[ORL_MAX_RING];
+    uint8_t active_list[256];          // functional silos ascending (HASH_SPREAD placement)
+    uint32_t running[8];               // 256-bit masks
+    uint32_t functional[8];
+    uint32_t local[8];
+    uint32_t ring_n;
+    uint32_t seed;
+    uint32_t policy;
+    uint32_t n_active;
+    uint32_t n_act;
+    uint32_t pad0[3];
+    uint64_t mem_tcd, mem_n0, mem_n1;  // Constants.SystemMembershipTableId
+    uint64_t pad1;
+};
+static_assert(sizeof(RouteParams) % 16 == 0, "params must be 16-B granular");
+
+constexpr uint32_t kRouteThreads = 256;
+constexpr uint32_t kItems = 16;                               // messages per thread per tile
+constexpr uint32_t kTile = kRouteThreads * kItems;            // 4096 messages per tile
+constexpr uint32_t kMaxDigitBits = 11;                        // radix digit width cap (2048 bins)
+
+// Radix plan for keys in [0, n_buckets): passes of <= kMaxDigitBits bits, low digit first (LSD).
+struct RadixPlan {
+    int passes;
+    int shift[4];
+    int bits[4];
+};
+
+inline RadixPlan make_plan(uint32_t max_key) {
+    int total = 0;
+    while ((max_key >> total) != 0 && total < 32) ++total;
+    if (total == 0) total = 1;
+    RadixPlan p{};
+    p.passes = (total + (int)kMaxDigitBits - 1) / (int)kMaxDigitBits;
+    int base = total / p.passes, extra = total % p.passes, s = 0;
+    for (int i = 0; i < p.passes; ++i) {
+        p.bits[i] = base + (i < extra ? 1 : 0);
+        p.shift[i] = s;
+        s += p.bits[i];
+    }
+    return p;
+}
+
+// ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
+// All return hipError_t as int; they only enqueue on `stream`.
+struct Scratch {
+    uint32_t* keys_a;       // [max_batch]
+    uint32_t* idx_a;        // [max_batch]
+    uint32_t* sorted_keys;  // [max_batch]
+    uint32_t* tile_hist;    // [2048 * max_tiles]
+    uint32_t* scan_sums;    // [scan blocks]
+    uint8_t* digits;        // [max_batch] (partition by owner)
+    uint64_t max_batch;
+    uint64_t max_tiles;
+};
+
+int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
+int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
+                        const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
+                        uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
+                        void* ev_route_begin, void* ev_route_end);
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
+                               const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const uint32_t* d_pubs,
+                               const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                               uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
+                               uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out,
+                               const Scratch& s, void* stream);
+int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                              const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
+                              uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);
+
+}  // namespace orl

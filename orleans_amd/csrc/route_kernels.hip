@@ -1,0 +1,794 @@
+// route_kernels.hip — CDNA4 (gfx950) kernels of the batched grain-message routing pipeline.
+//
+// Stage map (reference paths relative to randa1/orleans):
+//   k_route          stages 1-3: JenkinsHash (JenkinsHash.cs:126-144) → CalculateTargetSilo ring
+//                    predecessor search (LocalGrainDirectory.cs:439-497) → GrainDirectoryPartition.LookUpGrain
+//                    + IsValidSilo (GrainDirectoryPartition.cs:326-344) → placement of misses
+//                    (PlacementDirectorsManager.cs:70-91).  Fused with the first radix digit's tile histogram.
+//   k_radix_up/down  stage 4: stable LSD radix partition by activation handle = per-activation FIFO
+//                    (ActivationData.EnqueueMessage, ActivationData.cs:483-514).
+//   k_offsets        per-activation bucket offsets from the sorted keys.
+//   k_fanout_*       stage 5: CSR multicast expansion (ChirperAccount.cs:154-157) feeding stages 1-4.
+//   k_part_*         stable partition of headers by destination rank (exchange).
+//
+// Everything is integer/byte work and HBM-bound: no MFMA.  Tiles are 4096 messages (256 threads x 16),
+// so a 64M batch is 16384 workgroups (>> 256 CUs).  All LDS lives in one __shared__ block per kernel.
+#include <hip/hip_runtime.h>
+
+#include "orl_internal.h"
+
+namespace orl {
+
+namespace {
+
+constexpr uint32_t kWaves = kRouteThreads / 64;
+
+__device__ __forceinline__ bool mask_bit(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31u)) & 1u; }
+
+__device__ __forceinline__ uint32_t pack_route(uint32_t owner, uint32_t host, uint32_t st, uint32_t fl) {
+    return (owner & 0xFFu) | ((host & 0xFFu) << 8) | ((st & 0xFFu) << 16) | ((fl & 0xFFu) << 24);
+}
+
+// Cooperative copy of the launch parameters into LDS (1.8 KB, 16-B granules).
+__device__ __forceinline__ void stage_params(RouteParams* sp, const RouteParams* __restrict__ gp) {
+    const uint4* src = reinterpret_cast<const uint4*>(gp);
+    uint4* dst = reinterpret_cast<uint4*>(sp);
+    for (uint32_t i = threadIdx.x; i < sizeof(RouteParams) / 16; i += blockDim.x) dst[i] = src[i];
+}
+
+// Directory owner of a non-special grain: LocalGrainDirectory.CalculateTargetSilo(:466-494).
+// Ring sorted ascending by signed hash; FindLast(hash_s <= h && !(s == me && excludeMySelf)) is the
+// upper bound minus one, stepped back over the (single) excluded entry; none found → wrap to ring[n-1]
+// (ring[n-2] if that is the excluded me, null if n == 1).  Returns 0xFF for null.
+__device__ __forceinline__ uint32_t ring_owner(const RouteParams& P, int32_t h, uint32_t me, bool exclude_me) {
+    const int n = (int)P.ring_n;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (P.ring_hash[mid] <= h) lo = mid + 1; else hi = mid;
+    }
+    int idx = lo - 1;
+    if (idx >= 0 && exclude_me && P.ring_silo[idx] == me) --idx;
+    if (idx < 0) {
+        idx = n - 1;
+        if (exclude_me && P.ring_silo[idx] == me) {
+            if (n > 1) idx = n - 2; else return 0xFFu;
+        }
+    }
+    return P.ring_silo[idx];
+}
+
+struct Msg {
+    uint64_t tcd, n0, n1;
+    uint32_t meta;  // sending_silo | category<<8 | flags<<16 | target_silo<<24
+    uint32_t aux;
+};
+
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+
+// Headers are streamed once: non-temporal loads keep them from evicting the directory table from L2/MALL.
+__device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint32_t e) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(in + e);
+    const u32x4 a = __builtin_nontemporal_load(p);
+    const u32x4 b = __builtin_nontemporal_load(p + 1);
+    Msg m;
+    m.tcd = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    m.n0 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    m.n1 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    m.meta = b.z;
+    m.aux = b.w;
+    return m;
+}
+
+// Stages 1-3 for one message.  Mirrors oracle route_one (Dispatcher.AddressMessage, Dispatcher.cs:555-579).
+__device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t mask,
+                                              const Msg& m, bool excl_opt, uint32_t& act) {
+    act = ORL_NO_ACT;
+    const uint32_t me = m.meta & 0xFFu;
+    const uint32_t hflags = (m.meta >> 16) & 0xFFu;
+    if (hflags & ORL_HDR_ADDRESS_COMPLETE) {  // TargetAddress.IsComplete (Dispatcher.cs:557-558)
+        const uint32_t ts = m.meta >> 24;
+        return pack_route(0xFFu, ts, ORL_ST_ADDRESS_COMPLETE, ts == me ? ORL_RF_LOOPBACK : 0u);
+    }
+    const uint32_t cat = (uint32_t)(m.tcd >> 56);
+    const uint32_t h = (hflags & ORL_HDR_HASH_VALID) ? m.aux : jenkins3(m.tcd, m.n0, m.n1);  // stage 1
+    if (cat == ORL_CAT_SYSTEM_TARGET)  // every silo owns its system targets (:442-447)
+        return pack_route(me, me, ORL_ST_SYSTEM_TARGET, ORL_RF_LOOPBACK);
+    uint32_t owner, rf = 0;
+    if (m.tcd == P.mem_tcd && m.n0 == P.mem_n0 && m.n1 == P.mem_n1) {  // membership table grain (:449-464)
+        if (P.seed == 0xFFu) return pack_route(0xFFu, 0xFFu, ORL_ST_NO_SEED, 0);
+        owner = P.seed;
+        rf = ORL_RF_OWNER_IS_SEED;
+    } else {  // stage 2
+        const bool running = mask_bit(P.running, me);
+        if (P.ring_n == 0) {
+            if (excl_opt && !running) return pack_route(0xFFu, 0xFFu, ORL_ST_OWNER_NULL, 0);
+            owner = me;
+        } else {
+            owner = ring_owner(P, (int32_t)h, me, excl_opt && !running);
+            if (owner == 0xFFu) return pack_route(0xFFu, 0xFFu, ORL_ST_OWNER_NULL, 0);
+        }
+    }
+    if (cat == ORL_CAT_KEYEXT_GRAIN) return pack_route(owner, 0xFFu, ORL_ST_KEYEXT_UNRESOLVED, rf);
+    if (!mask_bit(P.local, owner)) return pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, rf);
+    // stage 3: open-addressed partition probe; tombstones are skipped, an empty slot ends the chain.
+    uint64_t slot = fmix32(h) & mask;
+    bool found = false;
+    uint32_t fact = 0, fsilo = 0;
+    for (uint64_t step = 0; step <= mask; ++step) {
+        const uint4* sp = reinterpret_cast<const uint4*>(dir + slot);
+        const uint4 a = sp[0];
+        const uint4 b = sp[1];
+        const uint32_t state = (b.w >> 8) & 0xFFu;
+        if (state == SLOT_EMPTY) break;
+        if (state == SLOT_FULL && a.x == (uint32_t)m.tcd && a.y == (uint32_t)(m.tcd >> 32) &&
+            a.z == (uint32_t)m.n0 && a.w == (uint32_t)(m.n0 >> 32) && b.x == (uint32_t)m.n1 &&
+            b.y == (uint32_t)(m.n1 >> 32)) {
+            found = true;
+            fact = b.z;
+            fsilo = b.w & 0xFFu;
+            break;
+        }
+        slot = (slot + 1) & mask;
+    }
+    if (found && mask_bit(P.functional, fsilo)) {  // LookUpGrain filtered by IsValidSilo
+        act = fact;
+        return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u));
+    }
+    if (cat == ORL_CAT_CLIENT) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
+    uint32_t host;
+    if (P.policy == ORL_POLICY_PREFER_LOCAL) host = me;
+    else host = P.n_active ? P.active_list[h % P.n_active] : 0xFFu;
+    rf |= ORL_RF_NEW_PLACEMENT | (host == me ? ORL_RF_LOOPBACK : 0u);
+    return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf);
+}
+
+__device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
+
+// ---------------------------------------------------------------------------------------------------
+// stage 1 alone
+__global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = jenkins3(keys[i].type_code_data, keys[i].n0, keys[i].n1);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// stages 1-3 (+ tile histogram of the first radix digit).  Tile t covers messages [t*4096, t*4096+4096);
+// thread x handles e = t*4096 + j*256 + x, j = 0..15 (coalesced 8-KB header rows per j).
+struct RouteSmem {
+    RouteParams P;
+    uint32_t hist[1u << kMaxDigitBits];
+};
+
+template <bool HIST>
+__global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
+                                                         uint64_t mask, const orl_msg_hdr* __restrict__ in, uint32_t n,
+                                                         uint32_t excl, uint32_t* __restrict__ route,
+                                                         uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
+                                                         uint32_t ntiles, uint32_t bins, uint32_t shift) {
+    __shared__ RouteSmem sm;
+    stage_params(&sm.P, gp);
+    if (HIST)
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
+    __syncthreads();
+    const uint32_t n_act = sm.P.n_act;
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 2
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
+        if (e < n) {
+            const Msg m = load_hdr(in, e);
+            uint32_t act;
+            const uint32_t r = route_msg(sm.P, dir, mask, m, excl != 0, act);
+            route[e] = r;
+            act_out[e] = act;
+            if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+        }
+    }
+    if (HIST) {
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) tile_hist[(size_t)b * ntiles + blockIdx.x] = sm.hist[b];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Device-wide exclusive scan of u32 (3 launches): per-block sums, one-block scan of the sums, and a
+// down-sweep that rescans each block's chunk with its prefix.  Chunk = 4096 elements per block.
+constexpr uint32_t kScanChunk = 4096;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one value per thread (256 threads); returns the exclusive prefix and the total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    total = 0;
+    for (uint32_t i = 0; i < kWaves; ++i) {
+        const uint32_t s = wsum[i];
+        if (i < w) pre += s;
+        total += s;
+    }
+    __syncthreads();
+    return pre + incl - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t wsum[kWaves];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < kScanChunk; i += 256) {
+        const uint64_t e = base + i;
+        if (e < m) s += a[e];
+    }
+    uint32_t total;
+    block_excl_scan(s, wsum, total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb) {
+    __shared__ uint32_t wsum[kWaves];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? sums[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan(v, wsum, total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+// Each thread owns 16 consecutive elements of the block's 4096-chunk.
+__global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums) {
+    __shared__ uint32_t wsum[kWaves];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16u;
+    uint32_t v[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        v[i] = (base + i < m) ? a[base + i] : 0u;
+        s += v[i];
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, wsum, total) + sums[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (base + i < m) a[base + i] = run;
+        run += v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Stage 4, one LSD digit.  Up-sweep: per-tile digit histogram, stored bin-major ([bin][tile]) so one
+// exclusive scan of the whole matrix yields every (bin, tile) output base.
+__global__ __launch_bounds__(256) void k_radix_up(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t bins,
+                                                  uint32_t* __restrict__ tile_hist, uint32_t ntiles) {
+    __shared__ uint32_t hist[1u << kMaxDigitBits];
+    for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 4
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = base + j * 256 + threadIdx.x;
+        if (e < n) atomicAdd(&hist[(keys[e] >> shift) & (bins - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < bins; b += 256) tile_hist[(size_t)b * ntiles + blockIdx.x] = hist[b];
+}
+
+// Down-sweep: stable rank of each key inside the tile, then scatter through an LDS staging image so the
+// global writes are runs of consecutive positions per bin.  Wave w owns tile elements
+// [w*1024, w*1024+1024) processed 64 at a time in order, so (wave, iteration, lane) order == arrival
+// order and the ranks are stable.  Lanes with equal digits are found with BITS ballots.
+template <int BITS>
+struct DownSmem {
+    uint32_t cnt[kWaves][1u << BITS];  // per-wave running counts, then per-wave exclusive prefixes
+    uint32_t bin_start[1u << BITS];    // tile-local bin starts
+    uint32_t goff[1u << BITS];         // global base of (bin, this tile)
+    uint32_t stage_k[kTile];
+    uint32_t stage_i[kTile];
+    uint32_t wsum[kWaves];
+};
+
+template <int BITS, bool FIRST>
+__global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ idx_in,
+                                                    uint32_t n, uint32_t n_act, uint32_t shift,
+                                                    const uint32_t* __restrict__ tile_off, uint32_t ntiles,
+                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out) {
+    constexpr uint32_t B = 1u << BITS;
+    constexpr uint32_t PER = (B + 255u) / 256u;  // bins per thread in the bin loops
+    __shared__ DownSmem<BITS> sm;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    for (uint32_t b = threadIdx.x; b < B; b += 256) {
+#pragma unroll
+        for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
+    }
+    __syncthreads();
+
+    const uint32_t tbase = blockIdx.x * kTile;
+    const uint32_t wbase = tbase + w * (kItems * 64u);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
+    uint32_t key[kItems], idx[kItems], rank[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        const bool valid = e < n;
+        uint32_t k = 0, ix = 0;
+        if (valid) {
+            k = keys_in[e];
+            if (FIRST) { k = bucket_key(k, n_act); ix = e; } else { ix = idx_in[e]; }
+        }
+        key[j] = k;
+        idx[j] = ix;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        const bool valid = e < n;
+        const uint32_t d = (key[j] >> shift) & (B - 1u);
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < BITS; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t before = (uint32_t)__popcll(m & lt_mask);
+        const uint32_t c = sm.cnt[w][d];
+        rank[j] = c + before;
+        // the highest lane of each equal-digit group advances the wave's count for the next 64
+        if (valid && (m >> lane) == 1ull) sm.cnt[w][d] = c + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // per-bin: wave prefixes (in place) and tile totals; then exclusive scan of totals over bins.
+    uint32_t tot[PER];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t b = threadIdx.x * PER + q;
+        uint32_t t = 0;
+        if (b < B) {
+#pragma unroll
+            for (uint32_t ww = 0; ww < kWaves; ++ww) {
+                const uint32_t c = sm.cnt[ww][b];
+                sm.cnt[ww][b] = t;
+                t += c;
+            }
+            sm.goff[b] = tile_off[(size_t)b * ntiles + blockIdx.x];
+        }
+        tot[q] = t;
+        s += t;
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, sm.wsum, total);
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t b = threadIdx.x * PER + q;
+        if (b < B) sm.bin_start[b] = run;
+        run += tot[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e < n) {
+            const uint32_t d = (key[j] >> shift) & (B - 1u);
+            const uint32_t lpos = sm.bin_start[d] + sm.cnt[w][d] + rank[j];
+            sm.stage_k[lpos] = key[j];
+            sm.stage_i[lpos] = idx[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (n - tbase) < kTile ? (n - tbase) : kTile;
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        const uint32_t k = sm.stage_k[i];
+        const uint32_t d = (k >> shift) & (B - 1u);
+        const uint32_t g = sm.goff[d] + (i - sm.bin_start[d]);
+        keys_out[g] = k;
+        idx_out[g] = sm.stage_i[i];
+    }
+}
+
+// bucket_offsets[b] = lower_bound(sorted, b) for b in [0, nb).  Block handles 256 buckets: two binary
+// searches bound its slice of the sorted keys, which it then walks once.
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_offsets(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
+                                                 uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t bounds[2];
+    const uint32_t b0 = blockIdx.x * 256u;
+    const uint32_t b1 = (b0 + 256u < nb) ? b0 + 256u : nb;
+    if (threadIdx.x == 0) bounds[0] = lower_bound_u32(sorted, n, b0);
+    if (threadIdx.x == 64) bounds[1] = lower_bound_u32(sorted, n, b1);
+    __syncthreads();
+    const uint32_t p0 = bounds[0], p1 = bounds[1];
+    if (threadIdx.x == 0) offsets[b0] = p0;
+    for (uint32_t i = p0 + 1 + threadIdx.x; i < p1; i += 256) {
+        const uint32_t k = sorted[i], kp = sorted[i - 1];
+        for (uint32_t b = kp + 1; b <= k; ++b) offsets[b] = i;  // buckets (kp, k] start at i
+    }
+    // buckets after the last key in [b0, b1) start at p1
+    if (threadIdx.x == 0) {
+        const uint32_t from = (p1 > p0) ? sorted[p1 - 1] + 1 : b0 + 1;
+        for (uint32_t b = from; b < b1; ++b) offsets[b] = p1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
+// over emitted messages, each tile locating its publishers with one binary search into the scanned
+// degrees staged in LDS.
+__global__ __launch_bounds__(256) void k_fanout_deg(const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
+                                                    uint32_t n_pub, uint32_t* __restrict__ deg) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p < n_pub) {
+        const uint32_t s = pubs[p];
+        deg[p] = (uint32_t)(csr_off[s + 1] - csr_off[s]);
+    } else if (p == n_pub) {
+        deg[p] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_widen64(const uint32_t* __restrict__ a, uint32_t m, uint64_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < m) out[i] = a[i];
+}
+
+constexpr uint32_t kFanLds = 2048;  // publishers staged per tile; beyond that fall back to global search
+
+struct FanSmem {
+    RouteParams P;
+    uint32_t hist[1u << kMaxDigitBits];
+    uint32_t poff[kFanLds + 1];
+    uint32_t prange[2];
+};
+
+template <bool HIST>
+__global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
+    const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask,
+    const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
+    const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
+    uint32_t n, uint32_t excl, uint32_t* __restrict__ route, uint32_t* __restrict__ act_out,
+    uint32_t* __restrict__ tile_hist, uint32_t ntiles, uint32_t bins, uint32_t shift) {
+    __shared__ FanSmem sm;
+    stage_params(&sm.P, gp);
+    if (HIST)
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
+    const uint32_t base = blockIdx.x * kTile;
+    const uint32_t last = ((n - base) < kTile ? n : base + kTile) - 1;
+    // publisher of emitted message e = upper_bound(poff32[0..n_pub], e) - 1
+    if (threadIdx.x == 0 || threadIdx.x == 64) {
+        const uint32_t v = threadIdx.x == 0 ? base : last;
+        uint32_t lo = 0, hi = n_pub + 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (poff32[mid] <= v) lo = mid + 1; else hi = mid;
+        }
+        sm.prange[threadIdx.x == 0 ? 0 : 1] = lo - 1;
+    }
+    __syncthreads();
+    const uint32_t p_lo = sm.prange[0], p_hi = sm.prange[1];
+    const uint32_t span = p_hi - p_lo + 1;  // publishers touching this tile
+    const bool in_lds = span <= kFanLds;
+    if (in_lds)
+        for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
+    __syncthreads();
+    const uint32_t n_act = sm.P.n_act;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
+        if (e >= n) break;
+        uint32_t lo, hi, p, start;
+        if (in_lds) {
+            lo = 0; hi = span + 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (sm.poff[mid] <= e) lo = mid + 1; else hi = mid;
+            }
+            p = p_lo + lo - 1;
+            start = sm.poff[lo - 1];
+        } else {
+            lo = p_lo; hi = p_hi + 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (poff32[mid] <= e) lo = mid + 1; else hi = mid;
+            }
+            p = lo - 1;
+            start = poff32[p];
+        }
+        const uint32_t src = pubs[p];
+        const uint32_t tgt = csr_tgt[csr_off[src] + (e - start)];
+        Msg m;
+        m.tcd = follower_tcd;
+        m.n0 = 0;
+        m.n1 = (uint64_t)tgt;
+        m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
+        m.aux = 0;
+        uint32_t act;
+        route[e] = route_msg(sm.P, dir, mask, m, excl != 0, act);
+        act_out[e] = act;
+        if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+    }
+    if (HIST) {
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) tile_hist[(size_t)b * ntiles + blockIdx.x] = sm.hist[b];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Exchange partition: destination rank per message (stages 1-2 only) + per-tile rank histogram, then a
+// stable scatter of the 32-B headers.  Messages that are not directory-routed (complete, system target,
+// null owner, no seed) stay on the sending rank.
+__device__ __forceinline__ uint32_t dest_rank(const RouteParams& P, const uint8_t* __restrict__ rank_of_silo, const Msg& m,
+                                              bool excl_opt, uint32_t my_rank) {
+    const uint32_t me = m.meta & 0xFFu;
+    const uint32_t hflags = (m.meta >> 16) & 0xFFu;
+    if (hflags & ORL_HDR_ADDRESS_COMPLETE) return my_rank;
+    const uint32_t cat = (uint32_t)(m.tcd >> 56);
+    if (cat == ORL_CAT_SYSTEM_TARGET) return my_rank;
+    const uint32_t h = (hflags & ORL_HDR_HASH_VALID) ? m.aux : jenkins3(m.tcd, m.n0, m.n1);
+    uint32_t owner;
+    if (m.tcd == P.mem_tcd && m.n0 == P.mem_n0 && m.n1 == P.mem_n1) {
+        owner = P.seed;
+    } else {
+        const bool running = mask_bit(P.running, me);
+        if (P.ring_n == 0) owner = (excl_opt && !running) ? 0xFFu : me;
+        else owner = ring_owner(P, (int32_t)h, me, excl_opt && !running);
+    }
+    if (owner == 0xFFu) return my_rank;
+    return rank_of_silo[owner];
+}
+
+struct PartSmem {
+    RouteParams P;
+    uint8_t rank_of_silo[256];
+    uint32_t hist[8];
+};
+
+__global__ __launch_bounds__(kRouteThreads) void k_part_digits(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
+                                                               const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
+                                                               uint32_t my_rank, uint8_t* __restrict__ digits,
+                                                               uint32_t* __restrict__ tile_hist, uint32_t ntiles, uint32_t nranks) {
+    __shared__ PartSmem sm;
+    stage_params(&sm.P, gp);
+    sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
+    if (threadIdx.x < 8) sm.hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kTile;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
+        if (e < n) {
+            const Msg m = load_hdr(in, e);
+            const uint32_t d = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+            digits[e] = (uint8_t)d;
+            atomicAdd(&sm.hist[d], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks) tile_hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = sm.hist[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(const orl_msg_hdr* __restrict__ in, const uint8_t* __restrict__ digits,
+                                                      uint32_t n, const uint32_t* __restrict__ tile_off, uint32_t ntiles,
+                                                      uint32_t nranks, orl_msg_hdr* __restrict__ out,
+                                                      uint32_t* __restrict__ src_index) {
+    __shared__ uint32_t cnt[kWaves][8];
+    __shared__ uint32_t woff[kWaves][8];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    if (threadIdx.x < kWaves * 8) (&cnt[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t wbase = blockIdx.x * kTile + w * (kItems * 64u);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
+    uint32_t dig[kItems], rank[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        const bool valid = e < n;
+        const uint32_t d = valid ? digits[e] : 0u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t c = cnt[w][d];
+        rank[j] = c + (uint32_t)__popcll(m & lt_mask);
+        dig[j] = d;
+        if (valid && (m >> lane) == 1ull) cnt[w][d] = c + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks) {
+        uint32_t t = tile_off[(size_t)threadIdx.x * ntiles + blockIdx.x];
+        for (uint32_t q = 0; q < kWaves; ++q) {
+            woff[q][threadIdx.x] = t;
+            t += cnt[q][threadIdx.x];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e < n) {
+            const uint32_t g = woff[w][dig[j]] + rank[j];
+            const uint4* sp = reinterpret_cast<const uint4*>(in + e);
+            uint4* dp = reinterpret_cast<uint4*>(out + g);
+            dp[0] = sp[0];
+            dp[1] = sp[1];
+            src_index[g] = e;
+        }
+    }
+}
+
+__global__ void k_part_counts(const uint32_t* __restrict__ scanned, uint32_t ntiles, uint32_t nranks, uint32_t n,
+                              uint64_t* __restrict__ counts) {
+    const uint32_t d = threadIdx.x;
+    if (d < nranks) {
+        const uint32_t a = scanned[(size_t)d * ntiles];
+        const uint32_t b = (d + 1 < nranks) ? scanned[(size_t)(d + 1) * ntiles] : n;
+        counts[d] = b - a;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
+    const uint32_t nb = ceil_div(m, kScanChunk);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(256), 0, st, a, m, sums);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, sums, nb);
+    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(256), 0, st, a, m, sums);
+    return (int)hipGetLastError();
+}
+
+template <int BITS>
+void launch_down_bits(bool first, const uint32_t* kin, const uint32_t* iin, uint32_t n, uint32_t n_act, uint32_t shift,
+                      const uint32_t* toff, uint32_t ntiles, uint32_t* kout, uint32_t* iout, hipStream_t st) {
+    if (first)
+        hipLaunchKernelGGL((k_radix_down<BITS, true>), dim3(ntiles), dim3(256), 0, st, kin, iin, n, n_act, shift, toff, ntiles, kout, iout);
+    else
+        hipLaunchKernelGGL((k_radix_down<BITS, false>), dim3(ntiles), dim3(256), 0, st, kin, iin, n, n_act, shift, toff, ntiles, kout, iout);
+}
+
+void launch_down(int bits, bool first, const uint32_t* kin, const uint32_t* iin, uint32_t n, uint32_t n_act, uint32_t shift,
+                 const uint32_t* toff, uint32_t ntiles, uint32_t* kout, uint32_t* iout, hipStream_t st) {
+    switch (bits) {
+#define ORL_CASE(B) case B: launch_down_bits<B>(first, kin, iin, n, n_act, shift, toff, ntiles, kout, iout, st); break;
+        ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
+        ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
+#undef ORL_CASE
+        default: break;
+    }
+}
+
+// Stage 4 after a route kernel that already wrote the first digit's tile histogram into s.tile_hist.
+int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets,
+                       const Scratch& s, hipStream_t st) {
+    const RadixPlan plan = make_plan(n_act);  // keys in [0, n_act]
+    const uint32_t ntiles = ceil_div(n, kTile);
+    const uint32_t nb = n_act + 2;
+    for (int p = 0; p < plan.passes; ++p) {
+        const uint32_t bins = 1u << plan.bits[p];
+        if (p > 0) {
+            const uint32_t* kin = ((plan.passes - p) % 2 == 0) ? s.sorted_keys : s.keys_a;  // output of pass p-1
+            hipLaunchKernelGGL(k_radix_up, dim3(ntiles), dim3(256), 0, st, kin, n, (uint32_t)plan.shift[p], bins, s.tile_hist, ntiles);
+        }
+        scan_inplace(s.tile_hist, (uint64_t)bins * ntiles, s.scan_sums, st);
+        const bool to_final = ((plan.passes - 1 - p) % 2) == 0;
+        uint32_t* kout = to_final ? s.sorted_keys : s.keys_a;
+        uint32_t* iout = to_final ? d_order : s.idx_a;
+        const uint32_t* kin = (p == 0) ? d_act : (to_final ? s.keys_a : s.sorted_keys);
+        const uint32_t* iin = (p == 0) ? nullptr : (to_final ? s.idx_a : d_order);
+        launch_down(plan.bits[p], p == 0, kin, iin, n, n_act, (uint32_t)plan.shift[p], s.tile_hist, ntiles, kout, iout, st);
+    }
+    hipLaunchKernelGGL(k_offsets, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_hash, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_keys, (uint32_t)n, d_out);
+    return (int)hipGetLastError();
+}
+
+int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const orl_msg_hdr* d_in,
+                        size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                        uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
+    hipStream_t st = (hipStream_t)stream;
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    if (n == 0) {
+        if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
+        return 0;
+    }
+    const uint32_t ntiles = ceil_div(n, kTile);
+    const RadixPlan plan = make_plan(n_act);
+    if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
+    if (buckets)
+        hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
+                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, ntiles, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
+    else
+        hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
+                           (uint32_t)n, excl, d_route, d_act, nullptr, ntiles, 1u, 0u);
+    if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
+    int e = (int)hipGetLastError();
+    if (e) return e;
+    if (!buckets) return 0;
+    return bucket_after_route(d_act, (uint32_t)n, n_act, d_order, d_offsets, s, st);
+}
+
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const uint64_t* d_csr_off,
+                               const uint32_t* d_csr_tgt, const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub,
+                               uint64_t follower_tcd, uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets,
+                               uint32_t* d_route, uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out,
+                               uint64_t max_out, const Scratch& s, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    // degrees → exclusive scan (u32, in s.idx_a) → u64 publish offsets
+    uint32_t* poff32 = s.idx_a;
+    const uint32_t m = (uint32_t)n_pub + 1;
+    hipLaunchKernelGGL(k_fanout_deg, dim3(ceil_div(m, 256)), dim3(256), 0, st, d_csr_off, d_pubs, (uint32_t)n_pub, poff32);
+    scan_inplace(poff32, m, s.scan_sums, st);
+    hipLaunchKernelGGL(k_widen64, dim3(ceil_div(m, 256)), dim3(256), 0, st, poff32, m, d_pub_offsets);
+    uint32_t total = 0;
+    int e = (int)hipMemcpyAsync(&total, poff32 + n_pub, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+    if (e) return e;
+    e = (int)hipStreamSynchronize(st);
+    if (e) return e;
+    *n_out = total;
+    if (total > max_out) return -1;
+    if (total == 0) {
+        if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
+        return 0;
+    }
+    const uint32_t ntiles = ceil_div(total, kTile);
+    const RadixPlan plan = make_plan(n_act);
+    if (buckets)
+        hipLaunchKernelGGL(k_fanout_route<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
+                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, total, excl, d_route, d_act,
+                           s.tile_hist, ntiles, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
+    else
+        hipLaunchKernelGGL(k_fanout_route<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
+                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, total, excl, d_route, d_act,
+                           nullptr, ntiles, 1u, 0u);
+    e = (int)hipGetLastError();
+    if (e || !buckets) return e;
+    // poff32 lives in s.idx_a, which the radix passes reuse: it is dead once the route kernel has run.
+    return bucket_after_route(d_act, total, n_act, d_order, d_offsets, s, st);
+}
+
+int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                              const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
+                              uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return (int)hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
+    const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    const uint32_t ntiles = ceil_div(n, kTile);
+    hipLaunchKernelGGL(k_part_digits, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
+                       excl, my_rank, s.digits, s.tile_hist, ntiles, nranks);
+    scan_inplace(s.tile_hist, (uint64_t)nranks * ntiles, s.scan_sums, st);
+    hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(256), 0, st, d_in, s.digits, (uint32_t)n, s.tile_hist, ntiles, nranks,
+                       d_out, d_src_index);
+    hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, s.tile_hist, ntiles, nranks, (uint32_t)n, d_counts);
+    return (int)hipGetLastError();
+}
+
+}  // namespace orl

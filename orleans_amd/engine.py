@@ -1,0 +1,303 @@
+"""Host-side mirror of the reference's routing interfaces over the C ABI.
+
+``GrainDirectoryEngine`` is the batched stand-in for one GPU's worth of silos.  Its methods keep the
+names and argument meaning of the reference calls they replace (paths relative to randa1/orleans):
+
+=============================  ==================================================================
+engine method                  reference
+=============================  ==================================================================
+set_silos / add_server /       LocalGrainDirectory.SiloStatusChangeNotification → AddServer /
+remove_server                  RemoveServer (src/OrleansRuntime/GrainDirectory/LocalGrainDirectory.cs:243-304,390-419)
+calculate_target_silo          LocalGrainDirectory.CalculateTargetSilo (:439-497)
+register_single_activation     LocalGrainDirectory.RegisterSingleActivationAsync (:510-544) →
+                               GrainDirectoryPartition.AddSingleActivation (GrainDirectoryPartition.cs:270-287)
+unregister                     LocalGrainDirectory.UnregisterAsync (:587-612) → RemoveActivation(force)
+address_messages               Dispatcher.AddressMessage (src/OrleansRuntime/Core/Dispatcher.cs:555-579) for a
+                               batch, + per-activation FIFO grouping (ActivationData.cs:483-514)
+hash_batch                     GrainId.GetUniformHashCode (src/Orleans/IDs/GrainId.cs:211-214)
+=============================  ==================================================================
+
+Error behaviour: API errors raise ``OrleansRouteError`` (the reference throws ArgumentException /
+InvalidOperationException); per-message outcomes are status codes in the route word, which
+``decode_route`` unpacks, and ``raise_for_status`` maps to the reference's exception types.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import OrleansRouteError, ptr
+
+
+def _check(lib, ctx, rc: int) -> None:
+    if rc != L.OK:
+        msg = lib.orl_last_error(ctx) if ctx else b""
+        raise OrleansRouteError(rc, (msg or b"").decode(errors="replace"))
+
+
+# ---- identity helpers (no context, host only) ---------------------------------------------------------
+def calc_id_hash(text: str) -> int:
+    """Utils.CalculateIdHash (src/Orleans/Utils/Utils.cs:201-220)."""
+    lib = L.load()
+    b = text.encode("utf-8")
+    out = C.c_int32()
+    _check(lib, None, lib.orl_calc_id_hash(b, len(b), C.byref(out)))
+    return out.value
+
+
+def silo_consistent_hash(endpoint: str, generation: int) -> int:
+    """SiloAddress.GetConsistentHashCode (src/Orleans/IDs/SiloAddress.cs:197-206)."""
+    lib = L.load()
+    out = C.c_int32()
+    _check(lib, None, lib.orl_silo_consistent_hash(endpoint.encode("utf-8"), int(generation), C.byref(out)))
+    return out.value
+
+
+def jenkins_bytes(data: bytes) -> int:
+    """JenkinsHash.ComputeHash(byte[]) (src/Orleans/IDs/JenkinsHash.cs:68-115)."""
+    return L.load().orl_jenkins_bytes(data, len(data))
+
+
+def keyext_uniform_hash(tcd: int, n0: int, n1: int, key_ext: str) -> int:
+    """UniqueKey.GetUniformHashCode, KeyExt branch (src/Orleans/IDs/UniqueKey.cs:288-294)."""
+    k = np.zeros(1, L.KEY_DTYPE)
+    k["tcd"], k["n0"], k["n1"] = tcd, n0, n1
+    b = key_ext.encode("utf-8")
+    return L.load().orl_keyext_uniform_hash(ptr(k), b, len(b))
+
+
+def type_code_data(category: int, type_code: int) -> int:
+    """UniqueKey.NewKey: TypeCodeData = (category << 56) + (typeData & 0x00FFFFFFFFFFFFFF) (UniqueKey.cs:141);
+    an int type code is sign-extended to long first (GrainInterfaceMap.cs:437)."""
+    return ((category & 0xFF) << 56) + (type_code & 0xFFFFFFFFFFFFFFFF & 0x00FFFFFFFFFFFFFF)
+
+
+def grain_keys_from_longs(type_code: int, keys: np.ndarray, category: int = L.CAT_GRAIN) -> np.ndarray:
+    """GrainId.GetGrainId(typeCode, long) for an array of long keys (GrainId.cs:90-95, UniqueKey.cs:146-152)."""
+    out = np.zeros(len(keys), L.KEY_DTYPE)
+    out["tcd"] = np.uint64(type_code_data(category, type_code))
+    out["n1"] = np.asarray(keys).astype(np.int64).view(np.uint64)
+    return out
+
+
+def grain_keys_from_guid_bytes(type_code: int, guid_bytes: np.ndarray, category: int = L.CAT_GRAIN) -> np.ndarray:
+    """GrainId.GetGrainId(typeCode, Guid) with Guid.ToByteArray() rows (UniqueKey.cs:159-167)."""
+    gb = np.ascontiguousarray(guid_bytes, dtype=np.uint8).reshape(-1, 16)
+    out = np.zeros(len(gb), L.KEY_DTYPE)
+    out["tcd"] = np.uint64(type_code_data(category, type_code))
+    out["n0"] = gb[:, 0:8].copy().view("<u8").ravel()
+    out["n1"] = gb[:, 8:16].copy().view("<u8").ravel()
+    return out
+
+
+# ---- route word -------------------------------------------------------------------------------------
+@dataclass
+class RouteView:
+    owner: np.ndarray
+    host: np.ndarray
+    status: np.ndarray
+    flags: np.ndarray
+
+
+def decode_route(route: np.ndarray) -> RouteView:
+    r = np.asarray(route, dtype=np.uint32)
+    return RouteView((r & 0xFF).astype(np.uint8), ((r >> 8) & 0xFF).astype(np.uint8),
+                     ((r >> 16) & 0xFF).astype(np.uint8), ((r >> 24) & 0xFF).astype(np.uint8))
+
+
+class GrainDirectoryStopping(RuntimeError):
+    """InvalidOperationException("Grain directory is stopping") (LocalGrainDirectory.cs:514-518)."""
+
+
+class UnregisteredClient(KeyError):
+    """KeyNotFoundException for a client pseudo-grain (PlacementDirectorsManager.cs:75-81)."""
+
+
+class NoSeed(ValueError):
+    """ArgumentException: membership table grain without a Seed (LocalGrainDirectory.cs:449-460)."""
+
+
+def raise_for_status(route_word: int) -> None:
+    st = (int(route_word) >> 16) & 0xFF
+    if st == L.ST_OWNER_NULL:
+        raise GrainDirectoryStopping("Grain directory is stopping")
+    if st == L.ST_CLIENT_UNREGISTERED:
+        raise UnregisteredClient("No activation for client")
+    if st == L.ST_NO_SEED:
+        raise NoSeed("MembershipTableGrain cannot run without Seed node")
+
+
+@dataclass
+class RouteResult:
+    route: np.ndarray      # uint32[n]
+    act: np.ndarray        # uint32[n]
+    order: Optional[np.ndarray]    # uint32[n]: message indices grouped per activation (FIFO)
+    offsets: Optional[np.ndarray]  # uint32[n_act+2]
+
+    def bucket(self, act: int) -> np.ndarray:
+        return self.order[self.offsets[act]:self.offsets[act + 1]]
+
+
+class GrainDirectoryEngine:
+    """One context of liborleans_route.so (one GPU, one or more logical silos)."""
+
+    def __init__(self, n_act: int, dir_capacity: int, max_batch: int = 1 << 20, device: int = 0,
+                 placement: int = L.POLICY_PREFER_LOCAL):
+        self._lib = L.load()
+        cfg = L.orl_config(L.ABI_VERSION, int(device), int(dir_capacity), int(n_act), int(placement), int(max_batch))
+        h = C.c_void_p()
+        rc = self._lib.orl_ctx_create(C.byref(cfg), C.byref(h))
+        if rc != L.OK:
+            raise OrleansRouteError(rc, "orl_ctx_create failed (device=%d)" % device)
+        self._ctx = h
+        self.n_act = int(n_act)
+        self.max_batch = int(max_batch)
+        self.device = int(device)
+        self.n_silos = 0
+
+    # -- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.orl_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _ck(self, rc: int) -> None:
+        _check(self._lib, self._ctx, rc)
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._ctx
+
+    # -- membership view
+    def set_silos(self, n_silos: int, running: Optional[Sequence[bool]] = None,
+                  functional: Optional[Sequence[bool]] = None, local: Optional[Sequence[bool]] = None,
+                  seed: int = L.NULL_SILO) -> None:
+        def arr(v):
+            return None if v is None else np.ascontiguousarray(np.asarray(v, dtype=np.uint8))
+        r, f, lo = arr(running), arr(functional), arr(local)
+        self._ck(self._lib.orl_silos_set(self._ctx, int(n_silos), ptr(r), ptr(f), ptr(lo), int(seed)))
+        self.n_silos = int(n_silos)
+
+    def add_server(self, silo: int, consistent_hash: int) -> None:
+        self._ck(self._lib.orl_ring_add_server(self._ctx, int(silo), int(consistent_hash)))
+
+    def remove_server(self, silo: int) -> None:
+        self._ck(self._lib.orl_ring_remove_server(self._ctx, int(silo)))
+
+    def membership_ring(self):
+        n = C.c_uint32()
+        hs = np.zeros(256, np.int32)
+        ss = np.zeros(256, np.uint8)
+        self._ck(self._lib.orl_ring_get(self._ctx, ptr(hs), ptr(ss), 256, C.byref(n)))
+        return [(int(hs[i]), int(ss[i])) for i in range(n.value)]
+
+    # -- directory partition
+    def register_single_activation(self, keys: np.ndarray, acts: np.ndarray, silos: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        acts = np.ascontiguousarray(acts, dtype=np.uint32)
+        silos = np.ascontiguousarray(silos, dtype=np.uint8)
+        n = len(keys)
+        assert len(acts) == n and len(silos) == n
+        st = np.zeros(n, np.uint8)
+        wa = np.zeros(n, np.uint32)
+        ws = np.zeros(n, np.uint8)
+        self._ck(self._lib.orl_dir_insert_single(self._ctx, ptr(keys), ptr(acts), ptr(silos), n, ptr(wa), ptr(ws),
+                                                 ptr(st)))
+        return st, wa, ws
+
+    def unregister(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        out = np.zeros(len(keys), np.uint8)
+        self._ck(self._lib.orl_dir_remove(self._ctx, ptr(keys), len(keys), ptr(out)))
+        return out
+
+    def directory_count(self) -> int:
+        n = C.c_uint64()
+        self._ck(self._lib.orl_dir_count(self._ctx, C.byref(n)))
+        return n.value
+
+    def lookup_host(self, keys: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        a = np.zeros(len(keys), np.uint32)
+        s = np.zeros(len(keys), np.uint8)
+        self._ck(self._lib.orl_dir_lookup_host(self._ctx, ptr(keys), len(keys), ptr(a), ptr(s)))
+        return a, s
+
+    # -- hot path (host buffers)
+    def hash_batch(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        out = np.zeros(len(keys), np.uint32)
+        self._ck(self._lib.orl_hash_batch(self._ctx, ptr(keys), len(keys), ptr(out)))
+        return out
+
+    def address_messages(self, msgs: np.ndarray, opts: int = 0) -> RouteResult:
+        msgs = np.ascontiguousarray(msgs, dtype=L.MSG_DTYPE)
+        n = len(msgs)
+        route = np.zeros(n, np.uint32)
+        act = np.zeros(n, np.uint32)
+        buckets = not (opts & L.OPT_NO_BUCKETS)
+        order = np.zeros(n, np.uint32) if buckets else None
+        offsets = np.zeros(self.n_act + 2, np.uint32) if buckets else None
+        self._ck(self._lib.orl_route_batch(self._ctx, ptr(msgs), n, int(opts), ptr(route), ptr(act), ptr(order),
+                                           ptr(offsets)))
+        return RouteResult(route, act, order, offsets)
+
+    def calculate_target_silo(self, keys: np.ndarray, me: int, exclude_if_stopping: bool = True) -> np.ndarray:
+        """Owner silo per key as silo `me` computes it (0xFF = null)."""
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        m = np.zeros(len(keys), L.MSG_DTYPE)
+        m["tcd"], m["n0"], m["n1"] = keys["tcd"], keys["n0"], keys["n1"]
+        m["sending_silo"] = me
+        r = self.address_messages(m, L.OPT_NO_BUCKETS | (L.OPT_EXCLUDE_IF_STOPPING if exclude_if_stopping else 0))
+        return decode_route(r.route).owner
+
+    # -- hot path (device-resident; torch tensors or raw device pointers)
+    def address_messages_device(self, d_msgs, n: int, d_route, d_act, d_order=None, d_offsets=None, stream=None,
+                                opts: int = 0) -> None:
+        self._ck(self._lib.orl_route_batch_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(d_route),
+                                                  ptr(d_act), ptr(d_order), ptr(d_offsets), ptr(stream)))
+
+    def fanout_device(self, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, n_pub: int, follower_tcd: int,
+                      d_pub_offsets, d_route, d_act, d_order=None, d_offsets=None, stream=None, opts: int = 0) -> int:
+        n_out = C.c_uint64()
+        self._ck(self._lib.orl_fanout_route_device(self._ctx, ptr(d_csr_off), ptr(d_csr_tgt), ptr(d_pubs),
+                                                   ptr(d_pub_silo), int(n_pub), int(follower_tcd), int(opts),
+                                                   ptr(d_pub_offsets), ptr(d_route), ptr(d_act), ptr(d_order),
+                                                   ptr(d_offsets), C.byref(n_out), ptr(stream)))
+        return n_out.value
+
+    def partition_by_owner_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
+                                  d_out, d_src_index, d_counts, stream=None, opts: int = 0) -> None:
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        self._ck(self._lib.orl_partition_by_owner_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(ros),
+                                                         int(nranks), int(my_rank), ptr(d_out), ptr(d_src_index),
+                                                         ptr(d_counts), ptr(stream)))
+
+    def sync(self) -> None:
+        self._ck(self._lib.orl_sync(self._ctx))
+
+    def set_timing(self, enable: bool) -> None:
+        self._ck(self._lib.orl_set_timing(self._ctx, 1 if enable else 0))
+
+    def timing_summary(self):
+        """(batches, avg route-kernel ms, avg bucketing ms, avg call ms) over batches since set_timing(True)."""
+        n, a, b, t = C.c_uint32(), C.c_float(), C.c_float(), C.c_float()
+        self._ck(self._lib.orl_timing_summary(self._ctx, C.byref(n), C.byref(a), C.byref(b), C.byref(t)))
+        return n.value, a.value, b.value, t.value

@@ -1,0 +1,211 @@
+"""Deterministic synthetic workloads of BASELINE.json's configs.
+
+Fixed synthetic cluster for every config: silos ``10.0.0.{1..8}:11111`` generation 1; ring hashes are
+``SiloAddress.GetConsistentHashCode`` (SHA-256, computed by the library); silo s lives on GPU
+``s * k // 8`` when k GPUs run, so the routing decisions are identical at 1/2/4/8 GPUs.
+
+The grain population is ChirperAccount long-key grains (type code =
+CalculateIdHash("Orleans.Samples.Chirper.Grains.ChirperAccount")); activation handle of grain i = i;
+each activation lives on its directory owner silo (host silo = directory owner).
+
+Vectorised numpy helpers here are workload plumbing (they decide which silo registers which grain);
+routing decisions themselves come only from the HIP library, and parity is checked against oracle/.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .engine import calc_id_hash, grain_keys_from_longs, silo_consistent_hash
+
+CHIRPER_ACCOUNT_CLASS = "Orleans.Samples.Chirper.Grains.ChirperAccount"
+N_SILOS = 8
+PORT = 11111
+GENERATION = 1
+
+SEED_C2 = 0x5EED0002
+SEED_C3 = 0x5EED0003
+SEED_C4 = 0x5EED0004
+SEED_C5 = 0x5EED0005
+
+_M32 = np.uint32(0xFFFFFFFF)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over a uint64 array (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = (np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def stream(seed: int, start: int, n: int) -> np.ndarray:
+    """n pseudo-random u64 values for indices [start, start+n) of the stream `seed`."""
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return splitmix64(idx * np.uint64(0x2545F4914F6CDD1D) + np.uint64(seed & 0xFFFFFFFFFFFFFFFF))
+
+
+def jenkins3_np(u1: np.ndarray, u2: np.ndarray, u3: np.ndarray) -> np.ndarray:
+    """Vectorised JenkinsHash.ComputeHash(ulong,ulong,ulong) (JenkinsHash.cs:126-144) for workload setup."""
+    def lo(u):
+        return (u & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+    def hi(u):
+        return (u >> np.uint64(32)).astype(np.uint32)
+
+    a = np.full(len(u1), 0x9E3779B9, np.uint32)
+    b = a.copy()
+    c = np.zeros(len(u1), np.uint32)
+
+    def mix(a, b, c):
+        a -= b; a -= c; a ^= (c >> 13)
+        b -= c; b -= a; b ^= (a << 8)
+        c -= a; c -= b; c ^= (b >> 13)
+        a -= b; a -= c; a ^= (c >> 12)
+        b -= c; b -= a; b ^= (a << 16)
+        c -= a; c -= b; c ^= (b >> 5)
+        a -= b; a -= c; a ^= (c >> 3)
+        b -= c; b -= a; b ^= (a << 10)
+        c -= a; c -= b; c ^= (b >> 15)
+
+    with np.errstate(over="ignore"):
+        a += lo(u1); b += hi(u1); c += lo(u2)
+        mix(a, b, c)
+        a += hi(u2); b += lo(u3); c += hi(u3)
+        mix(a, b, c)
+        c += np.uint32(24)
+        mix(a, b, c)
+    return c
+
+
+@dataclass
+class Cluster:
+    n_silos: int
+    hashes: np.ndarray        # int32 consistent hash per silo index
+    ring_hash: np.ndarray     # int32, membershipRingList order
+    ring_silo: np.ndarray     # uint8
+    type_code: int
+
+    def owner_of(self, uniform: np.ndarray) -> np.ndarray:
+        """CalculateTargetSilo for running silos (no exclusion): predecessor-or-equal in signed order, wrap."""
+        h = uniform.astype(np.uint32).view(np.int32)
+        idx = np.searchsorted(self.ring_hash, h, side="right") - 1
+        idx = np.where(idx < 0, len(self.ring_hash) - 1, idx)
+        return self.ring_silo[idx]
+
+    def rank_of_silo(self, nranks: int) -> np.ndarray:
+        return np.array([s * nranks // self.n_silos for s in range(self.n_silos)], np.uint8)
+
+
+def default_cluster(n_silos: int = N_SILOS) -> Cluster:
+    hashes = np.array([silo_consistent_hash(f"10.0.0.{s + 1}:{PORT}", GENERATION) for s in range(n_silos)], np.int32)
+    # replay AddServer in silo-index order: insert at FindLastIndex(h < hash) + 1 (LocalGrainDirectory.cs:259-261)
+    ring = []
+    for s in range(n_silos):
+        h = int(hashes[s])
+        idx = max([i for i, (rh, _) in enumerate(ring) if rh < h], default=-1)
+        ring.insert(idx + 1, (h, s))
+    return Cluster(n_silos, hashes, np.array([h for h, _ in ring], np.int32), np.array([s for _, s in ring], np.uint8),
+                   calc_id_hash(CHIRPER_ACCOUNT_CLASS))
+
+
+def setup_engine(eng, cl: Cluster, local_silos: Optional[np.ndarray] = None, seed: int = 0) -> None:
+    local = None
+    if local_silos is not None:
+        local = np.zeros(cl.n_silos, np.uint8)
+        local[np.asarray(local_silos, dtype=np.int64)] = 1
+    eng.set_silos(cl.n_silos, local=local, seed=seed)
+    for s in range(cl.n_silos):
+        eng.add_server(s, int(cl.hashes[s]))
+
+
+def grain_population(cl: Cluster, n_grains: int, registered_frac: float = 1.0, seed: int = SEED_C2):
+    """Keys of grains 0..n-1, their uniform hashes, owner silos, and which ones are registered."""
+    keys = grain_keys_from_longs(cl.type_code, np.arange(n_grains, dtype=np.int64))
+    uni = jenkins3_np(keys["tcd"], keys["n0"], keys["n1"])
+    owner = cl.owner_of(uni)
+    if registered_frac >= 1.0:
+        reg = np.ones(n_grains, bool)
+    else:
+        r = stream(seed ^ 0xA11CE, 0, n_grains)
+        reg = (r % np.uint64(1_000_000)) < np.uint64(int(registered_frac * 1_000_000))
+    return keys, uni, owner, reg
+
+
+def register_population(eng, keys: np.ndarray, owner: np.ndarray, reg: np.ndarray,
+                        local_mask: Optional[np.ndarray] = None) -> int:
+    """RegisterSingleActivation of grain i with activation handle i on its owner silo."""
+    sel = reg.copy()
+    if local_mask is not None:
+        sel &= local_mask[owner].astype(bool)
+    idx = np.nonzero(sel)[0]
+    st, _, _ = eng.register_single_activation(keys[idx], idx.astype(np.uint32), owner[idx])
+    assert (st == L.INS_INSERTED).all(), np.unique(st, return_counts=True)
+    return len(idx)
+
+
+def uniform_messages(cl: Cluster, n_grains: int, n_msgs: int, seed: int = SEED_C2, start: int = 0,
+                     sender_silos: Optional[np.ndarray] = None) -> np.ndarray:
+    """Config 2 messages: targets Uniform[0, n_grains), sending silo from `sender_silos` (default all)."""
+    t = stream(seed, start, n_msgs) % np.uint64(n_grains)
+    s = stream(seed ^ 0x5E4D, start, n_msgs)
+    silos = np.arange(cl.n_silos, dtype=np.uint8) if sender_silos is None else np.asarray(sender_silos, np.uint8)
+    m = np.zeros(n_msgs, L.MSG_DTYPE)
+    m["tcd"] = np.uint64(((L.CAT_GRAIN << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF)
+    m["n1"] = t
+    m["sending_silo"] = silos[(s % np.uint64(len(silos))).astype(np.int64)]
+    m["category"] = 2  # Application
+    return m
+
+
+def zipf_messages(cl: Cluster, n_grains: int, n_msgs: int, s_exp: float = 1.1, seed: int = SEED_C3, start: int = 0,
+                  sender_silos: Optional[np.ndarray] = None) -> np.ndarray:
+    """Config 3 messages: rank ~ Zipf(s) over [1, n_grains] mapped through a seeded permutation."""
+    ranks = np.arange(1, n_grains + 1, dtype=np.float64)
+    cdf = np.cumsum(ranks ** -s_exp)
+    cdf /= cdf[-1]
+    u = (stream(seed, start, n_msgs) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    r = np.searchsorted(cdf, u, side="right")
+    r = np.minimum(r, n_grains - 1)
+    perm = np.random.default_rng(seed).permutation(n_grains)
+    m = uniform_messages(cl, n_grains, n_msgs, seed, start, sender_silos)
+    m["n1"] = perm[r].astype(np.uint64)
+    return m
+
+
+def chirper_graph_deterministic(n_accounts: int = 1000, followers: int = 10, first_id: int = 1):
+    """ChirperNetworkGenerator deterministic edges (NetworkGenerator/ChirperNetworkGenerator.cs:336-342):
+    edge e: source = e // k, target = (source + 1 + e % k) % n (relative ids); `source follows target`,
+    so target's followers include source (ChirperNetworkLoader.cs:231-242, 294-299)."""
+    e = np.arange(n_accounts * followers, dtype=np.int64)
+    src = e // followers
+    tgt = (src + 1 + e % followers) % n_accounts
+    return src + first_id, tgt + first_id
+
+
+def csr_from_edges(publisher: np.ndarray, follower: np.ndarray, n_nodes: int):
+    """Followers of each publisher in edge order (stable), as CSR offsets[n+1] (u64) / targets[E] (u32)."""
+    order = np.argsort(publisher, kind="stable")
+    counts = np.bincount(publisher, minlength=n_nodes)
+    off = np.zeros(n_nodes + 1, np.uint64)
+    off[1:] = np.cumsum(counts)
+    return off, follower[order].astype(np.uint32)
+
+
+def powerlaw_csr(n_nodes: int, exponent: float = 2.1, dmin: int = 1, dmax: int = 100_000, seed: int = SEED_C4):
+    """Config 4 CSR: follower counts ~ discrete power law, follower ids uniform."""
+    u = (stream(seed, 0, n_nodes) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    # inverse-CDF of continuous power law on [dmin, dmax], floored
+    a = 1.0 - exponent
+    d = ((dmax ** a - dmin ** a) * u + dmin ** a) ** (1.0 / a)
+    deg = np.clip(np.floor(d).astype(np.int64), dmin, dmax)
+    off = np.zeros(n_nodes + 1, np.uint64)
+    off[1:] = np.cumsum(deg)
+    e = int(off[-1])
+    tgt = (stream(seed ^ 0xF011, 0, e) % np.uint64(n_nodes)).astype(np.uint32)
+    return off, tgt

@@ -1,0 +1,255 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit for bit.
+
+Sizes the oracle finishes in seconds run message-for-message; the full config-2 batch (64M messages)
+is checked per message on a random sample plus size-independent properties of the bucketing (a
+permutation, stable, grouped, offsets consistent).  All integer/byte work: exact equality, no tolerance.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cpu_ref, pyref as P
+from orleans_amd import _lib as L
+from orleans_amd import workloads as W
+from orleans_amd.engine import GrainDirectoryEngine, decode_route
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need an MI355X"
+    return t
+
+
+def _pair(d, max_batch=1 << 20, n_act=None):
+    n = len(d["silo_hashes"])
+    n_act = int(d["n_act"]) if n_act is None else n_act
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=max(16, len(d["reg_keys"])), max_batch=max_batch, device=0,
+                               placement=int(d["policy"]))
+    eng.set_silos(n, running=d["running"], functional=d["functional"], seed=int(d["seed"]))
+    for s in range(n):
+        eng.add_server(s, int(d["silo_hashes"][s]))
+    keys = np.zeros(len(d["reg_keys"]), L.KEY_DTYPE)
+    keys["tcd"], keys["n0"], keys["n1"] = d["reg_keys"][:, 0], d["reg_keys"][:, 1], d["reg_keys"][:, 2]
+    eng.register_single_activation(keys, d["reg_acts"], d["reg_silos"])
+    return eng
+
+
+def test_hash_batch_golden(torch, golden_dir):
+    g = json.load(open(os.path.join(golden_dir, "jenkins.json")))
+    keys = np.zeros(len(g["keys"]) + len(g["u64"]), L.KEY_DTYPE)
+    exp = np.zeros(len(keys), np.uint32)
+    for i, c in enumerate(g["keys"]):
+        keys[i] = (int(c["tcd"], 16), int(c["n0"], 16), int(c["n1"], 16))
+        exp[i] = c["uniform"]
+    for j, c in enumerate(g["u64"]):
+        keys[len(g["keys"]) + j] = tuple(int(x, 16) for x in c["u"])
+        exp[len(g["keys"]) + j] = c["hash"]
+    eng = GrainDirectoryEngine(n_act=4, dir_capacity=16, device=0)
+    np.testing.assert_array_equal(eng.hash_batch(keys), exp)
+    rng = np.random.default_rng(3)
+    rk = rng.integers(0, 2**63, (100_000, 3), dtype=np.int64).view(np.uint64)
+    kk = np.zeros(len(rk), L.KEY_DTYPE)
+    kk["tcd"], kk["n0"], kk["n1"] = rk[:, 0], rk[:, 1], rk[:, 2]
+    np.testing.assert_array_equal(eng.hash_batch(kk), W.jenkins3_np(kk["tcd"], kk["n0"], kk["n1"]))
+    eng.close()
+
+
+@pytest.mark.parametrize("name", ["routing_basic", "routing_membership"])
+def test_routing_golden(torch, golden_dir, name):
+    d = np.load(os.path.join(golden_dir, name + ".npz"))
+    eng = _pair(d)
+    msgs = d["msgs"].reshape(-1).view(L.MSG_DTYPE)
+    res = eng.address_messages(msgs, int(d["opts"]))
+    np.testing.assert_array_equal(res.route, d["route"])
+    np.testing.assert_array_equal(res.act, d["act"])
+    np.testing.assert_array_equal(res.order, d["order"])
+    np.testing.assert_array_equal(res.offsets, d["offsets"])
+    eng.close()
+
+
+def test_chirper_fanout_golden(torch, golden_dir):
+    d = np.load(os.path.join(golden_dir, "chirper_fanout.npz"))
+    cl = W.default_cluster()
+    ids = d["node_ids"]
+    eng = GrainDirectoryEngine(n_act=len(ids), dir_capacity=len(ids), max_batch=1 << 16, device=0)
+    W.setup_engine(eng, cl)
+    keys = np.zeros(len(ids), L.KEY_DTYPE)
+    keys["tcd"] = np.uint64(int(d["follower_tcd"]))
+    keys["n1"] = ids.astype(np.uint64)
+    owner = cl.owner_of(W.jenkins3_np(keys["tcd"], keys["n0"], keys["n1"]))
+    st, _, _ = eng.register_single_activation(keys, np.arange(len(ids), dtype=np.uint32), owner)
+    assert (st == L.INS_INSERTED).all()
+    dev = "cuda"
+    t = torch
+    csr_off = t.from_numpy(d["csr_off"].astype(np.int64)).to(dev)
+    csr_tgt = t.from_numpy(d["csr_tgt"].astype(np.int32)).to(dev)
+    pubs = t.from_numpy(d["pubs"].astype(np.int32)).to(dev)
+    psilo = t.from_numpy(d["pub_silo"]).to(dev)
+    n_exp = len(d["route"])
+    poff = t.empty(len(d["pubs"]) + 1, dtype=t.int64, device=dev)
+    route = t.empty(n_exp, dtype=t.int32, device=dev)
+    act = t.empty(n_exp, dtype=t.int32, device=dev)
+    order = t.empty(n_exp, dtype=t.int32, device=dev)
+    off = t.empty(len(ids) + 2, dtype=t.int32, device=dev)
+    stream = t.cuda.current_stream().cuda_stream
+    n = eng.fanout_device(csr_off, csr_tgt, pubs, psilo, len(d["pubs"]), int(d["follower_tcd"]), poff, route, act,
+                          order, off, stream=stream)
+    t.cuda.synchronize()
+    assert n == n_exp
+    np.testing.assert_array_equal(route.cpu().numpy().view(np.uint32), d["route"])
+    np.testing.assert_array_equal(act.cpu().numpy().view(np.uint32), d["act"])
+    np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), d["order"])
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), d["offsets"])
+    exp_poff = np.zeros(len(d["pubs"]) + 1, np.uint64)
+    exp_poff[1:] = np.cumsum(np.diff(d["csr_off"].astype(np.int64))[d["pubs"]])
+    np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), exp_poff)
+    eng.close()
+
+
+def _random_setup(n_grains, n_act, n_silos=8, seed=11, functional=None, running=None, policy=0, n_registered=None):
+    cl = W.default_cluster(n_silos)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0, placement=policy)
+    eng.set_silos(n_silos, running=running, functional=functional, seed=0)
+    o = cpu_ref.Oracle(n_silos, running=running, functional=functional, seed=0, policy=policy)
+    for s in range(n_silos):
+        eng.add_server(s, int(cl.hashes[s]))
+        o.add_server(s, int(cl.hashes[s]))
+    keys, uni, owner, reg = W.grain_population(cl, n_grains, 0.9, seed)
+    rng = np.random.default_rng(seed)
+    acts = rng.integers(0, n_act, n_grains).astype(np.uint32)  # handles may collide: many grains, one bucket
+    silos = np.where(rng.random(n_grains) < 0.8, owner, rng.integers(0, n_silos, n_grains)).astype(np.uint8)
+    idx = np.nonzero(reg)[0]
+    st_e, wa_e, _ = eng.register_single_activation(keys[idx], acts[idx], silos[idx])
+    st_o, wa_o, _ = o.register(keys[idx], acts[idx], silos[idx])
+    np.testing.assert_array_equal(st_e, st_o)
+    return cl, eng, o
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 4095, 4096, 4097, 65536 + 17, 300_001])
+@pytest.mark.parametrize("n_act", [1, 5, 2048, 5000, 3_000_000])
+def test_random_batches_vs_oracle(torch, n, n_act):
+    cl, eng, o = _random_setup(20_000, n_act)
+    msgs = W.uniform_messages(cl, 22_000, n, seed=n * 7 + n_act)  # ~9% never-registered targets
+    for opts in (0, L.OPT_EXCLUDE_IF_STOPPING):
+        res = eng.address_messages(msgs, opts)
+        r, a = o.route(msgs, opts)
+        np.testing.assert_array_equal(res.route, r)
+        np.testing.assert_array_equal(res.act, a)
+        order, off = o.bucket(a, n_act)
+        np.testing.assert_array_equal(res.offsets, off)
+        np.testing.assert_array_equal(res.order, order)
+    eng.close()
+
+
+def test_membership_variants_vs_oracle(torch):
+    running = [1, 0, 1, 1, 0, 1, 1, 1]
+    functional = [1, 1, 0, 1, 1, 1, 0, 1]
+    for policy in (L.POLICY_PREFER_LOCAL, L.POLICY_HASH_SPREAD):
+        cl, eng, o = _random_setup(5000, 6000, running=running, functional=functional, policy=policy)
+        msgs = W.zipf_messages(cl, 6000, 200_000, seed=5)
+        for opts in (0, L.OPT_EXCLUDE_IF_STOPPING):
+            res = eng.address_messages(msgs, opts)
+            r, a = o.route(msgs, opts)
+            np.testing.assert_array_equal(res.route, r)
+            np.testing.assert_array_equal(res.act, a)
+        # ring shrinks (RemoveServer) between batches: snapshot semantics
+        eng.remove_server(3)
+        o.remove_server(3)
+        res = eng.address_messages(msgs)
+        r, a = o.route(msgs)
+        np.testing.assert_array_equal(res.route, r)
+        eng.close()
+
+
+def test_single_silo_ring_and_empty_ring(torch):
+    for n_ring in (0, 1):
+        eng = GrainDirectoryEngine(n_act=64, dir_capacity=64, device=0)
+        eng.set_silos(2, running=[0, 1])
+        o = cpu_ref.Oracle(2, running=[0, 1])
+        if n_ring:
+            eng.add_server(0, 5)
+            o.add_server(0, 5)
+        m = np.zeros(100, L.MSG_DTYPE)
+        m["tcd"] = P.CAT_GRAIN << 56
+        m["n1"] = np.arange(100)
+        m["sending_silo"] = np.arange(100) % 2
+        for opts in (0, 1):
+            res = eng.address_messages(m, opts)
+            r, a = o.route(m, opts)
+            np.testing.assert_array_equal(res.route, r)
+        eng.close()
+
+
+def test_partition_by_owner_vs_oracle(torch):
+    cl, eng, o = _random_setup(10_000, 10_000)
+    t = torch
+    for nranks in (1, 2, 4, 8):
+        ros = cl.rank_of_silo(nranks)
+        for my_rank in range(nranks):
+            msgs = W.uniform_messages(cl, 11_000, 100_003, seed=my_rank)
+            msgs["flags"][::97] = L.HDR_ADDRESS_COMPLETE
+            d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+            d_out = t.empty_like(d_in)
+            d_src = t.empty(len(msgs), dtype=t.int32, device="cuda")
+            d_cnt = t.empty(nranks, dtype=t.int64, device="cuda")
+            eng.partition_by_owner_device(d_in, len(msgs), ros, nranks, my_rank, d_out, d_src, d_cnt,
+                                          stream=t.cuda.current_stream().cuda_stream)
+            t.cuda.synchronize()
+            src, cnt = o.partition(msgs, ros, nranks, my_rank)
+            np.testing.assert_array_equal(d_cnt.cpu().numpy(), cnt.astype(np.int64))
+            np.testing.assert_array_equal(d_src.cpu().numpy().view(np.uint32), src)
+            np.testing.assert_array_equal(d_out.cpu().numpy().reshape(-1).view(L.MSG_DTYPE), msgs[src])
+    eng.close()
+
+
+def test_config2_full_size_properties(torch):
+    """BASELINE config 2 at full size (1M grains, 64M messages) on the device-resident path."""
+    t = torch
+    n_grains, n = 1_000_000, 64 * 1024 * 1024
+    cl = W.default_cluster()
+    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=n, device=0)
+    W.setup_engine(eng, cl)
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    W.register_population(eng, keys, owner, reg)
+    msgs = W.uniform_messages(cl, n_grains, n)
+    d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+    route = t.empty(n, dtype=t.int32, device="cuda")
+    act = t.empty(n, dtype=t.int32, device="cuda")
+    order = t.empty(n, dtype=t.int32, device="cuda")
+    off = t.empty(n_grains + 2, dtype=t.int32, device="cuda")
+    eng.address_messages_device(d_in, n, route, act, order, off, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    a = act.cpu().numpy().view(np.uint32)
+    r = route.cpu().numpy().view(np.uint32)
+    od = order.cpu().numpy().view(np.uint32)
+    of = off.cpu().numpy().view(np.uint32).astype(np.int64)
+    # every target is a registered grain 0..1M-1 whose handle is its key
+    np.testing.assert_array_equal(a, msgs["n1"].astype(np.uint32))
+    v = decode_route(r)
+    assert (v.status == L.ST_HIT).all()
+    np.testing.assert_array_equal(v.owner, owner[msgs["n1"].astype(np.int64)])
+    np.testing.assert_array_equal(v.host, v.owner)
+    # per-message oracle on a 1M random sample
+    o = cpu_ref.Oracle(8)
+    for s in range(8):
+        o.add_server(s, int(cl.hashes[s]))
+    o.register(keys, np.arange(n_grains, dtype=np.uint32), owner)
+    samp = np.random.default_rng(0).choice(n, 1_000_000, replace=False)
+    ro, ao = o.route(msgs[samp])
+    np.testing.assert_array_equal(r[samp], ro)
+    # bucketing: offsets = exclusive cumsum of per-activation counts; order groups by act, stable
+    cnt = np.bincount(a, minlength=n_grains + 1)
+    exp_off = np.zeros(n_grains + 2, np.int64)
+    exp_off[1:] = np.cumsum(cnt)
+    np.testing.assert_array_equal(of, exp_off)
+    assert (np.bincount(od, minlength=n) == 1).all()            # permutation
+    srt = a[od]
+    assert (np.diff(srt.astype(np.int64)) >= 0).all()           # grouped by activation
+    same = np.diff(srt.astype(np.int64)) == 0
+    assert (np.diff(od.astype(np.int64))[same] > 0).all()       # arrival order kept inside a bucket
+    eng.close()
