@@ -312,7 +312,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
-    f(c->s.keys_a); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits);
+    f(c->s.keys_a); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -374,6 +374,9 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.tile_hist, hist_words * 4)) != hipSuccess) return bail(e, "hipMalloc(tile_hist)");
         if ((e = hipMalloc((void**)&c->s.scan_sums, ((hist_words + 4095) / 4096 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(scan)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
+        if ((e = hipMalloc((void**)&c->s.col_sums, ((tiles + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
+            return bail(e, "hipMalloc(col_sums)");
+        if ((e = hipMalloc((void**)&c->s.col_tot, (1ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMalloc(col_tot)");
         if ((e = hipMalloc((void**)&c->st_off, ((size_t)cfg->n_act + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(offsets)");
     }
     *out = c;

@@ -124,6 +124,8 @@ struct Scratch {
     uint32_t* sorted_keys;  // [max_batch]
     uint32_t* tile_hist;    // [2048 * max_tiles]
     uint32_t* scan_sums;    // [scan blocks]
+    uint32_t* col_sums;     // [ceil(max_tiles/64) * 2048] column-scan chunk sums
+    uint32_t* col_tot;      // [2048] column totals
     uint8_t* digits;        // [max_batch] (partition by owner)
     uint64_t max_batch;
     uint64_t max_tiles;

@@ -80,21 +80,29 @@ __device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint
     return m;
 }
 
-// Stages 1-3 for one message.  Mirrors oracle route_one (Dispatcher.AddressMessage, Dispatcher.cs:555-579).
-__device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t mask,
-                                              const Msg& m, bool excl_opt, uint32_t& act) {
-    act = ORL_NO_ACT;
+// Stages 1-3 for one message, split so a thread can keep several messages' directory probes in flight:
+//   route_head  stages 1-2 + every decision that needs no directory (returns the final route word, or
+//               kNeedProbe when the owner's partition is local and must be probed);
+//   probe_slot  one 32-B slot compare (stage 3), continued by probe_rest along the linear-probe chain;
+//   route_tail  IsValidSilo filter + placement of misses.
+// Together they mirror the oracle's route_one (Dispatcher.AddressMessage, Dispatcher.cs:555-579).
+constexpr uint32_t kNeedProbe = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t route_head(const RouteParams& P, const Msg& m, bool excl_opt, uint32_t& h,
+                                               uint32_t& owner, uint32_t& rf) {
     const uint32_t me = m.meta & 0xFFu;
     const uint32_t hflags = (m.meta >> 16) & 0xFFu;
+    rf = 0;
+    owner = 0xFFu;
+    h = 0;
     if (hflags & ORL_HDR_ADDRESS_COMPLETE) {  // TargetAddress.IsComplete (Dispatcher.cs:557-558)
         const uint32_t ts = m.meta >> 24;
         return pack_route(0xFFu, ts, ORL_ST_ADDRESS_COMPLETE, ts == me ? ORL_RF_LOOPBACK : 0u);
     }
     const uint32_t cat = (uint32_t)(m.tcd >> 56);
-    const uint32_t h = (hflags & ORL_HDR_HASH_VALID) ? m.aux : jenkins3(m.tcd, m.n0, m.n1);  // stage 1
+    h = (hflags & ORL_HDR_HASH_VALID) ? m.aux : jenkins3(m.tcd, m.n0, m.n1);  // stage 1
     if (cat == ORL_CAT_SYSTEM_TARGET)  // every silo owns its system targets (:442-447)
         return pack_route(me, me, ORL_ST_SYSTEM_TARGET, ORL_RF_LOOPBACK);
-    uint32_t owner, rf = 0;
     if (m.tcd == P.mem_tcd && m.n0 == P.mem_n0 && m.n1 == P.mem_n1) {  // membership table grain (:449-464)
         if (P.seed == 0xFFu) return pack_route(0xFFu, 0xFFu, ORL_ST_NO_SEED, 0);
         owner = P.seed;
@@ -111,36 +119,61 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
     }
     if (cat == ORL_CAT_KEYEXT_GRAIN) return pack_route(owner, 0xFFu, ORL_ST_KEYEXT_UNRESOLVED, rf);
     if (!mask_bit(P.local, owner)) return pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, rf);
-    // stage 3: open-addressed partition probe; tombstones are skipped, an empty slot ends the chain.
-    uint64_t slot = fmix32(h) & mask;
-    bool found = false;
-    uint32_t fact = 0, fsilo = 0;
-    for (uint64_t step = 0; step <= mask; ++step) {
-        const uint4* sp = reinterpret_cast<const uint4*>(dir + slot);
-        const uint4 a = sp[0];
-        const uint4 b = sp[1];
-        const uint32_t state = (b.w >> 8) & 0xFFu;
-        if (state == SLOT_EMPTY) break;
-        if (state == SLOT_FULL && a.x == (uint32_t)m.tcd && a.y == (uint32_t)(m.tcd >> 32) &&
-            a.z == (uint32_t)m.n0 && a.w == (uint32_t)(m.n0 >> 32) && b.x == (uint32_t)m.n1 &&
-            b.y == (uint32_t)(m.n1 >> 32)) {
-            found = true;
-            fact = b.z;
-            fsilo = b.w & 0xFFu;
-            break;
-        }
-        slot = (slot + 1) & mask;
+    return kNeedProbe;
+}
+
+// One slot of the open-addressed partition: 0 = key found (act/silo set), 1 = empty (chain ends: miss),
+// 2 = occupied by another key or tombstone (continue with the next slot).
+__device__ __forceinline__ int probe_slot(const u32x4& a, const u32x4& b, const Msg& m, uint32_t& act, uint32_t& silo) {
+    const uint32_t state = (b.w >> 8) & 0xFFu;
+    if (state == SLOT_EMPTY) return 1;
+    if (state == SLOT_FULL && a.x == (uint32_t)m.tcd && a.y == (uint32_t)(m.tcd >> 32) && a.z == (uint32_t)m.n0 &&
+        a.w == (uint32_t)(m.n0 >> 32) && b.x == (uint32_t)m.n1 && b.y == (uint32_t)(m.n1 >> 32)) {
+        act = b.z;
+        silo = b.w & 0xFFu;
+        return 0;
     }
+    return 2;
+}
+
+__device__ __forceinline__ bool probe_rest(const u32x4* __restrict__ dir4, uint64_t mask, uint64_t slot, const Msg& m,
+                                           uint32_t& act, uint32_t& silo) {
+    for (uint64_t step = 1; step <= mask; ++step) {
+        slot = (slot + 1) & mask;
+        const int r = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, act, silo);
+        if (r != 2) return r == 0;
+    }
+    return false;
+}
+
+__device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
+                                               bool found, uint32_t fact, uint32_t fsilo, uint32_t& act) {
+    const uint32_t me = m.meta & 0xFFu;
     if (found && mask_bit(P.functional, fsilo)) {  // LookUpGrain filtered by IsValidSilo
         act = fact;
         return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u));
     }
-    if (cat == ORL_CAT_CLIENT) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
+    act = ORL_NO_ACT;
+    if ((uint32_t)(m.tcd >> 56) == ORL_CAT_CLIENT) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
     uint32_t host;
     if (P.policy == ORL_POLICY_PREFER_LOCAL) host = me;
     else host = P.n_active ? P.active_list[h % P.n_active] : 0xFFu;
     rf |= ORL_RF_NEW_PLACEMENT | (host == me ? ORL_RF_LOOPBACK : 0u);
     return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf);
+}
+
+__device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t mask,
+                                              const Msg& m, bool excl_opt, uint32_t& act) {
+    uint32_t h, owner, rf;
+    act = ORL_NO_ACT;
+    const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
+    if (r != kNeedProbe) return r;
+    const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
+    const uint64_t slot = fmix32(h) & mask;
+    uint32_t fact = 0, fsilo = 0;
+    const int pr = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
+    const bool found = pr == 0 || (pr == 2 && probe_rest(dir4, mask, slot, m, fact, fsilo));
+    return route_tail(P, m, h, owner, rf, found, fact, fsilo, act);
 }
 
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
@@ -153,8 +186,13 @@ __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------------
-// stages 1-3 (+ tile histogram of the first radix digit).  Tile t covers messages [t*4096, t*4096+4096);
-// thread x handles e = t*4096 + j*256 + x, j = 0..15 (coalesced 8-KB header rows per j).
+// stages 1-3 (+ tile histogram of the first radix digit, stored tile-major: one coalesced row per tile).
+// Tile t covers messages [t*4096, t*4096+4096); thread x handles e = t*4096 + j*256 + x (coalesced 8-KB
+// header rows per j).  Messages are taken kBatch at a time per thread: all kBatch headers are loaded,
+// then all kBatch first probes are issued before any is consumed, so each thread keeps kBatch
+// independent random slot reads in flight (the probe is a ~1 µs dependent load behind the header).
+constexpr uint32_t kBatch = 4;
+
 struct RouteSmem {
     RouteParams P;
     uint32_t hist[1u << kMaxDigitBits];
@@ -165,29 +203,59 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          uint64_t mask, const orl_msg_hdr* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
-                                                         uint32_t ntiles, uint32_t bins, uint32_t shift) {
+                                                         uint32_t bins, uint32_t shift) {
     __shared__ RouteSmem sm;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     __syncthreads();
+    const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
     const uint32_t n_act = sm.P.n_act;
     const uint32_t base = blockIdx.x * kTile;
-#pragma unroll 2
-    for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
-        if (e < n) {
-            const Msg m = load_hdr(in, e);
-            uint32_t act;
-            const uint32_t r = route_msg(sm.P, dir, mask, m, excl != 0, act);
-            route[e] = r;
-            act_out[e] = act;
-            if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+    for (uint32_t j0 = 0; j0 < kItems; j0 += kBatch) {
+        Msg m[kBatch];
+        uint32_t r[kBatch], h[kBatch], own[kBatch], rf[kBatch];
+        uint64_t slot[kBatch];
+        u32x4 sa[kBatch], sb[kBatch];
+#pragma unroll
+        for (uint32_t u = 0; u < kBatch; ++u) {
+            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
+            if (e < n) m[u] = load_hdr(in, e);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBatch; ++u) {
+            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
+            r[u] = 0;
+            if (e < n) {
+                r[u] = route_head(sm.P, m[u], excl != 0, h[u], own[u], rf[u]);
+                if (r[u] == kNeedProbe) {
+                    slot[u] = fmix32(h[u]) & mask;
+                    sa[u] = dir4[2 * slot[u]];
+                    sb[u] = dir4[2 * slot[u] + 1];
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBatch; ++u) {
+            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
+            if (e < n) {
+                uint32_t act = ORL_NO_ACT, rr = r[u];
+                if (rr == kNeedProbe) {
+                    uint32_t fact = 0, fsilo = 0;
+                    const int pr = probe_slot(sa[u], sb[u], m[u], fact, fsilo);
+                    const bool found = pr == 0 || (pr == 2 && probe_rest(dir4, mask, slot[u], m[u], fact, fsilo));
+                    rr = route_tail(sm.P, m[u], h[u], own[u], rf[u], found, fact, fsilo, act);
+                }
+                route[e] = rr;
+                act_out[e] = act;
+                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+            }
         }
     }
     if (HIST) {
         __syncthreads();
-        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) tile_hist[(size_t)b * ntiles + blockIdx.x] = sm.hist[b];
+        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
     }
 }
 
@@ -270,21 +338,107 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Stage 4, one LSD digit.  Up-sweep: per-tile digit histogram, stored bin-major ([bin][tile]) so one
-// exclusive scan of the whole matrix yields every (bin, tile) output base.
+// Stage 4, one LSD digit.  Per-tile digit histograms are stored TILE-major (row t = tile t's B counts),
+// so every histogram write and every offset read is one coalesced row.  The column scan below turns the
+// count matrix in place into global output bases: M[t][d] = sum_{d'<d} total[d'] + sum_{t'<t} M[t'][d].
 __global__ __launch_bounds__(256) void k_radix_up(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t bins,
-                                                  uint32_t* __restrict__ tile_hist, uint32_t ntiles) {
+                                                  uint32_t* __restrict__ tile_hist) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kTile;
-#pragma unroll 4
+    uint32_t k[kItems];
+#pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
         const uint32_t e = base + j * 256 + threadIdx.x;
-        if (e < n) atomicAdd(&hist[(keys[e] >> shift) & (bins - 1)], 1u);
+        k[j] = e < n ? keys[e] : 0xFFFFFFFFu;
     }
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j)
+        if (k[j] != 0xFFFFFFFFu) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < bins; b += 256) tile_hist[(size_t)b * ntiles + blockIdx.x] = hist[b];
+    uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
+    for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
+}
+
+// Column scan of the [ntiles][bins] count matrix, in chunks of kScanRows tiles.
+//   k_col_sum:   S[c][d] = sum of rows of chunk c                       (grid: chunks x ceil(bins/256))
+//   k_col_scan:  S[c][d] → exclusive prefix over chunks; T[d] = column total (grid: ceil(bins/16))
+//   k_col_apply: M[t][d] = base(d) + S[c][d] + rows of chunk c before t (grid: chunks x ceil(bins/256))
+constexpr uint32_t kScanRows = 64;
+
+__global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
+                                                 uint32_t* __restrict__ S) {
+    const uint32_t d = blockIdx.y * 256 + threadIdx.x;
+    if (d >= bins) return;
+    const uint32_t t0 = blockIdx.x * kScanRows;
+    const uint32_t t1 = min(t0 + kScanRows, ntiles);
+    uint32_t acc = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) acc += M[(size_t)t * bins + d];
+    S[(size_t)blockIdx.x * bins + d] = acc;
+}
+
+// 16 columns per block; 16 threads per column each own a contiguous run of chunks.
+__global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
+                                                  uint32_t* __restrict__ T) {
+    __shared__ uint32_t part[16][17];
+    const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
+    const uint32_t d = blockIdx.x * 16 + col;
+    const uint32_t per = (nchunks + 15) / 16;
+    const uint32_t c0 = grp * per, c1 = min(c0 + per, nchunks);
+    uint32_t acc = 0;
+    if (d < bins)
+        for (uint32_t c = c0; c < c1; ++c) acc += S[(size_t)c * bins + d];
+    part[grp][col] = acc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t g = 0; g < 16; ++g) {
+        const uint32_t v = part[g][col];
+        if (g < grp) pre += v;
+        tot += v;
+    }
+    if (d < bins) {
+        for (uint32_t c = c0; c < c1; ++c) {
+            const uint32_t v = S[(size_t)c * bins + d];
+            S[(size_t)c * bins + d] = pre;
+            pre += v;
+        }
+        if (grp == 0) T[d] = tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
+                                                   const uint32_t* __restrict__ S, const uint32_t* __restrict__ T) {
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t red;
+    const uint32_t d0 = blockIdx.y * 256;
+    const uint32_t d = d0 + threadIdx.x;
+    // base(d) = sum of column totals before d: columns before this block's 256, then an in-block scan
+    uint32_t before = 0;
+    for (uint32_t i = threadIdx.x; i < d0; i += 256) before += T[i];
+    if (threadIdx.x == 0) red = 0;
+    __syncthreads();
+    atomicAdd(&red, before);
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(d < bins ? T[d] : 0u, wsum, total);
+    if (d >= bins) return;
+    uint32_t run = red + ex + S[(size_t)blockIdx.x * bins + d];
+    const uint32_t t0 = blockIdx.x * kScanRows;
+    const uint32_t t1 = min(t0 + kScanRows, ntiles);
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t v = M[(size_t)t * bins + d];
+        M[(size_t)t * bins + d] = run;
+        run += v;
+    }
+}
+
+// XCD-aware tile order (cdna_hip_programming.md T1, bijective form): workgroups dispatched to one XCD
+// (b % 8 equal) get a contiguous range of tiles, so the short per-bin runs that consecutive tiles append
+// to the same output region meet in that XCD's L2 instead of leaving it as partial lines.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
+    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
 // Down-sweep: stable rank of each key inside the tile, then scatter through an LDS staging image so the
@@ -310,13 +464,14 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
     constexpr uint32_t PER = (B + 255u) / 256u;  // bins per thread in the bin loops
     __shared__ DownSmem<BITS> sm;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
     for (uint32_t b = threadIdx.x; b < B; b += 256) {
 #pragma unroll
         for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
     }
     __syncthreads();
 
-    const uint32_t tbase = blockIdx.x * kTile;
+    const uint32_t tbase = tile * kTile;
     const uint32_t wbase = tbase + w * (kItems * 64u);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
     uint32_t key[kItems], idx[kItems], rank[kItems];
@@ -351,6 +506,7 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
     }
     __syncthreads();
     // per-bin: wave prefixes (in place) and tile totals; then exclusive scan of totals over bins.
+    const uint32_t* orow = tile_off + (size_t)tile * B;
     uint32_t tot[PER];
     uint32_t s = 0;
 #pragma unroll
@@ -364,11 +520,11 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
                 sm.cnt[ww][b] = t;
                 t += c;
             }
-            sm.goff[b] = tile_off[(size_t)b * ntiles + blockIdx.x];
         }
         tot[q] = t;
         s += t;
     }
+    for (uint32_t b = threadIdx.x; b < B; b += 256) sm.goff[b] = orow[b];
     uint32_t total;
     uint32_t run = block_excl_scan(s, sm.wsum, total);
 #pragma unroll
@@ -419,7 +575,12 @@ __global__ __launch_bounds__(256) void k_offsets(const uint32_t* __restrict__ so
     if (threadIdx.x == 64) bounds[1] = lower_bound_u32(sorted, n, b1);
     __syncthreads();
     const uint32_t p0 = bounds[0], p1 = bounds[1];
-    if (threadIdx.x == 0) offsets[b0] = p0;
+    if (threadIdx.x == 0) {
+        offsets[b0] = p0;
+        // empty buckets before the first key of the slice start where that key does
+        if (p1 > p0)
+            for (uint32_t b = b0 + 1, k0 = sorted[p0]; b <= k0; ++b) offsets[b] = p0;
+    }
     for (uint32_t i = p0 + 1 + threadIdx.x; i < p1; i += 256) {
         const uint32_t k = sorted[i], kp = sorted[i - 1];
         for (uint32_t b = kp + 1; b <= k; ++b) offsets[b] = i;  // buckets (kp, k] start at i
@@ -527,7 +688,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     }
     if (HIST) {
         __syncthreads();
-        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) tile_hist[(size_t)b * ntiles + blockIdx.x] = sm.hist[b];
+        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
     }
 }
 
@@ -676,6 +838,15 @@ void launch_down(int bits, bool first, const uint32_t* kin, const uint32_t* iin,
     }
 }
 
+// Column scan of a tile-major [ntiles][bins] histogram into per-(tile, bin) output bases, in place.
+void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, const Scratch& s, hipStream_t st) {
+    const uint32_t nch = ceil_div(ntiles, kScanRows);
+    const uint32_t cb = ceil_div(bins, 256);
+    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums);
+    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot);
+    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot);
+}
+
 // Stage 4 after a route kernel that already wrote the first digit's tile histogram into s.tile_hist.
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets,
                        const Scratch& s, hipStream_t st) {
@@ -686,9 +857,9 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t bins = 1u << plan.bits[p];
         if (p > 0) {
             const uint32_t* kin = ((plan.passes - p) % 2 == 0) ? s.sorted_keys : s.keys_a;  // output of pass p-1
-            hipLaunchKernelGGL(k_radix_up, dim3(ntiles), dim3(256), 0, st, kin, n, (uint32_t)plan.shift[p], bins, s.tile_hist, ntiles);
+            hipLaunchKernelGGL(k_radix_up, dim3(ntiles), dim3(256), 0, st, kin, n, (uint32_t)plan.shift[p], bins, s.tile_hist);
         }
-        scan_inplace(s.tile_hist, (uint64_t)bins * ntiles, s.scan_sums, st);
+        col_scan(s.tile_hist, ntiles, bins, s, st);
         const bool to_final = ((plan.passes - 1 - p) % 2) == 0;
         uint32_t* kout = to_final ? s.sorted_keys : s.keys_a;
         uint32_t* iout = to_final ? d_order : s.idx_a;
@@ -723,10 +894,10 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     if (buckets)
         hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, ntiles, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
+                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
     else
         hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, nullptr, ntiles, 1u, 0u);
+                           (uint32_t)n, excl, d_route, d_act, nullptr, 1u, 0u);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();
     if (e) return e;
