@@ -25,6 +25,9 @@
 //
 // The reference is C#/.NET and cannot be built or run here; this restatement is checked against an
 // independent Python restatement (oracle/pyref.py) and the golden fixtures in tests/golden/.
+// PARITY UNPINNED beyond the reference's own property test (Identifiertests.cs:284-301, byte-path
+// Jenkins == u64-path Jenkins) and its shipped Chirper graph: ring ownership, directory lookup,
+// placement, bucketing and fan-out have no reference golden vector.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>

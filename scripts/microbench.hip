@@ -71,6 +71,81 @@ __global__ void k_route_mix(const u32x4* __restrict__ hdr, const u32x4* __restri
     }
 }
 
+// ILP form: each thread issues K independent random 32-B probes before consuming any
+template <int K>
+__global__ void k_gather_ilp(const u32x4* __restrict__ tab, uint64_t mask, uint32_t n, uint32_t* __restrict__ out) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * K) {
+        u32x4 a[K], b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = i0 + k * stride;
+            const uint64_t s = mix32(i * 2654435761u) & mask;
+            a[k] = tab[2 * s];
+            b[k] = tab[2 * s + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = i0 + k * stride;
+            if (i < n) out[i] = a[k].x ^ b[k].w;
+        }
+    }
+}
+
+// route mix with the next header group prefetched while the current probes are in flight
+template <int K>
+__global__ void k_route_mix_pipe(const u32x4* __restrict__ hdr, const u32x4* __restrict__ tab, uint64_t mask, uint32_t n,
+                                 uint32_t* __restrict__ o1, uint32_t* __restrict__ o2) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    u32x4 ha[K], hb[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const size_t i = t + (size_t)k * stride;
+        if (i < n) { ha[k] = __builtin_nontemporal_load(hdr + 2 * i); hb[k] = __builtin_nontemporal_load(hdr + 2 * i + 1); }
+    }
+    for (uint32_t i0 = t; i0 < n; i0 += stride * K) {
+        u32x4 c[K], d[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t s = mix32(ha[k].x ^ hb[k].x ^ ha[k].z) & mask;
+            c[k] = tab[2 * s];
+            d[k] = tab[2 * s + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const size_t i = i0 + (size_t)(K + k) * stride;
+            if (i < n) { ha[k] = __builtin_nontemporal_load(hdr + 2 * i); hb[k] = __builtin_nontemporal_load(hdr + 2 * i + 1); }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t i = i0 + k * stride;
+            if (i < n) { o1[i] = c[k].x ^ d[k].w; o2[i] = c[k].y ^ d[k].z; }
+        }
+    }
+}
+
+__global__ void k_fill_random(u32x4* __restrict__ a, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t x = (uint32_t)i;
+        a[i] = u32x4{mix32(x * 2654435761u + 1u), mix32(x * 2246822519u + 7u), mix32(x * 3266489917u + 3u), mix32(x ^ 0x9e3779b9u)};
+    }
+}
+
+// route mix with plain (temporal) header loads
+__global__ void k_route_mix_t(const u32x4* __restrict__ hdr, const u32x4* __restrict__ tab, uint64_t mask, uint32_t n,
+                              uint32_t* __restrict__ o1, uint32_t* __restrict__ o2) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const u32x4 a = hdr[2 * (size_t)i];
+        const u32x4 b = hdr[2 * (size_t)i + 1];
+        const uint64_t s = mix32(a.x ^ b.x ^ a.z) & mask;
+        const u32x4 c = tab[2 * s];
+        const u32x4 d = tab[2 * s + 1];
+        o1[i] = c.x ^ d.w;
+        o2[i] = c.y ^ d.z;
+    }
+}
+
 int main(int argc, char** argv) {
     const size_t stream_bytes = 2ull << 30;
     const uint32_t n = 64u << 20;
@@ -79,7 +154,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&a, stream_bytes));
     CK(hipMalloc(&b, stream_bytes));
     CK(hipMalloc(&out, (size_t)n * 8));
-    CK(hipMemset(a, 1, stream_bytes));
+    hipLaunchKernelGGL(k_fill_random, dim3(4096), dim3(256), 0, 0, a, stream_bytes / 16);
+    CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -111,6 +187,18 @@ int main(int argc, char** argv) {
         timeit(nm, 32.0 * n + 4.0 * n, n, [&] { hipLaunchKernelGGL(k_gather_pair, dim3(grid), dim3(256), 0, 0, b, mask, n, out); });
         snprintf(nm, sizeof nm, "route mix table %zu MB", tb >> 20);
         timeit(nm, 72.0 * n, n, [&] { hipLaunchKernelGGL(k_route_mix, dim3(grid), dim3(256), 0, 0, a, b, mask, n, out, out + n); });
+        snprintf(nm, sizeof nm, "route mix (temporal hdr) %zu MB", tb >> 20);
+        timeit(nm, 72.0 * n, n, [&] { hipLaunchKernelGGL(k_route_mix_t, dim3(grid), dim3(256), 0, 0, a, b, mask, n, out, out + n); });
+        snprintf(nm, sizeof nm, "gather32 ilp4 table %zu MB", tb >> 20);
+        timeit(nm, 32.0 * n + 4.0 * n, n, [&] { hipLaunchKernelGGL(k_gather_ilp<4>, dim3(grid), dim3(256), 0, 0, b, mask, n, out); });
+        snprintf(nm, sizeof nm, "gather32 ilp8 table %zu MB", tb >> 20);
+        timeit(nm, 32.0 * n + 4.0 * n, n, [&] { hipLaunchKernelGGL(k_gather_ilp<8>, dim3(grid), dim3(256), 0, 0, b, mask, n, out); });
+        for (int g : {1024, 4096, 16384}) {
+            snprintf(nm, sizeof nm, "route pipe4 g%d table %zu MB", g, tb >> 20);
+            timeit(nm, 72.0 * n, n, [&] { hipLaunchKernelGGL(k_route_mix_pipe<4>, dim3(g), dim3(256), 0, 0, a, b, mask, n, out, out + n); });
+        }
+        snprintf(nm, sizeof nm, "route pipe8 g4096 table %zu MB", tb >> 20);
+        timeit(nm, 72.0 * n, n, [&] { hipLaunchKernelGGL(k_route_mix_pipe<8>, dim3(4096), dim3(256), 0, 0, a, b, mask, n, out, out + n); });
     }
     return 0;
 }
