@@ -312,7 +312,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
-    f(c->s.keys_a); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -368,7 +368,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         c->s.max_batch = mb;
         c->s.max_tiles = tiles;
         const uint64_t hist_words = (1ull << kMaxDigitBits) * tiles;
-        if ((e = hipMalloc((void**)&c->s.keys_a, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(keys)");
+        if ((e = hipMalloc((void**)&c->s.pairs_a, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_a)");
+        if ((e = hipMalloc((void**)&c->s.pairs_b, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_b)");
         if ((e = hipMalloc((void**)&c->s.idx_a, (mb + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(idx)");
         if ((e = hipMalloc((void**)&c->s.sorted_keys, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(sorted)");
         if ((e = hipMalloc((void**)&c->s.tile_hist, hist_words * 4)) != hipSuccess) return bail(e, "hipMalloc(tile_hist)");

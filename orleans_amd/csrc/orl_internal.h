@@ -119,8 +119,9 @@ inline RadixPlan make_plan(uint32_t max_key) {
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
 // All return hipError_t as int; they only enqueue on `stream`.
 struct Scratch {
-    uint32_t* keys_a;       // [max_batch]
-    uint32_t* idx_a;        // [max_batch]
+    uint2* pairs_a;         // [max_batch] {key, index} between radix passes
+    uint2* pairs_b;         // [max_batch]
+    uint32_t* idx_a;        // [max_batch + 1] fan-out publish offsets
     uint32_t* sorted_keys;  // [max_batch]
     uint32_t* tile_hist;    // [2048 * max_tiles]
     uint32_t* scan_sums;    // [scan blocks]

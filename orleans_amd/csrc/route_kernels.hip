@@ -5,8 +5,9 @@
 //                    predecessor search (LocalGrainDirectory.cs:439-497) → GrainDirectoryPartition.LookUpGrain
 //                    + IsValidSilo (GrainDirectoryPartition.cs:326-344) → placement of misses
 //                    (PlacementDirectorsManager.cs:70-91).  Fused with the first radix digit's tile histogram.
-//   k_radix_up/down  stage 4: stable LSD radix partition by activation handle = per-activation FIFO
-//                    (ActivationData.EnqueueMessage, ActivationData.cs:483-514).
+//   k_radix_pass     stage 4: stable LSD radix partition by activation handle = per-activation FIFO
+//                    (ActivationData.EnqueueMessage, ActivationData.cs:483-514); k_hist_pairs + k_col_* give
+//                    each (tile, digit) its global output base.
 //   k_offsets        per-activation bucket offsets from the sorted keys.
 //   k_fanout_*       stage 5: CSR multicast expansion (ChirperAccount.cs:154-157) feeding stages 1-4.
 //   k_part_*         stable partition of headers by destination rank (exchange).
@@ -83,7 +84,7 @@ __device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint
 // Stages 1-3 for one message, split so a thread can keep several messages' directory probes in flight:
 //   route_head  stages 1-2 + every decision that needs no directory (returns the final route word, or
 //               kNeedProbe when the owner's partition is local and must be probed);
-//   probe_slot  one 32-B slot compare (stage 3), continued by probe_rest along the linear-probe chain;
+//   probe_slot  one 32-B slot compare (stage 3), repeated along the linear-probe chain;
 //   route_tail  IsValidSilo filter + placement of misses.
 // Together they mirror the oracle's route_one (Dispatcher.AddressMessage, Dispatcher.cs:555-579).
 constexpr uint32_t kNeedProbe = 0xFFFFFFFFu;
@@ -136,16 +137,6 @@ __device__ __forceinline__ int probe_slot(const u32x4& a, const u32x4& b, const 
     return 2;
 }
 
-__device__ __forceinline__ bool probe_rest(const u32x4* __restrict__ dir4, uint64_t mask, uint64_t slot, const Msg& m,
-                                           uint32_t& act, uint32_t& silo) {
-    for (uint64_t step = 1; step <= mask; ++step) {
-        slot = (slot + 1) & mask;
-        const int r = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, act, silo);
-        if (r != 2) return r == 0;
-    }
-    return false;
-}
-
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
                                                bool found, uint32_t fact, uint32_t fsilo, uint32_t& act) {
     const uint32_t me = m.meta & 0xFFu;
@@ -162,6 +153,8 @@ __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& 
     return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf);
 }
 
+// Stages 1-3 for one message.  The linear-probe chain is continued by a flag loop (measured 13 % faster in
+// k_route than an early-return helper loop).
 __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t mask,
                                               const Msg& m, bool excl_opt, uint32_t& act) {
     uint32_t h, owner, rf;
@@ -169,11 +162,14 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
     const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
     if (r != kNeedProbe) return r;
     const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
-    const uint64_t slot = fmix32(h) & mask;
+    uint64_t slot = fmix32(h) & mask;
     uint32_t fact = 0, fsilo = 0;
-    const int pr = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
-    const bool found = pr == 0 || (pr == 2 && probe_rest(dir4, mask, slot, m, fact, fsilo));
-    return route_tail(P, m, h, owner, rf, found, fact, fsilo, act);
+    int st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
+    for (uint64_t step = 0; st == 2 && step < mask; ++step) {
+        slot = (slot + 1) & mask;
+        st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
+    }
+    return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act);
 }
 
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
@@ -187,12 +183,12 @@ __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ 
 
 // ---------------------------------------------------------------------------------------------------
 // stages 1-3 (+ tile histogram of the first radix digit, stored tile-major: one coalesced row per tile).
-// Tile t covers messages [t*4096, t*4096+4096); thread x handles e = t*4096 + j*256 + x (coalesced 8-KB
-// header rows per j).  Messages are taken kBatch at a time per thread: all kBatch headers are loaded,
-// then all kBatch first probes are issued before any is consumed, so each thread keeps kBatch
-// independent random slot reads in flight (the probe is a ~1 µs dependent load behind the header).
-constexpr uint32_t kBatch = 4;
-
+// Tile t covers messages [t*4096, t*4096+4096); step j of thread x handles e = t*4096 + j*256 + x (coalesced
+// 8-KB header rows per step).  One message per thread per step: the kernel needs 36 VGPRs, so 8 waves per
+// SIMD are resident and the random 32-B directory probes are hidden by wave-level parallelism.  (Batching
+// 4 messages per thread to keep 4 probes in flight per lane needs 134 VGPRs = 3 waves/SIMD and ran 1.6x
+// slower: profiles/r01_route_variants.txt.)  The probe chain is continued by a flag loop in the same
+// basic block as the first probe (an early-return helper loop for the chain cost 13 %: 1.76 vs 1.56 ms).
 struct RouteSmem {
     RouteParams P;
     uint32_t hist[1u << kMaxDigitBits];
@@ -211,45 +207,37 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     __syncthreads();
     const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
     const uint32_t n_act = sm.P.n_act;
-    const uint32_t base = blockIdx.x * kTile;
-    for (uint32_t j0 = 0; j0 < kItems; j0 += kBatch) {
-        Msg m[kBatch];
-        uint32_t r[kBatch], h[kBatch], own[kBatch], rf[kBatch];
-        uint64_t slot[kBatch];
-        u32x4 sa[kBatch], sb[kBatch];
-#pragma unroll
-        for (uint32_t u = 0; u < kBatch; ++u) {
-            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
-            if (e < n) m[u] = load_hdr(in, e);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kBatch; ++u) {
-            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
-            r[u] = 0;
-            if (e < n) {
-                r[u] = route_head(sm.P, m[u], excl != 0, h[u], own[u], rf[u]);
-                if (r[u] == kNeedProbe) {
-                    slot[u] = fmix32(h[u]) & mask;
-                    sa[u] = dir4[2 * slot[u]];
-                    sb[u] = dir4[2 * slot[u] + 1];
-                }
+    const uint32_t base = blockIdx.x * kTile + threadIdx.x;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = base + j * kRouteThreads;
+        Msg m;
+        if (e < n) m = load_hdr(in, e);
+        uint32_t h = 0, own = 0, rf = 0, r = 0;
+        uint64_t slot = 0;
+        u32x4 sa, sb;
+        if (e < n) {
+            r = route_head(sm.P, m, excl != 0, h, own, rf);
+            if (r == kNeedProbe) {
+                slot = fmix32(h) & mask;
+                sa = dir4[2 * slot];
+                sb = dir4[2 * slot + 1];
             }
         }
-#pragma unroll
-        for (uint32_t u = 0; u < kBatch; ++u) {
-            const uint32_t e = base + (j0 + u) * kRouteThreads + threadIdx.x;
-            if (e < n) {
-                uint32_t act = ORL_NO_ACT, rr = r[u];
-                if (rr == kNeedProbe) {
-                    uint32_t fact = 0, fsilo = 0;
-                    const int pr = probe_slot(sa[u], sb[u], m[u], fact, fsilo);
-                    const bool found = pr == 0 || (pr == 2 && probe_rest(dir4, mask, slot[u], m[u], fact, fsilo));
-                    rr = route_tail(sm.P, m[u], h[u], own[u], rf[u], found, fact, fsilo, act);
-                }
-                route[e] = rr;
-                act_out[e] = act;
-                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
-            }
+        int st = 3;
+        uint32_t fact = 0, fsilo = 0;
+        if (r == kNeedProbe) st = probe_slot(sa, sb, m, fact, fsilo);
+        for (uint64_t step = 0; st == 2 && step < mask; ++step) {
+            slot = (slot + 1) & mask;
+            sa = dir4[2 * slot];
+            sb = dir4[2 * slot + 1];
+            st = probe_slot(sa, sb, m, fact, fsilo);
+        }
+        if (e < n) {
+            uint32_t act = ORL_NO_ACT, rr = r;
+            if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act);
+            route[e] = rr;
+            act_out[e] = act;
+            if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
         }
     }
     if (HIST) {
@@ -338,24 +326,25 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Stage 4, one LSD digit.  Per-tile digit histograms are stored TILE-major (row t = tile t's B counts),
-// so every histogram write and every offset read is one coalesced row.  The column scan below turns the
-// count matrix in place into global output bases: M[t][d] = sum_{d'<d} total[d'] + sum_{t'<t} M[t'][d].
-__global__ __launch_bounds__(256) void k_radix_up(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift, uint32_t bins,
-                                                  uint32_t* __restrict__ tile_hist) {
+// Stage 4, one LSD digit per pass.  Per-tile digit histograms are stored TILE-major (row t = tile t's B
+// counts), so every histogram write and every offset read is one coalesced row.  The column scan below
+// turns the count matrix in place into global output bases: M[t][d] = sum_{d'<d} total[d'] + sum_{t'<t} M[t'][d].
+// Pass 0's histogram is built by k_route itself; later passes read the previous pass's {key, index} pairs.
+__global__ __launch_bounds__(256) void k_hist_pairs(const uint2* __restrict__ pairs, uint32_t n, uint32_t shift, uint32_t bins,
+                                                    uint32_t* __restrict__ tile_hist) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kTile;
     uint32_t k[kItems];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
         const uint32_t e = base + j * 256 + threadIdx.x;
-        k[j] = e < n ? keys[e] : 0xFFFFFFFFu;
+        k[j] = pairs[e < n ? e : n - 1].x;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j)
-        if (k[j] != 0xFFFFFFFFu) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
+        if (base + j * 256 + threadIdx.x < n) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
     __syncthreads();
     uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
@@ -441,36 +430,43 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// Down-sweep: stable rank of each key inside the tile, then scatter through an LDS staging image so the
-// global writes are runs of consecutive positions per bin.  Wave w owns tile elements
-// [w*1024, w*1024+1024) processed 64 at a time in order, so (wave, iteration, lane) order == arrival
-// order and the ranks are stable.  Lanes with equal digits are found with BITS ballots.
+// One stable LSD pass over a tile of 4096 elements:
+//   1. load the tile (IN_ACT: activation handles, clamped to the unresolved bucket n_act, index = position;
+//      IN_PAIR: {key, index} pairs of the previous pass) with unconditional loads, all in flight together;
+//   2. stable rank inside the tile: wave w owns elements [w*1024, w*1024+1024) processed 64 at a time in
+//      order, lanes with equal digits found with BITS ballots, per-wave running counts in LDS, so
+//      (wave, step, lane) order == arrival order;
+//   3. per-bin tile-local starts (block scan) and delta[d] = global base of (tile, d) - local start;
+//   4. scatter into an LDS image sorted by digit, then write it out in image order, so the global stores
+//      are runs of consecutive positions per bin.  OUT_PAIR writes 8-B {key, index} pairs (one store
+//      request per run instead of two); OUT_FINAL writes the index to `order` and the key to `keys`.
+// Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
+enum : int { IN_ACT = 0, IN_PAIR = 1 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1 };
+
 template <int BITS>
-struct DownSmem {
-    uint32_t cnt[kWaves][1u << BITS];  // per-wave running counts, then per-wave exclusive prefixes
-    uint32_t bin_start[1u << BITS];    // tile-local bin starts
-    uint32_t goff[1u << BITS];         // global base of (bin, this tile)
+struct PassSmem {
+    uint32_t cnt[kWaves][1u << BITS];  // per-wave running counts, then per-(wave, bin) tile-local starts
+    uint32_t delta[1u << BITS];        // global base - tile-local start, per bin
     uint32_t stage_k[kTile];
     uint32_t stage_i[kTile];
     uint32_t wsum[kWaves];
 };
 
-template <int BITS, bool FIRST>
-__global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ idx_in,
-                                                    uint32_t n, uint32_t n_act, uint32_t shift,
+template <int BITS, int IN, int OUT>
+__global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     const uint32_t* __restrict__ tile_off, uint32_t ntiles,
-                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ idx_out) {
+                                                    uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
+                                                    uint32_t* __restrict__ key_out) {
     constexpr uint32_t B = 1u << BITS;
-    constexpr uint32_t PER = (B + 255u) / 256u;  // bins per thread in the bin loops
-    __shared__ DownSmem<BITS> sm;
+    constexpr uint32_t PER = (B + 255u) / 256u;
+    __shared__ PassSmem<BITS> sm;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
     for (uint32_t b = threadIdx.x; b < B; b += 256) {
 #pragma unroll
         for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
     }
-    __syncthreads();
-
     const uint32_t tbase = tile * kTile;
     const uint32_t wbase = tbase + w * (kItems * 64u);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
@@ -478,15 +474,17 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
-        const bool valid = e < n;
-        uint32_t k = 0, ix = 0;
-        if (valid) {
-            k = keys_in[e];
-            if (FIRST) { k = bucket_key(k, n_act); ix = e; } else { ix = idx_in[e]; }
+        const uint32_t ec = e < n ? e : n - 1;
+        if (IN == IN_ACT) {
+            key[j] = bucket_key(static_cast<const uint32_t*>(in)[ec], n_act);
+            idx[j] = e;
+        } else {
+            const uint2 v = static_cast<const uint2*>(in)[ec];
+            key[j] = v.x;
+            idx[j] = v.y;
         }
-        key[j] = k;
-        idx[j] = ix;
     }
+    __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
@@ -498,14 +496,12 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
             const uint64_t bb = __ballot((d >> b) & 1u);
             m &= ((d >> b) & 1u) ? bb : ~bb;
         }
-        const uint32_t before = (uint32_t)__popcll(m & lt_mask);
         const uint32_t c = sm.cnt[w][d];
-        rank[j] = c + before;
+        rank[j] = c + (uint32_t)__popcll(m & lt_mask);
         // the highest lane of each equal-digit group advances the wave's count for the next 64
         if (valid && (m >> lane) == 1ull) sm.cnt[w][d] = c + (uint32_t)__popcll(m);
     }
     __syncthreads();
-    // per-bin: wave prefixes (in place) and tile totals; then exclusive scan of totals over bins.
     const uint32_t* orow = tile_off + (size_t)tile * B;
     uint32_t tot[PER];
     uint32_t s = 0;
@@ -524,34 +520,43 @@ __global__ __launch_bounds__(256) void k_radix_down(const uint32_t* __restrict__
         tot[q] = t;
         s += t;
     }
-    for (uint32_t b = threadIdx.x; b < B; b += 256) sm.goff[b] = orow[b];
     uint32_t total;
     uint32_t run = block_excl_scan(s, sm.wsum, total);
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t b = threadIdx.x * PER + q;
-        if (b < B) sm.bin_start[b] = run;
+        if (b < B) {
+#pragma unroll
+            for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][b] += run;
+            sm.delta[b] = orow[b] - run;
+        }
         run += tot[q];
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = wbase + j * 64u + lane;
-        if (e < n) {
+        if (wbase + j * 64u + lane < n) {
             const uint32_t d = (key[j] >> shift) & (B - 1u);
-            const uint32_t lpos = sm.bin_start[d] + sm.cnt[w][d] + rank[j];
+            const uint32_t lpos = sm.cnt[w][d] + rank[j];
             sm.stage_k[lpos] = key[j];
             sm.stage_i[lpos] = idx[j];
         }
     }
     __syncthreads();
     const uint32_t cnt = (n - tbase) < kTile ? (n - tbase) : kTile;
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
-        const uint32_t k = sm.stage_k[i];
-        const uint32_t d = (k >> shift) & (B - 1u);
-        const uint32_t g = sm.goff[d] + (i - sm.bin_start[d]);
-        keys_out[g] = k;
-        idx_out[g] = sm.stage_i[i];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t i = j * 256u + threadIdx.x;
+        if (i < cnt) {
+            const uint32_t k = sm.stage_k[i];
+            const uint32_t g = sm.delta[(k >> shift) & (B - 1u)] + i;
+            if (OUT == OUT_PAIR) {
+                pair_out[g] = make_uint2(k, sm.stage_i[i]);
+            } else {
+                key_out[g] = k;
+                order_out[g] = sm.stage_i[i];
+            }
+        }
     }
 }
 
@@ -783,16 +788,27 @@ __global__ __launch_bounds__(256) void k_part_scatter(const orl_msg_hdr* __restr
         }
     }
     __syncthreads();
+    // header copies: unconditional (clamped) loads in groups of 4 so their latencies overlap
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = wbase + j * 64u + lane;
-        if (e < n) {
-            const uint32_t g = woff[w][dig[j]] + rank[j];
-            const uint4* sp = reinterpret_cast<const uint4*>(in + e);
-            uint4* dp = reinterpret_cast<uint4*>(out + g);
-            dp[0] = sp[0];
-            dp[1] = sp[1];
-            src_index[g] = e;
+    for (uint32_t j0 = 0; j0 < kItems; j0 += 4) {
+        u32x4 h0[4], h1[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t e = wbase + (j0 + u) * 64u + lane;
+            const u32x4* sp = reinterpret_cast<const u32x4*>(in + (e < n ? e : n - 1));
+            h0[u] = __builtin_nontemporal_load(sp);
+            h1[u] = __builtin_nontemporal_load(sp + 1);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t e = wbase + (j0 + u) * 64u + lane;
+            if (e < n) {
+                const uint32_t g = woff[w][dig[j0 + u]] + rank[j0 + u];
+                u32x4* dp = reinterpret_cast<u32x4*>(out + g);
+                dp[0] = h0[u];
+                dp[1] = h1[u];
+                src_index[g] = e;
+            }
         }
     }
 }
@@ -819,18 +835,23 @@ int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
 }
 
 template <int BITS>
-void launch_down_bits(bool first, const uint32_t* kin, const uint32_t* iin, uint32_t n, uint32_t n_act, uint32_t shift,
-                      const uint32_t* toff, uint32_t ntiles, uint32_t* kout, uint32_t* iout, hipStream_t st) {
-    if (first)
-        hipLaunchKernelGGL((k_radix_down<BITS, true>), dim3(ntiles), dim3(256), 0, st, kin, iin, n, n_act, shift, toff, ntiles, kout, iout);
+void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
+                      uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
+    const dim3 g(ntiles), b(256);
+    if (in == IN_ACT && out == OUT_PAIR)
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+    else if (in == IN_ACT)
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+    else if (out == OUT_PAIR)
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
     else
-        hipLaunchKernelGGL((k_radix_down<BITS, false>), dim3(ntiles), dim3(256), 0, st, kin, iin, n, n_act, shift, toff, ntiles, kout, iout);
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
 }
 
-void launch_down(int bits, bool first, const uint32_t* kin, const uint32_t* iin, uint32_t n, uint32_t n_act, uint32_t shift,
-                 const uint32_t* toff, uint32_t ntiles, uint32_t* kout, uint32_t* iout, hipStream_t st) {
+void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
+                 uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     switch (bits) {
-#define ORL_CASE(B) case B: launch_down_bits<B>(first, kin, iin, n, n_act, shift, toff, ntiles, kout, iout, st); break;
+#define ORL_CASE(B) case B: launch_pass_bits<B>(in, out, kin, n, n_act, shift, toff, ntiles, pout, order, keys, st); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -848,24 +869,23 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, const Scratch& s, hip
 }
 
 // Stage 4 after a route kernel that already wrote the first digit's tile histogram into s.tile_hist.
+// Passes: act → pairs_a → pairs_b → ... → (order, sorted keys); then bucket offsets from the sorted keys.
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets,
                        const Scratch& s, hipStream_t st) {
     const RadixPlan plan = make_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
+    uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
-        if (p > 0) {
-            const uint32_t* kin = ((plan.passes - p) % 2 == 0) ? s.sorted_keys : s.keys_a;  // output of pass p-1
-            hipLaunchKernelGGL(k_radix_up, dim3(ntiles), dim3(256), 0, st, kin, n, (uint32_t)plan.shift[p], bins, s.tile_hist);
-        }
+        if (p > 0)
+            hipLaunchKernelGGL(k_hist_pairs, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, (uint32_t)plan.shift[p], bins,
+                               s.tile_hist);
         col_scan(s.tile_hist, ntiles, bins, s, st);
-        const bool to_final = ((plan.passes - 1 - p) % 2) == 0;
-        uint32_t* kout = to_final ? s.sorted_keys : s.keys_a;
-        uint32_t* iout = to_final ? d_order : s.idx_a;
-        const uint32_t* kin = (p == 0) ? d_act : (to_final ? s.keys_a : s.sorted_keys);
-        const uint32_t* iin = (p == 0) ? nullptr : (to_final ? s.idx_a : d_order);
-        launch_down(plan.bits[p], p == 0, kin, iin, n, n_act, (uint32_t)plan.shift[p], s.tile_hist, ntiles, kout, iout, st);
+        const bool last = p == plan.passes - 1;
+        const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
+        launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
+                    s.tile_hist, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
     hipLaunchKernelGGL(k_offsets, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
     return (int)hipGetLastError();
@@ -942,7 +962,6 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
                            nullptr, ntiles, 1u, 0u);
     e = (int)hipGetLastError();
     if (e || !buckets) return e;
-    // poff32 lives in s.idx_a, which the radix passes reuse: it is dead once the route kernel has run.
     return bucket_after_route(d_act, total, n_act, d_order, d_offsets, s, st);
 }
 
