@@ -8,7 +8,7 @@
 //   k_radix_pass     stage 4: stable LSD radix partition by activation handle = per-activation FIFO
 //                    (ActivationData.EnqueueMessage, ActivationData.cs:483-514); k_hist_pairs + k_col_* give
 //                    each (tile, digit) its global output base.
-//   k_offsets        per-activation bucket offsets from the sorted keys.
+//   k_offsets_*      per-activation bucket offsets from the sorted keys.
 //   k_fanout_*       stage 5: CSR multicast expansion (ChirperAccount.cs:154-157) feeding stages 1-4.
 //   k_part_*         stable partition of headers by destination rank (exchange).
 //
@@ -571,30 +571,40 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__
     return lo;
 }
 
-__global__ __launch_bounds__(256) void k_offsets(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
-                                                 uint32_t* __restrict__ offsets) {
-    __shared__ uint32_t bounds[2];
-    const uint32_t b0 = blockIdx.x * 256u;
-    const uint32_t b1 = (b0 + 256u < nb) ? b0 + 256u : nb;
-    if (threadIdx.x == 0) bounds[0] = lower_bound_u32(sorted, n, b0);
-    if (threadIdx.x == 64) bounds[1] = lower_bound_u32(sorted, n, b1);
-    __syncthreads();
-    const uint32_t p0 = bounds[0], p1 = bounds[1];
-    if (threadIdx.x == 0) {
-        offsets[b0] = p0;
-        // empty buckets before the first key of the slice start where that key does
-        if (p1 > p0)
-            for (uint32_t b = b0 + 1, k0 = sorted[p0]; b <= k0; ++b) offsets[b] = p0;
+// Bucket offsets in two steps over an offsets array pre-filled with kNoOffset:
+//   k_offsets_mark: one streaming read of the sorted keys; every position i whose key differs from key[i-1]
+//                   starts bucket key[i] (16 keys per thread, 4 x 16-B loads);
+//   k_offsets_fill: empty buckets (still kNoOffset) get lower_bound(sorted, b): where the next key starts.
+constexpr uint32_t kNoOffset = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict__ sorted, uint32_t n,
+                                                      uint32_t* __restrict__ offsets) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u;
+    if (i0 >= n) return;
+    uint32_t k[16];
+    if (i0 + 16 <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(sorted + i0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[q];
+            k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) k[q] = (i0 + q < n) ? sorted[i0 + q] : k[q > 0 ? q - 1 : 0];
     }
-    for (uint32_t i = p0 + 1 + threadIdx.x; i < p1; i += 256) {
-        const uint32_t k = sorted[i], kp = sorted[i - 1];
-        for (uint32_t b = kp + 1; b <= k; ++b) offsets[b] = i;  // buckets (kp, k] start at i
+    uint32_t prev = i0 ? sorted[i0 - 1] : kNoOffset;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        if (i0 + q < n && k[q] != prev) offsets[k[q]] = (uint32_t)(i0 + q);
+        prev = k[q];
     }
-    // buckets after the last key in [b0, b1) start at p1
-    if (threadIdx.x == 0) {
-        const uint32_t from = (p1 > p0) ? sorted[p1 - 1] + 1 : b0 + 1;
-        for (uint32_t b = from; b < b1; ++b) offsets[b] = p1;
-    }
+}
+
+__global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
+                                                      uint32_t* __restrict__ offsets) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b < nb && offsets[b] == kNoOffset) offsets[b] = lower_bound_u32(sorted, n, b);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -887,7 +897,10 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
                     s.tile_hist, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
-    hipLaunchKernelGGL(k_offsets, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
+    const hipError_t me = hipMemsetD32Async((hipDeviceptr_t)d_offsets, kNoOffset, nb, st);
+    if (me != hipSuccess) return (int)me;
+    hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, d_offsets);
+    hipLaunchKernelGGL(k_offsets_fill, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
     return (int)hipGetLastError();
 }
 

@@ -24,4 +24,5 @@ for grp in "${GRPS[@]}"; do
   case $rc in 124|134|137|139) exit $rc;; esac
 done
 python3 scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt
+[ -z "$PMC_GROUPS" ] && python3 scripts/make_traffic_json.py $OUT ${MSGS:-67108864} $OUT/route_kernel_pmc.json
 echo "=== done"

@@ -310,7 +310,9 @@ int main() {
 #undef LAB
                 shift += bits[p];
             }
-            hipLaunchKernelGGL(k_offsets, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs);
+            { (void)hipMemsetD32Async((hipDeviceptr_t)offs, kNoOffset, n_act + 2, st);
+              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, offs);
+              hipLaunchKernelGGL(k_offsets_fill, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs); }
         };
         timeit("pipeline 10+10 (AoS mid) excl. hist0", 28.0 * n, [&] {
             hipLaunchKernelGGL(k_lab_hist<16>, dim3(nt), dim3(256), 0, st, keys, n, 0u, 1024u, hist);
@@ -325,7 +327,9 @@ int main() {
             pipeline({8, 8, 4});
         });
         timeit("k_offsets", 4.0 * n, [&] {
-            hipLaunchKernelGGL(k_offsets, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs);
+            { (void)hipMemsetD32Async((hipDeviceptr_t)offs, kNoOffset, n_act + 2, st);
+              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, offs);
+              hipLaunchKernelGGL(k_offsets_fill, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs); }
         });
         prep(10, 4096);
         timeit("prod k_radix_pass<10,act,pair> again", 12.0 * n, [&] {
