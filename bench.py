@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — routed grain messages/sec on MI355X (BASELINE.json metric), one process per GPU.
 
-Workload (BASELINE.json configs[1]): 8 logical silos 10.0.0.{1..8}:11111 gen 1,
+Default workload (BASELINE.json configs[1]): 8 logical silos 10.0.0.{1..8}:11111 gen 1,
 1M ChirperAccount long-key grains all registered (activation on the directory owner), 64M single-target
 messages per GPU per step, targets Uniform[0,1M) (splitmix64 seed 0x5EED0002), resident in HBM before the
 timed region.  A step = one pass of the hot path over the batch: stages 1-4 (hash, ring owner, directory
@@ -9,7 +9,14 @@ probe + placement, stable per-activation bucketing).  With N GPUs (torchrun), ea
 s*N//8 == rank, holds their directory partition, originates 64M messages from its own silos (weak
 scaling) and the step adds the owner partition + RCCL all-to-all exchange.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Other SURVEY §8(d) workloads (measurement legs, recorded under profiles/; not the driver's bench line):
+  --config 3   Zipf(1.1) over 16M grains (seeded permutation), 64M messages per GPU, stages 1-4
+  --config 4   Chirper-scale CSR: 10M accounts, power-law followers (exp 2.1, 1..1e5), 1M publishers per
+               step → fan-out + stages 1-4 (1 GPU)
+  --config 5   Presence: 100k Guid-keyed games x 8 players, 64k heartbeats per step = 64k game messages +
+               512k player messages (fan-out), per-step latency p50/p99, eager and hipGraph-replayed (1 GPU)
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
        python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 """
 from __future__ import annotations
@@ -28,6 +35,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 ROUTE_KERNEL_BYTES_PER_MSG = 72  # 32 B header + 32 B directory slot + 4 B route word + 4 B activation handle
 PIPELINE_BYTES_PER_MSG = 76      # + 4 B stable position
+FANOUT_BYTES_PER_MSG = 48        # 4 B CSR target + 32 B slot + 12 B outputs per emitted message
+FANOUT_BYTES_PER_PUB = 40        # + 32 B header + 8 B CSR offset per publish
 
 
 def log(*a):
@@ -39,8 +48,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--grains", type=int, default=1_000_000)
-    ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--grains", type=int, default=None)
+    ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "route_kernel_pmc.json"))
@@ -58,17 +68,72 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.config in (4, 5):
+            raise SystemExit("--config 4/5 are single-GPU measurement legs")
 
-    from orleans_amd import _lib as L
+    if args.config in (2, 3):
+        res = run_single_target(args, torch, dist, rank, world, local_rank)
+    elif args.config == 4:
+        res = run_fanout(args, torch)
+    else:
+        res = run_presence(args, torch)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def timed_steps(args, torch, dist, world, step, sync):
+    """W untimed warmup steps, then exactly K steps between barrier + synchronize; max over ranks."""
+    for _ in range(args.warmup):
+        step()
+    sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    units = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        units += step()
+    sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed, units
+
+
+def read_traffic(path, msgs_per_launch, world):
+    if world != 1 or not os.path.exists(path):
+        return None
+    try:
+        tj = json.load(open(path))
+        if tj.get("msgs_per_launch") == msgs_per_launch:
+            return tj.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+# ---- configs 2 and 3: single-target messages ---------------------------------------------------------------
+def run_single_target(args, torch, dist, rank, world, local_rank):
     from orleans_amd import workloads as W
     from orleans_amd.engine import GrainDirectoryEngine
     from orleans_amd.node import HipExecutor, ShardedRouter, local_silos, rank_of_silo
 
-    n_grains, n_msgs = args.grains, args.msgs
+    zipf = args.config == 3
+    n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
+    n_msgs = args.msgs
     cl = W.default_cluster()
     ros = rank_of_silo(cl.n_silos, world)
     mine = local_silos(cl.n_silos, world, rank)
-    cap = n_msgs if world == 1 else int(n_msgs * 1.25)
+    cap = n_msgs if world == 1 else int(n_msgs * (2.0 if zipf else 1.25))
     t_setup = time.perf_counter()
     eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=cap, device=local_rank)
     W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
@@ -78,9 +143,10 @@ def main():
         local_mask = np.zeros(cl.n_silos, np.uint8)
         local_mask[mine] = 1
     n_reg = W.register_population(eng, keys, owner, reg, local_mask)
-    log(f"rank {rank}/{world}: silos {list(mine)}, {n_reg} grains registered; generating {n_msgs} messages")
-    msgs = W.uniform_messages(cl, n_grains, n_msgs, seed=W.SEED_C2, start=rank * n_msgs,
-                              sender_silos=mine if world > 1 else None)
+    log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered; generating {n_msgs} messages")
+    gen = W.zipf_messages if zipf else W.uniform_messages
+    seed = W.SEED_C3 if zipf else W.SEED_C2
+    msgs = gen(cl, n_grains, n_msgs, seed=seed, start=rank * n_msgs, sender_silos=mine if world > 1 else None)
     d_msgs = torch.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -99,29 +165,18 @@ def main():
         def step():
             return router.step(d_msgs, n_msgs).n_recv
     log(f"setup {time.perf_counter() - t_setup:.1f}s; warmup {args.warmup}")
+    eng.set_timing(False)
 
+    def sync():
+        eng.sync()
+
+    # timing events are enabled after warmup so the summary covers the timed steps only
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     eng.set_timing(True)
-    recv_total = 0
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        recv_total += step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    args_w = argparse.Namespace(**{**vars(args), "warmup": 0})
+    elapsed, recv_total = timed_steps(args_w, torch, dist, world, step, sync)
     nb, route_ms, bucket_ms, total_ms = eng.timing_summary()
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n_msgs * args.steps / elapsed
@@ -129,54 +184,40 @@ def main():
     achieved = ROUTE_KERNEL_BYTES_PER_MSG * per_launch_msgs / (route_ms * 1e-3) / 1e9
     log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms, bucketing {bucket_ms:.3f} ms, "
         f"call {total_ms:.3f} ms over {nb} batches")
-
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("msgs_per_launch") == per_launch_msgs and world == 1:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    traffic = read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cl, keys, owner, msgs, n_grains, args.cpu_wall)
-
-    if world > 1:
-        dist.barrier()
-    if rank == 0:
-        line = {
-            "metric": "routed grain messages/sec (node)",
-            "value": value,
-            "unit": "messages/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32/u64 integer",
-            "data": "synthetic (seeded splitmix64; config 2 of BASELINE.json)",
-            "config": {"workload": "config2: uniform 1M long-key grains, 64M single-target messages per GPU, "
-                                   "8-silo ring, stages 1-4" + (", + owner partition + RCCL all-to-all" if world > 1 else ""),
-                       "grains": n_grains, "messages_per_gpu": n_msgs, "silos": cl.n_silos,
-                       "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_msg": ROUTE_KERNEL_BYTES_PER_MSG, "msgs_per_launch": per_launch_msgs,
-                         "avg_launch_ms": route_ms},
-            "pipeline": {"bytes_per_msg": PIPELINE_BYTES_PER_MSG, "route_kernel_ms": route_ms,
-                         "bucketing_ms": bucket_ms, "call_ms": total_ms,
-                         "algorithmic_GBs": PIPELINE_BYTES_PER_MSG * value / world / 1e9,
-                         "frac_of_hbm_peak": PIPELINE_BYTES_PER_MSG * value / world / 1e9 / HBM_PEAK_GBS},
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
     eng.close()
+    name = ("config3: Zipf(1.1) over 16M long-key grains" if zipf else
+            "config2: uniform 1M long-key grains") + f", {n_msgs >> 20}M single-target messages per GPU, 8-silo ring, stages 1-4"
+    if world > 1:
+        name += ", + owner partition + RCCL all-to-all"
+    return {
+        "metric": "routed grain messages/sec (node)",
+        "value": value,
+        "unit": "messages/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/u64 integer",
+        "data": f"synthetic (seeded splitmix64; config {args.config} of SURVEY §8(d))",
+        "config": {"workload": name, "grains": n_grains, "messages_per_gpu": n_msgs, "silos": cl.n_silos,
+                   "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_msg": ROUTE_KERNEL_BYTES_PER_MSG, "msgs_per_launch": per_launch_msgs,
+                     "avg_launch_ms": route_ms},
+        "pipeline": {"bytes_per_msg": PIPELINE_BYTES_PER_MSG, "route_kernel_ms": route_ms,
+                     "bucketing_ms": bucket_ms, "call_ms": total_ms,
+                     "algorithmic_GBs": PIPELINE_BYTES_PER_MSG * value / world / 1e9,
+                     "frac_of_hbm_peak": PIPELINE_BYTES_PER_MSG * value / world / 1e9 / HBM_PEAK_GBS},
+        "cpu_baseline": cpu,
+    }
 
 
 def cpu_baseline(cl, keys, owner, msgs, n_grains, target_wall):
@@ -200,8 +241,196 @@ def cpu_baseline(cl, keys, owner, msgs, n_grains, target_wall):
     wall = time.perf_counter() - t0
     log(f"cpu baseline: {n} messages in {wall:.2f}s on {threads} threads")
     return {"value": n / wall, "unit": "messages/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of the {len(msgs)} config-2 messages (same directory, stages 1-4), "
+            "sample": f"first {n} of the {len(msgs)} messages of this workload (same directory, stages 1-4), "
                       f"oracle/cpu_ref.cpp ref_route_bucket_mt, {wall:.2f}s wall"}
+
+
+# ---- config 4: CSR multicast fan-out ---------------------------------------------------------------------
+def run_fanout(args, torch):
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine, grain_keys_from_longs
+
+    n_acc = args.grains or 10_000_000
+    n_pub = 1_000_000
+    cl = W.default_cluster()
+    t_setup = time.perf_counter()
+    csr_off, csr_tgt = W.powerlaw_csr(n_acc)
+    keys = grain_keys_from_longs(cl.type_code, np.arange(n_acc, dtype=np.int64))
+    owner = cl.owner_of(W.jenkins3_np(keys["tcd"], keys["n0"], keys["n1"]))
+    # publishers per step: 1M uniformly random accounts (a fresh sample each step, pre-generated)
+    n_sets = max(1, min(4, args.steps + args.warmup))
+    pub_sets = [(W.stream(W.SEED_C4 ^ 0xB0B, i * n_pub, n_pub) % np.uint64(n_acc)).astype(np.uint32)
+                for i in range(n_sets)]
+    deg = np.diff(csr_off.astype(np.int64))
+    totals = [int(deg[p].sum()) for p in pub_sets]
+    cap = max(totals) + 1
+    eng = GrainDirectoryEngine(n_act=n_acc, dir_capacity=n_acc, max_batch=cap, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, keys, owner, np.ones(n_acc, bool))
+    log(f"config 4: {n_acc} accounts, {len(csr_tgt)} edges, {n_pub} publishers/step, emitted {totals}")
+    dev = "cuda"
+    d_off = torch.from_numpy(csr_off.view(np.int64)).to(dev)
+    d_tgt = torch.from_numpy(csr_tgt.view(np.int32)).to(dev)
+    d_pubs = [torch.from_numpy(p.view(np.int32)).to(dev) for p in pub_sets]
+    d_psilo = [torch.from_numpy(owner[p]).to(dev) for p in pub_sets]
+    poff = torch.empty(n_pub + 1, dtype=torch.int64, device=dev)
+    route = torch.empty(cap, dtype=torch.int32, device=dev)
+    act = torch.empty(cap, dtype=torch.int32, device=dev)
+    order = torch.empty(cap, dtype=torch.int32, device=dev)
+    offs = torch.empty(n_acc + 2, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    k = [0]
+    tcd = (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+
+    def step():
+        i = k[0] % n_sets
+        k[0] += 1
+        return eng.fanout_device(d_off, d_tgt, d_pubs[i], d_psilo[i], n_pub, tcd, poff, route, act, order, offs,
+                                 stream=stream, total=totals[i])
+    log(f"setup {time.perf_counter() - t_setup:.1f}s")
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.set_timing(True)
+    args_w = argparse.Namespace(**{**vars(args), "warmup": 0})
+    elapsed, emitted = timed_steps(args_w, torch, None, 1, step, eng.sync)
+    nb, route_ms, bucket_ms, total_ms = eng.timing_summary()
+    eng.close()
+    per_step = emitted / args.steps
+    bytes_launch = FANOUT_BYTES_PER_MSG * per_step + FANOUT_BYTES_PER_PUB * n_pub
+    achieved = bytes_launch / (route_ms * 1e-3) / 1e9
+    log(f"config 4: {elapsed * 1e3 / args.steps:.3f} ms/step, fan-out route kernel {route_ms:.3f} ms, "
+        f"bucketing {bucket_ms:.3f} ms")
+    return {"metric": "routed grain messages/sec (node)", "value": emitted / elapsed, "unit": "messages/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64 integer",
+            "data": "synthetic (seeded power-law CSR; config 4 of SURVEY §8(d))",
+            "config": {"workload": f"config4: {n_acc} accounts, power-law followers (exp 2.1, 1..1e5), "
+                                   f"{n_pub} publishers per step, fan-out + stages 1-4",
+                       "edges": int(len(csr_tgt)), "emitted_per_step": per_step},
+            "roofline": {"bound": "hbm", "kernel": "k_fanout_route (stage 5 + 1-3)", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_msg": FANOUT_BYTES_PER_MSG, "bytes_per_publish": FANOUT_BYTES_PER_PUB,
+                         "avg_launch_ms": route_ms},
+            "pipeline": {"route_kernel_ms": route_ms, "bucketing_ms": bucket_ms, "call_ms": total_ms},
+            "cpu_baseline": None}
+
+
+# ---- config 5: Presence heartbeats, small batches, hipGraph --------------------------------------------
+def run_presence(args, torch):
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+
+    n_games, per_game, n_hb = 100_000, 8, 64 * 1024
+    log("config 5: building population")
+    cl = W.default_cluster()
+    pr = W.presence_population(n_games, per_game)
+    n_keys = n_games * (1 + per_game)
+    all_keys = np.concatenate([pr.game_keys, pr.player_keys])
+    owner = cl.owner_of(W.jenkins3_np(all_keys["tcd"], all_keys["n0"], all_keys["n1"]))
+    n_fan = n_hb * per_game
+    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, all_keys, owner, np.ones(n_keys, bool))
+    n_sets = 8
+    batches = [W.heartbeat_batch(pr, cl, n_hb, b) for b in range(n_sets)]
+    dev = "cuda"
+    d_msgs = [torch.from_numpy(m.view(np.int32).reshape(-1, 8)).to(dev) for _, m in batches]
+    d_games = [torch.from_numpy(g.view(np.int32)).to(dev) for g, _ in batches]
+    d_gsilo = [torch.from_numpy(owner[g.astype(np.int64)]).to(dev) for g, _ in batches]
+    d_off = torch.from_numpy(pr.csr_off.view(np.int64)).to(dev)
+    d_tgt = torch.from_numpy(pr.csr_tgt.view(np.int32)).to(dev)
+    d_pkeys = torch.from_numpy(pr.player_keys.view(np.uint8).reshape(-1, 24)).to(dev)
+    o1 = [torch.empty(n_hb, dtype=torch.int32, device=dev) for _ in range(3)]
+    o2 = [torch.empty(n_fan, dtype=torch.int32, device=dev) for _ in range(3)]
+    off1 = torch.empty(n_keys + 2, dtype=torch.int32, device=dev)
+    off2 = torch.empty(n_keys + 2, dtype=torch.int32, device=dev)
+    poff = torch.empty(n_hb + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream()
+    sp = s.cuda_stream
+
+    def one(i):
+        # 1 game message per heartbeat (PresenceGrain.Heartbeat → GameGrain.UpdateGameStatus) ...
+        eng.address_messages_device(d_msgs[i], n_hb, o1[0], o1[1], o1[2], off1, stream=sp)
+        # ... + the 8-way player fan-out (GameGrain.UpdateGameStatus → PlayerGrain.JoinGame/LeaveGame)
+        eng.fanout_keys_device(d_off, d_tgt, d_pkeys, d_games[i], d_gsilo[i], n_hb, poff, o2[0], o2[1], o2[2], off2,
+                               stream=sp, total=n_fan)
+
+    per_step = n_hb + n_fan
+    log("config 5: warmup")
+    with torch.cuda.stream(s):
+        for i in range(max(2, args.warmup)):
+            one(i % n_sets)
+    s.synchronize()
+
+    # every launch and every graph replay goes to stream s (CUDAGraph.replay() runs on the current stream)
+    def lat_run(fn, steps):
+        lat = []
+        with torch.cuda.stream(s):
+            for i in range(steps):
+                t0 = time.perf_counter()
+                fn(i)
+                s.synchronize()
+                lat.append((time.perf_counter() - t0) * 1e3)
+        return np.array(lat)
+
+    def thr_run(fn, steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            for i in range(steps):
+                fn(i)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    steps = max(args.steps, 20)
+    lat_eager = lat_run(lambda i: one(i % n_sets), steps)
+    thr_eager = thr_run(lambda i: one(i % n_sets), steps)
+    # hipGraph: capture one batch per heartbeat set, replay
+    log("config 5: eager done, capturing graphs")
+    graphs = []
+    for i in range(n_sets):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            one(i)
+        graphs.append(g)
+    s.synchronize()
+    # the replayed graphs must produce the eager call's words (guards against an empty or stale capture)
+    outs = o1 + o2 + [off1, off2]
+    for i in range(n_sets):
+        for x in outs:
+            x.fill_(-1)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            graphs[i].replay()
+        s.synchronize()
+        rep = [x.clone() for x in outs]
+        with torch.cuda.stream(s):
+            one(i)
+        s.synchronize()
+        if not all(bool(torch.equal(a, b)) for a, b in zip(rep, outs)):
+            raise RuntimeError(f"graph replay of heartbeat batch {i} differs from the eager call")
+    log("config 5: graphs verified")
+    lat_graph = lat_run(lambda i: graphs[i % n_sets].replay(), steps)
+    thr_graph = thr_run(lambda i: graphs[i % n_sets].replay(), steps)
+    eng.close()
+    value = per_step * steps / thr_graph
+    log(f"config 5: eager {thr_eager * 1e3 / steps:.3f} ms/step (p50 {np.percentile(lat_eager, 50):.3f}, "
+        f"p99 {np.percentile(lat_eager, 99):.3f} ms); graph {thr_graph * 1e3 / steps:.3f} ms/step "
+        f"(p50 {np.percentile(lat_graph, 50):.3f}, p99 {np.percentile(lat_graph, 99):.3f} ms)")
+    return {"metric": "routed grain messages/sec (node)", "value": value, "unit": "messages/s", "n_gpus": 1,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": thr_graph * 1e3 / steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64 integer",
+            "data": "synthetic (seeded Guids; config 5 of SURVEY §8(d))",
+            "config": {"workload": f"config5: {n_games} Guid-keyed games x {per_game} players, {n_hb} heartbeats per "
+                                   f"step = {n_hb} game + {n_fan} player messages, stages 1-5, hipGraph replay",
+                       "messages_per_step": per_step},
+            "latency_ms": {"eager_p50": float(np.percentile(lat_eager, 50)),
+                           "eager_p99": float(np.percentile(lat_eager, 99)),
+                           "graph_p50": float(np.percentile(lat_graph, 50)),
+                           "graph_p99": float(np.percentile(lat_graph, 99))},
+            "throughput_msgs_per_s": {"eager": per_step * steps / thr_eager, "graph": value},
+            "roofline": None, "cpu_baseline": None}
 
 
 if __name__ == "__main__":

@@ -112,6 +112,8 @@ typedef struct orl_msg_hdr {
 /* Route options (bit set) */
 #define ORL_OPT_EXCLUDE_IF_STOPPING 0x1u /* CalculateTargetSilo(grain, excludeThisSiloIfStopping=true) */
 #define ORL_OPT_NO_BUCKETS 0x2u          /* skip stage 4 (order/offsets not written) */
+#define ORL_OPT_TOTAL_GIVEN 0x4u         /* fan-out: *n_out holds the exact emitted count on entry (no stream sync,
+                                            so the call can be captured in a hipGraph) */
 
 /* Directory insert outcome (orl_dir_insert_single status[]) */
 #define ORL_INS_INSERTED 0u
@@ -195,11 +197,21 @@ int orl_route_batch_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint
  * one send per follower csr_tgt[csr_off[pubs[p]] .. csr_off[pubs[p]+1]) in CSR order; follower grain =
  * GrainId(follower_tcd, long id) = key {follower_tcd, 0, id}.  Output message j (publisher-major) is
  * routed as in orl_route_batch_device; pub_offsets[n_pub+1] (device) maps publishes to output ranges.
- * *n_out (host) receives the number of emitted messages (this call synchronises `stream` once to read it). */
+ * *n_out (host) receives the number of emitted messages (this call synchronises `stream` once to read it,
+ * unless opts has ORL_OPT_TOTAL_GIVEN and *n_out already holds that count).
+ * Reference: ChirperAccount.PublishMessage fan-out loop (Samples/Chirper/ChirperGrains/ChirperAccount.cs:154-157),
+ * ObserverSubscriptionManager.Notify (src/Orleans/Async/ObserverSubscriptionManager.cs:111-139). */
 int orl_fanout_route_device(orl_ctx* ctx, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
                             const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
                             uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                             uint32_t* d_order, uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
+/* As orl_fanout_route_device, with followers named by a device key table: follower of CSR entry j is
+ * d_follower_keys[csr_tgt[j]] (any GrainId, e.g. the Guid-keyed players of Samples/Presence
+ * GameGrain.UpdateGameStatus, Samples/Presence/PresenceGrains/GameGrain.cs:62-113). */
+int orl_fanout_route_keys_device(orl_ctx* ctx, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                                 const orl_grain_key* d_follower_keys, const uint32_t* d_pubs, const uint8_t* d_pub_silo,
+                                 size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
+                                 uint32_t* d_order, uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
 
 /* ---- multi-GPU exchange support --------------------------------------------
  * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is
@@ -213,7 +225,7 @@ int orl_partition_by_owner_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t 
 int orl_sync(orl_ctx* ctx);
 
 /* ---- introspection for benchmarks / profiling ------------------------------------------------ */
-/* With timing enabled, every orl_route_batch_device brackets its route kernel (stages 1-3), its bucketing
+/* With timing enabled, every orl_route_batch_device / orl_fanout_route*_device brackets its route kernel (stages 1-3), its bucketing
  * kernels (stage 4) and the whole call with HIP events on the submission stream (no host sync per batch;
  * up to ORL_TIMING_SLOTS batches are kept).  orl_set_timing(ctx, 1) clears the record.
  * orl_timing_summary waits for the last recorded batch and returns the per-batch averages in ms. */

@@ -45,6 +45,7 @@ POLICY_HASH_SPREAD = 1
 
 OPT_EXCLUDE_IF_STOPPING = 0x1
 OPT_NO_BUCKETS = 0x2
+OPT_TOTAL_GIVEN = 0x4
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -85,6 +86,8 @@ _SIGS = {
     "orl_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
     "orl_fanout_route_device": (C.c_int, [_P, _P, _P, _P, _P, C.c_size_t, C.c_uint64, C.c_uint32, _P, _P, _P, _P, _P,
                                           C.POINTER(C.c_uint64), _P]),
+    "orl_fanout_route_keys_device": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P,
+                                               C.POINTER(C.c_uint64), _P]),
     "orl_partition_by_owner_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P, _P, _P,
                                                 _P]),
     "orl_sync": (C.c_int, [_P]),

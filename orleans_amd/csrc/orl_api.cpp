@@ -367,7 +367,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         const uint64_t tiles = (mb + kTile - 1) / kTile;
         c->s.max_batch = mb;
         c->s.max_tiles = tiles;
-        const uint64_t hist_words = (1ull << kMaxDigitBits) * tiles;
+        // histogram rows: one per 4096-element radix tile, or one per route workgroup for small batches (route
+        // tiles shrink to 256 messages while a batch has < 2048 x 256 x 2 messages: at most 4096 rows)
+        const uint64_t rows = std::max<uint64_t>(tiles, std::min<uint64_t>(4096, (mb + 255) / 256));
+        const uint64_t hist_words = (1ull << kMaxDigitBits) * rows;
         if ((e = hipMalloc((void**)&c->s.pairs_a, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_a)");
         if ((e = hipMalloc((void**)&c->s.pairs_b, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_b)");
         if ((e = hipMalloc((void**)&c->s.idx_a, (mb + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(idx)");
@@ -375,7 +378,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.tile_hist, hist_words * 4)) != hipSuccess) return bail(e, "hipMalloc(tile_hist)");
         if ((e = hipMalloc((void**)&c->s.scan_sums, ((hist_words + 4095) / 4096 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(scan)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
-        if ((e = hipMalloc((void**)&c->s.col_sums, ((tiles + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
+        if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
             return bail(e, "hipMalloc(col_sums)");
         if ((e = hipMalloc((void**)&c->s.col_tot, (1ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMalloc(col_tot)");
         if ((e = hipMalloc((void**)&c->st_off, ((size_t)cfg->n_act + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(offsets)");
@@ -619,25 +622,56 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
     return ORL_OK;
 }
 
-int orl_fanout_route_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const uint32_t* d_pubs,
-                            const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
-                            uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
-                            uint32_t* d_off, uint64_t* n_out, void* stream) {
+namespace {
+int fanout_impl(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_keys,
+                const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order, uint32_t* d_off,
+                uint64_t* n_out, void* stream) {
     if (!c || !n_out) return ORL_E_INVALID;
     if (!d_csr_off || !d_csr_tgt || !d_pub_offsets || !d_route || !d_act) return fail(c, ORL_E_INVALID, "null device buffer");
     if (n_pub && (!d_pubs || !d_pub_silo)) return fail(c, ORL_E_INVALID, "null publisher buffer");
     if (!(opts & ORL_OPT_NO_BUCKETS) && (!d_order || !d_off)) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
     if (n_pub + 1 > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "too many publishers");
+    if ((opts & ORL_OPT_TOTAL_GIVEN) && *n_out > c->s.max_batch)
+        return fail(c, ORL_E_CAPACITY, "given fan-out total %llu > max_batch", (unsigned long long)*n_out);
     if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
     int r = sync_device_state(c);
     if (r) return r;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    int e = launch_fanout_route_bucket(c->d_params, c->d_table, c->mask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, n_pub,
+    hipEvent_t* ev = nullptr;
+    if (c->timing && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
+    if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
+    int e = launch_fanout_route_bucket(c->d_params, c->d_table, c->mask, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub,
                                        follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
-                                       c->s.max_batch, c->s, st);
+                                       c->s.max_batch, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > max_batch", (unsigned long long)*n_out);
     if (e) return hipfail(c, (hipError_t)e, "fanout launch");
+    if (ev) {
+        if (*n_out == 0) {  // no route kernel ran: mark it empty
+            ORL_HIP(c, hipEventRecord(ev[1], st));
+            ORL_HIP(c, hipEventRecord(ev[2], st));
+        }
+        ORL_HIP(c, hipEventRecord(ev[3], st));
+    }
     return ORL_OK;
+}
+}  // namespace
+
+int orl_fanout_route_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const uint32_t* d_pubs,
+                            const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                            uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                            uint32_t* d_off, uint64_t* n_out, void* stream) {
+    return fanout_impl(c, d_csr_off, d_csr_tgt, nullptr, d_pubs, d_pub_silo, n_pub, follower_tcd, opts, d_pub_offsets, d_route,
+                       d_act, d_order, d_off, n_out, stream);
+}
+
+int orl_fanout_route_keys_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                                 const orl_grain_key* d_keys, const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub,
+                                 uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                                 uint32_t* d_off, uint64_t* n_out, void* stream) {
+    if (c && !d_keys) return fail(c, ORL_E_INVALID, "null follower key table");
+    return fanout_impl(c, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub, 0, opts, d_pub_offsets, d_route, d_act,
+                       d_order, d_off, n_out, stream);
 }
 
 int orl_partition_by_owner_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,

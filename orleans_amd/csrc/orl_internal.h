@@ -138,11 +138,11 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
                         void* ev_route_begin, void* ev_route_end);
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
-                               const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const uint32_t* d_pubs,
-                               const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
-                               uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
+                               const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
+                               const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
+                               uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out,
-                               const Scratch& s, void* stream);
+                               const Scratch& s, void* stream, void* ev_route_begin, void* ev_route_end);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          uint64_t mask, const orl_msg_hdr* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
-                                                         uint32_t bins, uint32_t shift) {
+                                                         uint32_t bins, uint32_t shift, uint32_t items) {
     __shared__ RouteSmem sm;
     stage_params(&sm.P, gp);
     if (HIST)
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     __syncthreads();
     const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
     const uint32_t n_act = sm.P.n_act;
-    const uint32_t base = blockIdx.x * kTile + threadIdx.x;
-    for (uint32_t j = 0; j < kItems; ++j) {
+    const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
+    for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
         Msg m;
         if (e < n) m = load_hdr(in, e);
@@ -455,7 +455,7 @@ struct PassSmem {
 
 template <int BITS, int IN, int OUT>
 __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
-                                                    const uint32_t* __restrict__ tile_off, uint32_t ntiles,
+                                                    const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out) {
     constexpr uint32_t B = 1u << BITS;
@@ -550,6 +550,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         if (i < cnt) {
             const uint32_t k = sm.stage_k[i];
             const uint32_t g = sm.delta[(k >> shift) & (B - 1u)] + i;
+            if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = make_uint2(k, sm.stage_i[i]);
             } else {
@@ -577,7 +578,12 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__
 //   k_offsets_fill: empty buckets (still kNoOffset) get lower_bound(sorted, b): where the next key starts.
 constexpr uint32_t kNoOffset = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict__ sorted, uint32_t n,
+__global__ __launch_bounds__(256) void k_fill_u32(uint32_t* __restrict__ a, uint32_t m, uint32_t v) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < m) a[i] = v;
+}
+
+__global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
                                                       uint32_t* __restrict__ offsets) {
     const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u;
     if (i0 >= n) return;
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict
     uint32_t prev = i0 ? sorted[i0 - 1] : kNoOffset;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        if (i0 + q < n && k[q] != prev) offsets[k[q]] = (uint32_t)(i0 + q);
+        if (i0 + q < n && k[q] != prev && k[q] < nb) offsets[k[q]] = (uint32_t)(i0 + q);
         prev = k[q];
     }
 }
@@ -641,14 +647,15 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask,
     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
-    uint32_t n, uint32_t excl, uint32_t* __restrict__ route, uint32_t* __restrict__ act_out,
-    uint32_t* __restrict__ tile_hist, uint32_t ntiles, uint32_t bins, uint32_t shift) {
+    const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
+    uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist, uint32_t bins, uint32_t shift, uint32_t items) {
     __shared__ FanSmem sm;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
-    const uint32_t base = blockIdx.x * kTile;
-    const uint32_t last = ((n - base) < kTile ? n : base + kTile) - 1;
+    const uint32_t rtile = kRouteThreads * items;
+    const uint32_t base = blockIdx.x * rtile;
+    const uint32_t last = ((n - base) < rtile ? n : base + rtile) - 1;
     // publisher of emitted message e = upper_bound(poff32[0..n_pub], e) - 1
     if (threadIdx.x == 0 || threadIdx.x == 64) {
         const uint32_t v = threadIdx.x == 0 ? base : last;
@@ -667,7 +674,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads + threadIdx.x;
         if (e >= n) break;
         uint32_t lo, hi, p, start;
@@ -691,9 +698,16 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         const uint32_t src = pubs[p];
         const uint32_t tgt = csr_tgt[csr_off[src] + (e - start)];
         Msg m;
-        m.tcd = follower_tcd;
-        m.n0 = 0;
-        m.n1 = (uint64_t)tgt;
+        if (follower_keys) {  // followers named by a key table (e.g. Guid-keyed players)
+            const orl_grain_key k = follower_keys[tgt];
+            m.tcd = k.type_code_data;
+            m.n0 = k.n0;
+            m.n1 = k.n1;
+        } else {  // GrainId(follower_tcd, long id)
+            m.tcd = follower_tcd;
+            m.n0 = 0;
+            m.n1 = (uint64_t)tgt;
+        }
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
@@ -844,24 +858,33 @@ int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
+// Messages per thread in the route / fan-out kernels: 16 (one 4096-message radix tile per workgroup) for
+// large batches; fewer for small batches so the grid still has >= 2048 workgroups to hide the probe latency
+// (a 64k-message batch at 16 per thread is 16 workgroups on a 256-CU chip).
+uint32_t route_items(uint64_t n) {
+    uint32_t items = kItems;
+    while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < 2048) items >>= 1;
+    return items;
+}
+
 template <int BITS>
 void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
-                      uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
+                      uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     const dim3 g(ntiles), b(256);
     if (in == IN_ACT && out == OUT_PAIR)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
     else if (in == IN_ACT)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
     else if (out == OUT_PAIR)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
     else
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, ntiles, pout, order, keys);
+        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
 }
 
 void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
-                 uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
+                 uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     switch (bits) {
-#define ORL_CASE(B) case B: launch_pass_bits<B>(in, out, kin, n, n_act, shift, toff, ntiles, pout, order, keys, st); break;
+#define ORL_CASE(B) case B: launch_pass_bits<B>(in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -880,26 +903,28 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, const Scratch& s, hip
 
 // Stage 4 after a route kernel that already wrote the first digit's tile histogram into s.tile_hist.
 // Passes: act → pairs_a → pairs_b → ... → (order, sorted keys); then bucket offsets from the sorted keys.
-int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets,
-                       const Scratch& s, hipStream_t st) {
+int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t route_items, uint32_t* d_order,
+                       uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
     const RadixPlan plan = make_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
+        // pass 0's histogram rows were written by the route kernel, one per route tile of 256 * route_items
+        const uint32_t row_step = (p == 0) ? kItems / route_items : 1u;
+        const uint32_t nrows = (p == 0) ? ceil_div(n, kRouteThreads * route_items) : ntiles;
         if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, (uint32_t)plan.shift[p], bins,
                                s.tile_hist);
-        col_scan(s.tile_hist, ntiles, bins, s, st);
+        col_scan(s.tile_hist, nrows, bins, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
         launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
-                    s.tile_hist, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
+                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
-    const hipError_t me = hipMemsetD32Async((hipDeviceptr_t)d_offsets, kNoOffset, nb, st);
-    if (me != hipSuccess) return (int)me;
-    hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, d_offsets);
+    hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
+    hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
     hipLaunchKernelGGL(k_offsets_fill, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
     return (int)hipGetLastError();
 }
@@ -922,27 +947,29 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t ntiles = ceil_div(n, kTile);
+    const uint32_t items = route_items(n);
+    const uint32_t nwg = ceil_div(n, kRouteThreads * items);
     const RadixPlan plan = make_plan(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     if (buckets)
-        hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
+        hipLaunchKernelGGL(k_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
+                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0], items);
     else
-        hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, nullptr, 1u, 0u);
+        hipLaunchKernelGGL(k_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
+                           (uint32_t)n, excl, d_route, d_act, nullptr, 1u, 0u, items);
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();
     if (e) return e;
     if (!buckets) return 0;
-    return bucket_after_route(d_act, (uint32_t)n, n_act, d_order, d_offsets, s, st);
+    return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st);
 }
 
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const uint64_t* d_csr_off,
-                               const uint32_t* d_csr_tgt, const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub,
-                               uint64_t follower_tcd, uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets,
-                               uint32_t* d_route, uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out,
-                               uint64_t max_out, const Scratch& s, void* stream) {
+                               const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys, const uint32_t* d_pubs,
+                               const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts, uint32_t n_act,
+                               uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                               uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out, const Scratch& s, void* stream,
+                               void* ev_route_begin, void* ev_route_end) {
     hipStream_t st = (hipStream_t)stream;
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
@@ -952,30 +979,37 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
     hipLaunchKernelGGL(k_fanout_deg, dim3(ceil_div(m, 256)), dim3(256), 0, st, d_csr_off, d_pubs, (uint32_t)n_pub, poff32);
     scan_inplace(poff32, m, s.scan_sums, st);
     hipLaunchKernelGGL(k_widen64, dim3(ceil_div(m, 256)), dim3(256), 0, st, poff32, m, d_pub_offsets);
-    uint32_t total = 0;
-    int e = (int)hipMemcpyAsync(&total, poff32 + n_pub, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-    if (e) return e;
-    e = (int)hipStreamSynchronize(st);
-    if (e) return e;
-    *n_out = total;
+    uint64_t total = *n_out;
+    if (!(opts & ORL_OPT_TOTAL_GIVEN)) {  // read the emitted count back (one stream sync)
+        uint32_t t32 = 0;
+        int e = (int)hipMemcpyAsync(&t32, poff32 + n_pub, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        if (e) return e;
+        e = (int)hipStreamSynchronize(st);
+        if (e) return e;
+        total = t32;
+        *n_out = total;
+    }
     if (total > max_out) return -1;
     if (total == 0) {
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t ntiles = ceil_div(total, kTile);
+    const uint32_t items = route_items(total);
+    const uint32_t nwg = ceil_div(total, kRouteThreads * items);
     const RadixPlan plan = make_plan(n_act);
+    if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     if (buckets)
-        hipLaunchKernelGGL(k_fanout_route<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
-                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, total, excl, d_route, d_act,
-                           s.tile_hist, ntiles, 1u << plan.bits[0], (uint32_t)plan.shift[0]);
+        hipLaunchKernelGGL(k_fanout_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
+                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
+                           excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0], items);
     else
-        hipLaunchKernelGGL(k_fanout_route<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
-                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, total, excl, d_route, d_act,
-                           nullptr, ntiles, 1u, 0u);
-    e = (int)hipGetLastError();
+        hipLaunchKernelGGL(k_fanout_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
+                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
+                           excl, d_route, d_act, nullptr, 1u, 0u, items);
+    if (ev_route_end) (void)hipEventRecord((hipEvent_t)ev_route_end, st);
+    int e = (int)hipGetLastError();
     if (e || !buckets) return e;
-    return bucket_after_route(d_act, total, n_act, d_order, d_offsets, s, st);
+    return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st);
 }
 
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,

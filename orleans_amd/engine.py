@@ -274,12 +274,31 @@ class GrainDirectoryEngine:
                                                   ptr(d_act), ptr(d_order), ptr(d_offsets), ptr(stream)))
 
     def fanout_device(self, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, n_pub: int, follower_tcd: int,
-                      d_pub_offsets, d_route, d_act, d_order=None, d_offsets=None, stream=None, opts: int = 0) -> int:
-        n_out = C.c_uint64()
+                      d_pub_offsets, d_route, d_act, d_order=None, d_offsets=None, stream=None, opts: int = 0,
+                      total: Optional[int] = None) -> int:
+        """ChirperAccount.PublishMessage fan-out (Samples/Chirper/ChirperGrains/ChirperAccount.cs:154-157) + stages 1-4.
+        `total` (exact emitted count) makes the call sync-free and hipGraph-capturable."""
+        if total is not None:
+            opts |= L.OPT_TOTAL_GIVEN
+        n_out = C.c_uint64(int(total or 0))
         self._ck(self._lib.orl_fanout_route_device(self._ctx, ptr(d_csr_off), ptr(d_csr_tgt), ptr(d_pubs),
                                                    ptr(d_pub_silo), int(n_pub), int(follower_tcd), int(opts),
                                                    ptr(d_pub_offsets), ptr(d_route), ptr(d_act), ptr(d_order),
                                                    ptr(d_offsets), C.byref(n_out), ptr(stream)))
+        return n_out.value
+
+    def fanout_keys_device(self, d_csr_off, d_csr_tgt, d_follower_keys, d_pubs, d_pub_silo, n_pub: int, d_pub_offsets,
+                           d_route, d_act, d_order=None, d_offsets=None, stream=None, opts: int = 0,
+                           total: Optional[int] = None) -> int:
+        """Fan-out to followers named by a device key table (GameGrain.UpdateGameStatus players,
+        Samples/Presence/PresenceGrains/GameGrain.cs:62-113)."""
+        if total is not None:
+            opts |= L.OPT_TOTAL_GIVEN
+        n_out = C.c_uint64(int(total or 0))
+        self._ck(self._lib.orl_fanout_route_keys_device(self._ctx, ptr(d_csr_off), ptr(d_csr_tgt), ptr(d_follower_keys),
+                                                        ptr(d_pubs), ptr(d_pub_silo), int(n_pub), int(opts),
+                                                        ptr(d_pub_offsets), ptr(d_route), ptr(d_act), ptr(d_order),
+                                                        ptr(d_offsets), C.byref(n_out), ptr(stream)))
         return n_out.value
 
     def partition_by_owner_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,

@@ -209,3 +209,60 @@ def powerlaw_csr(n_nodes: int, exponent: float = 2.1, dmin: int = 1, dmax: int =
     e = int(off[-1])
     tgt = (stream(seed ^ 0xF011, 0, e) % np.uint64(n_nodes)).astype(np.uint32)
     return off, tgt
+
+
+# ---- config 5: Presence heartbeats (Samples/Presence) ------------------------------------------------------
+GAME_GRAIN_CLASS = "PresenceGrains.GameGrain"      # Samples/Presence/PresenceGrains/GameGrain.cs:32,39
+PLAYER_GRAIN_CLASS = "PresenceGrains.PlayerGrain"  # Samples/Presence/PresenceGrains/PlayerGrain.cs:32,37
+# LoadGenerator.GetPlayerId base Guid {2349992C-860A-4EDA-9590-000000000000} (Samples/Presence/LoadGenerator/
+# Program.cs:86-91) as Guid.ToByteArray(): Data1/2/3 little-endian, then the 8 trailing bytes.
+PLAYER_GUID_BASE = bytes([0x2C, 0x99, 0x49, 0x23, 0x0A, 0x86, 0xDA, 0x4E, 0x95, 0x90, 0, 0, 0, 0, 0, 0])
+
+
+def player_guid_bytes(n_players: int) -> np.ndarray:
+    """Player Guids.  The reference adds the player index to byte 15 only (wrapping at 256); for 800k distinct
+    players the index is written big-endian into bytes 10..15, which equals the reference for index < 256."""
+    g = np.tile(np.frombuffer(PLAYER_GUID_BASE, np.uint8), (n_players, 1))
+    idx = np.arange(n_players, dtype=np.uint64)
+    for b in range(6):
+        g[:, 15 - b] = ((idx >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+    return g
+
+
+def game_guid_bytes(n_games: int, seed: int = SEED_C5) -> np.ndarray:
+    """Game Guids: the reference uses Guid.NewGuid() (random); here 16 seeded splitmix64 bytes per game."""
+    r = stream(seed, 0, 2 * n_games).reshape(n_games, 2)
+    return r.view(np.uint8).reshape(n_games, 16).copy()
+
+
+@dataclass
+class Presence:
+    game_keys: np.ndarray     # KEY_DTYPE[n_games]
+    player_keys: np.ndarray   # KEY_DTYPE[n_games * per_game]
+    csr_off: np.ndarray       # u64[n_games + 1]: game g -> players [g*k, g*k+k)
+    csr_tgt: np.ndarray       # u32[n_games * k]
+    per_game: int
+
+
+def presence_population(n_games: int = 100_000, per_game: int = 8, seed: int = SEED_C5) -> Presence:
+    from .engine import grain_keys_from_guid_bytes
+    gtc = calc_id_hash(GAME_GRAIN_CLASS)
+    ptc = calc_id_hash(PLAYER_GRAIN_CLASS)
+    games = grain_keys_from_guid_bytes(gtc, game_guid_bytes(n_games, seed))
+    players = grain_keys_from_guid_bytes(ptc, player_guid_bytes(n_games * per_game))
+    off = (np.arange(n_games + 1, dtype=np.uint64) * np.uint64(per_game)).astype(np.uint64)
+    tgt = np.arange(n_games * per_game, dtype=np.uint32)
+    return Presence(games, players, off, tgt, per_game)
+
+
+def heartbeat_batch(pr: Presence, cl: Cluster, n_hb: int, batch: int, seed: int = SEED_C5):
+    """One batch of heartbeats: game index per heartbeat (uniform) and the game-message headers, sent from the
+    PresenceGrain's silo (a StatelessWorker, local to the receiving silo: uniform over silos)."""
+    g = (stream(seed ^ 0xB0B, batch * n_hb, n_hb) % np.uint64(len(pr.game_keys))).astype(np.int64)
+    s = stream(seed ^ 0x5E4D, batch * n_hb, n_hb)
+    m = np.zeros(n_hb, L.MSG_DTYPE)
+    k = pr.game_keys[g]
+    m["tcd"], m["n0"], m["n1"] = k["tcd"], k["n0"], k["n1"]
+    m["sending_silo"] = (s % np.uint64(cl.n_silos)).astype(np.uint8)
+    m["category"] = 2
+    return g.astype(np.uint32), m

@@ -311,7 +311,7 @@ int main() {
                 shift += bits[p];
             }
             { (void)hipMemsetD32Async((hipDeviceptr_t)offs, kNoOffset, n_act + 2, st);
-              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, offs);
+              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs);
               hipLaunchKernelGGL(k_offsets_fill, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs); }
         };
         timeit("pipeline 10+10 (AoS mid) excl. hist0", 28.0 * n, [&] {
@@ -328,7 +328,7 @@ int main() {
         });
         timeit("k_offsets", 4.0 * n, [&] {
             { (void)hipMemsetD32Async((hipDeviceptr_t)offs, kNoOffset, n_act + 2, st);
-              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, offs);
+              hipLaunchKernelGGL(k_offsets_mark, dim3((n / 16 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs);
               hipLaunchKernelGGL(k_offsets_fill, dim3((n_act + 2 + 255) / 256), dim3(256), 0, st, ko, n, n_act + 2, offs); }
         });
         prep(10, 4096);

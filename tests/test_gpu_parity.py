@@ -253,3 +253,94 @@ def test_config2_full_size_properties(torch):
     same = np.diff(srt.astype(np.int64)) == 0
     assert (np.diff(od.astype(np.int64))[same] > 0).all()       # arrival order kept inside a bucket
     eng.close()
+
+
+def test_presence_keyed_fanout_and_graph_capture(torch):
+    """Config-5 shape (small): Guid-keyed games fan out to 8 Guid-keyed players through a device key table
+    (GameGrain.UpdateGameStatus, Samples/Presence/PresenceGrains/GameGrain.cs:62-113), bit-exact vs the oracle;
+    the sync-free form (ORL_OPT_TOTAL_GIVEN) replayed from a captured graph gives the same words."""
+    t = torch
+    cl = W.default_cluster()
+    pr = W.presence_population(2000, 8)
+    all_keys = np.concatenate([pr.game_keys, pr.player_keys])
+    n_keys = len(all_keys)
+    owner = cl.owner_of(W.jenkins3_np(all_keys["tcd"], all_keys["n0"], all_keys["n1"]))
+    reg = np.random.default_rng(5).random(n_keys) < 0.9  # some players unregistered: new placements
+    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=1 << 16, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, all_keys, owner, reg)
+    o = cpu_ref.Oracle(cl.n_silos)
+    for s in range(cl.n_silos):
+        o.add_server(s, int(cl.hashes[s]))
+    idx = np.nonzero(reg)[0]
+    o.register(all_keys[idx], idx.astype(np.uint32), owner[idx])
+    games, _ = W.heartbeat_batch(pr, cl, 3000, 0)
+    gsilo = owner[games.astype(np.int64)]
+    # oracle: expand in CSR order, then name each follower by the key table
+    exp, poff_ref = cpu_ref.fanout_expand(pr.csr_off, pr.csr_tgt, games, gsilo, 0)
+    k = pr.player_keys[exp["n1"].astype(np.int64)]
+    exp["tcd"], exp["n0"], exp["n1"] = k["tcd"], k["n0"], k["n1"]
+    r_ref, a_ref = o.route(exp)
+    o_ref, f_ref = o.bucket(a_ref, n_keys)
+    dev = "cuda"
+    d_off = t.from_numpy(pr.csr_off.view(np.int64)).to(dev)
+    d_tgt = t.from_numpy(pr.csr_tgt.view(np.int32)).to(dev)
+    d_keys = t.from_numpy(pr.player_keys.view(np.uint8).reshape(-1, 24)).to(dev)
+    d_g = t.from_numpy(games.view(np.int32)).to(dev)
+    d_s = t.from_numpy(gsilo).to(dev)
+    n = len(exp)
+    poff = t.empty(len(games) + 1, dtype=t.int64, device=dev)
+    outs = [t.full((n,), -7, dtype=t.int32, device=dev) for _ in range(3)]
+    off = t.empty(n_keys + 2, dtype=t.int32, device=dev)
+    s = t.cuda.Stream()
+    got = eng.fanout_keys_device(d_off, d_tgt, d_keys, d_g, d_s, len(games), poff, *outs, off, stream=s.cuda_stream)
+    s.synchronize()
+    assert got == n
+    np.testing.assert_array_equal(outs[0].cpu().numpy().view(np.uint32), r_ref)
+    np.testing.assert_array_equal(outs[1].cpu().numpy().view(np.uint32), a_ref)
+    np.testing.assert_array_equal(outs[2].cpu().numpy().view(np.uint32), o_ref)
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), f_ref)
+    np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), poff_ref)
+    # sync-free form under graph capture, outputs cleared before replay
+    for x in outs:
+        x.fill_(-7)
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g, stream=s):
+        eng.fanout_keys_device(d_off, d_tgt, d_keys, d_g, d_s, len(games), poff, *outs, off, stream=s.cuda_stream,
+                               total=n)
+    for x in outs:
+        x.fill_(-7)
+    t.cuda.synchronize()
+    g.replay()
+    t.cuda.synchronize()
+    np.testing.assert_array_equal(outs[0].cpu().numpy().view(np.uint32), r_ref)
+    np.testing.assert_array_equal(outs[2].cpu().numpy().view(np.uint32), o_ref)
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), f_ref)
+    eng.close()
+
+
+def test_route_batch_graph_replay(torch):
+    """A captured orl_route_batch_device replays to the same words as the eager call (config-5 hipGraph path)."""
+    t = torch
+    cl, eng, o = _random_setup(5000, 6000)
+    msgs = W.uniform_messages(cl, 5500, 70_000, seed=77)
+    d_in = t.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
+    n = len(msgs)
+    outs = [t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)]
+    off = t.empty(6002, dtype=t.int32, device="cuda")
+    s = t.cuda.Stream()
+    eng.address_messages_device(d_in, n, *outs, off, stream=s.cuda_stream)
+    s.synchronize()
+    ref = [x.cpu().numpy().copy() for x in outs] + [off.cpu().numpy().copy()]
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g, stream=s):
+        eng.address_messages_device(d_in, n, *outs, off, stream=s.cuda_stream)
+    for x in outs + [off]:
+        x.fill_(0)
+    t.cuda.synchronize()
+    for _ in range(3):
+        g.replay()
+    t.cuda.synchronize()
+    for a, b in zip(ref, [x.cpu().numpy() for x in outs] + [off.cpu().numpy()]):
+        np.testing.assert_array_equal(a, b)
+    eng.close()
