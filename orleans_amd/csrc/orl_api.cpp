@@ -312,7 +312,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -376,7 +376,16 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.idx_a, (mb + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(idx)");
         if ((e = hipMalloc((void**)&c->s.sorted_keys, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(sorted)");
         if ((e = hipMalloc((void**)&c->s.tile_hist, hist_words * 4)) != hipSuccess) return bail(e, "hipMalloc(tile_hist)");
-        if ((e = hipMalloc((void**)&c->s.scan_sums, ((hist_words + 4095) / 4096 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(scan)");
+        // device-wide scans: tile histograms, fan-out degrees (mb + 1), bucket offsets (n_act + 2)
+        const uint64_t scan_words = std::max<uint64_t>(std::max<uint64_t>(hist_words, mb + 1), (uint64_t)cfg->n_act + 2);
+        if ((e = hipMalloc((void**)&c->s.scan_sums, ((scan_words + 4095) / 4096 + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(scan)");
+        // two-level stage 4: per-segment low-digit rows (segment size drops to kSegChunk below 16M messages)
+        const BucketPlan bp = make_bucket_plan(cfg->n_act);
+        const uint64_t seg_rows = std::max<uint64_t>(max_segments(mb, bp.hb), max_segments(std::min<uint64_t>(mb, (16u << 20) - 1), bp.hb));
+        const uint64_t seg_words = bp.two_level ? seg_rows << bp.lb : 1;
+        if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
+        if ((e = hipMalloc((void**)&c->s.bstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
+        if ((e = hipMalloc((void**)&c->s.sstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
             return bail(e, "hipMalloc(col_sums)");

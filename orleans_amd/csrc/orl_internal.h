@@ -7,6 +7,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/orleans_route.h"
 
 namespace orl {
@@ -116,18 +118,55 @@ inline RadixPlan make_plan(uint32_t max_key) {
     return p;
 }
 
+// Stage-4 plan for keys in [0, n_act] (n_act = the unresolved bucket).  Keys of up to 2 x kMaxDigitBits bits
+// take the two-level path: one stable MSD pass by the high `hb` bits (skipped when hb == 0) groups the
+// messages into 2^hb buckets, then each bucket is counting-sorted by its low `lb` bits in segments of at
+// most seg_elems() messages; the per-key counts of that second level ARE the bucket offsets (one scan).
+// Wider keys fall back to LSD passes (`lsd`) + offsets from the sorted keys.
+constexpr uint32_t kSegChunk = kTile;  // messages per LDS round inside a segment
+
+struct BucketPlan {
+    bool two_level;
+    int hb, lb;
+    RadixPlan lsd;
+};
+
+inline BucketPlan make_bucket_plan(uint32_t max_key) {
+    int total = 0;
+    while ((max_key >> total) != 0 && total < 32) ++total;
+    if (total == 0) total = 1;
+    BucketPlan p{};
+    p.two_level = total <= 2 * (int)kMaxDigitBits;
+    p.lb = total <= (int)kMaxDigitBits ? total : (total + 1) / 2;
+    p.hb = total - p.lb;
+    p.lsd = make_plan(max_key);
+    return p;
+}
+
+// Segment size of the two-level path: 4 LDS rounds per segment for large batches, 1 for small ones (more
+// workgroups).  The segment count is bounded by ceil(n / seg) + min(2^hb, n) (each nonempty bucket adds at
+// most one partial segment).
+inline uint32_t seg_elems(uint64_t n) { return n >= (16u << 20) ? 4 * kSegChunk : kSegChunk; }
+inline uint64_t max_segments(uint64_t n, int hb) {
+    const uint64_t s = seg_elems(n);
+    return (n + s - 1) / s + std::min<uint64_t>(1ull << hb, n);
+}
+
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
 // All return hipError_t as int; they only enqueue on `stream`.
 struct Scratch {
     uint2* pairs_a;         // [max_batch] {key, index} between radix passes
     uint2* pairs_b;         // [max_batch]
     uint32_t* idx_a;        // [max_batch + 1] fan-out publish offsets
-    uint32_t* sorted_keys;  // [max_batch]
+    uint32_t* sorted_keys;  // [max_batch] (LSD fallback only)
     uint32_t* tile_hist;    // [2048 * max_tiles]
     uint32_t* scan_sums;    // [scan blocks]
     uint32_t* col_sums;     // [ceil(max_tiles/64) * 2048] column-scan chunk sums
     uint32_t* col_tot;      // [2048] column totals
     uint8_t* digits;        // [max_batch] (partition by owner)
+    uint32_t* seg_hist;     // [max segments][2^lb] two-level path: per-segment low-digit counts → bases
+    uint32_t* bstart;       // [2049] bucket starts (two-level path)
+    uint32_t* sstart;       // [2049] first segment of each bucket
     uint64_t max_batch;
     uint64_t max_tiles;
 };

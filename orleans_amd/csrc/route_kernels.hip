@@ -174,6 +174,15 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
 
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
 
+// Stable rank of this lane's digit among the wave's earlier elements with the same digit: one returning LDS
+// atomic on the wave's private counter row.  The LDS services the same-address lanes of one ds_add_rtn_u32
+// in lane order, so lane order == arrival order inside each 64-element step, and consecutive steps of the
+// wave are ordered by the wave's instruction order.  Measured on MI355X (scripts/rank_lab.hip,
+// profiles/r01_rank_lab.txt): identical ranks to the BITS-ballot match over 4 x 64M elements (uniform,
+// 50 % on 8 hot digits, all-equal, 4 distinct) at 1.8x its speed; every GPU parity test re-checks it
+// bit-exactly against the oracle.  Exec-masked (inactive) lanes do not count.
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) { return atomicAdd(&wave_cnt[d], 1u); }
+
 // ---------------------------------------------------------------------------------------------------
 // stage 1 alone
 __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ out) {
@@ -434,7 +443,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //   1. load the tile (IN_ACT: activation handles, clamped to the unresolved bucket n_act, index = position;
 //      IN_PAIR: {key, index} pairs of the previous pass) with unconditional loads, all in flight together;
 //   2. stable rank inside the tile: wave w owns elements [w*1024, w*1024+1024) processed 64 at a time in
-//      order, lanes with equal digits found with BITS ballots, per-wave running counts in LDS, so
+//      order, each lane ranked by wave_rank on the wave's running counts in LDS, so
 //      (wave, step, lane) order == arrival order;
 //   3. per-bin tile-local starts (block scan) and delta[d] = global base of (tile, d) - local start;
 //   4. scatter into an LDS image sorted by digit, then write it out in image order, so the global stores
@@ -469,7 +478,6 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     }
     const uint32_t tbase = tile * kTile;
     const uint32_t wbase = tbase + w * (kItems * 64u);
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
     uint32_t key[kItems], idx[kItems], rank[kItems];
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
@@ -486,23 +494,12 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = wbase + j * 64u + lane;
-        const bool valid = e < n;
-        const uint32_t d = (key[j] >> shift) & (B - 1u);
-        uint64_t m = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < BITS; ++b) {
-            const uint64_t bb = __ballot((d >> b) & 1u);
-            m &= ((d >> b) & 1u) ? bb : ~bb;
-        }
-        const uint32_t c = sm.cnt[w][d];
-        rank[j] = c + (uint32_t)__popcll(m & lt_mask);
-        // the highest lane of each equal-digit group advances the wave's count for the next 64
-        if (valid && (m >> lane) == 1ull) sm.cnt[w][d] = c + (uint32_t)__popcll(m);
-    }
+    for (uint32_t j = 0; j < kItems; ++j)
+        if (wbase + j * 64u + lane < n) rank[j] = wave_rank(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u));
     __syncthreads();
-    const uint32_t* orow = tile_off + (size_t)tile * B;
+    // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
+    // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
+    const uint32_t* orow = tile_off + (size_t)tile * row_step * B;
     uint32_t tot[PER];
     uint32_t s = 0;
 #pragma unroll
@@ -611,6 +608,260 @@ __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict
                                                       uint32_t* __restrict__ offsets) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     if (b < nb && offsets[b] == kNoOffset) offsets[b] = lower_bound_u32(sorted, n, b);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Stage 4, two-level path (keys of <= 22 bits; BucketPlan in orl_internal.h).  After the MSD pass the
+// messages are grouped by bucket b = key >> lb (stable), so each bucket is a contiguous range
+// [bstart[b], bstart[b+1]) in arrival order.  Buckets are cut into segments of <= seg messages; every segment
+// is counted (k_seg_count), the counts are column-scanned per bucket (k_seg_scan: segment bases inside the
+// bucket, and per-key totals = the bucket sizes of stage 4), one exclusive scan turns the per-key totals into
+// bucket offsets, and k_seg_scatter ranks each segment stably and writes `order`.  Without an MSD pass
+// (hb == 0) the whole batch is one bucket read straight from the activation handles.
+//
+// k_seg_plan: one workgroup; bstart = exclusive scan of the MSD column totals (or {0, n}), sstart = exclusive
+// scan of ceil(count / seg).  nbk <= 2048 buckets, two per thread.
+__global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
+                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
+    __shared__ uint32_t wsum[2][16];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t c[2], p[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t b = threadIdx.x * 2 + q;
+        c[q] = b < nbk ? (col_tot ? col_tot[b] : n) : 0u;
+        p[q] = (c[q] + seg - 1) / seg;
+    }
+    const uint32_t ci = wave_incl_scan(c[0] + c[1]), pi = wave_incl_scan(p[0] + p[1]);
+    if (lane == 63) {
+        wsum[0][w] = ci;
+        wsum[1][w] = pi;
+    }
+    __syncthreads();
+    uint32_t cb = ci - c[0] - c[1], pb = pi - p[0] - p[1], ct = 0, pt = 0;
+    for (uint32_t i = 0; i < 16; ++i) {
+        if (i < w) {
+            cb += wsum[0][i];
+            pb += wsum[1][i];
+        }
+        ct += wsum[0][i];
+        pt += wsum[1][i];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t b = threadIdx.x * 2 + q;
+        if (b < nbk) {
+            bstart[b] = cb;
+            sstart[b] = pb;
+        }
+        cb += c[q];
+        pb += p[q];
+    }
+    if (threadIdx.x == 0) {
+        bstart[nbk] = ct;
+        sstart[nbk] = pt;
+    }
+}
+
+// Segment j of the launch: blocks [0, nseg) map XCD-contiguously onto segments (consecutive segments of one
+// bucket write adjacent output runs, which then meet in one L2); blocks >= nseg have no segment.
+struct SegRange {
+    uint32_t bucket, index, lo, hi;
+};
+
+__device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                             uint32_t nbk, uint32_t seg, SegRange& r) {
+    const uint32_t nseg = sstart[nbk];
+    if (blockIdx.x >= nseg) return false;
+    const uint32_t j = xcd_tile(blockIdx.x, nseg);
+    uint32_t lo = 0, hi = nbk + 1;  // bucket = upper_bound(sstart, j) - 1 (skips empty buckets)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sstart[mid] <= j) lo = mid + 1; else hi = mid;
+    }
+    r.bucket = lo - 1;
+    r.index = j;
+    r.lo = bstart[r.bucket] + (j - sstart[r.bucket]) * seg;
+    r.hi = min(r.lo + seg, bstart[r.bucket + 1]);
+    return true;
+}
+
+template <int IN>
+__device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t e, uint32_t n_act, uint32_t& key, uint32_t& idx) {
+    if (IN == IN_ACT) {
+        key = bucket_key(static_cast<const uint32_t*>(in)[e], n_act);
+        idx = e;
+    } else {
+        const uint2 v = static_cast<const uint2*>(in)[e];
+        key = v.x;
+        idx = v.y;
+    }
+}
+
+template <int LB, int IN>
+__global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_act, uint32_t nbk, uint32_t seg,
+                                                   const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                                   uint32_t* __restrict__ seg_hist) {
+    constexpr uint32_t BL = 1u << LB;
+    __shared__ uint32_t hist[BL];
+    SegRange r;
+    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
+    for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
+    __syncthreads();
+    for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
+        uint32_t key[kItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {  // clamped loads: all 16 in flight at once
+            const uint32_t e = c0 + j * 256u + threadIdx.x;
+            uint32_t idx;
+            seg_load<IN>(in, e < r.hi ? e : r.hi - 1, n_act, key[j], idx);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+            if (c0 + j * 256u + threadIdx.x < r.hi) atomicAdd(&hist[key[j] & (BL - 1u)], 1u);
+    }
+    __syncthreads();
+    uint32_t* row = seg_hist + (size_t)r.index * BL;
+    for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
+}
+
+// grid (nbk, ceil(BL/256)): per bucket and low digit, the segment rows become exclusive prefixes inside the
+// bucket and the column total (messages with key = b << lb | l) goes to counts[key] (keys < nb only).
+template <int LB>
+__global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
+                                                  uint32_t nb, uint32_t* __restrict__ counts) {
+    constexpr uint32_t BL = 1u << LB;
+    const uint32_t l = blockIdx.y * 256u + threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    if (b == 0 && l == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+        for (uint32_t k = gridDim.x << LB; k < nb; ++k) counts[k] = 0;
+    if (l >= BL) return;
+    const uint32_t j0 = sstart[b], j1 = sstart[b + 1];
+    uint32_t run = 0, j = j0;
+    for (; j + 4 <= j1; j += 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = seg_hist[(size_t)(j + q) * BL + l];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            seg_hist[(size_t)(j + q) * BL + l] = run;
+            run += v[q];
+        }
+    }
+    for (; j < j1; ++j) {
+        const uint32_t v = seg_hist[(size_t)j * BL + l];
+        seg_hist[(size_t)j * BL + l] = run;
+        run += v;
+    }
+    const uint32_t key = (b << LB) | l;
+    if (key < nb) counts[key] = run;
+}
+
+// One segment: LDS rounds of kSegChunk messages.  Each round ranks its messages with wave_rank (wave w owns
+// [w*1024, w*1024+1024) of the round, 16 steps of 64 lanes, so (round, wave, step, lane) order is arrival
+// order), turns the per-wave counts into round-local sorted starts, stages the indices in LDS in sorted
+// order and writes them out as runs of consecutive positions: global position of round-local slot i with
+// digit l = offsets[b << lb | l] + (segment base inside the bucket) + (earlier rounds) + i - (round-local
+// start of l).  The running part lives in registers of the thread owning digit l.
+template <int LB>
+struct SegSmem {
+    uint32_t cnt[kWaves][1u << LB];
+    uint32_t delta[1u << LB];
+    uint32_t stage_i[kSegChunk];
+    uint16_t stage_d[kSegChunk];
+    uint32_t wsum[kWaves];
+};
+
+template <int LB, int IN>
+__global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in, uint32_t n_act, uint32_t nbk, uint32_t seg,
+                                                     const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                                     const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
+                                                     uint32_t nb, uint32_t n, uint32_t* __restrict__ order) {
+    constexpr uint32_t BL = 1u << LB;
+    constexpr uint32_t PER = (BL + 255u) / 256u;
+    __shared__ SegSmem<LB> sm;
+    SegRange r;
+    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t run[PER];  // global position of the next message with digit threadIdx.x * PER + q
+    const uint32_t* hrow = seg_hist + (size_t)r.index * BL;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t l = threadIdx.x * PER + q;
+        const uint32_t key = (r.bucket << LB) | l;
+        run[q] = (l < BL && key < nb) ? offsets[key] + hrow[l] : 0u;
+    }
+    for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
+        const uint32_t wbase = c0 + w * (kItems * 64u);
+        uint32_t key[kItems], idx[kItems], rank[kItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+            const uint32_t e = wbase + j * 64u + lane;
+            seg_load<IN>(in, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t l = threadIdx.x * PER + q;
+            if (l < BL)
+#pragma unroll
+                for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][l] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank(&sm.cnt[w][0], key[j] & (BL - 1u));
+        __syncthreads();
+        uint32_t tot[PER], s = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t l = threadIdx.x * PER + q;
+            uint32_t t = 0;
+            if (l < BL) {
+#pragma unroll
+                for (uint32_t ww = 0; ww < kWaves; ++ww) {
+                    const uint32_t c = sm.cnt[ww][l];
+                    sm.cnt[ww][l] = t;
+                    t += c;
+                }
+            }
+            tot[q] = t;
+            s += t;
+        }
+        uint32_t total;
+        uint32_t lstart = block_excl_scan(s, sm.wsum, total);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t l = threadIdx.x * PER + q;
+            if (l < BL) {
+#pragma unroll
+                for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][l] += lstart;
+                sm.delta[l] = run[q] - lstart;
+                run[q] += tot[q];
+            }
+            lstart += tot[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+            if (wbase + j * 64u + lane < r.hi) {
+                const uint32_t d = key[j] & (BL - 1u);
+                const uint32_t lpos = sm.cnt[w][d] + rank[j];
+                sm.stage_i[lpos] = idx[j];
+                sm.stage_d[lpos] = (uint16_t)d;
+            }
+        }
+        __syncthreads();
+        const uint32_t cnt = min(r.hi - c0, kSegChunk);
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+            const uint32_t i = j * 256u + threadIdx.x;
+            if (i < cnt) {
+                const uint32_t g = sm.delta[sm.stage_d[i]] + i;
+                if (g < n) order[g] = sm.stage_i[i];  // always true with consistent counts; bounds a corrupt input
+            }
+        }
+        __syncthreads();  // LDS is reused by the next round
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -901,19 +1152,80 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, const Scratch& s, hip
     hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot);
 }
 
-// Stage 4 after a route kernel that already wrote the first digit's tile histogram into s.tile_hist.
-// Passes: act → pairs_a → pairs_b → ... → (order, sorted keys); then bucket offsets from the sorted keys.
+// Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
+// two-level path; none when the two-level path has no MSD pass).
+struct RouteHist {
+    bool on;
+    uint32_t bins, shift;
+};
+
+RouteHist route_hist(uint32_t n_act) {
+    const BucketPlan bp = make_bucket_plan(n_act);
+    if (bp.two_level) return {bp.hb > 0, 1u << bp.hb, (uint32_t)bp.lb};
+    return {true, 1u << bp.lsd.bits[0], (uint32_t)bp.lsd.shift[0]};
+}
+
+template <int LB>
+void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
+                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
+    const uint32_t nb = n_act + 2;
+    if (in == IN_ACT)
+        hipLaunchKernelGGL((k_seg_count<LB, IN_ACT>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart, s.seg_hist);
+    else
+        hipLaunchKernelGGL((k_seg_count<LB, IN_PAIR>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart, s.seg_hist);
+    hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
+    scan_inplace(d_offsets, nb, s.scan_sums, st);  // per-key counts → bucket offsets
+    if (in == IN_ACT)
+        hipLaunchKernelGGL((k_seg_scatter<LB, IN_ACT>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart,
+                           s.seg_hist, d_offsets, nb, n, d_order);
+    else
+        hipLaunchKernelGGL((k_seg_scatter<LB, IN_PAIR>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart,
+                           s.seg_hist, d_offsets, nb, n, d_order);
+}
+
+void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
+                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
+    switch (lb) {
+#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st); break;
+        ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
+        ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
+#undef ORL_CASE
+        default: break;
+    }
+}
+
+// Stage 4 after a route kernel that already wrote route_hist()'s tile histogram into s.tile_hist.
+//   two-level: [MSD pass by the high digit → pairs_a] → segment count → segment scan → offsets scan → scatter;
+//   LSD fallback: passes act → pairs_a → pairs_b → ... → (order, sorted keys); offsets from the sorted keys.
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t route_items, uint32_t* d_order,
                        uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
-    const RadixPlan plan = make_plan(n_act);  // keys in [0, n_act]
+    const BucketPlan bp = make_bucket_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
+    // pass 0's histogram rows were written by the route kernel, one per route tile of 256 * route_items
+    const uint32_t row_step0 = kItems / route_items;
+    const uint32_t nrows0 = ceil_div(n, kRouteThreads * route_items);
+    if (bp.two_level) {
+        const uint32_t nbk = 1u << bp.hb;
+        const uint32_t seg = seg_elems(n);
+        const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
+        const void* kin = d_act;
+        if (bp.hb > 0) {
+            col_scan(s.tile_hist, nrows0, nbk, s, st);
+            launch_pass(bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
+                        nullptr, nullptr, st);
+            kin = s.pairs_a;
+        }
+        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
+        launch_seg(bp.lb, bp.hb > 0 ? IN_PAIR : IN_ACT, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st);
+        return (int)hipGetLastError();
+    }
+    const RadixPlan& plan = bp.lsd;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
-        // pass 0's histogram rows were written by the route kernel, one per route tile of 256 * route_items
-        const uint32_t row_step = (p == 0) ? kItems / route_items : 1u;
-        const uint32_t nrows = (p == 0) ? ceil_div(n, kRouteThreads * route_items) : ntiles;
+        const uint32_t row_step = (p == 0) ? row_step0 : 1u;
+        const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
         if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, (uint32_t)plan.shift[p], bins,
                                s.tile_hist);
@@ -949,11 +1261,11 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
     }
     const uint32_t items = route_items(n);
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
-    const RadixPlan plan = make_plan(n_act);
+    const RouteHist rh = route_hist(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
-    if (buckets)
+    if (buckets && rh.on)
         hipLaunchKernelGGL(k_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0], items);
+                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, rh.bins, rh.shift, items);
     else
         hipLaunchKernelGGL(k_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
                            (uint32_t)n, excl, d_route, d_act, nullptr, 1u, 0u, items);
@@ -996,12 +1308,12 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
     }
     const uint32_t items = route_items(total);
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
-    const RadixPlan plan = make_plan(n_act);
+    const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
-    if (buckets)
+    if (buckets && rh.on)
         hipLaunchKernelGGL(k_fanout_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
                            d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
-                           excl, d_route, d_act, s.tile_hist, 1u << plan.bits[0], (uint32_t)plan.shift[0], items);
+                           excl, d_route, d_act, s.tile_hist, rh.bins, rh.shift, items);
     else
         hipLaunchKernelGGL(k_fanout_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
                            d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
