@@ -143,10 +143,11 @@ inline BucketPlan make_bucket_plan(uint32_t max_key) {
     return p;
 }
 
-// Segment size of the two-level path: 4 LDS rounds per segment for large batches, 1 for small ones (more
-// workgroups).  The segment count is bounded by ceil(n / seg) + min(2^hb, n) (each nonempty bucket adds at
-// most one partial segment).
-inline uint32_t seg_elems(uint64_t n) { return n >= (16u << 20) ? 4 * kSegChunk : kSegChunk; }
+// Segment size of the two-level path: one LDS round per segment.  (Four rounds per segment cut the segment
+// histogram traffic but left each key's output lines partially written for a whole segment lifetime: 3.5x
+// write amplification at config 2, profiles/r01c_config2_pmc.txt.)  The segment count is bounded by
+// ceil(n / seg) + min(2^hb, n) (each nonempty bucket adds at most one partial segment).
+inline uint32_t seg_elems(uint64_t) { return kSegChunk; }
 inline uint64_t max_segments(uint64_t n, int hb) {
     const uint64_t s = seg_elems(n);
     return (n + s - 1) / s + std::min<uint64_t>(1ull << hb, n);

@@ -457,8 +457,7 @@ template <int BITS>
 struct PassSmem {
     uint32_t cnt[kWaves][1u << BITS];  // per-wave running counts, then per-(wave, bin) tile-local starts
     uint32_t delta[1u << BITS];        // global base - tile-local start, per bin
-    uint32_t stage_k[kTile];
-    uint32_t stage_i[kTile];
+    uint2 stage[kTile];  // {key, index}: one 8-B LDS write per element (half the conflicted scatter instructions)
     uint32_t wsum[kWaves];
 };
 
@@ -535,8 +534,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         if (wbase + j * 64u + lane < n) {
             const uint32_t d = (key[j] >> shift) & (B - 1u);
             const uint32_t lpos = sm.cnt[w][d] + rank[j];
-            sm.stage_k[lpos] = key[j];
-            sm.stage_i[lpos] = idx[j];
+            sm.stage[lpos] = make_uint2(key[j], idx[j]);
         }
     }
     __syncthreads();
@@ -545,14 +543,15 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     for (uint32_t j = 0; j < kItems; ++j) {
         const uint32_t i = j * 256u + threadIdx.x;
         if (i < cnt) {
-            const uint32_t k = sm.stage_k[i];
+            const uint2 kv = sm.stage[i];
+            const uint32_t k = kv.x;
             const uint32_t g = sm.delta[(k >> shift) & (B - 1u)] + i;
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
-                pair_out[g] = make_uint2(k, sm.stage_i[i]);
+                pair_out[g] = kv;
             } else {
                 key_out[g] = k;
-                order_out[g] = sm.stage_i[i];
+                order_out[g] = kv.y;
             }
         }
     }
@@ -767,8 +766,7 @@ template <int LB>
 struct SegSmem {
     uint32_t cnt[kWaves][1u << LB];
     uint32_t delta[1u << LB];
-    uint32_t stage_i[kSegChunk];
-    uint16_t stage_d[kSegChunk];
+    uint2 stage[kSegChunk];  // {digit, index}
     uint32_t wsum[kWaves];
 };
 
@@ -846,8 +844,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             if (wbase + j * 64u + lane < r.hi) {
                 const uint32_t d = key[j] & (BL - 1u);
                 const uint32_t lpos = sm.cnt[w][d] + rank[j];
-                sm.stage_i[lpos] = idx[j];
-                sm.stage_d[lpos] = (uint16_t)d;
+                sm.stage[lpos] = make_uint2(d, idx[j]);
             }
         }
         __syncthreads();
@@ -856,8 +853,9 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
         for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t i = j * 256u + threadIdx.x;
             if (i < cnt) {
-                const uint32_t g = sm.delta[sm.stage_d[i]] + i;
-                if (g < n) order[g] = sm.stage_i[i];  // always true with consistent counts; bounds a corrupt input
+                const uint2 dv = sm.stage[i];
+                const uint32_t g = sm.delta[dv.x] + i;
+                if (g < n) order[g] = dv.y;  // always true with consistent counts; bounds a corrupt input
             }
         }
         __syncthreads();  // LDS is reused by the next round
