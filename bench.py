@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--router", action="store_true",
+                    help="configs 2/3 at N=1: go through the pipelined multi-GPU router (partition + routing on two "
+                         "streams; exercises the N>1 code path on one GPU)")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "route_kernel_pmc.json"))
     args = ap.parse_args()
@@ -125,7 +128,7 @@ def read_traffic(path, msgs_per_launch, world):
 def run_single_target(args, torch, dist, rank, world, local_rank):
     from orleans_amd import workloads as W
     from orleans_amd.engine import GrainDirectoryEngine
-    from orleans_amd.node import HipExecutor, ShardedRouter, local_silos, rank_of_silo
+    from orleans_amd.node import HipExecutor, PipelinedRouter, local_silos, rank_of_silo
 
     zipf = args.config == 3
     n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
@@ -150,7 +153,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     d_msgs = torch.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
     stream = torch.cuda.current_stream().cuda_stream
 
-    if world == 1:
+    part_eng = None
+    if world == 1 and not args.router:
         route = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         act = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         order = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
@@ -160,10 +164,15 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
             eng.address_messages_device(d_msgs, n_msgs, route, act, order, offsets, stream=stream)
             return n_msgs
     else:
-        router = ShardedRouter(HipExecutor(eng, cap, torch), rank, world, ros, cap, torch)
+        # a ring-only context for the owner partition, so it runs beside the route context on its own stream
+        part_eng = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=cap, device=local_rank)
+        W.setup_engine(part_eng, cl, local_silos=mine if world > 1 else None)
+        router = PipelinedRouter(HipExecutor(eng, cap, torch, part_eng=part_eng, slots=2, nranks=world,
+                                             part_capacity=n_msgs), rank, world, ros, cap, torch)
 
-        def step():
-            return router.step(d_msgs, n_msgs).n_recv
+        def step():  # partition + exchange this batch, route the previous one (two batches in flight)
+            res = router.submit(d_msgs, n_msgs)
+            return 0 if res is None else res.n_recv
     log(f"setup {time.perf_counter() - t_setup:.1f}s; warmup {args.warmup}")
     eng.set_timing(False)
 
@@ -171,7 +180,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         eng.sync()
 
     # timing events are enabled after warmup so the summary covers the timed steps only
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1 if (world > 1 or args.router) else 0)):  # the router's first step fills its pipeline
         step()
     sync()
     eng.set_timing(True)
@@ -189,10 +198,12 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cl, keys, owner, msgs, n_grains, args.cpu_wall)
     eng.close()
+    if part_eng is not None:
+        part_eng.close()
     name = ("config3: Zipf(1.1) over 16M long-key grains" if zipf else
             "config2: uniform 1M long-key grains") + f", {n_msgs >> 20}M single-target messages per GPU, 8-silo ring, stages 1-4"
-    if world > 1:
-        name += ", + owner partition + RCCL all-to-all"
+    if world > 1 or args.router:
+        name += ", + owner partition + RCCL all-to-all (two batches in flight)"
     return {
         "metric": "routed grain messages/sec (node)",
         "value": value,

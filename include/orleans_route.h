@@ -221,6 +221,14 @@ int orl_fanout_route_keys_device(orl_ctx* ctx, const uint64_t* d_csr_off, const 
 int orl_partition_by_owner_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                                   const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank,
                                   orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, void* stream);
+/* One-pass form for the exchange: the headers for rank r go to the padded send region
+ * d_out[r * stride .. r * stride + d_counts[r]) (stride >= n; d_out holds nranks * stride headers), so
+ * each region can be sent as is (grouped send/recv, RCCL over xGMI).  Same order and counts as
+ * orl_partition_by_owner_device; d_src_index may be NULL (same padded layout otherwise).
+ * Reference: OutboundMessageQueue.SendMessage's per-target-silo queues (OutboundMessageQueue.cs:137-145). */
+int orl_partition_by_owner_padded_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                                         const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
+                                         orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, void* stream);
 
 int orl_sync(orl_ctx* ctx);
 

@@ -177,6 +177,8 @@ struct orl_ctx {
     RouteParams* d_params = nullptr;
     bool params_dirty = true;
     uint8_t* d_rank_of_silo = nullptr;
+    uint8_t h_rank_of_silo[256] = {};  // last uploaded rank_of_silo (uploads only on change: no per-batch sync)
+    bool ros_valid = false;
     Scratch s{};
     hipStream_t stream = nullptr;
     // host-buffer staging (orl_route_batch / orl_hash_batch)
@@ -312,7 +314,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -386,6 +388,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
         if ((e = hipMalloc((void**)&c->s.bstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
         if ((e = hipMalloc((void**)&c->s.sstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
+        if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
             return bail(e, "hipMalloc(col_sums)");
@@ -683,12 +686,12 @@ int orl_fanout_route_keys_device(orl_ctx* c, const uint64_t* d_csr_off, const ui
                        d_order, d_off, n_out, stream);
 }
 
-int orl_partition_by_owner_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
-                                  uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out, uint32_t* d_src, uint64_t* d_counts,
-                                  void* stream) {
-    if (!c || !rank_of_silo) return ORL_E_INVALID;
+namespace {
+// Shared checks of the two partition entry points + the rank_of_silo upload (only when it changes).
+int partition_prologue(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, const uint8_t* rank_of_silo, uint32_t nranks,
+                       uint32_t my_rank, const void* d_out, uint64_t* d_counts, hipStream_t st) {
     if (nranks == 0 || nranks > 8 || my_rank >= nranks) return fail(c, ORL_E_INVALID, "nranks must be 1..8 and my_rank < nranks");
-    if (n && (!d_in || !d_out || !d_src)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n && (!d_in || !d_out)) return fail(c, ORL_E_INVALID, "null device buffer");
     if (!d_counts) return fail(c, ORL_E_INVALID, "null counts buffer");
     if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch too large");
     int r = sync_device_state(c);
@@ -699,12 +702,41 @@ int orl_partition_by_owner_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n,
         if (rank_of_silo[s] >= nranks) return fail(c, ORL_E_INVALID, "rank_of_silo[%u] = %u >= nranks", s, rank_of_silo[s]);
         ros[s] = rank_of_silo[s];
     }
+    if (!c->ros_valid || std::memcmp(ros, c->h_rank_of_silo, sizeof ros) != 0) {  // a membership change: rare
+        ORL_HIP(c, hipStreamSynchronize(st));
+        ORL_HIP(c, hipMemcpy(c->d_rank_of_silo, ros, 256, hipMemcpyHostToDevice));
+        std::memcpy(c->h_rank_of_silo, ros, sizeof ros);
+        c->ros_valid = true;
+    }
+    return ORL_OK;
+}
+}  // namespace
+
+int orl_partition_by_owner_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                  uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out, uint32_t* d_src, uint64_t* d_counts,
+                                  void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (n && !d_src) return fail(c, ORL_E_INVALID, "null device buffer");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    ORL_HIP(c, hipMemcpyAsync(c->d_rank_of_silo, ros, 256, hipMemcpyHostToDevice, st));
-    ORL_HIP(c, hipStreamSynchronize(st));
+    int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
+    if (r) return r;
     int e = launch_partition_by_owner(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, d_out, d_src, d_counts,
                                       c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "partition launch");
+    return ORL_OK;
+}
+
+int orl_partition_by_owner_padded_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                                         const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
+                                         orl_msg_hdr* d_out, uint32_t* d_src, uint64_t* d_counts, void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
+    if (r) return r;
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, d_src,
+                                    d_counts, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "padded partition launch");
     return ORL_OK;
 }
 

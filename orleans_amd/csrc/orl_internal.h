@@ -168,6 +168,7 @@ struct Scratch {
     uint32_t* seg_hist;     // [max segments][2^lb] two-level path: per-segment low-digit counts → bases
     uint32_t* bstart;       // [2049] bucket starts (two-level path)
     uint32_t* sstart;       // [2049] first segment of each bucket
+    uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile
     uint64_t max_batch;
     uint64_t max_tiles;
 };
@@ -183,6 +184,9 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
                                uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out,
                                const Scratch& s, void* stream, void* ev_route_begin, void* ev_route_end);
+int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                            const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
+                            orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

@@ -1097,6 +1097,119 @@ __global__ void k_part_counts(const uint32_t* __restrict__ scanned, uint32_t nti
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Exchange partition in ONE pass: each 2048-message tile loads its headers once,
+// computes every message's destination rank (stages 1-2), ranks them stably per rank (wave_rank), finds
+// its per-rank output base by a decoupled look-back over the tiles before it, and writes every header
+// straight into the per-rank send region r (at d_out + r * stride: the regions are padded to the batch
+// size, so no global total is needed before the scatter).  32 B read + 32 B (+ 4 B source index) written
+// per message, vs 102 B for digits + scan + scatter.
+//
+// Look-back state (zeroed by the launcher before every launch): u32 ticket, u32 error, then one 8-byte
+// granule {tag, count} per (tile, rank): tag 1 = this tile's own count (aggregate), tag 2 = count of this
+// and every earlier tile (inclusive).  Granules are written by ONE 8-B agent-scope store and polled by
+// agent-scope loads (both sc1: cdna_hip_programming.md §6 G16 R2, the data is the flag).  Tiles are
+// numbered by a ticket taken when the workgroup starts, so every tile a look-back waits on has started
+// and publishes its aggregate without waiting on anything: the spin always ends (bounded anyway:
+// on timeout the error word is set and the tile stops waiting).
+constexpr uint32_t kPartItems = 8;
+constexpr uint32_t kPartTile = kRouteThreads * kPartItems;
+constexpr uint32_t kLbSpinLimit = 1u << 24;
+
+struct PartLbSmem {
+    RouteParams P;
+    uint8_t rank_of_silo[256];
+    uint32_t cnt[kWaves][8];   // per-wave running counts, then per-wave bases inside the tile
+    uint32_t base[8];          // exclusive prefix of this tile per rank
+    uint32_t tile;
+};
+
+__device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_t value) {
+    __hip_atomic_store(g, ((uint64_t)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
+                                                           const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
+                                                           uint32_t my_rank, uint32_t nranks, uint64_t stride,
+                                                           orl_msg_hdr* __restrict__ out, uint32_t* __restrict__ src_index,
+                                                           uint32_t* __restrict__ state, uint32_t ntiles,
+                                                           uint64_t* __restrict__ counts) {
+    __shared__ PartLbSmem sm;
+    stage_params(&sm.P, gp);
+    sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
+    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sm.tile = atomicAdd(&state[0], 1u);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = sm.tile;
+    const uint32_t wbase = t * kPartTile + w * (kPartItems * 64u);
+    uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
+    u32x4 h0[kPartItems], h1[kPartItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {  // unconditional (clamped) loads: all in flight together
+        const uint32_t e = wbase + j * 64u + lane;
+        const u32x4* sp = reinterpret_cast<const u32x4*>(in + (e < n ? e : n - 1));
+        h0[j] = __builtin_nontemporal_load(sp);
+        h1[j] = __builtin_nontemporal_load(sp + 1);
+    }
+    uint32_t dig[kPartItems], rank[kPartItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {
+        dig[j] = 0;
+        if (wbase + j * 64u + lane < n) {
+            Msg m;
+            m.tcd = (uint64_t)h0[j].x | ((uint64_t)h0[j].y << 32);
+            m.n0 = (uint64_t)h0[j].z | ((uint64_t)h0[j].w << 32);
+            m.n1 = (uint64_t)h1[j].x | ((uint64_t)h1[j].y << 32);
+            m.meta = h1[j].z;
+            m.aux = h1[j].w;
+            dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+            rank[j] = wave_rank(&sm.cnt[w][0], dig[j]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks) {  // one lane per rank: publish, look back, publish inclusive
+        const uint32_t r = threadIdx.x;
+        uint32_t tc = 0;
+        for (uint32_t q = 0; q < kWaves; ++q) {
+            const uint32_t c = sm.cnt[q][r];
+            sm.cnt[q][r] = tc;
+            tc += c;
+        }
+        store_granule(status + (size_t)t * 8 + r, 1u, tc);
+        uint32_t before = 0;
+        for (int64_t tt = (int64_t)t - 1; tt >= 0; --tt) {
+            uint64_t v;
+            uint32_t spins = 0;
+            while (((v = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0) {
+                if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
+                    atomicOr(&state[1], 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            before += (uint32_t)v;
+            if ((v >> 32) == 2u || spins > kLbSpinLimit) break;
+        }
+        store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
+        sm.base[r] = before;
+        if (t == ntiles - 1) counts[r] = before + tc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e < n) {
+            const uint32_t d = dig[j];
+            const uint64_t g = (uint64_t)d * stride + sm.base[d] + sm.cnt[w][d] + rank[j];
+            u32x4* dp = reinterpret_cast<u32x4*>(out + g);
+            dp[0] = h0[j];
+            dp[1] = h1[j];
+            if (src_index) src_index[g] = e;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
@@ -1335,6 +1448,22 @@ int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_
     hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(256), 0, st, d_in, s.digits, (uint32_t)n, s.tile_hist, ntiles, nranks,
                        d_out, d_src_index);
     hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, s.tile_hist, ntiles, nranks, (uint32_t)n, d_counts);
+    return (int)hipGetLastError();
+}
+
+int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                            const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
+                            orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
+    if (e != hipSuccess || n == 0) return (int)e;
+    const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    const uint32_t ntiles = ceil_div(n, kPartTile);
+    // ticket + error word + one 64-B granule row per tile, zeroed before every launch (16-B multiple)
+    e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ntiles * 64, st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_part_lb, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n, excl,
+                       my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts);
     return (int)hipGetLastError();
 }
 

@@ -309,6 +309,17 @@ class GrainDirectoryEngine:
                                                          int(nranks), int(my_rank), ptr(d_out), ptr(d_src_index),
                                                          ptr(d_counts), ptr(stream)))
 
+    def partition_by_owner_padded_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int,
+                                         my_rank: int, stride: int, d_out, d_counts, d_src_index=None, stream=None,
+                                         opts: int = 0) -> None:
+        """One-pass owner partition into padded per-rank send regions d_out[r * stride:] (the per-target-silo
+        queues of OutboundMessageQueue.SendMessage, OutboundMessageQueue.cs:137-145)."""
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        self._ck(self._lib.orl_partition_by_owner_padded_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(ros),
+                                                                int(nranks), int(my_rank), int(stride), ptr(d_out),
+                                                                ptr(d_src_index), ptr(d_counts), ptr(stream)))
+
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 

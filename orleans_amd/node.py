@@ -1,21 +1,23 @@
 """Multi-GPU silo node: one process per GPU, the directory sharded by ring range.
 
 Per batch (messages originate on the rank that hosts their sending silo):
-  1. stages 1-2 + stable partition of the local batch by the rank holding each message's directory owner
-     (``orl_partition_by_owner_device``);
-  2. all-to-all of the per-rank counts, then all-to-all of the 32-B headers (torch.distributed: RCCL over
-     xGMI on GPUs, gloo on CPU) — the reference's per-target-silo sender queues + TCP
-     (OutboundMessageQueue.cs:113-145) collapsed into one collective;
+  1. stages 1-2 + stable partition of the local batch by the rank holding each message's directory owner,
+     in one pass into padded per-rank send regions (``orl_partition_by_owner_padded_device``);
+  2. all-to-all of the per-rank counts, then grouped send/recv of the 32-B headers (torch.distributed
+     batch_isend_irecv: RCCL over xGMI on GPUs, gloo on CPU) — the reference's per-target-silo sender
+     queues + TCP (OutboundMessageQueue.cs:113-145) collapsed into one grouped exchange;
   3. on the owner rank: stages 1-4 over the received messages (``orl_route_batch_device``).
 Received messages are concatenated in source-rank order and each source's block keeps its arrival
 order, so the per-activation FIFO order is the stable order by (source rank, source index): per-sender
 order holds because a sender's messages all originate on one rank.
 
+PipelinedRouter keeps two batches in flight so the exchange of one overlaps the routing of the previous.
 The exchange logic is independent of what computes the two local steps: ``HipExecutor`` drives the HIP
 library; tests substitute a CPU executor built on the oracle to run the same protocol over gloo.
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 from typing import List, Optional, Protocol, Sequence
 
@@ -27,10 +29,11 @@ HDR_WORDS = 8  # orl_msg_hdr as 8 int32 words (exchange unit)
 
 
 class Executor(Protocol):
-    def partition(self, msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int):
-        """-> (partitioned headers [n, 8] int32, source index [n] int32, counts [nranks] int64)"""
+    def partition(self, msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int, slot: int = 0,
+                  stream=None):
+        """-> (per-rank send regions: list of [>= count_r, 8] int32 tensors, counts [nranks] int64)"""
 
-    def route(self, msgs, n: int):
+    def route(self, msgs, n: int, slot: int = 0, stream=None):
         """-> (route [n], act [n], order [n], offsets [n_act+2]) for the received batch"""
 
 
@@ -46,68 +49,163 @@ class StepResult:
 
 
 class HipExecutor:
-    """Drives liborleans_route.so on this rank's GPU with preallocated device buffers."""
+    """Drives liborleans_route.so on this rank's GPU with preallocated device buffers.
 
-    def __init__(self, eng, capacity: int, torch_mod, device: str = "cuda", opts: int = 0):
+    `part_eng` (default: `eng`) runs the owner partition; giving it its own context (ring only) lets a partition
+    and a route run concurrently on two streams without sharing scratch.  `slots` output sets let the
+    pipelined router keep two batches in flight.  Send regions: `nranks` x `part_capacity` headers per slot
+    (the largest local batch; HBM is plentiful, so the one-pass partition needs no totals first)."""
+
+    def __init__(self, eng, capacity: int, torch_mod, device: str = "cuda", opts: int = 0, part_eng=None,
+                 slots: int = 1, nranks: int = 1, part_capacity: Optional[int] = None):
         t = torch_mod
         self.t = t
         self.eng = eng
+        self.part_eng = part_eng or eng
         self.opts = opts
         self.cap = capacity
-        self.part = t.empty((capacity, HDR_WORDS), dtype=t.int32, device=device)
-        self.src = t.empty(capacity, dtype=t.int32, device=device)
-        self.counts = t.empty(8, dtype=t.int64, device=device)
-        self.route_buf = t.empty(capacity, dtype=t.int32, device=device)
-        self.act = t.empty(capacity, dtype=t.int32, device=device)
-        self.order = t.empty(capacity, dtype=t.int32, device=device)
-        self.offsets = t.empty(eng.n_act + 2, dtype=t.int32, device=device)
+        self.pcap = part_capacity or capacity
+        self.nranks = nranks
+        mk = lambda *shape, dt=t.int32: t.empty(shape, dtype=dt, device=device)  # noqa: E731
+        self.part = [mk(nranks * self.pcap, HDR_WORDS) for _ in range(slots)]
+        self.counts = [mk(8, dt=t.int64) for _ in range(slots)]
+        self.route_buf = [mk(capacity) for _ in range(slots)]
+        self.act = [mk(capacity) for _ in range(slots)]
+        self.order = [mk(capacity) for _ in range(slots)]
+        self.offsets = [mk(eng.n_act + 2) for _ in range(slots)]
 
-    def _stream(self):
-        return self.t.cuda.current_stream().cuda_stream
+    def _stream(self, stream):
+        return (stream or self.t.cuda.current_stream()).cuda_stream
 
-    def partition(self, msgs, n, rank_of_silo, nranks, my_rank):
+    def partition(self, msgs, n, rank_of_silo, nranks, my_rank, slot: int = 0, stream=None):
+        assert n <= self.pcap and nranks <= self.nranks
+        self.part_eng.partition_by_owner_padded_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap,
+                                                       self.part[slot], self.counts[slot],
+                                                       stream=self._stream(stream), opts=self.opts)
+        regions = [self.part[slot][r * self.pcap:(r + 1) * self.pcap] for r in range(nranks)]
+        return regions, self.counts[slot][:nranks]
+
+    def route(self, msgs, n, slot: int = 0, stream=None):
         assert n <= self.cap
-        self.eng.partition_by_owner_device(msgs, n, rank_of_silo, nranks, my_rank, self.part, self.src,
-                                           self.counts, stream=self._stream(), opts=self.opts)
-        return self.part[:n], self.src[:n], self.counts[:nranks]
-
-    def route(self, msgs, n):
-        assert n <= self.cap
-        self.eng.address_messages_device(msgs, n, self.route_buf, self.act, self.order, self.offsets,
-                                         stream=self._stream(), opts=self.opts)
-        return self.route_buf[:n], self.act[:n], self.order[:n], self.offsets
+        self.eng.address_messages_device(msgs, n, self.route_buf[slot], self.act[slot], self.order[slot],
+                                         self.offsets[slot], stream=self._stream(stream), opts=self.opts)
+        return self.route_buf[slot][:n], self.act[slot][:n], self.order[slot][:n], self.offsets[slot]
 
 
-class ShardedRouter:
-    """The exchange protocol of one rank."""
+class PipelinedRouter:
+    """The exchange protocol of one rank, with two batches in flight (overlap the exchange
+    with stages 1-4).
 
-    def __init__(self, executor: Executor, rank: int, world: int, rank_of_silo: Sequence[int], capacity: int,
-                 torch_mod, device: str = "cuda", group=None):
+    submit(batch k) enqueues, in this order:
+      1. route(k-1) on stream R, after the exchange of batch k-1 (its Works' wait() on R);
+      2. owner partition(k) on stream P, after route(k-2) released slot k % 2;
+      3. the all-to-all of the per-rank counts of batch k (the host reads them: the exchange sizes);
+      4. the grouped send/recv of batch k's headers (async; RCCL's stream, after P).
+    So on a GPU the RCCL exchange of batch k overlaps the routing of batch k-1, and the partition of batch
+    k+1 overlaps the exchange of batch k.  submit returns batch k-1's StepResult (None for the first batch);
+    flush() routes the last one; step() = submit + flush (one batch, nothing in flight).  Batch k's outputs
+    live in slot k % 2 and stay valid until submit(k + 2); on a GPU they are complete once stream R is
+    (flush() makes the current stream wait for it).  The executor needs 2 slots and, on a GPU, separate
+    contexts for partition and route (HipExecutor(part_eng=...)).  On the CPU (gloo) it all runs in order."""
+
+    def __init__(self, executor, rank: int, world: int, rank_of_silo: Sequence[int], capacity: int, torch_mod,
+                 device: str = "cuda", group=None):
+        t = torch_mod
         self.ex = executor
         self.rank = rank
         self.world = world
         self.ros = list(rank_of_silo)
-        self.t = torch_mod
+        self.t = t
         self.group = group
-        self.recv = torch_mod.empty((capacity, HDR_WORDS), dtype=torch_mod.int32, device=device)
-        self.recv_counts = torch_mod.empty(world, dtype=torch_mod.int64, device=device)
         self.cap = capacity
+        self.gpu = device != "cpu"
+        self.recv = [t.empty((capacity, HDR_WORDS), dtype=t.int32, device=device) for _ in range(2)]
+        self.recv_counts = [t.empty(world, dtype=t.int64, device=device) for _ in range(2)]
+        if self.gpu:
+            self.sp, self.sr = t.cuda.Stream(), t.cuda.Stream()
+        self.route_done = [None, None]
+        self.pending = None  # (slot, works, exchanged event, n_recv, send_splits, recv_splits)
+        self.k = 0
+
+    def _on(self, stream):
+        return self.t.cuda.stream(stream) if self.gpu else contextlib.nullcontext()
+
+    def _route_pending(self) -> Optional[StepResult]:
+        if self.pending is None:
+            return None
+        slot, works, exchanged, n_recv, send_splits, recv_splits = self.pending
+        self.pending = None
+        with self._on(self.sr if self.gpu else None):
+            for w in works:
+                w.wait()
+            if exchanged is not None:
+                self.sr.wait_event(exchanged)
+            r = self.ex.route(self.recv[slot][:n_recv], n_recv, slot=slot, stream=self.sr if self.gpu else None)
+            if self.gpu:
+                ev = self.t.cuda.Event()
+                ev.record(self.sr)
+                self.route_done[slot] = ev
+        return StepResult(recv_splits, send_splits, *r, n_recv=n_recv)
+
+    def _exchange(self, slot, regions, send_splits, recv_splits):
+        """Grouped send/recv of every rank's region (self: a device copy).  Returns the Works to wait on."""
+        dist = self.t.distributed
+        recv_views, o = [], 0
+        for c in recv_splits:
+            recv_views.append(self.recv[slot][o:o + c])
+            o += c
+        ops = []
+        for r in range(self.world):
+            if r == self.rank:
+                if send_splits[r]:
+                    recv_views[r].copy_(regions[r][:send_splits[r]])
+                continue
+            if send_splits[r]:
+                ops.append(dist.P2POp(dist.isend, regions[r][:send_splits[r]], r, self.group))
+            if recv_splits[r]:
+                ops.append(dist.P2POp(dist.irecv, recv_views[r], r, self.group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def submit(self, msgs, n: int) -> Optional[StepResult]:
+        dist = self.t.distributed
+        slot = self.k % 2
+        self.k += 1
+        prev = self._route_pending()
+        exchanged = None
+        with self._on(self.sp if self.gpu else None):
+            if self.gpu:
+                self.sp.wait_stream(self.t.cuda.current_stream())  # the caller's batch is ready
+                if self.route_done[slot] is not None:
+                    self.sp.wait_event(self.route_done[slot])
+            regions, counts = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot,
+                                                stream=self.sp if self.gpu else None)
+            if self.world == 1:
+                send_splits = recv_splits = [n]
+            else:
+                dist.all_to_all_single(self.recv_counts[slot], counts.contiguous(), group=self.group)
+                send_splits = [int(x) for x in counts.tolist()]
+                recv_splits = [int(x) for x in self.recv_counts[slot].tolist()]
+            n_recv = sum(recv_splits)
+            if n_recv > self.cap:
+                raise RuntimeError(f"rank {self.rank}: received {n_recv} messages > capacity {self.cap}")
+            works = self._exchange(slot, regions, send_splits, recv_splits)
+            if self.gpu:
+                exchanged = self.t.cuda.Event()
+                exchanged.record(self.sp)
+        self.pending = (slot, works, exchanged, n_recv, send_splits, recv_splits)
+        return prev
+
+    def flush(self) -> Optional[StepResult]:
+        r = self._route_pending()
+        if self.gpu:
+            self.t.cuda.current_stream().wait_stream(self.sr)
+        return r
 
     def step(self, msgs, n: int) -> StepResult:
-        dist = self.t.distributed
-        part, _src, counts = self.ex.partition(msgs, n, self.ros, self.world, self.rank)
-        if self.world == 1:
-            r = self.ex.route(part, n)
-            return StepResult([n], [n], *r, n_recv=n)
-        dist.all_to_all_single(self.recv_counts, counts.contiguous(), group=self.group)
-        send_splits = [int(x) for x in counts.tolist()]
-        recv_splits = [int(x) for x in self.recv_counts.tolist()]
-        n_recv = sum(recv_splits)
-        if n_recv > self.cap:
-            raise RuntimeError(f"rank {self.rank}: received {n_recv} messages > capacity {self.cap}")
-        dist.all_to_all_single(self.recv[:n_recv], part, recv_splits, send_splits, group=self.group)
-        r = self.ex.route(self.recv[:n_recv], n_recv)
-        return StepResult(recv_splits, send_splits, *r, n_recv=n_recv)
+        """One batch with nothing in flight (submit + flush)."""
+        assert self.pending is None, "step() with a batch in flight: flush() first"
+        self.submit(msgs, n)
+        return self.flush()
 
 
 def rank_of_silo(n_silos: int, world: int) -> np.ndarray:

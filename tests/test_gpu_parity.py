@@ -207,6 +207,62 @@ def test_partition_by_owner_vs_oracle(torch):
     eng.close()
 
 
+def test_partition_padded_vs_oracle(torch):
+    """One-pass owner partition (decoupled look-back) into padded per-rank regions == the oracle's partition,
+    region by region, for 1..8 ranks, ragged tile tails, complete-address messages, with and without the
+    source-index output; plus a 24M-message batch (11.7k tiles of look-back) checked for counts + stability."""
+    cl, eng, o = _random_setup(10_000, 10_000)
+    t = torch
+    for n in (0, 1, 2047, 2049, 100_003):
+        for nranks in (1, 2, 3, 8):
+            ros = cl.rank_of_silo(nranks) if nranks != 3 else np.array([s % 3 for s in range(8)], np.uint8)
+            my_rank = (n + nranks) % nranks
+            msgs = W.uniform_messages(cl, 11_000, n, seed=my_rank + n)
+            msgs["flags"][::97] = L.HDR_ADDRESS_COMPLETE
+            stride = n + 5
+            d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+            d_out = t.full((nranks * stride, 32), 0xEE, dtype=t.uint8, device="cuda")
+            d_src = t.full((nranks * stride,), -1, dtype=t.int32, device="cuda")
+            d_cnt = t.full((nranks,), -1, dtype=t.int64, device="cuda")
+            eng.partition_by_owner_padded_device(d_in, n, ros, nranks, my_rank, stride, d_out, d_cnt, d_src,
+                                                 stream=t.cuda.current_stream().cuda_stream)
+            t.cuda.synchronize()
+            src, cnt = o.partition(msgs, ros, nranks, my_rank)
+            np.testing.assert_array_equal(d_cnt.cpu().numpy(), cnt.astype(np.int64))
+            out = d_out.cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+            srcs = d_src.cpu().numpy().view(np.uint32)
+            o0 = 0
+            for r in range(nranks):
+                c = int(cnt[r])
+                np.testing.assert_array_equal(out[r * stride:r * stride + c], msgs[src[o0:o0 + c]])
+                np.testing.assert_array_equal(srcs[r * stride:r * stride + c], src[o0:o0 + c])
+                assert (srcs[r * stride + c:(r + 1) * stride] == 0xFFFFFFFF).all()  # nothing past the count
+                o0 += c
+    # large: many look-back tiles, no source index
+    n, nranks = 24_000_000, 8
+    ros = cl.rank_of_silo(nranks)
+    msgs = W.uniform_messages(cl, 11_000, n, seed=5)
+    d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+    eng2 = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=n, device=0)
+    W.setup_engine(eng2, cl)
+    d_out = t.empty((nranks * n, 32), dtype=t.uint8, device="cuda")
+    d_cnt = t.empty((nranks,), dtype=t.int64, device="cuda")
+    for rep in range(2):
+        eng2.partition_by_owner_padded_device(d_in, n, ros, nranks, 3, n, d_out, d_cnt,
+                                              stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    owner = decode_route(o.route(msgs[:2_000_000])[0]).owner
+    cnt = d_cnt.cpu().numpy()
+    assert cnt.sum() == n
+    dest = ros[owner.astype(np.int64)]
+    for r in range(nranks):  # the first 2M messages' share of each region is its head, in order
+        exp = msgs[:2_000_000][dest == r]
+        got = d_out[r * n:r * n + len(exp)].cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+        np.testing.assert_array_equal(got, exp)
+    eng2.close()
+    eng.close()
+
+
 def test_config2_full_size_properties(torch):
     """BASELINE config 2 at full size (1M grains, 64M messages) on the device-resident path."""
     t = torch
@@ -343,4 +399,36 @@ def test_route_batch_graph_replay(torch):
     t.cuda.synchronize()
     for a, b in zip(ref, [x.cpu().numpy() for x in outs] + [off.cpu().numpy()]):
         np.testing.assert_array_equal(a, b)
+    eng.close()
+
+
+def test_pipelined_router_single_rank(torch):
+    """The N>1 code path on one GPU: PipelinedRouter with separate partition / route contexts on two streams,
+    two batches in flight; every batch's results equal the direct call's (world 1: the partition keeps the order)."""
+    from orleans_amd.node import HipExecutor, PipelinedRouter, rank_of_silo
+
+    t = torch
+    cl, eng, o = _random_setup(20_000, 20_000)
+    part_eng = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=1 << 20, device=0)
+    W.setup_engine(part_eng, cl)
+    cap = 300_000
+    router = PipelinedRouter(HipExecutor(eng, cap, t, part_eng=part_eng, slots=2, nranks=1), 0, 1, rank_of_silo(8, 1),
+                             cap, t)
+    batches = [W.uniform_messages(cl, 22_000, 250_000 - 1000 * b, seed=40 + b) for b in range(4)]
+    d_in = [t.from_numpy(m.view(np.int32).reshape(-1, 8)).cuda() for m in batches]
+    got = []
+    for b in range(len(batches) + 1):
+        res = router.submit(d_in[b], len(batches[b])) if b < len(batches) else router.flush()
+        if res is not None:
+            t.cuda.synchronize()
+            got.append([x.cpu().numpy().view(np.uint32).copy() for x in (res.route, res.act, res.order, res.offsets)])
+    assert len(got) == len(batches)
+    for m, (r, a, od, off) in zip(batches, got):
+        r_ref, a_ref = o.route(m)
+        np.testing.assert_array_equal(r, r_ref)
+        np.testing.assert_array_equal(a, a_ref)
+        o_ref, f_ref = o.bucket(a_ref, 20_000)
+        np.testing.assert_array_equal(od, o_ref)
+        np.testing.assert_array_equal(off, f_ref)
+    part_eng.close()
     eng.close()
