@@ -133,23 +133,32 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     zipf = args.config == 3
     n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
     n_msgs = args.msgs
-    cl = W.default_cluster()
+    # balanced ring (silo generations, W.balanced_cluster): the reference's one-point-per-silo ring with
+    # generation-1 silos gives one of 8 GPUs 2.85x the average share
+    cl = W.balanced_cluster()
     ros = rank_of_silo(cl.n_silos, world)
     mine = local_silos(cl.n_silos, world, rank)
-    cap = n_msgs if world == 1 else int(n_msgs * (2.0 if zipf else 1.25))
     t_setup = time.perf_counter()
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    gen = W.zipf_messages if zipf else W.uniform_messages
+    seed = W.SEED_C3 if zipf else W.SEED_C2
+    msgs = gen(cl, n_grains, n_msgs, seed=seed, start=rank * n_msgs, sender_silos=mine if world > 1 else None)
+    cap = n_msgs
+    if world > 1 or args.router:  # exact receive capacity: every rank's per-destination counts, summed
+        dest = ros[owner[msgs["n1"].astype(np.int64)].astype(np.int64)]
+        per_dest = torch.from_numpy(np.bincount(dest, minlength=world).astype(np.int64)).cuda()
+        if world > 1:
+            dist.all_reduce(per_dest)
+        cap = max(n_msgs, int(per_dest.max().item()))
     eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=cap, device=local_rank)
     W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
-    keys, uni, owner, reg = W.grain_population(cl, n_grains)
     local_mask = None
     if world > 1:
         local_mask = np.zeros(cl.n_silos, np.uint8)
         local_mask[mine] = 1
     n_reg = W.register_population(eng, keys, owner, reg, local_mask)
-    log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered; generating {n_msgs} messages")
-    gen = W.zipf_messages if zipf else W.uniform_messages
-    seed = W.SEED_C3 if zipf else W.SEED_C2
-    msgs = gen(cl, n_grains, n_msgs, seed=seed, start=rank * n_msgs, sender_silos=mine if world > 1 else None)
+    log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
+        f"receive capacity {cap}")
     d_msgs = torch.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -218,6 +227,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         "dtype": "u32/u64 integer",
         "data": f"synthetic (seeded splitmix64; config {args.config} of SURVEY §8(d))",
         "config": {"workload": name, "grains": n_grains, "messages_per_gpu": n_msgs, "silos": cl.n_silos,
+                   "ring": "balanced (silo generations %s)" % W.balanced_generations(cl.n_silos),
                    "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -102,8 +102,9 @@ class Cluster:
         return np.array([s * nranks // self.n_silos for s in range(self.n_silos)], np.uint8)
 
 
-def default_cluster(n_silos: int = N_SILOS) -> Cluster:
-    hashes = np.array([silo_consistent_hash(f"10.0.0.{s + 1}:{PORT}", GENERATION) for s in range(n_silos)], np.int32)
+def default_cluster(n_silos: int = N_SILOS, generations=None) -> Cluster:
+    gens = [GENERATION] * n_silos if generations is None else list(generations)
+    hashes = np.array([silo_consistent_hash(f"10.0.0.{s + 1}:{PORT}", gens[s]) for s in range(n_silos)], np.int32)
     # replay AddServer in silo-index order: insert at FindLastIndex(h < hash) + 1 (LocalGrainDirectory.cs:259-261)
     ring = []
     for s in range(n_silos):
@@ -209,6 +210,29 @@ def powerlaw_csr(n_nodes: int, exponent: float = 2.1, dmin: int = 1, dmax: int =
     e = int(off[-1])
     tgt = (stream(seed ^ 0xF011, 0, e) % np.uint64(n_nodes)).astype(np.uint32)
     return off, tgt
+
+
+def balanced_generations(n_silos: int = N_SILOS, tol: float = 0.004) -> list:
+    """Smallest silo generations >= 1 that put silo s's ring point within +-tol of s/n of the hash ring.
+
+    The reference's directory ring has ONE point per silo (LocalGrainDirectory.AddServer, :243-268), so with
+    generation-1 silos the 8 arcs are 0.4 % .. 35.7 % of the ring (a GPU hosting one silo would receive up to
+    2.85x the average share at 8 GPUs).  Silo generations are deployment timestamps (SiloAddress.Generation),
+    so choosing them is a deployment choice: the multi-GPU bench uses this balanced ring so weak scaling
+    measures the engine, not the accident of 8 random ring points."""
+    out = []
+    span = 1 << 32
+    for s in range(n_silos):
+        target = -(1 << 31) + s * span // n_silos + span // (2 * n_silos)
+        g = 1
+        while abs(silo_consistent_hash(f"10.0.0.{s + 1}:{PORT}", g) - target) > tol * span:
+            g += 1
+        out.append(g)
+    return out
+
+
+def balanced_cluster(n_silos: int = N_SILOS) -> Cluster:
+    return default_cluster(n_silos, balanced_generations(n_silos))
 
 
 # ---- config 5: Presence heartbeats (Samples/Presence) ------------------------------------------------------
