@@ -84,6 +84,18 @@ typedef struct orl_msg_hdr {
     uint32_t aux;           /* precomputed uniform hash when ORL_HDR_HASH_VALID */
 } orl_msg_hdr;
 
+/* Compact 16-byte exchange record (multi-GPU wire format) for the common key shape: N0 == 0 and
+ * TypeCodeData = (grain category << 56) + sign-extended 32-bit type code (UniqueKey.NewKey, UniqueKey.cs:131-152:
+ * every long-key grain, GrainId.GetGrainId(int typeCode, long key), GrainId.cs:90-97).  meta packs
+ * sending_silo (bits 0-7), message category (8-9), header flags (10-15; ORL_HDR_HASH_VALID not allowed:
+ * the hash is recomputed), grain category (16-23) and target_silo (24-31).  Lossless: decoding gives back
+ * the 32-byte orl_msg_hdr (aux = 0). */
+typedef struct orl_wire_msg {
+    uint64_t n1;
+    uint32_t type_code_lo;  /* low 32 bits of TypeCodeData */
+    uint32_t meta;
+} orl_wire_msg;
+
 /* ---- Per-message route word ---------------------------------------------------------------
  * bits 0-7 directory owner silo, 8-15 target (host) silo, 16-23 ORL_ST_*, 24-31 ORL_RF_*      */
 #define ORL_ST_HIT 0u                  /* single activation found on a functional silo */
@@ -229,6 +241,16 @@ int orl_partition_by_owner_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t 
 int orl_partition_by_owner_padded_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                                          const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
                                          orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, void* stream);
+/* As orl_partition_by_owner_padded_device, writing 16-byte orl_wire_msg records (half the exchange
+ * bytes).  *d_status (device u32) is set to 0, or to 1 if some message of the batch has no compact form
+ * (then the records are invalid and the caller uses the 32-byte form for this batch). */
+int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                                 const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
+                                 orl_wire_msg* d_out, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_status,
+                                 void* stream);
+/* orl_route_batch_device over received compact records (the owner side of the exchange). */
+int orl_route_compact_device(orl_ctx* ctx, const orl_wire_msg* d_in, size_t n, uint32_t opts, uint32_t* d_route,
+                             uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
 
 int orl_sync(orl_ctx* ctx);
 

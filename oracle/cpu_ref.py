@@ -180,3 +180,40 @@ def fanout_expand(csr_off: np.ndarray, csr_tgt: np.ndarray, pubs: np.ndarray, pu
     lib.ref_fanout_expand(_p(csr_off), _p(csr_tgt), _p(pubs), _p(pub_silo), len(pubs), follower_tcd, _p(out), n,
                           _p(poff))
     return out, poff
+
+
+# ---- compact exchange record (orl_wire_msg, include/orleans_route.h) --------------------------------------
+# Independent numpy restatement of the 16-byte wire codec, used to check the GPU encoder / decoder.
+# Compact form exists iff N0 == 0 and TypeCodeData = (category << 56) + sign-extended int type code
+# (UniqueKey.NewKey, UniqueKey.cs:131-152), message category < 4, flags < 64 without HASH_VALID.
+WIRE_DTYPE = np.dtype([("n1", "<u8"), ("type_code_lo", "<u4"), ("meta", "<u4")])
+_LOW56 = np.uint64(0x00FFFFFFFFFFFFFF)
+
+
+def wire_encode(msgs: np.ndarray):
+    """-> (records, compactable mask)."""
+    tcd = msgs["tcd"].astype(np.uint64)
+    lo = (tcd & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    sext = lo.view(np.int32).astype(np.int64).view(np.uint64) & _LOW56
+    ok = (msgs["n0"] == 0) & ((tcd & _LOW56) == sext) & (msgs["category"] < 4) & (msgs["flags"] < 64) & \
+         ((msgs["flags"] & 0x02) == 0)
+    r = np.zeros(len(msgs), WIRE_DTYPE)
+    r["n1"] = msgs["n1"]
+    r["type_code_lo"] = lo
+    r["meta"] = (msgs["sending_silo"].astype(np.uint32) | (msgs["category"].astype(np.uint32) << 8) |
+                 (msgs["flags"].astype(np.uint32) << 10) | ((tcd >> np.uint64(56)).astype(np.uint32) << 16) |
+                 (msgs["target_silo"].astype(np.uint32) << 24))
+    return r, ok
+
+
+def wire_decode(recs: np.ndarray) -> np.ndarray:
+    m = np.zeros(len(recs), MSG_DTYPE)
+    meta = recs["meta"].astype(np.uint32)
+    sext = recs["type_code_lo"].view(np.int32).astype(np.int64).view(np.uint64) & _LOW56
+    m["tcd"] = (((meta >> 16) & 0xFF).astype(np.uint64) << np.uint64(56)) | sext
+    m["n1"] = recs["n1"]
+    m["sending_silo"] = (meta & 0xFF).astype(np.uint8)
+    m["category"] = ((meta >> 8) & 0x3).astype(np.uint8)
+    m["flags"] = ((meta >> 10) & 0x3F).astype(np.uint8)
+    m["target_silo"] = (meta >> 24).astype(np.uint8)
+    return m

@@ -587,8 +587,9 @@ int orl_hash_batch(orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* ou
     return ORL_OK;
 }
 
-int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
-                           uint32_t* d_order, uint32_t* d_off, void* stream) {
+namespace {
+int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+               uint32_t* d_order, uint32_t* d_off, void* stream) {
     if (!c) return ORL_E_INVALID;
     if (n && (!d_in || !d_route || !d_act)) return fail(c, ORL_E_INVALID, "null device buffer");
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
@@ -601,11 +602,22 @@ int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32
     hipEvent_t* ev = nullptr;
     if (c->timing && n > 0 && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
-    int e = launch_route_bucket(c->d_params, c->d_table, c->mask, d_in, n, opts, c->cfg.n_act, d_route, d_act, d_order, d_off,
-                                c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
+    int e = launch_route_bucket(c->d_params, c->d_table, c->mask, d_in, wire, n, opts, c->cfg.n_act, d_route, d_act, d_order,
+                                d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e) return hipfail(c, (hipError_t)e, "route launch");
     if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
     return ORL_OK;
+}
+}  // namespace
+
+int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                           uint32_t* d_order, uint32_t* d_off, void* stream) {
+    return route_impl(c, d_in, false, n, opts, d_route, d_act, d_order, d_off, stream);
+}
+
+int orl_route_compact_device(orl_ctx* c, const orl_wire_msg* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                             uint32_t* d_order, uint32_t* d_off, void* stream) {
+    return route_impl(c, d_in, true, n, opts, d_route, d_act, d_order, d_off, stream);
 }
 
 int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
@@ -734,9 +746,24 @@ int orl_partition_by_owner_padded_device(orl_ctx* c, const orl_msg_hdr* d_in, si
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
     if (r) return r;
-    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, d_src,
-                                    d_counts, c->s, st);
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, false, d_src,
+                                    d_counts, nullptr, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "padded partition launch");
+    return ORL_OK;
+}
+
+int orl_partition_compact_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                 uint32_t nranks, uint32_t my_rank, size_t stride, orl_wire_msg* d_out, uint32_t* d_src,
+                                 uint64_t* d_counts, uint32_t* d_status, void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
+    if (!d_status) return fail(c, ORL_E_INVALID, "null status word");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
+    if (r) return r;
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, true, d_src,
+                                    d_counts, d_status, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "compact partition launch");
     return ORL_OK;
 }
 

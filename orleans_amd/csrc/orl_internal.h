@@ -175,7 +175,7 @@ struct Scratch {
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
 int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
-                        const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
+                        const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
                         void* ev_route_begin, void* ev_route_end);
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
@@ -186,7 +186,8 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
                                const Scratch& s, void* stream, void* ev_route_begin, void* ev_route_end);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
-                            orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);
+                            void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
+                            const Scratch& s, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

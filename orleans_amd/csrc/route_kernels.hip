@@ -81,6 +81,35 @@ __device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint
     return m;
 }
 
+// Compact 16-B exchange record (orl_wire_msg, include/orleans_route.h): {n1, type code lo, meta'}.
+__device__ __forceinline__ Msg load_wire(const orl_wire_msg* __restrict__ in, uint32_t e) {
+    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + e));
+    const uint32_t meta = a.w;
+    Msg m;
+    m.tcd = ((uint64_t)((meta >> 16) & 0xFFu) << 56) | ((uint64_t)(int64_t)(int32_t)a.z & 0x00FFFFFFFFFFFFFFull);
+    m.n0 = 0;
+    m.n1 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    m.meta = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) | (meta & 0xFF000000u);
+    m.aux = 0;
+    return m;
+}
+
+// Encode a header as a wire record; false when it has no compact form (N0 != 0, a type-code-data that is
+// not category + sign-extended int, a precomputed hash to carry, or flag/category bits out of range).
+__device__ __forceinline__ bool encode_wire(const u32x4& h0, const u32x4& h1, u32x4& w) {
+    const uint64_t tcd = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    const uint32_t meta = h1.z;
+    const uint32_t cat = (meta >> 8) & 0xFFu, fl = (meta >> 16) & 0xFFu;
+    const bool ok = h0.z == 0 && h0.w == 0 &&
+                    (tcd & 0x00FFFFFFFFFFFFFFull) == ((uint64_t)(int64_t)(int32_t)h0.x & 0x00FFFFFFFFFFFFFFull) &&
+                    cat < 4 && fl < 64 && !(fl & ORL_HDR_HASH_VALID);
+    w.x = h1.x;
+    w.y = h1.y;
+    w.z = h0.x;
+    w.w = (meta & 0xFFu) | (cat << 8) | (fl << 10) | ((uint32_t)(tcd >> 56) << 16) | (meta & 0xFF000000u);
+    return ok;
+}
+
 // Stages 1-3 for one message, split so a thread can keep several messages' directory probes in flight:
 //   route_head  stages 1-2 + every decision that needs no directory (returns the final route word, or
 //               kNeedProbe when the owner's partition is local and must be probed);
@@ -203,9 +232,10 @@ struct RouteSmem {
     uint32_t hist[1u << kMaxDigitBits];
 };
 
-template <bool HIST>
+// WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
+template <bool HIST, bool WIRE>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
-                                                         uint64_t mask, const orl_msg_hdr* __restrict__ in, uint32_t n,
+                                                         uint64_t mask, const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
                                                          uint32_t bins, uint32_t shift, uint32_t items) {
@@ -220,7 +250,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
         Msg m;
-        if (e < n) m = load_hdr(in, e);
+        if (e < n) m = WIRE ? load_wire(static_cast<const orl_wire_msg*>(in), e) : load_hdr(static_cast<const orl_msg_hdr*>(in), e);
         uint32_t h = 0, own = 0, rf = 0, r = 0;
         uint64_t slot = 0;
         u32x4 sa, sb;
@@ -1127,12 +1157,14 @@ __device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_
     __hip_atomic_store(g, ((uint64_t)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// COMPACT: write orl_wire_msg records (16 B) and set *wire_status = 1 if a message has no compact form.
+template <bool COMPACT>
 __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
-                                                           orl_msg_hdr* __restrict__ out, uint32_t* __restrict__ src_index,
+                                                           void* __restrict__ out, uint32_t* __restrict__ src_index,
                                                            uint32_t* __restrict__ state, uint32_t ntiles,
-                                                           uint64_t* __restrict__ counts) {
+                                                           uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status) {
     __shared__ PartLbSmem sm;
     stage_params(&sm.P, gp);
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
@@ -1201,9 +1233,15 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
         if (e < n) {
             const uint32_t d = dig[j];
             const uint64_t g = (uint64_t)d * stride + sm.base[d] + sm.cnt[w][d] + rank[j];
-            u32x4* dp = reinterpret_cast<u32x4*>(out + g);
-            dp[0] = h0[j];
-            dp[1] = h1[j];
+            if (COMPACT) {
+                u32x4 wr;
+                if (!encode_wire(h0[j], h1[j], wr)) atomicOr(wire_status, 1u);
+                reinterpret_cast<u32x4*>(out)[g] = wr;
+            } else {
+                u32x4* dp = reinterpret_cast<u32x4*>(static_cast<orl_msg_hdr*>(out) + g);
+                dp[0] = h0[j];
+                dp[1] = h1[j];
+            }
             if (src_index) src_index[g] = e;
         }
     }
@@ -1360,7 +1398,7 @@ int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* st
     return (int)hipGetLastError();
 }
 
-int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const orl_msg_hdr* d_in,
+int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const void* d_in, bool wire,
                         size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                         uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
     hipStream_t st = (hipStream_t)stream;
@@ -1374,12 +1412,17 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
-    if (buckets && rh.on)
-        hipLaunchKernelGGL(k_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, s.tile_hist, rh.bins, rh.shift, items);
-    else
-        hipLaunchKernelGGL(k_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in,
-                           (uint32_t)n, excl, d_route, d_act, nullptr, 1u, 0u, items);
+    const bool hist = buckets && rh.on;
+    uint32_t* th = hist ? s.tile_hist : nullptr;
+    const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
+#define ORL_ROUTE(H, W) hipLaunchKernelGGL((k_route<H, W>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in, \
+                                           (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
+    if (hist) {
+        if (wire) ORL_ROUTE(true, true); else ORL_ROUTE(true, false);
+    } else {
+        if (wire) ORL_ROUTE(false, true); else ORL_ROUTE(false, false);
+    }
+#undef ORL_ROUTE
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();
     if (e) return e;
@@ -1453,17 +1496,23 @@ int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_
 
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
-                            orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream) {
+                            void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
+                            const Scratch& s, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
+    if (e == hipSuccess && compact) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
     if (e != hipSuccess || n == 0) return (int)e;
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
     const uint32_t ntiles = ceil_div(n, kPartTile);
     // ticket + error word + one 64-B granule row per tile, zeroed before every launch (16-B multiple)
     e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ntiles * 64, st);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_part_lb, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n, excl,
-                       my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts);
+    if (compact)
+        hipLaunchKernelGGL(k_part_lb<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
+                           excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, d_wire_status);
+    else
+        hipLaunchKernelGGL(k_part_lb<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
+                           excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, d_wire_status);
     return (int)hipGetLastError();
 }
 

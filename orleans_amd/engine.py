@@ -320,6 +320,23 @@ class GrainDirectoryEngine:
                                                                 int(nranks), int(my_rank), int(stride), ptr(d_out),
                                                                 ptr(d_src_index), ptr(d_counts), ptr(stream)))
 
+    def partition_compact_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
+                                 stride: int, d_out, d_counts, d_status, d_src_index=None, stream=None,
+                                 opts: int = 0) -> None:
+        """partition_by_owner_padded_device writing 16-B orl_wire_msg records; d_status[0] = 1 if a message
+        of the batch has no compact form (the caller then uses the 32-B form for this batch)."""
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        self._ck(self._lib.orl_partition_compact_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(ros), int(nranks),
+                                                        int(my_rank), int(stride), ptr(d_out), ptr(d_src_index),
+                                                        ptr(d_counts), ptr(d_status), ptr(stream)))
+
+    def address_compact_device(self, d_recs, n: int, d_route, d_act, d_order=None, d_offsets=None, stream=None,
+                               opts: int = 0) -> None:
+        """address_messages_device over compact exchange records (orl_wire_msg)."""
+        self._ck(self._lib.orl_route_compact_device(self._ctx, ptr(d_recs), int(n), int(opts), ptr(d_route), ptr(d_act),
+                                                    ptr(d_order), ptr(d_offsets), ptr(stream)))
+
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 

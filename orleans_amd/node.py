@@ -25,16 +25,21 @@ import numpy as np
 
 from . import _lib as L
 
-HDR_WORDS = 8  # orl_msg_hdr as 8 int32 words (exchange unit)
+HDR_WORDS = 8   # orl_msg_hdr as 8 int32 words
+WIRE_WORDS = 4  # orl_wire_msg (compact exchange record) as 4 int32 words
+
+
+HEAD_LEN = 9     # partition head: per-rank counts at [0, nranks), wire status at [8]
 
 
 class Executor(Protocol):
     def partition(self, msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int, slot: int = 0,
-                  stream=None):
-        """-> (per-rank send regions: list of [>= count_r, 8] int32 tensors, counts [nranks] int64)"""
+                  stream=None, compact: bool = True):
+        """-> (per-rank send regions: list of [>= count_r, W] int32 tensors (W = 8: orl_msg_hdr, 4: orl_wire_msg),
+               head: int64 [HEAD_LEN] = per-rank counts, then at [8] 1 if the batch has no compact form)"""
 
     def route(self, msgs, n: int, slot: int = 0, stream=None):
-        """-> (route [n], act [n], order [n], offsets [n_act+2]) for the received batch"""
+        """-> (route [n], act [n], order [n], offsets [n_act+2]) for the received records ([n, W] int32)"""
 
 
 @dataclass
@@ -53,11 +58,12 @@ class HipExecutor:
 
     `part_eng` (default: `eng`) runs the owner partition; giving it its own context (ring only) lets a partition
     and a route run concurrently on two streams without sharing scratch.  `slots` output sets let the
-    pipelined router keep two batches in flight.  Send regions: `nranks` x `part_capacity` headers per slot
-    (the largest local batch; HBM is plentiful, so the one-pass partition needs no totals first)."""
+    pipelined router keep two batches in flight.  Send regions: `nranks` x `part_capacity` records per slot
+    (the largest local batch; HBM is plentiful, so the one-pass partition needs no totals first).  `compact`
+    sends 16-B orl_wire_msg records (half the exchange bytes) whenever the batch has that form."""
 
     def __init__(self, eng, capacity: int, torch_mod, device: str = "cuda", opts: int = 0, part_eng=None,
-                 slots: int = 1, nranks: int = 1, part_capacity: Optional[int] = None):
+                 slots: int = 1, nranks: int = 1, part_capacity: Optional[int] = None, compact: bool = True):
         t = torch_mod
         self.t = t
         self.eng = eng
@@ -66,9 +72,10 @@ class HipExecutor:
         self.cap = capacity
         self.pcap = part_capacity or capacity
         self.nranks = nranks
+        self.compact = compact
         mk = lambda *shape, dt=t.int32: t.empty(shape, dtype=dt, device=device)  # noqa: E731
-        self.part = [mk(nranks * self.pcap, HDR_WORDS) for _ in range(slots)]
-        self.counts = [mk(8, dt=t.int64) for _ in range(slots)]
+        self.part = [mk(nranks * self.pcap * HDR_WORDS) for _ in range(slots)]  # flat: either record width
+        self.head = [mk(HEAD_LEN, dt=t.int64) for _ in range(slots)]
         self.route_buf = [mk(capacity) for _ in range(slots)]
         self.act = [mk(capacity) for _ in range(slots)]
         self.order = [mk(capacity) for _ in range(slots)]
@@ -77,18 +84,29 @@ class HipExecutor:
     def _stream(self, stream):
         return (stream or self.t.cuda.current_stream()).cuda_stream
 
-    def partition(self, msgs, n, rank_of_silo, nranks, my_rank, slot: int = 0, stream=None):
+    def partition(self, msgs, n, rank_of_silo, nranks, my_rank, slot: int = 0, stream=None, compact: bool = True):
         assert n <= self.pcap and nranks <= self.nranks
-        self.part_eng.partition_by_owner_padded_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap,
-                                                       self.part[slot], self.counts[slot],
-                                                       stream=self._stream(stream), opts=self.opts)
-        regions = [self.part[slot][r * self.pcap:(r + 1) * self.pcap] for r in range(nranks)]
-        return regions, self.counts[slot][:nranks]
+        head = self.head[slot]
+        st = self._stream(stream)
+        wide = not (compact and self.compact)
+        width = HDR_WORDS if wide else WIRE_WORDS
+        out = self.part[slot][:nranks * self.pcap * width].view(-1, width)
+        if wide:
+            self.part_eng.partition_by_owner_padded_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap, out,
+                                                           head, stream=st, opts=self.opts)
+            head[8:].zero_()
+        else:
+            head[8:].zero_()  # the kernel sets the low word of [8]
+            self.part_eng.partition_compact_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap, out, head,
+                                                   head[8:], stream=st, opts=self.opts)
+        regions = [out[r * self.pcap:(r + 1) * self.pcap] for r in range(nranks)]
+        return regions, head
 
     def route(self, msgs, n, slot: int = 0, stream=None):
         assert n <= self.cap
-        self.eng.address_messages_device(msgs, n, self.route_buf[slot], self.act[slot], self.order[slot],
-                                         self.offsets[slot], stream=self._stream(stream), opts=self.opts)
+        fn = self.eng.address_compact_device if msgs.shape[1] == WIRE_WORDS else self.eng.address_messages_device
+        fn(msgs, n, self.route_buf[slot], self.act[slot], self.order[slot], self.offsets[slot],
+           stream=self._stream(stream), opts=self.opts)
         return self.route_buf[slot][:n], self.act[slot][:n], self.order[slot][:n], self.offsets[slot]
 
 
@@ -99,8 +117,9 @@ class PipelinedRouter:
     submit(batch k) enqueues, in this order:
       1. route(k-1) on stream R, after the exchange of batch k-1 (its Works' wait() on R);
       2. owner partition(k) on stream P, after route(k-2) released slot k % 2;
-      3. the all-to-all of the per-rank counts of batch k (the host reads them: the exchange sizes);
-      4. the grouped send/recv of batch k's headers (async; RCCL's stream, after P).
+      3. an all-gather of every rank's per-rank counts and wire status (the host reads them: the exchange
+         sizes, and whether the batch travels as 16-B compact records or, if any rank cannot, as 32-B headers);
+      4. the grouped send/recv of batch k's records (async; RCCL's stream, after P).
     So on a GPU the RCCL exchange of batch k overlaps the routing of batch k-1, and the partition of batch
     k+1 overlaps the exchange of batch k.  submit returns batch k-1's StepResult (None for the first batch);
     flush() routes the last one; step() = submit + flush (one batch, nothing in flight).  Batch k's outputs
@@ -119,8 +138,9 @@ class PipelinedRouter:
         self.group = group
         self.cap = capacity
         self.gpu = device != "cpu"
-        self.recv = [t.empty((capacity, HDR_WORDS), dtype=t.int32, device=device) for _ in range(2)]
-        self.recv_counts = [t.empty(world, dtype=t.int64, device=device) for _ in range(2)]
+        self.recv_flat = [t.empty(capacity * HDR_WORDS, dtype=t.int32, device=device) for _ in range(2)]
+        self.recv = [None, None]  # [n_recv, W] view of the received records of each slot
+        self.heads = [t.empty((world, HEAD_LEN), dtype=t.int64, device=device) for _ in range(2)]
         if self.gpu:
             self.sp, self.sr = t.cuda.Stream(), t.cuda.Stream()
         self.route_done = [None, None]
@@ -140,7 +160,7 @@ class PipelinedRouter:
                 w.wait()
             if exchanged is not None:
                 self.sr.wait_event(exchanged)
-            r = self.ex.route(self.recv[slot][:n_recv], n_recv, slot=slot, stream=self.sr if self.gpu else None)
+            r = self.ex.route(self.recv[slot], n_recv, slot=slot, stream=self.sr if self.gpu else None)
             if self.gpu:
                 ev = self.t.cuda.Event()
                 ev.record(self.sr)
@@ -177,17 +197,25 @@ class PipelinedRouter:
                 self.sp.wait_stream(self.t.cuda.current_stream())  # the caller's batch is ready
                 if self.route_done[slot] is not None:
                     self.sp.wait_event(self.route_done[slot])
-            regions, counts = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot,
-                                                stream=self.sp if self.gpu else None)
+            st = self.sp if self.gpu else None
+            regions, head = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot, stream=st)
+            # every rank's counts + wire status in one collective: the exchange sizes, and whether all ranks
+            # can send compact records this batch (if one cannot, everyone re-partitions in the 32-B form)
             if self.world == 1:
-                send_splits = recv_splits = [n]
+                heads = [[int(x) for x in head.tolist()]]
             else:
-                dist.all_to_all_single(self.recv_counts[slot], counts.contiguous(), group=self.group)
-                send_splits = [int(x) for x in counts.tolist()]
-                recv_splits = [int(x) for x in self.recv_counts[slot].tolist()]
+                dist.all_gather_into_tensor(self.heads[slot], head.contiguous().view(1, -1), group=self.group)
+                heads = self.heads[slot].tolist()
+            if any(h[8] for h in heads):
+                regions, head = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot, stream=st,
+                                                  compact=False)
+            send_splits = [int(x) for x in heads[self.rank][:self.world]]
+            recv_splits = [int(h[self.rank]) for h in heads]
             n_recv = sum(recv_splits)
             if n_recv > self.cap:
                 raise RuntimeError(f"rank {self.rank}: received {n_recv} messages > capacity {self.cap}")
+            width = regions[0].shape[1]
+            self.recv[slot] = self.recv_flat[slot][:n_recv * width].view(n_recv, width)
             works = self._exchange(slot, regions, send_splits, recv_splits)
             if self.gpu:
                 exchanged = self.t.cuda.Event()

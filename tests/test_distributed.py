@@ -17,31 +17,48 @@ import torch.multiprocessing as mp
 from oracle import cpu_ref
 from orleans_amd import _lib as L
 from orleans_amd import workloads as W
-from orleans_amd.node import PipelinedRouter, local_silos, rank_of_silo
+from orleans_amd.node import HEAD_LEN, PipelinedRouter, local_silos, rank_of_silo
 
 N_GRAINS = 3000
 N_MSGS = 5000
 
 
 class OracleExecutor:
-    """CPU stand-in for HipExecutor: same contract, computed by the oracle (test only)."""
+    """CPU stand-in for HipExecutor: same contract, computed by the oracle (test only).  With compact=True the
+    regions are 16-B wire records (oracle restatement of the codec) whenever the whole batch has that form."""
 
-    def __init__(self, oracle, n_act):
+    def __init__(self, oracle, n_act, compact=False):
         self.o = oracle
         self.n_act = n_act
+        self.compact = compact
 
-    def partition(self, msgs, n, ros, nranks, my_rank, slot=0, stream=None):
+    def partition(self, msgs, n, ros, nranks, my_rank, slot=0, stream=None, compact=True):
         m = msgs[:n].numpy().reshape(-1).view(L.MSG_DTYPE)
         src, counts = self.o.partition(m, ros, nranks, my_rank)
-        part = torch.from_numpy(m[src].view(np.int32).reshape(-1, 8).copy())
-        regions = list(torch.split(part, [int(c) for c in counts]))
-        return regions, torch.from_numpy(counts.astype(np.int64))
+        head = torch.zeros(HEAD_LEN, dtype=torch.int64)
+        head[:nranks] = torch.from_numpy(counts.astype(np.int64))
+        rec = m[src]
+        width = 8
+        if self.compact and compact:
+            w, ok = cpu_ref.wire_encode(rec)
+            head[8] = int(not ok.all())
+            rec, width = w, 4
+        part = torch.from_numpy(rec.view(np.int32).reshape(-1, width).copy())
+        return list(torch.split(part, [int(c) for c in counts])), head
 
     def route(self, msgs, n, slot=0, stream=None):
-        m = msgs[:n].numpy().reshape(-1).view(L.MSG_DTYPE)
+        rec = msgs[:n].numpy().reshape(-1)
+        m = cpu_ref.wire_decode(rec.view(cpu_ref.WIRE_DTYPE)) if msgs.shape[1] == 4 else rec.view(L.MSG_DTYPE)
         r, a = self.o.route(m)
         order, off = self.o.bucket(a, self.n_act)
         return r, a, order, off
+
+
+def _received(router, slot, n_recv):
+    rec = router.recv[slot][:n_recv].numpy().reshape(-1)
+    if router.recv[slot].shape[1] == 4:
+        return cpu_ref.wire_decode(rec.view(cpu_ref.WIRE_DTYPE))
+    return rec.view(L.MSG_DTYPE).copy()
 
 
 def _free_port():
@@ -83,30 +100,35 @@ def _worker(rank, world, port, q):
         msgs = W.uniform_messages(cl, N_GRAINS + 200, N_MSGS, seed=99, start=rank * N_MSGS, sender_silos=mine)
         router = PipelinedRouter(OracleExecutor(o, N_GRAINS), rank, world, ros, 4 * N_MSGS, torch, device="cpu")
         res = router.step(torch.from_numpy(msgs.view(np.int32).reshape(-1, 8).copy()), N_MSGS)
-        recv = router.recv[0][:res.n_recv].numpy().reshape(-1).view(L.MSG_DTYPE).copy()
+        recv = _received(router, 0, res.n_recv)
         q.put((rank, [_result_tuple(msgs, res, recv)]))
     finally:
         dist.destroy_process_group()
 
 
-def _worker_pipelined(rank, world, port, q, n_batches=3):
+def _worker_pipelined(rank, world, port, q, n_batches=3, compact=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cl, ros, mine, o = _setup_rank(rank, world)
-        router = PipelinedRouter(OracleExecutor(o, N_GRAINS), rank, world, ros, 4 * N_MSGS, torch, device="cpu")
+        router = PipelinedRouter(OracleExecutor(o, N_GRAINS, compact=compact), rank, world, ros, 4 * N_MSGS, torch,
+                                 device="cpu")
         batches = [W.uniform_messages(cl, N_GRAINS + 200, N_MSGS - 97 * b, seed=99 + b, start=(rank * 7 + b) * N_MSGS,
                                       sender_silos=mine) for b in range(n_batches)]
+        if rank == 1:  # batch 1 of rank 1 has a Guid-keyed (N0 != 0) message: every rank sends 32-B headers
+            batches[1]["n0"][17] = 5
+        widths = []
         outs = []
         for b, m in enumerate(batches + [None]):
             res = router.submit(torch.from_numpy(m.view(np.int32).reshape(-1, 8).copy()), len(m)) if m is not None \
                 else router.flush()
-            if b > 0:  # result of batch b-1; its received headers are still in slot (b-1) % 2
-                recv = router.recv[(b - 1) % 2][:res.n_recv].numpy().reshape(-1).view(L.MSG_DTYPE).copy()
-                outs.append(_result_tuple(batches[b - 1], res, recv))
+            if b > 0:  # result of batch b-1; its received records are still in slot (b-1) % 2
+                widths.append(router.recv[(b - 1) % 2].shape[1])
+                outs.append(_result_tuple(batches[b - 1], res, _received(router, (b - 1) % 2, res.n_recv)))
             else:
                 assert res is None
+        assert widths == ([4, 8, 4] if compact else [8, 8, 8]), widths
         q.put((rank, outs))
     finally:
         dist.destroy_process_group()
