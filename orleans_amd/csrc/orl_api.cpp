@@ -386,8 +386,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         const uint64_t seg_rows = std::max<uint64_t>(max_segments(mb, bp.hb), max_segments(std::min<uint64_t>(mb, (16u << 20) - 1), bp.hb));
         const uint64_t seg_words = bp.two_level ? seg_rows << bp.lb : 1;
         if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
-        if ((e = hipMalloc((void**)&c->s.bstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
-        if ((e = hipMalloc((void**)&c->s.sstart, 2049 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
+        if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
+        if ((e = hipMalloc((void**)&c->s.sstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)

@@ -210,7 +210,17 @@ __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { r
 // profiles/r01_rank_lab.txt): identical ranks to the BITS-ballot match over 4 x 64M elements (uniform,
 // 50 % on 8 hot digits, all-equal, 4 distinct) at 1.8x its speed; every GPU parity test re-checks it
 // bit-exactly against the oracle.  Exec-masked (inactive) lanes do not count.
-__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) { return atomicAdd(&wave_cnt[d], 1u); }
+// The counters are packed two per LDS word (digit d: word d >> 1, bits 16 * (d & 1)); a wave ranks at most 1024
+// elements per round, so a half never carries into its neighbour, and 12-bit digits fit the LDS.
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) {
+    const uint32_t sh = (d & 1u) << 4;
+    return (atomicAdd(&wave_cnt[d >> 1], 1u << sh) >> sh) & 0xFFFFu;
+}
+
+// Unpacked form (one counter per word) for the few-digit exchange partition.
+__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d) { return atomicAdd(&wave_cnt[d], 1u); }
+
+__device__ __forceinline__ uint32_t packed_get(const uint32_t* row, uint32_t d) { return (row[d >> 1] >> ((d & 1u) << 4)) & 0xFFFFu; }
 
 // ---------------------------------------------------------------------------------------------------
 // stage 1 alone
@@ -227,19 +237,22 @@ __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ 
 // 4 messages per thread to keep 4 probes in flight per lane needs 134 VGPRs = 3 waves/SIMD and ran 1.6x
 // slower: profiles/r01_route_variants.txt.)  The probe chain is continued by a flag loop in the same
 // basic block as the first probe (an early-return helper loop for the chain cost 13 %: 1.76 vs 1.56 ms).
+// HB: capacity of the fused digit histogram in bits (0: none; 11 or 12 so the LDS is sized for the digit).
+template <int HB>
 struct RouteSmem {
     RouteParams P;
-    uint32_t hist[1u << kMaxDigitBits];
+    uint32_t hist[HB ? (1u << HB) : 1u];
 };
 
 // WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
-template <bool HIST, bool WIRE>
+template <int HB, bool WIRE>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t mask, const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
                                                          uint32_t bins, uint32_t shift, uint32_t items) {
-    __shared__ RouteSmem sm;
+    __shared__ RouteSmem<HB> sm;
+    constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
@@ -483,10 +496,58 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 enum : int { IN_ACT = 0, IN_PAIR = 1 };
 enum : int { OUT_PAIR = 0, OUT_FINAL = 1 };
 
+// Digits per thread in the per-round column phase: digit pairs (one packed word) are never split between threads.
+template <int BITS>
+constexpr uint32_t kDigitsPerThread = (1u << BITS) / 256u > 2u ? (1u << BITS) / 256u : 2u;
+
+// After a round of wave_rank: turns every wave's packed count of digit d into the round-local sorted start of
+// (wave, d) (digits in order, waves in order inside a digit).  Thread t owns digits [t*P, t*P + P); returns
+// their totals and round-local starts (block scan over the threads in digit order).  Starts stay < 2^13.
+template <int BITS>
+__device__ __forceinline__ void round_starts(uint32_t (*cnt)[(1u << BITS) / 2u], uint32_t* wsum,
+                                             uint32_t (&tot)[kDigitsPerThread<BITS>],
+                                             uint32_t (&start)[kDigitsPerThread<BITS>]) {
+    constexpr uint32_t B = 1u << BITS, P = kDigitsPerThread<BITS>;
+    const uint32_t d0 = threadIdx.x * P;
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < P; q += 2) {
+        uint32_t lo = 0, hi = 0;
+        if (d0 + q < B) {
+            const uint32_t k = (d0 + q) >> 1;
+#pragma unroll
+            for (uint32_t ww = 0; ww < kWaves; ++ww) {
+                const uint32_t c = cnt[ww][k];
+                cnt[ww][k] = lo | (hi << 16);
+                lo += c & 0xFFFFu;
+                hi += c >> 16;
+            }
+        }
+        tot[q] = lo;
+        tot[q + 1] = hi;
+        s += lo + hi;
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, wsum, total);
+#pragma unroll
+    for (uint32_t q = 0; q < P; ++q) {
+        start[q] = run;
+        run += tot[q];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < P; q += 2) {
+        if (d0 + q < B) {
+            const uint32_t add = start[q] | (start[q + 1] << 16);
+#pragma unroll
+            for (uint32_t ww = 0; ww < kWaves; ++ww) cnt[ww][(d0 + q) >> 1] += add;
+        }
+    }
+}
+
 template <int BITS>
 struct PassSmem {
-    uint32_t cnt[kWaves][1u << BITS];  // per-wave running counts, then per-(wave, bin) tile-local starts
-    uint32_t delta[1u << BITS];        // global base - tile-local start, per bin
+    uint32_t cnt[kWaves][(1u << BITS) / 2u];  // packed per-wave running counts, then per-(wave, bin) tile-local starts
+    uint32_t delta[1u << BITS];               // global base - tile-local start, per bin
     uint2 stage[kTile];  // {key, index}: one 8-B LDS write per element (half the conflicted scatter instructions)
     uint32_t wsum[kWaves];
 };
@@ -497,11 +558,11 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out) {
     constexpr uint32_t B = 1u << BITS;
-    constexpr uint32_t PER = (B + 255u) / 256u;
+    constexpr uint32_t PER = kDigitsPerThread<BITS>;
     __shared__ PassSmem<BITS> sm;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
-    for (uint32_t b = threadIdx.x; b < B; b += 256) {
+    for (uint32_t b = threadIdx.x; b < B / 2u; b += 256) {
 #pragma unroll
         for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
     }
@@ -529,41 +590,19 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
     // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
     const uint32_t* orow = tile_off + (size_t)tile * row_step * B;
-    uint32_t tot[PER];
-    uint32_t s = 0;
+    uint32_t tot[PER], start[PER];
+    round_starts<BITS>(sm.cnt, sm.wsum, tot, start);
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t b = threadIdx.x * PER + q;
-        uint32_t t = 0;
-        if (b < B) {
-#pragma unroll
-            for (uint32_t ww = 0; ww < kWaves; ++ww) {
-                const uint32_t c = sm.cnt[ww][b];
-                sm.cnt[ww][b] = t;
-                t += c;
-            }
-        }
-        tot[q] = t;
-        s += t;
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, sm.wsum, total);
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint32_t b = threadIdx.x * PER + q;
-        if (b < B) {
-#pragma unroll
-            for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][b] += run;
-            sm.delta[b] = orow[b] - run;
-        }
-        run += tot[q];
+        if (b < B) sm.delta[b] = orow[b] - start[q];
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
         if (wbase + j * 64u + lane < n) {
             const uint32_t d = (key[j] >> shift) & (B - 1u);
-            const uint32_t lpos = sm.cnt[w][d] + rank[j];
+            const uint32_t lpos = packed_get(sm.cnt[w], d) + rank[j];
             sm.stage[lpos] = make_uint2(key[j], idx[j]);
         }
     }
@@ -649,25 +688,28 @@ __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict
 // (hb == 0) the whole batch is one bucket read straight from the activation handles.
 //
 // k_seg_plan: one workgroup; bstart = exclusive scan of the MSD column totals (or {0, n}), sstart = exclusive
-// scan of ceil(count / seg).  nbk <= 2048 buckets, two per thread.
+// scan of ceil(count / seg).  nbk <= 4096 buckets (2048 with 11-bit digits), four per thread.
 __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
+    constexpr uint32_t Q = 4;
     __shared__ uint32_t wsum[2][16];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t c[2], p[2];
+    uint32_t c[Q], p[Q], cs = 0, ps = 0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t b = threadIdx.x * 2 + q;
+    for (uint32_t q = 0; q < Q; ++q) {
+        const uint32_t b = threadIdx.x * Q + q;
         c[q] = b < nbk ? (col_tot ? col_tot[b] : n) : 0u;
         p[q] = (c[q] + seg - 1) / seg;
+        cs += c[q];
+        ps += p[q];
     }
-    const uint32_t ci = wave_incl_scan(c[0] + c[1]), pi = wave_incl_scan(p[0] + p[1]);
+    const uint32_t ci = wave_incl_scan(cs), pi = wave_incl_scan(ps);
     if (lane == 63) {
         wsum[0][w] = ci;
         wsum[1][w] = pi;
     }
     __syncthreads();
-    uint32_t cb = ci - c[0] - c[1], pb = pi - p[0] - p[1], ct = 0, pt = 0;
+    uint32_t cb = ci - cs, pb = pi - ps, ct = 0, pt = 0;
     for (uint32_t i = 0; i < 16; ++i) {
         if (i < w) {
             cb += wsum[0][i];
@@ -677,8 +719,8 @@ __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ 
         pt += wsum[1][i];
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t b = threadIdx.x * 2 + q;
+    for (uint32_t q = 0; q < Q; ++q) {
+        const uint32_t b = threadIdx.x * Q + q;
         if (b < nbk) {
             bstart[b] = cb;
             sstart[b] = pb;
@@ -794,7 +836,7 @@ __global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_his
 // start of l).  The running part lives in registers of the thread owning digit l.
 template <int LB>
 struct SegSmem {
-    uint32_t cnt[kWaves][1u << LB];
+    uint32_t cnt[kWaves][(1u << LB) / 2u];  // packed (wave_rank)
     uint32_t delta[1u << LB];
     uint2 stage[kSegChunk];  // {digit, index}
     uint32_t wsum[kWaves];
@@ -806,7 +848,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, uint32_t* __restrict__ order) {
     constexpr uint32_t BL = 1u << LB;
-    constexpr uint32_t PER = (BL + 255u) / 256u;
+    constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
     SegRange r;
     if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
@@ -827,53 +869,31 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             const uint32_t e = wbase + j * 64u + lane;
             seg_load<IN>(in, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
         }
+        for (uint32_t k = threadIdx.x; k < BL / 2u; k += 256) {
 #pragma unroll
-        for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t l = threadIdx.x * PER + q;
-            if (l < BL)
-#pragma unroll
-                for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][l] = 0;
+            for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][k] = 0;
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
             if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank(&sm.cnt[w][0], key[j] & (BL - 1u));
         __syncthreads();
-        uint32_t tot[PER], s = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t l = threadIdx.x * PER + q;
-            uint32_t t = 0;
-            if (l < BL) {
-#pragma unroll
-                for (uint32_t ww = 0; ww < kWaves; ++ww) {
-                    const uint32_t c = sm.cnt[ww][l];
-                    sm.cnt[ww][l] = t;
-                    t += c;
-                }
-            }
-            tot[q] = t;
-            s += t;
-        }
-        uint32_t total;
-        uint32_t lstart = block_excl_scan(s, sm.wsum, total);
+        uint32_t tot[PER], start[PER];
+        round_starts<LB>(sm.cnt, sm.wsum, tot, start);
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t l = threadIdx.x * PER + q;
             if (l < BL) {
-#pragma unroll
-                for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][l] += lstart;
-                sm.delta[l] = run[q] - lstart;
+                sm.delta[l] = run[q] - start[q];
                 run[q] += tot[q];
             }
-            lstart += tot[q];
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
             if (wbase + j * 64u + lane < r.hi) {
                 const uint32_t d = key[j] & (BL - 1u);
-                const uint32_t lpos = sm.cnt[w][d] + rank[j];
+                const uint32_t lpos = packed_get(sm.cnt[w], d) + rank[j];
                 sm.stage[lpos] = make_uint2(d, idx[j]);
             }
         }
@@ -914,21 +934,23 @@ __global__ __launch_bounds__(256) void k_widen64(const uint32_t* __restrict__ a,
 
 constexpr uint32_t kFanLds = 2048;  // publishers staged per tile; beyond that fall back to global search
 
+template <int HB>
 struct FanSmem {
     RouteParams P;
-    uint32_t hist[1u << kMaxDigitBits];
+    uint32_t hist[HB ? (1u << HB) : 1u];
     uint32_t poff[kFanLds + 1];
     uint32_t prange[2];
 };
 
-template <bool HIST>
+template <int HB>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask,
     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
     uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist, uint32_t bins, uint32_t shift, uint32_t items) {
-    __shared__ FanSmem sm;
+    __shared__ FanSmem<HB> sm;
+    constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
@@ -1195,7 +1217,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
             m.meta = h1[j].z;
             m.aux = h1[j].w;
             dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
-            rank[j] = wave_rank(&sm.cnt[w][0], dig[j]);
+            rank[j] = wave_rank_wide(&sm.cnt[w][0], dig[j]);
         }
     }
     __syncthreads();
@@ -1418,9 +1440,9 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
 #define ORL_ROUTE(H, W) hipLaunchKernelGGL((k_route<H, W>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in, \
                                            (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
     if (hist) {
-        if (wire) ORL_ROUTE(true, true); else ORL_ROUTE(true, false);
+        if (wire) ORL_ROUTE(kMaxDigitBits, true); else ORL_ROUTE(kMaxDigitBits, false);
     } else {
-        if (wire) ORL_ROUTE(false, true); else ORL_ROUTE(false, false);
+        if (wire) ORL_ROUTE(0, true); else ORL_ROUTE(0, false);
     }
 #undef ORL_ROUTE
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
@@ -1464,14 +1486,15 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
-    if (buckets && rh.on)
-        hipLaunchKernelGGL(k_fanout_route<true>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
-                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
-                           excl, d_route, d_act, s.tile_hist, rh.bins, rh.shift, items);
-    else
-        hipLaunchKernelGGL(k_fanout_route<false>, dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_csr_off,
-                           d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total,
-                           excl, d_route, d_act, nullptr, 1u, 0u, items);
+    const bool hist = buckets && rh.on;
+
+#define ORL_FAN(H, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir,   \
+                                                       dir_mask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
+                                                       follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \
+                                                       SHIFT, items)
+    if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);
+    else ORL_FAN(0, nullptr, 1u, 0u);
+#undef ORL_FAN
     if (ev_route_end) (void)hipEventRecord((hipEvent_t)ev_route_end, st);
     int e = (int)hipGetLastError();
     if (e || !buckets) return e;

@@ -131,7 +131,7 @@ def _random_setup(n_grains, n_act, n_silos=8, seed=11, functional=None, running=
 
 
 @pytest.mark.parametrize("n", [0, 1, 63, 4095, 4096, 4097, 65536 + 17, 300_001])
-@pytest.mark.parametrize("n_act", [1, 5, 2048, 5000, 3_000_000])
+@pytest.mark.parametrize("n_act", [1, 5, 2048, 5000, 3_000_000, 12_000_000, 40_000_000])
 def test_random_batches_vs_oracle(torch, n, n_act):
     cl, eng, o = _random_setup(20_000, n_act)
     msgs = W.uniform_messages(cl, 22_000, n, seed=n * 7 + n_act)  # ~9% never-registered targets
