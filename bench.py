@@ -150,13 +150,15 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         if world > 1:
             dist.all_reduce(per_dest)
         cap = max(n_msgs, int(per_dest.max().item()))
-    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=cap, device=local_rank)
-    W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
     local_mask = None
-    if world > 1:
+    n_act = n_grains
+    if world > 1:  # this rank's silos hold only their own partition; their catalog numbers its activations densely
         local_mask = np.zeros(cl.n_silos, np.uint8)
         local_mask[mine] = 1
-    n_reg = W.register_population(eng, keys, owner, reg, local_mask)
+        n_act = max(1, int((reg & local_mask[owner].astype(bool)).sum()))
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=cap, device=local_rank)
+    W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
+    n_reg = W.register_population(eng, keys, owner, reg, local_mask, dense_local=world > 1)
     log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
         f"receive capacity {cap}")
     d_msgs = torch.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
@@ -167,7 +169,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         route = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         act = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         order = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
-        offsets = torch.empty(n_grains + 2, dtype=torch.int32, device="cuda")
+        offsets = torch.empty(n_act + 2, dtype=torch.int32, device="cuda")
 
         def step():
             eng.address_messages_device(d_msgs, n_msgs, route, act, order, offsets, stream=stream)

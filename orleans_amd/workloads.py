@@ -139,13 +139,15 @@ def grain_population(cl: Cluster, n_grains: int, registered_frac: float = 1.0, s
 
 
 def register_population(eng, keys: np.ndarray, owner: np.ndarray, reg: np.ndarray,
-                        local_mask: Optional[np.ndarray] = None) -> int:
-    """RegisterSingleActivation of grain i with activation handle i on its owner silo."""
+                        local_mask: Optional[np.ndarray] = None, dense_local: bool = False) -> int:
+    """RegisterSingleActivation of grain i on its owner silo, activation handle i (or, with dense_local, the
+    grain's rank among the registered grains of the local silos: a silo catalog numbers its own activations)."""
     sel = reg.copy()
     if local_mask is not None:
         sel &= local_mask[owner].astype(bool)
     idx = np.nonzero(sel)[0]
-    st, _, _ = eng.register_single_activation(keys[idx], idx.astype(np.uint32), owner[idx])
+    acts = np.arange(len(idx), dtype=np.uint32) if dense_local else idx.astype(np.uint32)
+    st, _, _ = eng.register_single_activation(keys[idx], acts, owner[idx])
     assert (st == L.INS_INSERTED).all(), np.unique(st, return_counts=True)
     return len(idx)
 
