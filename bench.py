@@ -48,7 +48,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6],
+                    help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches")
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -71,13 +72,15 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if args.config in (4, 5):
-            raise SystemExit("--config 4/5 are single-GPU measurement legs")
+        if args.config in (4, 5, 6):
+            raise SystemExit("--config 4/5/6 are single-GPU measurement legs")
 
     if args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
     elif args.config == 4:
         res = run_fanout(args, torch)
+    elif args.config == 6:
+        res = run_directory(args, torch)
     else:
         res = run_presence(args, torch)
     if world > 1:
@@ -337,6 +340,60 @@ def run_fanout(args, torch):
                          "avg_launch_ms": route_ms},
             "pipeline": {"route_kernel_ms": route_ms, "bucketing_ms": bucket_ms, "call_ms": total_ms},
             "cpu_baseline": None}
+
+
+# ---- leg 6: directory mutation (f1) ------------------------------------------------------------------------
+def run_directory(args, torch):
+    """16M ChirperAccount grains registered on the device in batches of 4M (RegisterSingleActivation with
+    batch-order first-writer-wins), then 10 % unregistered and re-registered; registrations/s per batch."""
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+
+    n, batch = args.grains or 16_000_000, 4 << 20
+    cl = W.balanced_cluster()
+    keys, uni, owner, reg = W.grain_population(cl, n)
+    eng = GrainDirectoryEngine(n_act=n, dir_capacity=n, max_batch=batch, device=0)
+    W.setup_engine(eng, cl)
+    dev = "cuda"
+    d_keys = torch.from_numpy(keys.view(np.uint8).reshape(-1, 24)).to(dev)
+    d_acts = torch.arange(n, dtype=torch.int32, device=dev)
+    d_silos = torch.from_numpy(owner.astype(np.uint8)).to(dev)
+    d_st = torch.empty(batch, dtype=torch.uint8, device=dev)
+    d_wa = torch.empty(batch, dtype=torch.int32, device=dev)
+    d_ws = torch.empty(batch, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b0 in range(0, n, batch):
+        m = min(batch, n - b0)
+        eng.register_single_activation_device(d_keys[b0:b0 + m], d_acts[b0:b0 + m], d_silos[b0:b0 + m], m, d_st, d_wa,
+                                              d_ws, stream=stream)
+    torch.cuda.synchronize()
+    t_ins = time.perf_counter() - t0
+    assert eng.directory_count() == n
+    m = n // 10
+    d_rm = torch.empty(m, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b0 in range(0, m, batch):
+        k = min(batch, m - b0)
+        eng.unregister_device(d_keys[b0:b0 + k], k, d_rm[b0:b0 + k], stream=stream)
+    for b0 in range(0, m, batch):
+        k = min(batch, m - b0)
+        eng.register_single_activation_device(d_keys[b0:b0 + k], d_acts[b0:b0 + k], d_silos[b0:b0 + k], k, d_st, d_wa,
+                                              d_ws, stream=stream)
+    torch.cuda.synchronize()
+    t_churn = time.perf_counter() - t0
+    assert eng.directory_count() == n
+    eng.close()
+    log(f"directory: {n} registrations in {t_ins * 1e3:.1f} ms; {m} removals + {m} re-registrations in "
+        f"{t_churn * 1e3:.1f} ms")
+    return {"metric": "directory registrations/sec", "value": n / t_ins, "unit": "registrations/s", "n_gpus": 1,
+            "steps": 1, "warmup": 0, "ms_per_step": t_ins * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32/u64 integer", "data": "synthetic (config-3 population)",
+            "config": {"workload": f"leg 6: {n} long-key grains registered on the device in batches of {batch}, then "
+                                   f"{m} unregistered + re-registered", "table_slots": 2 * n},
+            "churn_ops_per_s": 2 * m / t_churn, "roofline": None, "cpu_baseline": None}
 
 
 # ---- config 5: Presence heartbeats, small batches, hipGraph --------------------------------------------

@@ -185,6 +185,19 @@ int orl_dir_insert_single(orl_ctx* ctx, const orl_grain_key* keys, const uint32_
                           size_t n, uint32_t* winner_act, uint8_t* winner_silo, uint8_t* status);
 /* RemoveGrain / RemoveActivation(force) of a single-activation grain (:290-318).  removed[i] = 1 if present. */
 int orl_dir_remove(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint8_t* removed);
+/* Device-resident registration / unregistration batches: same per-message outcomes as
+ * orl_dir_insert_single / orl_dir_remove applied one message at a time in batch order (first writer of a
+ * key wins, its activation is every later writer's winner; the first removal of a key removes it), computed
+ * by kernels on the device table.  Keys, acts, silos and outputs are device arrays; nothing synchronises.
+ * Out-of-range act / silo values give ORL_INS_UNSUPPORTED for that message (no host-side validation).
+ * Fails with ORL_E_CAPACITY before launching if the batch could push the table past load 0.5.
+ * The host mirror (orl_dir_lookup_host, orl_dir_count, the host insert/remove) is re-read from the device
+ * on its next use.  Reference: LocalGrainDirectory.RegisterSingleActivationAsync / UnregisterAsync
+ * (LocalGrainDirectory.cs:510-612) → GrainDirectoryPartition.AddSingleActivation / RemoveActivation
+ * (GrainDirectoryPartition.cs:270-318). */
+int orl_dir_insert_single_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
+                                 size_t n, uint32_t* d_winner_act, uint8_t* d_winner_silo, uint8_t* d_status, void* stream);
+int orl_dir_remove_device(orl_ctx* ctx, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream);
 int orl_dir_count(const orl_ctx* ctx, uint64_t* n_out);
 /* Host lookup (LookUpGrain without the IsValidSilo filter): act/silo or ORL_NO_ACT/ORL_NULL_SILO */
 int orl_dir_lookup_host(const orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint32_t* act, uint8_t* silo);

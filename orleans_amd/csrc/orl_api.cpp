@@ -171,8 +171,13 @@ struct orl_ctx {
     std::vector<DirSlot> table;
     uint64_t mask = 0, count = 0, tombs = 0;
     bool dir_dirty = true;
+    bool mirror_stale = false;       // device mutations since the mirror was last downloaded
+    uint64_t count_ub = 0, tombs_ub = 0;  // upper bounds while the mirror is stale (capacity checks without a sync)
     // device state
     DirSlot* d_table = nullptr;
+    uint32_t* d_claim = nullptr;     // per-slot claim word of the device insert/remove kernels (0xFFFFFFFF at rest)
+    uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
+    uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
     RouteParams hp{};
     RouteParams* d_params = nullptr;
     bool params_dirty = true;
@@ -270,8 +275,29 @@ int sync_device_state(orl_ctx* c) {
     }
     if (c->dir_dirty) {
         ORL_HIP(c, hipMemcpy(c->d_table, c->table.data(), c->table.size() * sizeof(DirSlot), hipMemcpyHostToDevice));
+        const uint64_t st[3] = {c->count, c->tombs, 0};
+        ORL_HIP(c, hipMemcpy(c->d_dirstate, st, sizeof st, hipMemcpyHostToDevice));
         c->dir_dirty = false;
+        c->count_ub = c->count;
+        c->tombs_ub = c->tombs;
     }
+    return ORL_OK;
+}
+
+// The host mirror after device mutations: download the table (synchronises the device) and recount.
+int ensure_mirror(orl_ctx* c) {
+    if (!c->mirror_stale) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());
+    ORL_HIP(c, hipMemcpy(c->table.data(), c->d_table, c->table.size() * sizeof(DirSlot), hipMemcpyDeviceToHost));
+    uint64_t full = 0, tomb = 0;
+    for (const DirSlot& d : c->table) {
+        full += d.state == SLOT_FULL;
+        tomb += d.state == SLOT_TOMB;
+    }
+    c->count = c->count_ub = full;
+    c->tombs = c->tombs_ub = tomb;
+    c->mirror_stale = false;
     return ORL_OK;
 }
 
@@ -313,7 +339,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -363,6 +389,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
         if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
+        if ((e = hipMalloc((void**)&c->d_claim, slots * 4)) != hipSuccess) return bail(e, "hipMalloc(claim)");
+        if ((e = hipMemset(c->d_claim, 0xFF, slots * 4)) != hipSuccess) return bail(e, "hipMemset(claim)");
+        if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
+        if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
         if ((e = hipMalloc((void**)&c->d_rank_of_silo, 256)) != hipSuccess) return bail(e, "hipMalloc(rank map)");
         const uint64_t mb = std::max<uint64_t>(cfg->max_batch, kTile);
@@ -388,6 +418,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
         if ((e = hipMalloc((void**)&c->s.sstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
+        if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
@@ -497,6 +528,7 @@ uint32_t orl_keyext_uniform_hash(const orl_grain_key* k, const char* ext, size_t
 int orl_dir_insert_single(orl_ctx* c, const orl_grain_key* keys, const uint32_t* acts, const uint8_t* silos, size_t n,
                           uint32_t* wact, uint8_t* wsilo, uint8_t* status) {
     if (!c || (n && (!keys || !acts || !silos))) return ORL_E_INVALID;
+    if (int r = ensure_mirror(c)) return r;
     for (size_t i = 0; i < n; ++i) {
         uint8_t st;
         uint32_t a = ORL_NO_ACT;
@@ -543,6 +575,7 @@ int orl_dir_insert_single(orl_ctx* c, const orl_grain_key* keys, const uint32_t*
 
 int orl_dir_remove(orl_ctx* c, const orl_grain_key* keys, size_t n, uint8_t* removed) {
     if (!c || (n && !keys)) return ORL_E_INVALID;
+    if (int r = ensure_mirror(c)) return r;
     for (size_t i = 0; i < n; ++i) {
         const int64_t at = dir_find(c, keys[i], nullptr);
         if (at >= 0) {
@@ -558,12 +591,14 @@ int orl_dir_remove(orl_ctx* c, const orl_grain_key* keys, size_t n, uint8_t* rem
 
 int orl_dir_count(const orl_ctx* c, uint64_t* n) {
     if (!c || !n) return ORL_E_INVALID;
+    if (int r = ensure_mirror(const_cast<orl_ctx*>(c))) return r;  // the mirror is a cache of the device table
     *n = c->count;
     return ORL_OK;
 }
 
 int orl_dir_lookup_host(const orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* act, uint8_t* silo) {
     if (!c || (n && !keys)) return ORL_E_INVALID;
+    if (int r = ensure_mirror(const_cast<orl_ctx*>(c))) return r;
     for (size_t i = 0; i < n; ++i) {
         const int64_t at = dir_find(c, keys[i], nullptr);
         if (act) act[i] = at >= 0 ? c->table[at].act : ORL_NO_ACT;
@@ -764,6 +799,44 @@ int orl_partition_compact_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, 
     int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, true, d_src,
                                     d_counts, d_status, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "compact partition launch");
+    return ORL_OK;
+}
+
+int orl_dir_insert_single_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
+                                 size_t n, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_keys || !d_acts || !d_silos || !d_status)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
+    int r = sync_device_state(c);
+    if (r) return r;
+    if ((c->count_ub + c->tombs_ub + n) * 2 > c->table.size()) {  // every message might insert: keep load <= 0.5
+        if ((r = ensure_mirror(c))) return r;
+        if ((c->count + c->tombs + n) * 2 > c->table.size())
+            return fail(c, ORL_E_CAPACITY, "directory full (%llu entries + %llu tombstones + batch %zu)",
+                        (unsigned long long)c->count, (unsigned long long)c->tombs, n);
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_dir_insert(c->d_params, c->d_table, c->mask, c->d_claim, c->d_dirstate, d_keys, d_acts, d_silos, n,
+                              c->cfg.n_act, c->n_silos, c->d_dslot, d_wact, d_wsilo, d_status,
+                              reinterpret_cast<uint32_t*>(c->d_dirstate + 2), st);
+    if (e) return hipfail(c, (hipError_t)e, "directory insert launch");
+    c->count_ub += n;
+    c->mirror_stale = true;
+    return ORL_OK;
+}
+
+int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_keys || !d_removed)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    int r = sync_device_state(c);
+    if (r) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_dir_remove(c->d_table, c->mask, c->d_claim, c->d_dirstate, d_keys, n, c->d_dslot, d_removed, st);
+    if (e) return hipfail(c, (hipError_t)e, "directory remove launch");
+    c->tombs_ub += n;
+    c->mirror_stale = true;
     return ORL_OK;
 }
 

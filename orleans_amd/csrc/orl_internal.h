@@ -18,7 +18,9 @@ namespace orl {
 // the full 24-B GrainId key (UniqueKey.Equals compares N0,N1,TCD: UniqueKey.cs:248-255), the dense
 // activation handle, the activation's silo (ActivationInfo.SiloAddress) and a state byte.  Two slots
 // share a 64-B line, so a probe that steps once usually stays in the line it already fetched.
-enum : uint8_t { SLOT_EMPTY = 0, SLOT_FULL = 1, SLOT_TOMB = 2 };
+enum : uint8_t { SLOT_EMPTY = 0, SLOT_FULL = 1, SLOT_TOMB = 2,
+                 SLOT_CLAIMING = 3,  // device insert: slot won by CAS, key being written (never outlives an insert call)
+                 SLOT_CLAIMED = 4 }; // device insert: key written, activation not yet committed
 
 struct alignas(32) DirSlot {
     uint64_t tcd;
@@ -186,6 +188,14 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
                                uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out,
                                const Scratch& s, void* stream, void* ev_route_begin, void* ev_route_end);
+// Directory mutation on the device (dir kernels in route_kernels.hip).  d_claim: one u32 per table slot, all
+// 0xFFFFFFFF between calls; d_cnt: {entries, tombstones} device counters; d_slot: one u32 per batch message.
+int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt,
+                      const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act,
+                      uint32_t n_silos, uint32_t* d_slot, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status, uint32_t* d_err,
+                      void* stream);
+int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                      size_t n, uint32_t* d_slot, uint8_t* d_removed, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

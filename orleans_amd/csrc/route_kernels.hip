@@ -1270,6 +1270,207 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Directory mutation on the device: RegisterSingleActivation / Unregister batches with
+// the reference's sequential semantics (GrainDirectoryPartition.AddSingleActivation, GrainDirectoryPartition.cs:
+// 270-287 + GrainInfo.AddSingleActivation :100-114: an existing instance wins; RemoveActivation :290-318),
+// i.e. equal to applying the batch one message at a time in batch order:
+//   probe   : each registration walks its key's probe chain; an equal FULL entry → EXISTING; an equal key just
+//             claimed by another registration of this batch → join it; an EMPTY slot → claim it by CAS
+//             (EMPTY → CLAIMING), write the key write-through, publish CLAIMED.  Every registration of one key
+//             meets in one slot, and atomicMin on the slot's claim word keeps the earliest batch index;
+//   resolve : the earliest registration of a claimed key is INSERTED, later ones EXISTING with its activation;
+//   commit  : the winner writes activation + silo + FULL and resets the claim word.
+// Tombstones are not reused by device inserts (the chain stays correct; the load bound counts them).
+// The probe loop takes ONE step per iteration for every lane (a lane that meets another lane's CLAIMING slot
+// retries next iteration), so lanes of one wave never wait on each other inside the loop.
+__device__ __forceinline__ uint32_t* slot_word28(DirSlot* dir, uint64_t slot) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dir + slot) + 28);  // {silo, state, pad}
+}
+
+__device__ __forceinline__ bool slot_key_eq(const DirSlot* dir, uint64_t slot, const orl_grain_key& k, bool sc1) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(dir + slot);
+    if (sc1)
+        return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.type_code_data &&
+               __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.n0 &&
+               __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.n1;
+    return w[0] == k.type_code_data && w[1] == k.n0 && w[2] == k.n1;
+}
+
+// CalculateTargetSilo(grain, excludeThisSiloIfStopping = true) seen from the registering silo `me`
+// (LocalGrainDirectory.RegisterSingleActivationAsync :510-544; the host mirror's host_owner).
+__device__ __forceinline__ uint32_t dir_owner(const RouteParams& P, const orl_grain_key& k, uint32_t me) {
+    if (k.type_code_data == P.mem_tcd && k.n0 == P.mem_n0 && k.n1 == P.mem_n1) return P.seed;
+    const uint32_t h = jenkins3(k.type_code_data, k.n0, k.n1);
+    const bool running = mask_bit(P.running, me);
+    if (P.ring_n == 0) return running ? me : 0xFFu;
+    return ring_owner(P, (int32_t)h, me, !running);
+}
+
+constexpr uint32_t kSlotNone = 0xFFFFFFFFu;
+constexpr uint8_t kInsCandidate = 0xFE;  // probe outcome: joined / claimed a slot (resolved by k_dir_ins_resolve)
+constexpr uint32_t kRetryLimit = 1u << 22;
+
+__global__ __launch_bounds__(256) void k_dir_ins_probe(const RouteParams* __restrict__ gp, DirSlot* __restrict__ dir, uint64_t mask,
+                                                       uint32_t* __restrict__ claim, const orl_grain_key* __restrict__ keys,
+                                                       const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                       uint32_t n, uint32_t n_act, uint32_t n_silos, uint32_t* __restrict__ slot_out,
+                                                       uint8_t* __restrict__ status, uint32_t* __restrict__ err) {
+    __shared__ RouteParams P;
+    stage_params(&P, gp);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const orl_grain_key k = keys[i];
+    const uint32_t silo = silos[i], cat = (uint32_t)(k.type_code_data >> 56);
+    uint8_t st;
+    if (acts[i] >= n_act || silo >= n_silos || cat == ORL_CAT_KEYEXT_GRAIN || cat == ORL_CAT_SYSTEM_TARGET) {
+        st = ORL_INS_UNSUPPORTED;
+    } else {
+        const uint32_t owner = dir_owner(P, k, silo);
+        if (owner == 0xFFu) st = ORL_INS_OWNER_NULL;
+        else if (!mask_bit(P.local, owner)) st = ORL_INS_REMOTE_OWNER;
+        else if (!mask_bit(P.functional, silo)) st = ORL_INS_INVALID_SILO;  // AddSingleActivation :277-279
+        else st = kInsCandidate;
+    }
+    uint32_t out_slot = kSlotNone;
+    if (st == kInsCandidate) {
+        uint64_t slot = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
+        uint64_t steps = 0;
+        uint32_t retries = 0;
+        int outcome = -1;  // 0 = existing FULL entry, 1 = candidate for a claimed slot
+        while (outcome < 0) {
+            uint32_t* w28 = slot_word28(dir, slot);
+            const uint32_t v = __hip_atomic_load(w28, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t state = (v >> 8) & 0xFFu;
+            bool advance = false;
+            if (state == SLOT_EMPTY) {
+                uint32_t expect = v;
+                if (__hip_atomic_compare_exchange_strong(w28, &expect, (uint32_t)SLOT_CLAIMING << 8, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    uint64_t* kw = reinterpret_cast<uint64_t*>(dir + slot);
+                    __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key write-through before the state flips
+                    __hip_atomic_store(w28, (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicMin(&claim[slot], i);
+                    outcome = 1;
+                } else if (++retries > kRetryLimit) {
+                    break;
+                }
+            } else if (state == SLOT_CLAIMING) {  // another registration is writing its key: look again
+                if (++retries > kRetryLimit) break;
+                __builtin_amdgcn_s_sleep(1);
+            } else if (state == SLOT_CLAIMED) {
+                if (slot_key_eq(dir, slot, k, true)) {
+                    atomicMin(&claim[slot], i);
+                    outcome = 1;
+                } else {
+                    advance = true;
+                }
+            } else if (state == SLOT_FULL) {
+                if (slot_key_eq(dir, slot, k, false)) outcome = 0; else advance = true;
+            } else {
+                advance = true;  // tombstone
+            }
+            if (advance) {
+                if (++steps > mask) break;
+                slot = (slot + 1) & mask;
+            }
+        }
+        if (outcome < 0) {  // no free slot on the chain (or a stuck claim): the batch overran the table
+            atomicOr(err, 1u);
+            st = ORL_INS_UNSUPPORTED;
+        } else {
+            out_slot = (uint32_t)slot;
+            st = outcome == 0 ? (uint8_t)ORL_INS_EXISTING : kInsCandidate;
+        }
+    }
+    slot_out[i] = out_slot;
+    status[i] = st;
+}
+
+__global__ __launch_bounds__(256) void k_dir_ins_resolve(const DirSlot* __restrict__ dir, const uint32_t* __restrict__ claim,
+                                                         const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                         uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ wact,
+                                                         uint8_t* __restrict__ wsilo) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t st = status[i];
+    const uint32_t slot = slot_in[i];
+    uint32_t a = ORL_NO_ACT;
+    uint8_t sl = (uint8_t)ORL_NULL_SILO;
+    if (st == kInsCandidate) {
+        const uint32_t c = claim[slot];
+        a = acts[c];
+        sl = silos[c];
+        status[i] = c == i ? (uint8_t)ORL_INS_INSERTED : (uint8_t)ORL_INS_EXISTING;
+    } else if (st == ORL_INS_EXISTING) {
+        a = dir[slot].act;
+        sl = dir[slot].silo;
+    }
+    if (wact) wact[i] = a;
+    if (wsilo) wsilo[i] = sl;
+}
+
+__global__ __launch_bounds__(256) void k_dir_ins_commit(DirSlot* __restrict__ dir, uint32_t* __restrict__ claim,
+                                                        const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                        uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                        const uint8_t* __restrict__ status, uint64_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || status[i] != ORL_INS_INSERTED) return;
+    const uint32_t slot = slot_in[i];
+    uint64_t* w24 = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(dir + slot) + 24);
+    *w24 = (uint64_t)acts[i] | ((uint64_t)silos[i] << 32) | ((uint64_t)SLOT_FULL << 40);
+    claim[slot] = kSlotNone;
+    atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
+}
+
+// Unregister: the first removal of a key in batch order removes it (RemoveActivation on the entry; later ones
+// find nothing).  probe → atomicMin on the entry's claim word; resolve; commit (FULL → TOMB).
+__global__ __launch_bounds__(256) void k_dir_rm_probe(const DirSlot* __restrict__ dir, uint64_t mask, uint32_t* __restrict__ claim,
+                                                      const orl_grain_key* __restrict__ keys, uint32_t n,
+                                                      uint32_t* __restrict__ slot_out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const orl_grain_key k = keys[i];
+    uint64_t slot = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
+    uint32_t out = kSlotNone;
+    for (uint64_t step = 0; step <= mask; ++step) {
+        const uint8_t state = dir[slot].state;
+        if (state == SLOT_EMPTY) break;
+        if (state == SLOT_FULL && slot_key_eq(dir, slot, k, false)) {
+            atomicMin(&claim[slot], i);
+            out = (uint32_t)slot;
+            break;
+        }
+        slot = (slot + 1) & mask;
+    }
+    slot_out[i] = out;
+}
+
+__global__ __launch_bounds__(256) void k_dir_rm_resolve(const uint32_t* __restrict__ claim, uint32_t n,
+                                                        const uint32_t* __restrict__ slot_in, uint8_t* __restrict__ removed) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = slot_in[i];
+    removed[i] = (slot != kSlotNone && claim[slot] == i) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_dir_rm_commit(DirSlot* __restrict__ dir, uint32_t* __restrict__ claim, uint32_t n,
+                                                       const uint32_t* __restrict__ slot_in, const uint8_t* __restrict__ removed,
+                                                       uint64_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || !removed[i]) return;
+    const uint32_t slot = slot_in[i];
+    dir[slot].state = SLOT_TOMB;
+    claim[slot] = kSlotNone;
+    atomicAdd(reinterpret_cast<unsigned long long*>(cnt), ~0ull);      // entries - 1
+    atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), 1ull);   // tombstones + 1
+}
+
+// ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
@@ -1514,6 +1715,32 @@ int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_
     hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(256), 0, st, d_in, s.digits, (uint32_t)n, s.tile_hist, ntiles, nranks,
                        d_out, d_src_index);
     hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, s.tile_hist, ntiles, nranks, (uint32_t)n, d_counts);
+    return (int)hipGetLastError();
+}
+
+int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt,
+                      const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act,
+                      uint32_t n_silos, uint32_t* d_slot, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status, uint32_t* d_err,
+                      void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return 0;
+    const dim3 g(ceil_div(n, 256)), b(256);
+    hipLaunchKernelGGL(k_dir_ins_probe, g, b, 0, st, d_params, d_dir, dir_mask, d_claim, d_keys, d_acts, d_silos, (uint32_t)n,
+                       n_act, n_silos, d_slot, d_status, d_err);
+    hipLaunchKernelGGL(k_dir_ins_resolve, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_wact,
+                       d_wsilo);
+    hipLaunchKernelGGL(k_dir_ins_commit, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_cnt);
+    return (int)hipGetLastError();
+}
+
+int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                      size_t n, uint32_t* d_slot, uint8_t* d_removed, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return 0;
+    const dim3 g(ceil_div(n, 256)), b(256);
+    hipLaunchKernelGGL(k_dir_rm_probe, g, b, 0, st, d_dir, dir_mask, d_claim, d_keys, (uint32_t)n, d_slot);
+    hipLaunchKernelGGL(k_dir_rm_resolve, g, b, 0, st, d_claim, (uint32_t)n, d_slot, d_removed);
+    hipLaunchKernelGGL(k_dir_rm_commit, g, b, 0, st, d_dir, d_claim, (uint32_t)n, d_slot, d_removed, d_cnt);
     return (int)hipGetLastError();
 }
 

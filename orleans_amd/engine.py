@@ -337,6 +337,17 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_route_compact_device(self._ctx, ptr(d_recs), int(n), int(opts), ptr(d_route), ptr(d_act),
                                                     ptr(d_order), ptr(d_offsets), ptr(stream)))
 
+    def register_single_activation_device(self, d_keys, d_acts, d_silos, n: int, d_status, d_winner_act=None,
+                                          d_winner_silo=None, stream=None) -> None:
+        """Batched RegisterSingleActivation on the device table (GrainDirectoryPartition.AddSingleActivation,
+        GrainDirectoryPartition.cs:270-287), sequential batch-order semantics."""
+        self._ck(self._lib.orl_dir_insert_single_device(self._ctx, ptr(d_keys), ptr(d_acts), ptr(d_silos), int(n),
+                                                        ptr(d_winner_act), ptr(d_winner_silo), ptr(d_status), ptr(stream)))
+
+    def unregister_device(self, d_keys, n: int, d_removed, stream=None) -> None:
+        """Batched Unregister on the device table (GrainDirectoryPartition.RemoveActivation, :290-318)."""
+        self._ck(self._lib.orl_dir_remove_device(self._ctx, ptr(d_keys), int(n), ptr(d_removed), ptr(stream)))
+
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 

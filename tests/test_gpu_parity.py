@@ -493,3 +493,67 @@ def test_pipelined_router_single_rank(torch):
         np.testing.assert_array_equal(off, f_ref)
     part_eng.close()
     eng.close()
+
+
+def test_device_directory_mutation_vs_oracle(torch):
+    """batched RegisterSingleActivation / Unregister on the device table == the oracle applying
+    the same batches one message at a time (statuses, winners, removed flags), then routing over the mutated
+    directory == the oracle's.  Batches carry duplicate keys (first writer wins), re-registrations after
+    removal, invalid silos, remote owners (two local silos), system targets and the membership grain."""
+    t = torch
+    cl = W.default_cluster()
+    local = [1, 0, 0, 1, 0, 0, 0, 0]
+    functional = [1, 1, 1, 1, 1, 0, 1, 1]
+    n_grains, n_act = 60_000, 50_000
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+    eng.set_silos(8, functional=functional, local=local, seed=3)
+    o = cpu_ref.Oracle(8, functional=functional, local=local, seed=3)
+    for s in range(8):
+        eng.add_server(s, int(cl.hashes[s]))
+        o.add_server(s, int(cl.hashes[s]))
+    keys_all, _, owner, _ = W.grain_population(cl, n_grains)
+    rng = np.random.default_rng(7)
+    st_ = t.cuda.current_stream().cuda_stream
+
+    def dev(a):
+        return t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+
+    for rnd in range(4):
+        m = 40_000
+        pick = rng.integers(0, n_grains, m)
+        hot = rng.random(m) < 0.2  # a fifth of the batch re-targets 500 hot grains: many duplicates per batch
+        pick[hot] = rng.integers(0, 500, int(hot.sum()))
+        keys = keys_all[pick].copy()
+        keys[::997]["tcd"] = (np.uint64(L.CAT_SYSTEM_TARGET) << np.uint64(56)) | np.uint64(7)
+        acts = rng.integers(0, n_act, m).astype(np.uint32)
+        silos = np.where(rng.random(m) < 0.7, owner[pick], rng.integers(0, 8, m)).astype(np.uint8)
+        d_st = t.empty(m, dtype=t.uint8, device="cuda")
+        d_wa = t.empty(m, dtype=t.int32, device="cuda")
+        d_ws = t.empty(m, dtype=t.uint8, device="cuda")
+        eng.register_single_activation_device(dev(keys), dev(acts), dev(silos), m, d_st, d_wa, d_ws, stream=st_)
+        t.cuda.synchronize()
+        st_o, wa_o, ws_o = o.register(keys, acts, silos)
+        np.testing.assert_array_equal(d_st.cpu().numpy(), st_o)
+        np.testing.assert_array_equal(d_wa.cpu().numpy().view(np.uint32), wa_o)
+        np.testing.assert_array_equal(d_ws.cpu().numpy(), ws_o)
+        assert (st_o == L.INS_INSERTED).sum() > 1000 and (st_o == L.INS_EXISTING).sum() > 100, np.bincount(st_o)
+        # remove a random subset (with duplicates) on the device and in the oracle
+        rm = keys_all[rng.integers(0, n_grains, 15_000)]
+        d_rm = t.empty(len(rm), dtype=t.uint8, device="cuda")
+        eng.unregister_device(dev(rm), len(rm), d_rm, stream=st_)
+        t.cuda.synchronize()
+        np.testing.assert_array_equal(d_rm.cpu().numpy(), o.unregister(rm))
+        assert eng.directory_count() == o.size()
+        # routing over the mutated directory
+        msgs = W.uniform_messages(cl, n_grains, 100_000, seed=rnd)
+        res = eng.address_messages(msgs)
+        r_ref, a_ref = o.route(msgs)
+        np.testing.assert_array_equal(res.route, r_ref)
+        np.testing.assert_array_equal(res.act, a_ref)
+    # host-side registration after device mutations sees the device table (the mirror is re-read)
+    k = keys_all[:1000]
+    st_h, wa_h, _ = eng.register_single_activation(k, np.arange(1000, dtype=np.uint32), owner[:1000])
+    st_o, wa_o, _ = o.register(k, np.arange(1000, dtype=np.uint32), owner[:1000])
+    np.testing.assert_array_equal(st_h, st_o)
+    np.testing.assert_array_equal(wa_h, wa_o)
+    eng.close()
