@@ -392,7 +392,7 @@ def run_directory(args, torch):
             "steps": 1, "warmup": 0, "ms_per_step": t_ins * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32/u64 integer", "data": "synthetic (config-3 population)",
             "config": {"workload": f"leg 6: {n} long-key grains registered on the device in batches of {batch}, then "
-                                   f"{m} unregistered + re-registered", "table_slots": 2 * n},
+                                   f"{m} unregistered + re-registered", "table_slots": 1 << (2 * n - 1).bit_length()},
             "churn_ops_per_s": 2 * m / t_churn, "roofline": None, "cpu_baseline": None}
 
 

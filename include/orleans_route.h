@@ -190,7 +190,8 @@ int orl_dir_remove(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint8_t* r
  * key wins, its activation is every later writer's winner; the first removal of a key removes it), computed
  * by kernels on the device table.  Keys, acts, silos and outputs are device arrays; nothing synchronises.
  * Out-of-range act / silo values give ORL_INS_UNSUPPORTED for that message (no host-side validation).
- * Fails with ORL_E_CAPACITY before launching if the batch could push the table past load 0.5.
+ * Fails with ORL_E_CAPACITY before launching if the batch could push live entries past 1/2 of the slots or
+ * entries + tombstones past 7/8.  Registrations reuse tombstones (the first one on the key's chain).
  * The host mirror (orl_dir_lookup_host, orl_dir_count, the host insert/remove) is re-read from the device
  * on its next use.  Reference: LocalGrainDirectory.RegisterSingleActivationAsync / UnregisterAsync
  * (LocalGrainDirectory.cs:510-612) → GrainDirectoryPartition.AddSingleActivation / RemoveActivation
@@ -198,6 +199,9 @@ int orl_dir_remove(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint8_t* r
 int orl_dir_insert_single_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
                                  size_t n, uint32_t* d_winner_act, uint8_t* d_winner_silo, uint8_t* d_status, void* stream);
 int orl_dir_remove_device(orl_ctx* ctx, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream);
+/* Rebuild the partition without tombstones (GrainDirectoryPartition keeps a Dictionary: no tombstones there;
+ * long-running silos call this when orl_dir_insert_single_device reports ORL_E_CAPACITY with tombstones). */
+int orl_dir_compact(orl_ctx* ctx);
 int orl_dir_count(const orl_ctx* ctx, uint64_t* n_out);
 /* Host lookup (LookUpGrain without the IsValidSilo filter): act/silo or ORL_NO_ACT/ORL_NULL_SILO */
 int orl_dir_lookup_host(const orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint32_t* act, uint8_t* silo);

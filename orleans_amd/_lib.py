@@ -97,6 +97,7 @@ _SIGS = {
     "orl_route_compact_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
     "orl_dir_insert_single_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "orl_dir_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "orl_dir_compact": (C.c_int, [_P]),
     "orl_sync": (C.c_int, [_P]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),

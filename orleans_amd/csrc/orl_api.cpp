@@ -274,13 +274,29 @@ int sync_device_state(orl_ctx* c) {
         c->params_dirty = false;
     }
     if (c->dir_dirty) {
-        ORL_HIP(c, hipMemcpy(c->d_table, c->table.data(), c->table.size() * sizeof(DirSlot), hipMemcpyHostToDevice));
+        if (c->count == 0 && c->tombs == 0)  // an empty partition: no 32 B/slot upload
+            ORL_HIP(c, hipMemset(c->d_table, 0, c->table.size() * sizeof(DirSlot)));
+        else
+            ORL_HIP(c, hipMemcpy(c->d_table, c->table.data(), c->table.size() * sizeof(DirSlot), hipMemcpyHostToDevice));
         const uint64_t st[3] = {c->count, c->tombs, 0};
         ORL_HIP(c, hipMemcpy(c->d_dirstate, st, sizeof st, hipMemcpyHostToDevice));
         c->dir_dirty = false;
         c->count_ub = c->count;
         c->tombs_ub = c->tombs;
     }
+    return ORL_OK;
+}
+
+// Exact device-table counters after device mutations (synchronises the device; 24 bytes, no table download).
+int refresh_counts(orl_ctx* c) {
+    if (!c->mirror_stale) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());
+    uint64_t st[3];
+    ORL_HIP(c, hipMemcpy(st, c->d_dirstate, sizeof st, hipMemcpyDeviceToHost));
+    c->count_ub = st[0];
+    c->tombs_ub = st[1];
+    if (st[2]) return fail(c, ORL_E_CAPACITY, "a device registration found no free slot (directory overrun)");
     return ORL_OK;
 }
 
@@ -591,7 +607,11 @@ int orl_dir_remove(orl_ctx* c, const orl_grain_key* keys, size_t n, uint8_t* rem
 
 int orl_dir_count(const orl_ctx* c, uint64_t* n) {
     if (!c || !n) return ORL_E_INVALID;
-    if (int r = ensure_mirror(const_cast<orl_ctx*>(c))) return r;  // the mirror is a cache of the device table
+    if (c->mirror_stale) {  // device mutations since the mirror was read: the device counters are exact
+        if (int r = refresh_counts(const_cast<orl_ctx*>(c))) return r;
+        *n = c->count_ub;
+        return ORL_OK;
+    }
     *n = c->count;
     return ORL_OK;
 }
@@ -810,11 +830,15 @@ int orl_dir_insert_single_device(orl_ctx* c, const orl_grain_key* d_keys, const 
     if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
     int r = sync_device_state(c);
     if (r) return r;
-    if ((c->count_ub + c->tombs_ub + n) * 2 > c->table.size()) {  // every message might insert: keep load <= 0.5
-        if ((r = ensure_mirror(c))) return r;
-        if ((c->count + c->tombs + n) * 2 > c->table.size())
-            return fail(c, ORL_E_CAPACITY, "directory full (%llu entries + %llu tombstones + batch %zu)",
-                        (unsigned long long)c->count, (unsigned long long)c->tombs, n);
+    // every message might insert: live entries stay <= 1/2 of the slots, entries + tombstones <= 7/8
+    auto fits = [&](uint64_t cnt, uint64_t tombs) {
+        return (cnt + n) * 2 <= c->table.size() && (cnt + tombs + n) * 8 <= c->table.size() * 7;
+    };
+    if (!fits(c->count_ub, c->tombs_ub)) {
+        if ((r = refresh_counts(c))) return r;
+        if (!fits(c->count_ub, c->tombs_ub))
+            return fail(c, ORL_E_CAPACITY, "directory full (%llu entries + %llu tombstones + batch %zu; orl_dir_compact "
+                        "drops tombstones)", (unsigned long long)c->count_ub, (unsigned long long)c->tombs_ub, n);
     }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int e = launch_dir_insert(c->d_params, c->d_table, c->mask, c->d_claim, c->d_dirstate, d_keys, d_acts, d_silos, n,
@@ -838,6 +862,26 @@ int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uin
     c->tombs_ub += n;
     c->mirror_stale = true;
     return ORL_OK;
+}
+
+int orl_dir_compact(orl_ctx* c) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return ORL_OK;
+    if (int r = ensure_mirror(c)) return r;
+    if (c->tombs == 0) return ORL_OK;
+    std::vector<DirSlot> old;
+    old.swap(c->table);
+    c->table.assign(old.size(), DirSlot{});
+    c->count = c->tombs = 0;
+    for (const DirSlot& d : old) {  // re-insert every live entry in slot order (lookups are layout-independent)
+        if (d.state != SLOT_FULL) continue;
+        uint64_t i = fmix32(jenkins3(d.tcd, d.n0, d.n1)) & c->mask;
+        while (c->table[i].state != SLOT_EMPTY) i = (i + 1) & c->mask;
+        c->table[i] = d;
+        ++c->count;
+    }
+    c->dir_dirty = true;
+    return sync_device_state(c);
 }
 
 int orl_sync(orl_ctx* c) {

@@ -1280,9 +1280,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
 //             meets in one slot, and atomicMin on the slot's claim word keeps the earliest batch index;
 //   resolve : the earliest registration of a claimed key is INSERTED, later ones EXISTING with its activation;
 //   commit  : the winner writes activation + silo + FULL and resets the claim word.
-// Tombstones are not reused by device inserts (the chain stays correct; the load bound counts them).
-// The probe loop takes ONE step per iteration for every lane (a lane that meets another lane's CLAIMING slot
-// retries next iteration), so lanes of one wave never wait on each other inside the loop.
+// A registration takes the first tombstone or the EMPTY end of its chain, once the whole chain shows the key
+// absent (as the host mirror does).  Each attempt of the probe walks the chain without waiting; a lane that
+// meets a slot some registration is still CLAIMING abandons the attempt and retries, and the claimer publishes
+// within its own attempt, so lanes of one wave never wait on each other.
 __device__ __forceinline__ uint32_t* slot_word28(DirSlot* dir, uint64_t slot) {
     return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dir + slot) + 28);  // {silo, state, pad}
 }
@@ -1307,6 +1308,8 @@ __device__ __forceinline__ uint32_t dir_owner(const RouteParams& P, const orl_gr
 }
 
 constexpr uint32_t kSlotNone = 0xFFFFFFFFu;
+constexpr uint32_t kSlotWasTomb = 0x80000000u;  // k_dir_ins_probe → commit: the claimed slot was a tombstone
+constexpr uint32_t kSlotMask = 0x7FFFFFFFu;
 constexpr uint8_t kInsCandidate = 0xFE;  // probe outcome: joined / claimed a slot (resolved by k_dir_ins_resolve)
 constexpr uint32_t kRetryLimit = 1u << 22;
 
@@ -1334,55 +1337,66 @@ __global__ __launch_bounds__(256) void k_dir_ins_probe(const RouteParams* __rest
     }
     uint32_t out_slot = kSlotNone;
     if (st == kInsCandidate) {
-        uint64_t slot = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
-        uint64_t steps = 0;
-        uint32_t retries = 0;
+        const uint64_t start = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
         int outcome = -1;  // 0 = existing FULL entry, 1 = candidate for a claimed slot
-        while (outcome < 0) {
-            uint32_t* w28 = slot_word28(dir, slot);
-            const uint32_t v = __hip_atomic_load(w28, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t state = (v >> 8) & 0xFFu;
-            bool advance = false;
-            if (state == SLOT_EMPTY) {
-                uint32_t expect = v;
-                if (__hip_atomic_compare_exchange_strong(w28, &expect, (uint32_t)SLOT_CLAIMING << 8, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    uint64_t* kw = reinterpret_cast<uint64_t*>(dir + slot);
-                    __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key write-through before the state flips
-                    __hip_atomic_store(w28, (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    atomicMin(&claim[slot], i);
-                    outcome = 1;
-                } else if (++retries > kRetryLimit) {
-                    break;
+        uint64_t slot = start;
+        bool was_tomb = false;
+        for (uint32_t attempt = 0; outcome < 0 && attempt < kRetryLimit; ++attempt) {
+            // one attempt: walk the chain to its end (EMPTY), looking for the key and remembering the first
+            // reusable slot (tombstone or the EMPTY end); a slot another registration is still CLAIMING hides
+            // its key, so the attempt is abandoned and retried (its owner publishes within its own iteration)
+            uint64_t cur = start, free_slot = ~0ull;
+            uint32_t free_word = 0;
+            bool blocked = false, ended = false;
+            for (uint64_t step = 0; step <= mask && outcome < 0 && !blocked && !ended; ++step) {
+                const uint32_t v = __hip_atomic_load(slot_word28(dir, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t state = (v >> 8) & 0xFFu;
+                if (state == SLOT_EMPTY || state == SLOT_TOMB) {
+                    if (free_slot == ~0ull) {
+                        free_slot = cur;
+                        free_word = v;
+                    }
+                    ended = state == SLOT_EMPTY;
+                } else if (state == SLOT_CLAIMING) {
+                    blocked = true;
+                } else if (state == SLOT_CLAIMED) {
+                    if (slot_key_eq(dir, cur, k, true)) {
+                        atomicMin(&claim[cur], i);
+                        slot = cur;
+                        outcome = 1;
+                    }
+                } else if (slot_key_eq(dir, cur, k, false)) {  // FULL
+                    slot = cur;
+                    outcome = 0;
                 }
-            } else if (state == SLOT_CLAIMING) {  // another registration is writing its key: look again
-                if (++retries > kRetryLimit) break;
+                cur = (cur + 1) & mask;
+            }
+            if (outcome >= 0) break;
+            if (blocked || free_slot == ~0ull) {
                 __builtin_amdgcn_s_sleep(1);
-            } else if (state == SLOT_CLAIMED) {
-                if (slot_key_eq(dir, slot, k, true)) {
-                    atomicMin(&claim[slot], i);
-                    outcome = 1;
-                } else {
-                    advance = true;
-                }
-            } else if (state == SLOT_FULL) {
-                if (slot_key_eq(dir, slot, k, false)) outcome = 0; else advance = true;
-            } else {
-                advance = true;  // tombstone
+                continue;
             }
-            if (advance) {
-                if (++steps > mask) break;
-                slot = (slot + 1) & mask;
-            }
+            uint32_t expect = free_word;
+            if (__hip_atomic_compare_exchange_strong(slot_word28(dir, free_slot), &expect, (uint32_t)SLOT_CLAIMING << 8,
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                uint64_t* kw = reinterpret_cast<uint64_t*>(dir + free_slot);
+                __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key write-through before the state flips
+                __hip_atomic_store(slot_word28(dir, free_slot), (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                atomicMin(&claim[free_slot], i);
+                slot = free_slot;
+                was_tomb = ((free_word >> 8) & 0xFFu) == SLOT_TOMB;
+                outcome = 1;
+            }  // else: another registration took that slot first: walk again
         }
-        if (outcome < 0) {  // no free slot on the chain (or a stuck claim): the batch overran the table
+        if (outcome < 0) {  // no free slot on the whole table (or a claim that never published)
             atomicOr(err, 1u);
             st = ORL_INS_UNSUPPORTED;
         } else {
-            out_slot = (uint32_t)slot;
+            out_slot = (uint32_t)slot | (was_tomb ? kSlotWasTomb : 0u);
             st = outcome == 0 ? (uint8_t)ORL_INS_EXISTING : kInsCandidate;
         }
     }
@@ -1398,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_dir_ins_resolve(const DirSlot* __restri
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const uint8_t st = status[i];
-    const uint32_t slot = slot_in[i];
+    const uint32_t slot = slot_in[i] & kSlotMask;
     uint32_t a = ORL_NO_ACT;
     uint8_t sl = (uint8_t)ORL_NULL_SILO;
     if (st == kInsCandidate) {
@@ -1420,11 +1434,12 @@ __global__ __launch_bounds__(256) void k_dir_ins_commit(DirSlot* __restrict__ di
                                                         const uint8_t* __restrict__ status, uint64_t* __restrict__ cnt) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n || status[i] != ORL_INS_INSERTED) return;
-    const uint32_t slot = slot_in[i];
+    const uint32_t slot = slot_in[i] & kSlotMask;
     uint64_t* w24 = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(dir + slot) + 24);
     *w24 = (uint64_t)acts[i] | ((uint64_t)silos[i] << 32) | ((uint64_t)SLOT_FULL << 40);
     claim[slot] = kSlotNone;
     atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
+    if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);  // tombstones - 1
 }
 
 // Unregister: the first removal of a key in batch order removes it (RemoveActivation on the entry; later ones

@@ -348,6 +348,10 @@ class GrainDirectoryEngine:
         """Batched Unregister on the device table (GrainDirectoryPartition.RemoveActivation, :290-318)."""
         self._ck(self._lib.orl_dir_remove_device(self._ctx, ptr(d_keys), int(n), ptr(d_removed), ptr(stream)))
 
+    def compact_directory(self) -> None:
+        """Rebuild the partition without tombstones."""
+        self._ck(self._lib.orl_dir_compact(self._ctx))
+
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 

@@ -550,6 +550,11 @@ def test_device_directory_mutation_vs_oracle(torch):
         r_ref, a_ref = o.route(msgs)
         np.testing.assert_array_equal(res.route, r_ref)
         np.testing.assert_array_equal(res.act, a_ref)
+    # compaction drops the tombstones and keeps every live entry
+    eng.compact_directory()
+    assert eng.directory_count() == o.size()
+    msgs = W.uniform_messages(cl, n_grains, 50_000, seed=99)
+    np.testing.assert_array_equal(eng.address_messages(msgs).route, o.route(msgs)[0])
     # host-side registration after device mutations sees the device table (the mirror is re-read)
     k = keys_all[:1000]
     st_h, wa_h, _ = eng.register_single_activation(k, np.arange(1000, dtype=np.uint32), owner[:1000])
