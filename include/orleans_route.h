@@ -199,6 +199,16 @@ int orl_dir_remove(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint8_t* r
 int orl_dir_insert_single_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
                                  size_t n, uint32_t* d_winner_act, uint8_t* d_winner_silo, uint8_t* d_status, void* stream);
 int orl_dir_remove_device(orl_ctx* ctx, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream);
+/* Hand-off split for a membership change (GrainDirectoryHandoffManager.ProcessSiloAddEvent,
+ * GrainDirectoryHandoffManager.cs:205-250): after orl_ring_add_server, every entry whose owner under the new
+ * ring, CalculateTargetSilo(grain) seen from silo `me`, is not null and not `me` (GrainDirectoryPartition.Split
+ * :384-425) and whose activation silo is valid (ToListOfActivations :427-443) is written to d_keys / d_acts /
+ * d_silos (device, table-slot order, at most cap entries); *d_n_out (device u64) receives the full count.
+ * With ORL_SPLIT_REMOVE the emitted entries are tombstoned here (the RemoveGrain that follows a successful
+ * hand-off).  The receiving silo registers them with orl_dir_insert_single_device (RegisterManySingleActivation). */
+#define ORL_SPLIT_REMOVE 0x1u
+int orl_dir_split_device(orl_ctx* ctx, uint32_t me, uint32_t flags, orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos,
+                         uint64_t cap, uint64_t* d_n_out, void* stream);
 /* Rebuild the partition without tombstones (GrainDirectoryPartition keeps a Dictionary: no tombstones there;
  * long-running silos call this when orl_dir_insert_single_device reports ORL_E_CAPACITY with tombstones). */
 int orl_dir_compact(orl_ctx* ctx);

@@ -864,6 +864,25 @@ int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uin
     return ORL_OK;
 }
 
+int orl_dir_split_device(orl_ctx* c, uint32_t me, uint32_t flags, orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos,
+                         uint64_t cap, uint64_t* d_n_out, void* stream) {
+    if (!c || !d_n_out) return ORL_E_INVALID;
+    if (cap && (!d_keys || !d_acts || !d_silos)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (!silo_ok(c, me)) return fail(c, ORL_E_INVALID, "silo %u out of range", me);
+    int r = sync_device_state(c);
+    if (r) return r;
+    // the tile counts live in the scratch histogram: a table of more slots than the scan scratch is split by the host
+    if ((c->table.size() + kTile - 1) / kTile > c->s.max_tiles * (1ull << kMaxDigitBits))
+        return fail(c, ORL_E_CAPACITY, "table too large for the split scratch");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const bool remove = flags & ORL_SPLIT_REMOVE;
+    int e = launch_dir_split(c->d_params, c->d_table, c->table.size(), me, remove, c->d_dirstate, d_keys, d_acts, d_silos, cap,
+                             d_n_out, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "directory split launch");
+    if (remove) c->mirror_stale = true;  // tombstones: the upper bounds stay valid (entries + tombstones unchanged)
+    return ORL_OK;
+}
+
 int orl_dir_compact(orl_ctx* c) {
     if (!c) return ORL_E_INVALID;
     if (!c->device_mode) return ORL_OK;

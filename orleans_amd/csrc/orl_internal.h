@@ -196,6 +196,9 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
                       void* stream);
 int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                       size_t n, uint32_t* d_slot, uint8_t* d_removed, void* stream);
+int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots, uint32_t me, bool remove, uint64_t* d_cnt,
+                     orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos, uint64_t cap, uint64_t* d_n_out,
+                     const Scratch& s, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

@@ -1485,6 +1485,79 @@ __global__ __launch_bounds__(256) void k_dir_rm_commit(DirSlot* __restrict__ dir
     atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), 1ull);   // tombstones + 1
 }
 
+// Hand-off split (GrainDirectoryHandoffManager.ProcessSiloAddEvent, GrainDirectoryHandoffManager.cs:205-250):
+// the entries of this partition whose owner under the current ring is another (non-null) silo
+// (Split(grain => CalculateTargetSilo(grain) is not null and not me), GrainDirectoryPartition.Split :384-425) and
+// whose activation silo is valid (ToListOfActivations, :427-443) are emitted in table-slot order and, with
+// `remove`, tombstoned here (RemoveGrain after the successor registered them).  Two passes over 4096-slot tiles:
+// count, (scan), emit with a stable in-tile rank.
+__device__ __forceinline__ bool split_pick(const RouteParams& P, const DirSlot& d, uint32_t me) {
+    if (d.state != SLOT_FULL) return false;
+    const orl_grain_key k{d.tcd, d.n0, d.n1};
+    const uint32_t owner = dir_owner(P, k, me);
+    return owner != 0xFFu && owner != me && mask_bit(P.functional, d.silo);
+}
+
+__global__ __launch_bounds__(256) void k_split_count(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
+                                                     uint64_t slots, uint32_t me, uint32_t* __restrict__ tile_cnt) {
+    __shared__ RouteParams P;
+    __shared__ uint32_t wsum[kWaves];
+    stage_params(&P, gp);
+    __syncthreads();
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint64_t sl = (uint64_t)blockIdx.x * kTile + j * 256u + threadIdx.x;
+        if (sl < slots && split_pick(P, dir[sl], me)) ++c;
+    }
+    uint32_t total;
+    block_excl_scan(c, wsum, total);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
+}
+
+// tile_base: exclusive scan of the tile counts; tile_base[ntiles] unused.  Writes *n_out from the last tile.
+__global__ __launch_bounds__(256) void k_split_emit(const RouteParams* __restrict__ gp, DirSlot* __restrict__ dir, uint64_t slots,
+                                                    uint32_t me, uint32_t remove, const uint32_t* __restrict__ tile_base,
+                                                    orl_grain_key* __restrict__ out_keys, uint32_t* __restrict__ out_acts,
+                                                    uint8_t* __restrict__ out_silos, uint64_t cap, uint64_t* __restrict__ n_out,
+                                                    uint64_t* __restrict__ cnt) {
+    __shared__ RouteParams P;
+    __shared__ uint32_t wsum[kWaves];
+    stage_params(&P, gp);
+    __syncthreads();
+    // thread t owns slots [t*16, t*16+16) of the tile (contiguous, so thread order = slot order)
+    const uint64_t s0 = (uint64_t)blockIdx.x * kTile + threadIdx.x * kItems;
+    uint32_t pick = 0, c = 0;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint64_t sl = s0 + j;
+        if (sl < slots && split_pick(P, dir[sl], me)) {
+            pick |= 1u << j;
+            ++c;
+        }
+    }
+    uint32_t total;
+    uint32_t r = tile_base[blockIdx.x] + block_excl_scan(c, wsum, total);
+    uint32_t removed = 0;
+    for (uint32_t j = 0; j < kItems; ++j) {
+        if (!(pick >> j & 1u)) continue;
+        DirSlot& d = dir[s0 + j];
+        if (r < cap) {
+            out_keys[r] = orl_grain_key{d.tcd, d.n0, d.n1};
+            out_acts[r] = d.act;
+            out_silos[r] = d.silo;
+        }
+        ++r;
+        if (remove) {
+            d.state = SLOT_TOMB;
+            ++removed;
+        }
+    }
+    if (removed) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(cnt), (unsigned long long)(0ull - removed));
+        atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), (unsigned long long)removed);
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) *n_out = r;  // the last thread of the last tile ends the list
+}
+
 // ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
@@ -1756,6 +1829,18 @@ int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint
     hipLaunchKernelGGL(k_dir_rm_probe, g, b, 0, st, d_dir, dir_mask, d_claim, d_keys, (uint32_t)n, d_slot);
     hipLaunchKernelGGL(k_dir_rm_resolve, g, b, 0, st, d_claim, (uint32_t)n, d_slot, d_removed);
     hipLaunchKernelGGL(k_dir_rm_commit, g, b, 0, st, d_dir, d_claim, (uint32_t)n, d_slot, d_removed, d_cnt);
+    return (int)hipGetLastError();
+}
+
+int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots, uint32_t me, bool remove, uint64_t* d_cnt,
+                     orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos, uint64_t cap, uint64_t* d_n_out,
+                     const Scratch& s, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t ntiles = ceil_div(slots, kTile);
+    hipLaunchKernelGGL(k_split_count, dim3(ntiles), dim3(256), 0, st, d_params, d_dir, slots, me, s.tile_hist);
+    scan_inplace(s.tile_hist, ntiles, s.scan_sums, st);
+    hipLaunchKernelGGL(k_split_emit, dim3(ntiles), dim3(256), 0, st, d_params, d_dir, slots, me, remove ? 1u : 0u, s.tile_hist,
+                       d_keys, d_acts, d_silos, cap, d_n_out, d_cnt);
     return (int)hipGetLastError();
 }
 

@@ -348,6 +348,13 @@ class GrainDirectoryEngine:
         """Batched Unregister on the device table (GrainDirectoryPartition.RemoveActivation, :290-318)."""
         self._ck(self._lib.orl_dir_remove_device(self._ctx, ptr(d_keys), int(n), ptr(d_removed), ptr(stream)))
 
+    def split_directory_device(self, me: int, d_keys, d_acts, d_silos, cap: int, d_n_out, remove: bool = True,
+                               stream=None) -> None:
+        """Hand-off split after a ring change (GrainDirectoryHandoffManager.ProcessSiloAddEvent): entries now owned
+        by another silo → (d_keys, d_acts, d_silos)[: *d_n_out], tombstoned here with `remove`."""
+        self._ck(self._lib.orl_dir_split_device(self._ctx, int(me), L.SPLIT_REMOVE if remove else 0, ptr(d_keys),
+                                                ptr(d_acts), ptr(d_silos), int(cap), ptr(d_n_out), ptr(stream)))
+
     def compact_directory(self) -> None:
         """Rebuild the partition without tombstones."""
         self._ck(self._lib.orl_dir_compact(self._ctx))

@@ -562,3 +562,86 @@ def test_device_directory_mutation_vs_oracle(torch):
     np.testing.assert_array_equal(st_h, st_o)
     np.testing.assert_array_equal(wa_h, wa_o)
     eng.close()
+
+
+def test_device_handoff_split_on_silo_add(torch):
+    """Membership change (GrainDirectoryHandoffManager.ProcessSiloAddEvent): a silo joins inside
+    our ring arc; the device split emits exactly the entries whose owner under the new ring is another silo and
+    whose activation silo is valid, tombstones them here, and the joining silo registers them; afterwards each
+    silo's partition routes its keys exactly as the single-view oracle does."""
+    t = torch
+    cl = W.default_cluster()
+    new = 7
+    ring7 = sorted((int(cl.hashes[s]), s) for s in range(7))
+    h_new = int(cl.hashes[new])
+    me = max([p for p in ring7 if p[0] <= h_new], default=ring7[-1])[1]  # the arc that silo 7 lands in
+    functional = [1] * 8
+    functional[5] = 0  # silo 5 dies before the join: its entries are not handed off (ToListOfActivations: IsValidSilo)
+    n_grains = 200_000
+    keys, _, _, _ = W.grain_population(cl, n_grains)
+    eng_a = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+    eng_a.set_silos(8, local=[int(s == me) for s in range(8)])
+    for s in range(7):
+        eng_a.add_server(s, int(cl.hashes[s]))
+    o7 = cpu_ref.Oracle(8, functional=functional)
+    for s in range(7):
+        o7.add_server(s, int(cl.hashes[s]))
+    msgs_all = np.zeros(n_grains, L.MSG_DTYPE)
+    msgs_all["tcd"], msgs_all["n1"] = keys["tcd"], keys["n1"]
+    msgs_all["sending_silo"] = me
+    owner7 = decode_route(o7.route(msgs_all)[0]).owner
+    mine = np.nonzero(owner7 == me)[0]
+    rng = np.random.default_rng(3)
+    acts = np.arange(n_grains, dtype=np.uint32)
+    silos = np.where(rng.random(n_grains) < 0.1, 5, me).astype(np.uint8)
+    st, _, _ = eng_a.register_single_activation(keys[mine], acts[mine], silos[mine])
+    assert (st == L.INS_INSERTED).all()
+    reg = mine
+    # silo 5 stops being functional, then silo 7 joins
+    eng_a.set_silos(8, functional=functional, local=[int(s == me) for s in range(8)])
+    eng_a.add_server(new, h_new)
+    o8 = cpu_ref.Oracle(8, functional=functional)
+    for s in range(8):
+        o8.add_server(s, int(cl.hashes[s]))
+    owner8 = decode_route(o8.route(msgs_all)[0]).owner
+    exp = reg[(owner8[reg] != me) & (owner8[reg] != 0xFF) & (silos[reg] != 5)]
+    assert len(exp) > 100, len(exp)  # silo 7 takes 0.4 % of the ring (generation-1 hashes)
+    cap = len(reg)
+    d_k = t.empty((cap, 24), dtype=t.uint8, device="cuda")
+    d_a = t.empty(cap, dtype=t.int32, device="cuda")
+    d_s = t.empty(cap, dtype=t.uint8, device="cuda")
+    d_n = t.zeros(1, dtype=t.int64, device="cuda")
+    eng_a.split_directory_device(me, d_k, d_a, d_s, cap, d_n, remove=True, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    n_out = int(d_n.item())
+    assert n_out == len(exp)
+    got_k = d_k[:n_out].cpu().numpy().reshape(-1).view(L.KEY_DTYPE)
+    got_a = d_a[:n_out].cpu().numpy().view(np.uint32)
+    assert sorted(got_a.tolist()) == sorted(exp.tolist())
+    np.testing.assert_array_equal(got_k, keys[got_a])
+    np.testing.assert_array_equal(d_s[:n_out].cpu().numpy(), silos[got_a])
+    assert eng_a.directory_count() == len(reg) - n_out
+    # the joining silo registers the hand-off (RegisterManySingleActivation) on its device table
+    eng_b = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+    eng_b.set_silos(8, functional=functional, local=[int(s == new) for s in range(8)])
+    for s in range(8):
+        eng_b.add_server(s, int(cl.hashes[s]))
+    d_st = t.empty(n_out, dtype=t.uint8, device="cuda")
+    eng_b.register_single_activation_device(d_k[:n_out], d_a[:n_out], d_s[:n_out], n_out, d_st,
+                                            stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    assert (d_st.cpu().numpy() == L.INS_INSERTED).all()
+    # each silo's view routes its keys like the oracle holding both partitions under the 8-silo ring (the
+    # silo-5 entries stayed in A's partition; IsValidSilo filters them from lookups on both sides)
+    kept = reg[(silos[reg] != 5) | (owner8[reg] == me)]
+    o8.register(keys[kept], acts[kept], np.where(silos[kept] == 5, me, silos[kept]).astype(np.uint8))
+    probe = msgs_all[reg[silos[reg] != 5]]
+    reg = reg[silos[reg] != 5]
+    ref_r, ref_a = o8.route(probe)
+    for eng, silo in ((eng_a, me), (eng_b, new)):
+        sel = owner8[reg] == silo
+        res = eng.address_messages(probe[sel])
+        np.testing.assert_array_equal(res.route, ref_r[sel])
+        np.testing.assert_array_equal(res.act, ref_a[sel])
+    eng_a.close()
+    eng_b.close()
