@@ -48,8 +48,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6],
-                    help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
+                    help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches; "
+                         "7 = stream / reminder ring leg (f3)")
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -72,8 +73,8 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if args.config in (4, 5, 6):
-            raise SystemExit("--config 4/5/6 are single-GPU measurement legs")
+        if args.config in (4, 5, 6, 7):
+            raise SystemExit("--config 4/5/6/7 are single-GPU measurement legs")
 
     if args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
@@ -81,6 +82,8 @@ def main():
         res = run_fanout(args, torch)
     elif args.config == 6:
         res = run_directory(args, torch)
+    elif args.config == 7:
+        res = run_rings(args, torch)
     else:
         res = run_presence(args, torch)
     if world > 1:
@@ -394,6 +397,53 @@ def run_directory(args, torch):
             "config": {"workload": f"leg 6: {n} long-key grains registered on the device in batches of {batch}, then "
                                    f"{m} unregistered + re-registered", "table_slots": 1 << (2 * n - 1).bit_length()},
             "churn_ops_per_s": 2 * m / t_churn, "roofline": None, "cpu_baseline": None}
+
+
+# ---- leg 7: stream / reminder rings (f3) -----------------------------------------------------------------
+def run_rings(args, torch):
+    """64M reminder keys → owning silo under the virtual-bucket ring (8 silos x 30 buckets) and the consistent
+    ring, and 64M stream Guids → queue (256 queues) + pulling silo; per-kind ms and keys/s."""
+    from orleans_amd import _lib as L
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+
+    n = args.msgs
+    cl = W.balanced_cluster()
+    eng = GrainDirectoryEngine(n_act=4, dir_capacity=16, max_batch=1024, device=0)
+    W.setup_engine(eng, cl)
+    gens = W.balanced_generations(cl.n_silos)
+    for s in range(cl.n_silos):
+        eng.vring_add_server(s, bytes(12) + bytes([10, 0, 0, s + 1]), W.PORT, gens[s])
+    d_keys = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device="cuda")
+    d_guids = torch.randint(0, 256, (n, 16), dtype=torch.uint8, device="cuda")
+    d_own = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_q = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for name, fn in (("vbuckets", lambda: eng.ring_owner_device(L.RING_VBUCKETS, d_keys, n, 0, d_own, stream=st)),
+                     ("consistent", lambda: eng.ring_owner_device(L.RING_CONSISTENT, d_keys, n, 0, d_own, stream=st)),
+                     ("stream_queue", lambda: eng.stream_queue_device(L.RING_VBUCKETS, d_guids, n, 256, 0, d_q, d_own,
+                                                                      stream=st))):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        out[name] = (time.perf_counter() - t0) * 1e3 / args.steps
+    eng.close()
+    log("rings: " + ", ".join(f"{k} {v:.3f} ms" for k, v in out.items()) + f" per {n} keys")
+    return {"metric": "ring lookups/sec", "value": n / (out["vbuckets"] * 1e-3), "unit": "keys/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": out["vbuckets"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 integer", "data": "synthetic (random keys / Guids)",
+            "config": {"workload": f"leg 7: {n} uniform-hash keys → silo (virtual-bucket ring, 8 x 30 buckets); also the "
+                                   f"consistent ring and {n} stream Guids → 256 queues + pulling silo"},
+            "ms": out, "roofline": {"bound": "hbm", "kernel": "k_ring_owner<VBUCKETS>",
+                                    "achieved": 5.0 * n / (out["vbuckets"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": 5.0 * n / (out["vbuckets"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "traffic": None, "bytes_per_key": 5},
+            "cpu_baseline": None}
 
 
 # ---- config 5: Presence heartbeats, small batches, hipGraph --------------------------------------------

@@ -252,6 +252,33 @@ int orl_fanout_route_keys_device(orl_ctx* ctx, const uint64_t* d_csr_off, const 
                                  size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                  uint32_t* d_order, uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
 
+/* ---- stream / reminder rings -------------------------------------------------
+ * Two ring providers route stream queues and reminders; both look CLOCKWISE (first ring point >= key):
+ *   ORL_RING_CONSISTENT  ConsistentRingProvider (src/OrleansRuntime/ConsistentRing/ConsistentRingProvider.cs:
+ *                        116-135, 342-379): the directory's membershipRingList (orl_ring_add_server); the
+ *                        signed silo hash is compared with the uint key as a long.
+ *   ORL_RING_VBUCKETS    VirtualBucketsRingProvider (VirtualBucketsRingProvider.cs:142-193, 277-313):
+ *                        buckets_per_silo uniform hashes per silo (SiloAddress.GetUniformHashCodes,
+ *                        SiloAddress.cs:208-230: Jenkins over IP16 | port | generation | i), lesser generation
+ *                        keeps a colliding bucket, RemoveServer drops all of the silo's hashes.
+ * Keys are uint32 uniform hashes (a grain's: orl_hash_batch, for reminders).  `me` + ORL_OPT_EXCLUDE_IF_STOPPING
+ * give excludeMySelf (when `me` is not running). */
+#define ORL_RING_CONSISTENT 0u
+#define ORL_RING_VBUCKETS 1u
+#define ORL_MAX_VBUCKETS_PER_SILO 64u
+int orl_vring_set_buckets(orl_ctx* ctx, uint32_t buckets_per_silo);  /* default 30; only while the ring is empty */
+int orl_vring_add_server(orl_ctx* ctx, uint32_t silo, const uint8_t* ip16, int32_t port, int32_t generation);
+int orl_vring_remove_server(orl_ctx* ctx, uint32_t silo);
+int orl_vring_get(const orl_ctx* ctx, uint32_t* hashes, uint8_t* silos, uint32_t cap, uint32_t* n_out);
+int orl_ring_owner_batch_device(orl_ctx* ctx, uint32_t kind, const uint32_t* d_keys, size_t n, uint32_t me,
+                                uint32_t opts, uint8_t* d_owner, void* stream);
+/* Stream queue of each stream Guid (16 bytes each, Guid.ToByteArray() order): HashRingBasedStreamQueueMapper
+ * .GetQueueForStream (src/Orleans/Streams/QueueAdapters/HashRingBasedStreamQueueMapper.cs:36-53,68-71,
+ * src/Orleans/Runtime/HashRing.cs:95-126) with n_queues queues; d_silo (optional) = the ring owner of the
+ * queue's hash under `kind` (the silo whose range holds the queue). */
+int orl_stream_queue_batch_device(orl_ctx* ctx, uint32_t kind, const uint8_t* d_guids, size_t n, uint32_t n_queues,
+                                  uint32_t me, uint32_t opts, uint32_t* d_queue, uint8_t* d_silo, void* stream);
+
 /* ---- multi-GPU exchange support --------------------------------------------
  * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is
  * null / system target / complete stay on the sending rank (dest = my_rank).  Writes the partitioned

@@ -520,3 +520,94 @@ def default_cluster(n_silos: int = 8, port: int = 11111, generation: int = 1):
 
 
 CHIRPER_ACCOUNT_CLASS = "Orleans.Samples.Chirper.Grains.ChirperAccount"
+
+
+# ---------------------------------------------------------------------------------------
+# f3: stream / reminder rings
+# ---------------------------------------------------------------------------------------
+class VirtualBucketsRing:
+    """VirtualBucketsRingProvider (src/OrleansRuntime/ConsistentRing/VirtualBucketsRingProvider.cs).
+
+    bucketsMap: SortedDictionary<uint, SiloAddress> (:41,58).  AddServer (:142-169): the silo's
+    GetUniformHashCodes(numBucketsPerSilo) (SiloAddress.cs:208-230); on an equal bucket hash the silo with the
+    lesser generation keeps it (SiloAddress.CompareTo compares Generation only, SiloAddress.cs:254-257;
+    `if (silo.CompareTo(other) > 0) continue`).  RemoveServer (:170-193): if the silo owns no bucket, nothing;
+    else every one of ITS hashes is removed from the map, whoever holds it."""
+
+    def __init__(self, buckets_per_silo: int = 30) -> None:
+        self.nb = buckets_per_silo
+        self.map: Dict[int, int] = {}
+        self.silo_hashes: Dict[int, List[int]] = {}
+        self.gen: Dict[int, int] = {}
+
+    def add_server(self, silo: int, ip16: bytes, port: int, generation: int) -> None:
+        hashes = [silo_uniform_hash(ip16, port, generation, i) for i in range(self.nb)]
+        self.silo_hashes[silo] = hashes
+        self.gen[silo] = generation
+        for h in hashes:
+            if h in self.map and generation > self.gen[self.map[h]]:
+                continue
+            self.map[h] = silo
+
+    def remove_server(self, silo: int) -> None:
+        if silo not in self.map.values():
+            return
+        for h in self.silo_hashes[silo]:
+            self.map.pop(h, None)
+
+    def sorted_list(self) -> List[Tuple[int, int]]:
+        return sorted(self.map.items())
+
+    def target(self, key: int, me: int, exclude_me: bool) -> int:
+        """CalculateTargetSilo(uint hash) (:277-313): first bucket >= hash (clockwise) that is not me while
+        excluding; none → bucket [0], or [1] if [0] is me and excluding (even if [1] is me too)."""
+        lst = self.sorted_list()
+        if not lst:
+            return NULL_SILO if exclude_me else me
+        for h, s in lst:
+            if h >= key and (s != me or not exclude_me):
+                return s
+        s = lst[0][1]
+        if s == me and exclude_me:
+            return lst[1][1] if len(lst) > 1 else NULL_SILO
+        return s
+
+
+def consistent_ring_target(ring: Ring, key: int, me: int, exclude_me: bool) -> int:
+    """ConsistentRingProvider.CalculateTargetSilo(uint hash) (ConsistentRingProvider.cs:342-379) over
+    membershipRingList (ascending signed consistent hash, inserted as in :116-135): first silo with
+    GetConsistentHashCode() >= hash — an int against a uint, so C# compares as long and a negative silo hash
+    never matches; none → [0], or [1] if [0] is me and excluding."""
+    lst = ring.entries
+    if not lst:
+        return NULL_SILO if exclude_me else me
+    for h, s in lst:
+        if h >= key and (s != me or not exclude_me):  # Python ints: the long promotion exactly
+            return s
+    s = lst[0][1]
+    if s == me and exclude_me:
+        return lst[1][1] if len(lst) > 1 else NULL_SILO
+    return s
+
+
+def stream_queue_hashes(n_queues: int) -> List[int]:
+    """HashRingBasedStreamQueueMapper ctor (src/Orleans/Streams/QueueAdapters/HashRingBasedStreamQueueMapper.cs:
+    36-53): one queue at hash 0, else queue i at portion * i, portion = (uint)(RING_SIZE / n + 1), RING_SIZE = 2^32
+    (RangeFactory)."""
+    if n_queues == 1:
+        return [0]
+    portion = (1 << 32) // n_queues + 1
+    return [(portion * i) & M32 for i in range(n_queues)]
+
+
+def stream_queue_for_guid(guid_bytes: bytes, n_queues: int) -> int:
+    """GetQueueForStream(streamGuid, ns) = HashRing.CalculateResponsible(Guid) (src/Orleans/Runtime/HashRing.cs:
+    95-126): Jenkins over Guid.ToByteArray(), then the first queue (ring sorted by uniform hash) with hash >= key,
+    else the first queue.  Returns the queue index."""
+    key = jenkins_bytes(guid_bytes)
+    hs = stream_queue_hashes(n_queues)
+    order = sorted(range(n_queues), key=lambda i: hs[i])
+    for i in order:
+        if hs[i] >= key:
+            return i
+    return order[0]

@@ -47,6 +47,7 @@ OPT_EXCLUDE_IF_STOPPING = 0x1
 OPT_NO_BUCKETS = 0x2
 OPT_TOTAL_GIVEN = 0x4
 SPLIT_REMOVE = 0x1
+RING_CONSISTENT, RING_VBUCKETS = 0, 1
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -100,6 +101,13 @@ _SIGS = {
     "orl_dir_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_dir_compact": (C.c_int, [_P]),
     "orl_dir_split_device": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_uint64, _P, _P]),
+    "orl_vring_set_buckets": (C.c_int, [_P, C.c_uint32]),
+    "orl_vring_add_server": (C.c_int, [_P, C.c_uint32, _P, C.c_int32, C.c_int32]),
+    "orl_vring_remove_server": (C.c_int, [_P, C.c_uint32]),
+    "orl_vring_get": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "orl_ring_owner_batch_device": (C.c_int, [_P, C.c_uint32, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P]),
+    "orl_stream_queue_batch_device": (C.c_int, [_P, C.c_uint32, _P, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, _P,
+                                                _P, _P]),
     "orl_sync": (C.c_int, [_P]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),

@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <new>
 #include <string>
 #include <vector>
@@ -190,6 +191,15 @@ struct orl_ctx {
     void* st_in = nullptr; size_t st_in_cap = 0;
     uint32_t* st_out = nullptr; size_t st_out_cap = 0;
     uint32_t* st_off = nullptr;
+    // stream / reminder virtual-bucket ring (VirtualBucketsRingProvider.bucketsMap)
+    uint32_t vr_nb = 30;
+    std::map<uint32_t, uint8_t> vr_map;                // bucket hash → silo
+    std::map<uint8_t, std::vector<uint32_t>> vr_hashes;  // silo → its GetUniformHashCodes
+    std::map<uint8_t, int32_t> vr_gen;
+    bool vr_dirty = false;
+    uint32_t vr_n_dev = 0;
+    uint32_t* d_vr_hash = nullptr;
+    uint8_t* d_vr_silo = nullptr;
     // timing: 4 events per recorded batch (call begin, route begin, route end, call end)
     bool timing = false;
     std::vector<hipEvent_t> tev;
@@ -273,6 +283,20 @@ int sync_device_state(orl_ctx* c) {
         ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
         c->params_dirty = false;
     }
+    if (c->vr_dirty) {
+        std::vector<uint32_t> h;
+        std::vector<uint8_t> sl;
+        for (const auto& e : c->vr_map) {  // SortedDictionary order: ascending bucket hash
+            h.push_back(e.first);
+            sl.push_back(e.second);
+        }
+        if (!h.empty()) {
+            ORL_HIP(c, hipMemcpy(c->d_vr_hash, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+            ORL_HIP(c, hipMemcpy(c->d_vr_silo, sl.data(), sl.size(), hipMemcpyHostToDevice));
+        }
+        c->vr_n_dev = (uint32_t)h.size();
+        c->vr_dirty = false;
+    }
     if (c->dir_dirty) {
         if (c->count == 0 && c->tombs == 0)  // an empty partition: no 32 B/slot upload
             ORL_HIP(c, hipMemset(c->d_table, 0, c->table.size() * sizeof(DirSlot)));
@@ -355,7 +379,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -407,6 +431,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
         if ((e = hipMalloc((void**)&c->d_claim, slots * 4)) != hipSuccess) return bail(e, "hipMalloc(claim)");
         if ((e = hipMemset(c->d_claim, 0xFF, slots * 4)) != hipSuccess) return bail(e, "hipMemset(claim)");
+        if ((e = hipMalloc((void**)&c->d_vr_hash, ORL_MAX_SILOS * ORL_MAX_VBUCKETS_PER_SILO * 4)) != hipSuccess)
+            return bail(e, "hipMalloc(vring)");
+        if ((e = hipMalloc((void**)&c->d_vr_silo, ORL_MAX_SILOS * ORL_MAX_VBUCKETS_PER_SILO)) != hipSuccess)
+            return bail(e, "hipMalloc(vring silos)");
         if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
         if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
@@ -901,6 +929,102 @@ int orl_dir_compact(orl_ctx* c) {
     }
     c->dir_dirty = true;
     return sync_device_state(c);
+}
+
+// ---- f3: stream / reminder rings -----------------------------------------------------------------
+int orl_vring_set_buckets(orl_ctx* c, uint32_t nb) {
+    if (!c) return ORL_E_INVALID;
+    if (nb == 0 || nb > ORL_MAX_VBUCKETS_PER_SILO) return fail(c, ORL_E_INVALID, "buckets per silo must be 1..%u", ORL_MAX_VBUCKETS_PER_SILO);
+    if (!c->vr_hashes.empty()) return fail(c, ORL_E_STATE, "virtual-bucket ring not empty");
+    c->vr_nb = nb;
+    return ORL_OK;
+}
+
+int orl_vring_add_server(orl_ctx* c, uint32_t silo, const uint8_t* ip16, int32_t port, int32_t gen) {
+    if (!c || !ip16) return ORL_E_INVALID;
+    if (!silo_ok(c, silo)) return fail(c, ORL_E_INVALID, "silo %u not in the silo table", silo);
+    // SiloAddress.GetUniformHashCodes (SiloAddress.cs:208-230): Jenkins over Write(SiloAddress) + Write(int i):
+    // 16-B IP (IPv4 as 12 zero bytes + 4), port LE4, generation LE4, i LE4 (BinaryTokenStreamWriter.cs:448-486)
+    std::vector<uint32_t> hs(c->vr_nb);
+    uint8_t b[28];
+    std::memcpy(b, ip16, 16);
+    for (int k = 0; k < 4; ++k) {
+        b[16 + k] = (uint8_t)((uint32_t)port >> (8 * k));
+        b[20 + k] = (uint8_t)((uint32_t)gen >> (8 * k));
+    }
+    for (uint32_t i = 0; i < c->vr_nb; ++i) {
+        for (int k = 0; k < 4; ++k) b[24 + k] = (uint8_t)(i >> (8 * k));
+        hs[i] = jenkins_bytes(b, 28);
+    }
+    c->vr_hashes[(uint8_t)silo] = hs;
+    c->vr_gen[(uint8_t)silo] = gen;
+    for (uint32_t h : hs) {  // AddServer (VirtualBucketsRingProvider.cs:142-169)
+        auto it = c->vr_map.find(h);
+        if (it != c->vr_map.end() && gen > c->vr_gen[it->second]) continue;  // lesser generation keeps the bucket
+        c->vr_map[h] = (uint8_t)silo;
+    }
+    c->vr_dirty = true;
+    return ORL_OK;
+}
+
+int orl_vring_remove_server(orl_ctx* c, uint32_t silo) {
+    if (!c) return ORL_E_INVALID;
+    bool owns = false;  // bucketsMap.ContainsValue(silo) (:174)
+    for (const auto& e : c->vr_map) owns |= e.second == silo;
+    if (!owns) return ORL_OK;
+    for (uint32_t h : c->vr_hashes[(uint8_t)silo]) c->vr_map.erase(h);  // every one of ITS hashes (:176-180)
+    c->vr_dirty = true;
+    return ORL_OK;
+}
+
+int orl_vring_get(const orl_ctx* c, uint32_t* hashes, uint8_t* silos, uint32_t cap, uint32_t* n_out) {
+    if (!c || !n_out) return ORL_E_INVALID;
+    uint32_t i = 0;
+    for (const auto& e : c->vr_map) {
+        if (i < cap) {
+            if (hashes) hashes[i] = e.first;
+            if (silos) silos[i] = e.second;
+        }
+        ++i;
+    }
+    *n_out = i;
+    return ORL_OK;
+}
+
+namespace {
+int ring_prologue(orl_ctx* c, uint32_t kind, uint32_t me, uint32_t opts, bool* excl) {
+    if (kind != ORL_RING_CONSISTENT && kind != ORL_RING_VBUCKETS) return fail(c, ORL_E_INVALID, "unknown ring kind %u", kind);
+    if (!silo_ok(c, me)) return fail(c, ORL_E_INVALID, "silo %u out of range", me);
+    *excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) && !c->running[me];  // excludeMySelf
+    return sync_device_state(c);
+}
+}  // namespace
+
+int orl_ring_owner_batch_device(orl_ctx* c, uint32_t kind, const uint32_t* d_keys, size_t n, uint32_t me, uint32_t opts,
+                                uint8_t* d_owner, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_keys || !d_owner)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    bool excl;
+    if (int r = ring_prologue(c, kind, me, opts, &excl)) return r;
+    int e = launch_ring_owner(kind, c->d_params, c->d_vr_hash, c->d_vr_silo, c->vr_n_dev, d_keys, n, me, excl, d_owner,
+                              stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "ring owner launch");
+    return ORL_OK;
+}
+
+int orl_stream_queue_batch_device(orl_ctx* c, uint32_t kind, const uint8_t* d_guids, size_t n, uint32_t n_queues, uint32_t me,
+                                  uint32_t opts, uint32_t* d_queue, uint8_t* d_silo, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_guids || !d_queue)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n_queues == 0 || n_queues >= 65536) return fail(c, ORL_E_INVALID, "n_queues must be 1..65535");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    bool excl;
+    if (int r = ring_prologue(c, kind, me, opts, &excl)) return r;
+    int e = launch_stream_queue(kind, c->d_params, c->d_vr_hash, c->d_vr_silo, c->vr_n_dev, d_guids, n, n_queues, me, excl,
+                                d_queue, d_silo, stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "stream queue launch");
+    return ORL_OK;
 }
 
 int orl_sync(orl_ctx* c) {

@@ -199,6 +199,14 @@ int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint
 int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots, uint32_t me, bool remove, uint64_t* d_cnt,
                      orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos, uint64_t cap, uint64_t* d_n_out,
                      const Scratch& s, void* stream);
+// Stream / reminder rings (f3).  kind: ORL_RING_CONSISTENT (the directory ring in RouteParams, clockwise, long
+// compare) or ORL_RING_VBUCKETS (vr_hash/vr_silo: ascending bucket hashes).  excl_me: excludeMySelf.
+int launch_ring_owner(uint32_t kind, const RouteParams* d_params, const uint32_t* d_vr_hash, const uint8_t* d_vr_silo,
+                      uint32_t vr_n, const uint32_t* d_keys, size_t n, uint32_t me, bool excl_me, uint8_t* d_owner,
+                      void* stream);
+int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32_t* d_vr_hash, const uint8_t* d_vr_silo,
+                        uint32_t vr_n, const uint8_t* d_guids, size_t n, uint32_t n_queues, uint32_t me, bool excl_me,
+                        uint32_t* d_queue, uint8_t* d_silo, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

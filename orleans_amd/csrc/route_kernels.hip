@@ -1559,6 +1559,115 @@ __global__ __launch_bounds__(256) void k_split_emit(const RouteParams* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------
+// f3: stream / reminder rings.  Both providers look clockwise: the first ring point >= the key that is not this
+// silo while it is excluded, else wrap to point [0] (or [1] if [0] is this silo and excluded — even when [1] is
+// this silo too, as the reference does).
+//   CONSISTENT: ConsistentRingProvider.CalculateTargetSilo (ConsistentRingProvider.cs:342-379) over the
+//               membershipRingList of the directory (ascending SIGNED consistent hashes); `int >= uint` compiles to
+//               a long compare in C#, so negative silo hashes never match a key.
+//   VBUCKETS:   VirtualBucketsRingProvider.CalculateTargetSilo (VirtualBucketsRingProvider.cs:277-313) over the
+//               sorted uint bucket list (buckets_per_silo uniform hashes per silo).
+// The ring is staged in LDS; one binary search per key, then the (short) exclusion skip.
+template <int KIND>
+__device__ __forceinline__ uint32_t ring_target(const int32_t* ch, const uint32_t* vh, const uint8_t* rs, uint32_t rn,
+                                                uint32_t key, uint32_t me, bool excl) {
+    if (rn == 0) return excl ? 0xFFu : me;
+    uint32_t lo = 0, hi = rn;
+    while (lo < hi) {  // lower bound: first point >= key
+        const uint32_t mid = (lo + hi) >> 1;
+        const bool less = KIND == ORL_RING_CONSISTENT ? (int64_t)ch[mid] < (int64_t)key : vh[mid] < key;
+        if (less) lo = mid + 1; else hi = mid;
+    }
+    if (excl)
+        while (lo < rn && rs[lo] == me) ++lo;
+    if (lo < rn) return rs[lo];
+    uint32_t s = rs[0];
+    if (s == me && excl) s = rn > 1 ? rs[1] : 0xFFu;
+    return s;
+}
+
+struct RingLds {
+    const int32_t* ch;
+    const uint32_t* vh;
+    const uint8_t* rs;
+    uint32_t rn;
+};
+
+// Stage the ring of `kind` into dynamic LDS (VBUCKETS: rn x (4 + 1) B; CONSISTENT: the 256-entry directory ring).
+template <int KIND>
+__device__ __forceinline__ RingLds stage_ring(uint8_t* lds, const RouteParams* __restrict__ gp, const uint32_t* __restrict__ vr_hash,
+                                              const uint8_t* __restrict__ vr_silo, uint32_t vr_n) {
+    RingLds r{};
+    if (KIND == ORL_RING_CONSISTENT) {
+        RouteParams* P = reinterpret_cast<RouteParams*>(lds);
+        stage_params(P, gp);
+        r.ch = P->ring_hash;
+        r.rs = P->ring_silo;
+        r.rn = gp->ring_n;
+    } else {
+        uint32_t* h = reinterpret_cast<uint32_t*>(lds);
+        uint8_t* sl = lds + 4 * (size_t)vr_n;
+        for (uint32_t i = threadIdx.x; i < vr_n; i += blockDim.x) {
+            h[i] = vr_hash[i];
+            sl[i] = vr_silo[i];
+        }
+        r.vh = h;
+        r.rs = sl;
+        r.rn = vr_n;
+    }
+    __syncthreads();
+    return r;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_ring_owner(const RouteParams* __restrict__ gp, const uint32_t* __restrict__ vr_hash,
+                                                    const uint8_t* __restrict__ vr_silo, uint32_t vr_n,
+                                                    const uint32_t* __restrict__ keys, uint32_t n, uint32_t me, uint32_t excl,
+                                                    uint8_t* __restrict__ owner) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring_lds[];
+    const RingLds r = stage_ring<KIND>(ring_lds, gp, vr_hash, vr_silo, vr_n);
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u)
+        owner[e] = (uint8_t)ring_target<KIND>(r.ch, r.vh, r.rs, r.rn, keys[e], me, excl != 0);
+}
+
+// Stream → queue (HashRingBasedStreamQueueMapper.GetQueueForStream → HashRing.CalculateResponsible(Guid),
+// HashRingBasedStreamQueueMapper.cs:36-53,68-71, HashRing.cs:95-126): key = Jenkins over Guid.ToByteArray()
+// (16 B: one 12-byte block + a 4-byte tail, JenkinsHash.cs:54-124); queue i sits at portion * i with
+// portion = 2^32 / n + 1 (ascending, no overflow for n < 2^16), so the first queue >= key is ceil(key / portion),
+// wrapping to queue 0.  With `silo`, also the silo that pulls the queue: the ring owner of the queue's hash
+// (the consistent-ring queue balancer's range test).
+__device__ __forceinline__ uint32_t jenkins16(const u32x4& w) {
+    uint32_t a = 0x9e3779b9u + w.x, b = 0x9e3779b9u + w.y, c = w.z;
+    ORL_MIX(a, b, c);
+    c += 16u;
+    a += w.w;
+    ORL_MIX(a, b, c);
+    return c;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_stream_queue(const RouteParams* __restrict__ gp, const uint32_t* __restrict__ vr_hash,
+                                                      const uint8_t* __restrict__ vr_silo, uint32_t vr_n,
+                                                      const u32x4* __restrict__ guids, uint32_t n, uint32_t n_queues,
+                                                      uint32_t me, uint32_t excl, uint32_t* __restrict__ queue,
+                                                      uint8_t* __restrict__ silo) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring_lds[];
+    RingLds r{};
+    if (silo) r = stage_ring<KIND>(ring_lds, gp, vr_hash, vr_silo, vr_n);
+    const uint64_t portion = n_queues == 1 ? 0 : (1ull << 32) / n_queues + 1;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        const uint32_t key = jenkins16(__builtin_nontemporal_load(guids + e));
+        uint32_t q = 0;
+        if (portion) {
+            const uint64_t c = ((uint64_t)key + portion - 1) / portion;
+            q = c < n_queues ? (uint32_t)c : 0u;
+        }
+        queue[e] = q;
+        if (silo) silo[e] = (uint8_t)ring_target<KIND>(r.ch, r.vh, r.rs, r.rn, (uint32_t)(portion * q), me, excl != 0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
@@ -1841,6 +1950,37 @@ int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots
     scan_inplace(s.tile_hist, ntiles, s.scan_sums, st);
     hipLaunchKernelGGL(k_split_emit, dim3(ntiles), dim3(256), 0, st, d_params, d_dir, slots, me, remove ? 1u : 0u, s.tile_hist,
                        d_keys, d_acts, d_silos, cap, d_n_out, d_cnt);
+    return (int)hipGetLastError();
+}
+
+int launch_ring_owner(uint32_t kind, const RouteParams* d_params, const uint32_t* d_vr_hash, const uint8_t* d_vr_silo,
+                      uint32_t vr_n, const uint32_t* d_keys, size_t n, uint32_t me, bool excl_me, uint8_t* d_owner,
+                      void* stream) {
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g(std::min<uint32_t>(ceil_div(n, 256), 8192)), b(256);
+    if (kind == ORL_RING_CONSISTENT)
+        hipLaunchKernelGGL(k_ring_owner<ORL_RING_CONSISTENT>, g, b, sizeof(RouteParams), st, d_params, d_vr_hash, d_vr_silo, vr_n,
+                           d_keys, (uint32_t)n, me, excl_me ? 1u : 0u, d_owner);
+    else
+        hipLaunchKernelGGL(k_ring_owner<ORL_RING_VBUCKETS>, g, b, 5 * (size_t)vr_n + 16, st, d_params, d_vr_hash, d_vr_silo,
+                           vr_n, d_keys, (uint32_t)n, me, excl_me ? 1u : 0u, d_owner);
+    return (int)hipGetLastError();
+}
+
+int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32_t* d_vr_hash, const uint8_t* d_vr_silo,
+                        uint32_t vr_n, const uint8_t* d_guids, size_t n, uint32_t n_queues, uint32_t me, bool excl_me,
+                        uint32_t* d_queue, uint8_t* d_silo, void* stream) {
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g(std::min<uint32_t>(ceil_div(n, 256), 8192)), b(256);
+    const u32x4* gu = reinterpret_cast<const u32x4*>(d_guids);
+    if (kind == ORL_RING_CONSISTENT)
+        hipLaunchKernelGGL(k_stream_queue<ORL_RING_CONSISTENT>, g, b, d_silo ? sizeof(RouteParams) : 0, st, d_params, d_vr_hash,
+                           d_vr_silo, vr_n, gu, (uint32_t)n, n_queues, me, excl_me ? 1u : 0u, d_queue, d_silo);
+    else
+        hipLaunchKernelGGL(k_stream_queue<ORL_RING_VBUCKETS>, g, b, d_silo ? 5 * (size_t)vr_n + 16 : 0, st, d_params, d_vr_hash,
+                           d_vr_silo, vr_n, gu, (uint32_t)n, n_queues, me, excl_me ? 1u : 0u, d_queue, d_silo);
     return (int)hipGetLastError();
 }
 

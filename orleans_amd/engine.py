@@ -355,6 +355,38 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_dir_split_device(self._ctx, int(me), L.SPLIT_REMOVE if remove else 0, ptr(d_keys),
                                                 ptr(d_acts), ptr(d_silos), int(cap), ptr(d_n_out), ptr(stream)))
 
+    # ---- stream / reminder rings ----
+    def vring_set_buckets(self, buckets_per_silo: int) -> None:
+        self._ck(self._lib.orl_vring_set_buckets(self._ctx, int(buckets_per_silo)))
+
+    def vring_add_server(self, silo: int, ip16: bytes, port: int, generation: int) -> None:
+        """VirtualBucketsRingProvider.AddServer (VirtualBucketsRingProvider.cs:142-169)."""
+        b = np.frombuffer(bytes(ip16), np.uint8).copy()
+        assert len(b) == 16
+        self._ck(self._lib.orl_vring_add_server(self._ctx, int(silo), ptr(b), int(port), int(generation)))
+
+    def vring_remove_server(self, silo: int) -> None:
+        self._ck(self._lib.orl_vring_remove_server(self._ctx, int(silo)))
+
+    def vring(self):
+        n = C.c_uint32()
+        self._ck(self._lib.orl_vring_get(self._ctx, None, None, 0, C.byref(n)))
+        hs = np.zeros(max(n.value, 1), np.uint32)
+        ss = np.zeros(max(n.value, 1), np.uint8)
+        self._ck(self._lib.orl_vring_get(self._ctx, ptr(hs), ptr(ss), n.value, C.byref(n)))
+        return hs[:n.value], ss[:n.value]
+
+    def ring_owner_device(self, kind: int, d_keys, n: int, me: int, d_owner, opts: int = 0, stream=None) -> None:
+        """CalculateTargetSilo(uint hash) of ConsistentRingProvider / VirtualBucketsRingProvider per key."""
+        self._ck(self._lib.orl_ring_owner_batch_device(self._ctx, int(kind), ptr(d_keys), int(n), int(me), int(opts),
+                                                       ptr(d_owner), ptr(stream)))
+
+    def stream_queue_device(self, kind: int, d_guids, n: int, n_queues: int, me: int, d_queue, d_silo=None,
+                            opts: int = 0, stream=None) -> None:
+        """HashRingBasedStreamQueueMapper.GetQueueForStream per stream Guid (+ the silo whose range holds it)."""
+        self._ck(self._lib.orl_stream_queue_batch_device(self._ctx, int(kind), ptr(d_guids), int(n), int(n_queues),
+                                                         int(me), int(opts), ptr(d_queue), ptr(d_silo), ptr(stream)))
+
     def compact_directory(self) -> None:
         """Rebuild the partition without tombstones."""
         self._ck(self._lib.orl_dir_compact(self._ctx))

@@ -645,3 +645,59 @@ def test_device_handoff_split_on_silo_add(torch):
         np.testing.assert_array_equal(res.act, ref_a[sel])
     eng_a.close()
     eng_b.close()
+
+
+def test_stream_reminder_rings_vs_oracle(torch):
+    """ring-owner lookups on the device (ConsistentRingProvider over the directory ring,
+    VirtualBucketsRingProvider over 30 buckets per silo) and stream → queue (+ pulling silo) mapping, against
+    the pure-Python restatement, for running and stopping `me` with and without excludeThisSiloIfStopping."""
+    t = torch
+    n_silos = 12
+    running = [1] * n_silos
+    running[4] = 0
+    eng = GrainDirectoryEngine(n_act=4, dir_capacity=16, max_batch=1024, device=0)
+    eng.set_silos(n_silos, running=running)
+    vr = P.VirtualBucketsRing()
+    ring = P.Ring()
+    for s in range(n_silos):
+        ip = bytes(12) + bytes([10, 0, 0, s + 1])
+        eng.vring_add_server(s, ip, 11111, 7 + s)
+        vr.add_server(s, ip, 11111, 7 + s)
+        h = P.silo_consistent_hash(f"10.0.0.{s + 1}:11111", 7 + s)
+        eng.add_server(s, h)
+        ring.add_server(s, h)
+    eng.vring_remove_server(9)
+    vr.remove_server(9)
+    rng = np.random.default_rng(5)
+    bucket_keys = np.array([h for h, _ in vr.sorted_list()], np.uint32)
+    keys = np.concatenate([rng.integers(0, 1 << 32, 6000, dtype=np.uint64).astype(np.uint32), bucket_keys,
+                           bucket_keys + 1, np.array([0, 1, 0xFFFFFFFF], np.uint32)])
+    d_keys = t.from_numpy(keys.view(np.int32)).cuda()
+    d_own = t.empty(len(keys), dtype=t.uint8, device="cuda")
+    st = t.cuda.current_stream().cuda_stream
+    for me in (0, 4):
+        for opts in (0, L.OPT_EXCLUDE_IF_STOPPING):
+            excl = bool(opts) and not running[me]
+            for kind in (L.RING_CONSISTENT, L.RING_VBUCKETS):
+                eng.ring_owner_device(kind, d_keys, len(keys), me, d_own, opts=opts, stream=st)
+                t.cuda.synchronize()
+                got = d_own.cpu().numpy()
+                if kind == L.RING_VBUCKETS:
+                    exp = [vr.target(int(k), me, excl) for k in keys]
+                else:
+                    exp = [P.consistent_ring_target(ring, int(k), me, excl) for k in keys]
+                np.testing.assert_array_equal(got, np.array(exp, np.uint8), err_msg=f"kind {kind} me {me} opts {opts}")
+    # stream → queue (+ the silo whose range holds the queue)
+    guids = rng.integers(0, 256, (5000, 16), dtype=np.uint8)
+    d_g = t.from_numpy(guids).cuda()
+    d_q = t.empty(len(guids), dtype=t.int32, device="cuda")
+    d_s = t.empty(len(guids), dtype=t.uint8, device="cuda")
+    for nq in (1, 3, 8, 256, 65535):
+        eng.stream_queue_device(L.RING_VBUCKETS, d_g, len(guids), nq, 0, d_q, d_s, stream=st)
+        t.cuda.synchronize()
+        exp_q = np.array([P.stream_queue_for_guid(bytes(g), nq) for g in guids], np.uint32)
+        np.testing.assert_array_equal(d_q.cpu().numpy().view(np.uint32), exp_q)
+        qh = P.stream_queue_hashes(nq)
+        exp_s = np.array([vr.target(qh[q], 0, False) for q in exp_q], np.uint8)
+        np.testing.assert_array_equal(d_s.cpu().numpy(), exp_s)
+    eng.close()
