@@ -279,6 +279,47 @@ int orl_ring_owner_batch_device(orl_ctx* ctx, uint32_t kind, const uint32_t* d_k
 int orl_stream_queue_batch_device(orl_ctx* ctx, uint32_t kind, const uint8_t* d_guids, size_t n, uint32_t n_queues,
                                   uint32_t me, uint32_t opts, uint32_t* d_queue, uint8_t* d_silo, void* stream);
 
+/* ---- directory cache -----------------------------------------------------------
+ * AdaptiveGrainDirectoryCache (src/OrleansRuntime/GrainDirectory/AdaptiveGrainDirectoryCache.cs) as a device
+ * table consulted by the route kernels for grains whose directory owner is remote: LocalGrainDirectory.LocalLookup's
+ * cache branch (LocalGrainDirectory.cs:691-702, GetLocalCacheData :711-717: entries on invalid silos are
+ * filtered).  A hit is ORL_ST_HIT with ORL_RF_CACHED (host = the cached activation's silo); a miss stays
+ * ORL_ST_REMOTE_OWNER (the FullLookup path).  Cached activations use the caller's activation-handle space
+ * [0, n_act), so stage 4 groups messages to a remote activation like a local one (its outbound batch, FIFO).
+ * AddOrUpdate: the batch's last writer of a key wins.  Remove = CACHE_INVALIDATION_HEADER handling
+ * (InsideGrainClient.cs:298-308).  Expiry / size policy (the maintainer) stays with the host: remove or clear. */
+#define ORL_RF_CACHED 0x08u
+int orl_cache_config(orl_ctx* ctx, uint64_t capacity);
+int orl_cache_clear(orl_ctx* ctx);
+int orl_cache_add_or_update_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
+                                   size_t n, void* stream);
+int orl_cache_remove_device(orl_ctx* ctx, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream);
+int orl_cache_count(orl_ctx* ctx, uint64_t* n_out);
+
+/* ---- outbound queues and client gateway buckets ------------------------------
+ * Per routed message, the queue OutboundMessageQueue.SendMessage (src/OrleansRuntime/Messaging/
+ * OutboundMessageQueue.cs:75-150) hands it to: ORL_OUTQ_REJECT when the route has no target (host) silo
+ * (SendRejection, :100-105), ORL_OUTQ_LOOPBACK when the target is the sending silo (InboundQueue, :113-119),
+ * ORL_OUTQ_PING / ORL_OUTQ_SYSTEM for those message categories, else the sender index
+ * Math.Abs(TargetSilo.GetConsistentHashCode()) % n_senders (:141), or ORL_OUTQ_OVERFLOW where Math.Abs
+ * throws (hash == int.MinValue; ORL_E_OVERFLOW's per-message form).  Silo consistent hashes are those given
+ * to orl_ring_add_server or orl_silo_hash_set (ORL_OUTQ_UNKNOWN_SILO otherwise). */
+#define ORL_OUTQ_LOOPBACK 0xFFFFFFF0u
+#define ORL_OUTQ_PING 0xFFFFFFF1u
+#define ORL_OUTQ_SYSTEM 0xFFFFFFF2u
+#define ORL_OUTQ_REJECT 0xFFFFFFF3u
+#define ORL_OUTQ_OVERFLOW 0xFFFFFFF4u
+#define ORL_OUTQ_UNKNOWN_SILO 0xFFFFFFF5u
+int orl_silo_hash_set(orl_ctx* ctx, uint32_t silo, int32_t consistent_hash);
+int orl_outbound_queues_device(orl_ctx* ctx, const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n,
+                               uint32_t n_senders, uint32_t* d_queue, void* stream);
+/* Client side: the gateway bucket of each message, TargetGrain.GetHashCode_Modulo(n_buckets)
+ * (src/Orleans/Messaging/ProxiedMessageCenter.cs:222, src/Orleans/IDs/UniqueIdentifier.cs:60-66: C#'s
+ * truncating % on the signed uniform hash, made non-negative), so all requests to a grain share a bucket.
+ * n_buckets in [1, 2^30] (above that, (key % mod) + mod can wrap and the reference's checked cast throws). */
+int orl_client_buckets_device(orl_ctx* ctx, const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket,
+                              void* stream);
+
 /* ---- multi-GPU exchange support --------------------------------------------
  * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is
  * null / system target / complete stay on the sending rank (dest = my_rank).  Writes the partitioned

@@ -611,3 +611,65 @@ def stream_queue_for_guid(guid_bytes: bytes, n_queues: int) -> int:
         if hs[i] >= key:
             return i
     return order[0]
+
+
+# ---------------------------------------------------------------------------------------
+# f4: outbound queues and client gateway buckets
+# ---------------------------------------------------------------------------------------
+OUTQ_LOOPBACK, OUTQ_PING, OUTQ_SYSTEM, OUTQ_REJECT, OUTQ_OVERFLOW, OUTQ_UNKNOWN_SILO = (
+    0xFFFFFFF0, 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3, 0xFFFFFFF4, 0xFFFFFFF5)
+
+
+def cs_mod(a: int, b: int) -> int:
+    """C#'s % on ints: truncating division, the remainder takes the dividend's sign."""
+    r = abs(a) % abs(b)
+    return -r if a < 0 else r
+
+
+def outbound_queue(target_silo: int, sending_silo: int, category: int, silo_hash: Dict[int, int],
+                   n_senders: int) -> int:
+    """OutboundMessageQueue.SendMessage (src/OrleansRuntime/Messaging/OutboundMessageQueue.cs:75-150): no target
+    silo → SendRejection (:100-105); target == MyAddress → InboundQueue (:113-119); Ping / System senders;
+    else senders[Math.Abs(TargetSilo.GetConsistentHashCode()) % senders.Length] (:141; Math.Abs(int.MinValue)
+    throws OverflowException)."""
+    if target_silo == NULL_SILO:
+        return OUTQ_REJECT
+    if target_silo == sending_silo:
+        return OUTQ_LOOPBACK
+    if category == 0:
+        return OUTQ_PING
+    if category == 1:
+        return OUTQ_SYSTEM
+    if target_silo not in silo_hash:
+        return OUTQ_UNKNOWN_SILO
+    h = silo_hash[target_silo]
+    if h == -(1 << 31):
+        return OUTQ_OVERFLOW
+    return abs(h) % n_senders
+
+
+def client_bucket(uniform_hash32: int, n_buckets: int) -> int:
+    """UniqueIdentifier.GetHashCode_Modulo (src/Orleans/IDs/UniqueIdentifier.cs:60-66) with
+    GetHashCode() = unchecked((int)GetUniformHashCode()) (UniqueKey.cs:275-278)."""
+    key = _to_int32(uniform_hash32)
+    mod = _to_int32(n_buckets)
+    return cs_mod(cs_mod(key, mod) + mod, mod)
+
+
+def apply_directory_cache(route: Sequence[int], act: Sequence[int], sending_silos: Sequence[int],
+                          keys: Sequence[Tuple[int, int, int]], cache: Dict[Tuple[int, int, int], Tuple[int, int]],
+                          functional: Sequence[int]):
+    """LocalGrainDirectory.LocalLookup's cache branch (LocalGrainDirectory.cs:691-702) + GetLocalCacheData
+    (:711-717): a grain whose owner is remote (REMOTE_OWNER without a cache) resolves to its cached activation
+    when that activation's silo is valid; the route becomes HIT | CACHED (+ LOOPBACK when it is the sender)."""
+    r_out, a_out = list(route), list(act)
+    for i, (r, k) in enumerate(zip(route, keys)):
+        if (r >> 16) & 0xFF != ST_REMOTE_OWNER or k not in cache:
+            continue
+        a, silo = cache[k]
+        if not functional[silo]:
+            continue
+        fl = ((r >> 24) & 0xFF) | 0x08 | (FL_LOOPBACK if silo == sending_silos[i] else 0)
+        r_out[i] = pack_route(r & 0xFF, silo, ST_HIT, fl)
+        a_out[i] = a
+    return r_out, a_out

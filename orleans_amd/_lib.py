@@ -47,7 +47,10 @@ OPT_EXCLUDE_IF_STOPPING = 0x1
 OPT_NO_BUCKETS = 0x2
 OPT_TOTAL_GIVEN = 0x4
 SPLIT_REMOVE = 0x1
+RF_CACHED = 0x08
 RING_CONSISTENT, RING_VBUCKETS = 0, 1
+OUTQ_LOOPBACK, OUTQ_PING, OUTQ_SYSTEM, OUTQ_REJECT, OUTQ_OVERFLOW, OUTQ_UNKNOWN_SILO = (
+    0xFFFFFFF0, 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3, 0xFFFFFFF4, 0xFFFFFFF5)
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -108,6 +111,14 @@ _SIGS = {
     "orl_ring_owner_batch_device": (C.c_int, [_P, C.c_uint32, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P]),
     "orl_stream_queue_batch_device": (C.c_int, [_P, C.c_uint32, _P, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, _P,
                                                 _P, _P]),
+    "orl_silo_hash_set": (C.c_int, [_P, C.c_uint32, C.c_int32]),
+    "orl_outbound_queues_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint32, _P, _P]),
+    "orl_client_buckets_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P]),
+    "orl_cache_config": (C.c_int, [_P, C.c_uint64]),
+    "orl_cache_clear": (C.c_int, [_P]),
+    "orl_cache_add_or_update_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),
+    "orl_cache_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "orl_cache_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_sync": (C.c_int, [_P]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),

@@ -179,6 +179,12 @@ struct orl_ctx {
     uint32_t* d_claim = nullptr;     // per-slot claim word of the device insert/remove kernels (0xFFFFFFFF at rest)
     uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
     uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
+    uint8_t* d_dflag = nullptr;      // per-message flag of a device cache batch
+    // directory cache (AdaptiveGrainDirectoryCache, f4): device table of remote-owned grains
+    DirSlot* d_cache = nullptr;
+    uint32_t* d_cclaim = nullptr;
+    uint64_t* d_cstate = nullptr;    // {entries, tombstones, error flag}
+    uint64_t cache_slots = 0, cache_ub = 0, cache_tombs_ub = 0;
     RouteParams hp{};
     RouteParams* d_params = nullptr;
     bool params_dirty = true;
@@ -191,6 +197,12 @@ struct orl_ctx {
     void* st_in = nullptr; size_t st_in_cap = 0;
     uint32_t* st_out = nullptr; size_t st_out_cap = 0;
     uint32_t* st_off = nullptr;
+    // silo consistent hashes (SiloAddress.GetConsistentHashCode) for outbound sender queues
+    int32_t silo_hash[256] = {};
+    uint8_t silo_known[256] = {};
+    bool silo_hash_dirty = true;
+    int32_t* d_silo_hash = nullptr;
+    uint8_t* d_silo_known = nullptr;
     // stream / reminder virtual-bucket ring (VirtualBucketsRingProvider.bucketsMap)
     uint32_t vr_nb = 30;
     std::map<uint32_t, uint8_t> vr_map;                // bucket hash → silo
@@ -257,8 +269,10 @@ uint32_t host_owner(const orl_ctx* c, const orl_grain_key& k, uint32_t me, bool 
 void rebuild_params(orl_ctx* c) {
     RouteParams& P = c->hp;
     const uint64_t mt = P.mem_tcd, m0 = P.mem_n0, m1 = P.mem_n1;
+    const uint32_t cache_on = P.cache_on;
     std::memset(&P, 0, sizeof P);
     P.mem_tcd = mt; P.mem_n0 = m0; P.mem_n1 = m1;
+    P.cache_on = cache_on;
     P.ring_n = (uint32_t)c->ring.size();
     for (size_t i = 0; i < c->ring.size(); ++i) {
         P.ring_hash[i] = c->ring[i].first;
@@ -282,6 +296,11 @@ int sync_device_state(orl_ctx* c) {
     if (c->params_dirty) {
         ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
         c->params_dirty = false;
+    }
+    if (c->silo_hash_dirty) {
+        ORL_HIP(c, hipMemcpy(c->d_silo_hash, c->silo_hash, sizeof c->silo_hash, hipMemcpyHostToDevice));
+        ORL_HIP(c, hipMemcpy(c->d_silo_known, c->silo_known, sizeof c->silo_known, hipMemcpyHostToDevice));
+        c->silo_hash_dirty = false;
     }
     if (c->vr_dirty) {
         std::vector<uint32_t> h;
@@ -309,6 +328,17 @@ int sync_device_state(orl_ctx* c) {
         c->tombs_ub = c->tombs;
     }
     return ORL_OK;
+}
+
+DirView dir_view(const orl_ctx* c) {
+    return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0};
+}
+
+void set_cache_on(orl_ctx* c, bool on) {
+    if (c->hp.cache_on != (on ? 1u : 0u)) {
+        c->hp.cache_on = on ? 1u : 0u;
+        c->params_dirty = true;
+    }
 }
 
 // Exact device-table counters after device mutations (synchronises the device; 24 bytes, no table download).
@@ -379,7 +409,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -435,6 +465,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
             return bail(e, "hipMalloc(vring)");
         if ((e = hipMalloc((void**)&c->d_vr_silo, ORL_MAX_SILOS * ORL_MAX_VBUCKETS_PER_SILO)) != hipSuccess)
             return bail(e, "hipMalloc(vring silos)");
+        if ((e = hipMalloc((void**)&c->d_silo_hash, 1024)) != hipSuccess) return bail(e, "hipMalloc(silo hashes)");
+        if ((e = hipMalloc((void**)&c->d_silo_known, 256)) != hipSuccess) return bail(e, "hipMalloc(silo known)");
         if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
         if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
@@ -463,6 +495,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
         if ((e = hipMalloc((void**)&c->s.sstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
+        if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
         if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
@@ -517,7 +550,19 @@ int orl_ring_add_server(orl_ctx* c, uint32_t silo, int32_t hash) {
     for (int i = 0; i < (int)c->ring.size(); ++i)
         if (c->ring[i].first < hash) idx = i;
     c->ring.insert(c->ring.begin() + (idx + 1), std::make_pair(hash, (uint8_t)silo));
+    c->silo_hash[silo] = hash;
+    c->silo_known[silo] = 1;
+    c->silo_hash_dirty = true;
     rebuild_params(c);
+    return ORL_OK;
+}
+
+int orl_silo_hash_set(orl_ctx* c, uint32_t silo, int32_t hash) {
+    if (!c) return ORL_E_INVALID;
+    if (silo >= 256) return fail(c, ORL_E_INVALID, "silo %u out of range", silo);
+    c->silo_hash[silo] = hash;
+    c->silo_known[silo] = 1;
+    c->silo_hash_dirty = true;
     return ORL_OK;
 }
 
@@ -685,7 +730,7 @@ int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts,
     hipEvent_t* ev = nullptr;
     if (c->timing && n > 0 && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
-    int e = launch_route_bucket(c->d_params, c->d_table, c->mask, d_in, wire, n, opts, c->cfg.n_act, d_route, d_act, d_order,
+    int e = launch_route_bucket(c->d_params, dir_view(c), d_in, wire, n, opts, c->cfg.n_act, d_route, d_act, d_order,
                                 d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e) return hipfail(c, (hipError_t)e, "route launch");
     if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
@@ -748,7 +793,7 @@ int fanout_impl(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt
     hipEvent_t* ev = nullptr;
     if (c->timing && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
-    int e = launch_fanout_route_bucket(c->d_params, c->d_table, c->mask, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub,
+    int e = launch_fanout_route_bucket(c->d_params, dir_view(c), d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub,
                                        follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
                                        c->s.max_batch, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > max_batch", (unsigned long long)*n_out);
@@ -1024,6 +1069,119 @@ int orl_stream_queue_batch_device(orl_ctx* c, uint32_t kind, const uint8_t* d_gu
     int e = launch_stream_queue(kind, c->d_params, c->d_vr_hash, c->d_vr_silo, c->vr_n_dev, d_guids, n, n_queues, me, excl,
                                 d_queue, d_silo, stream ? stream : c->stream);
     if (e) return hipfail(c, (hipError_t)e, "stream queue launch");
+    return ORL_OK;
+}
+
+// ---- f4: directory cache ---------------------------------------------------------------------------
+int orl_cache_config(orl_ctx* c, uint64_t capacity) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (capacity == 0) return fail(c, ORL_E_INVALID, "capacity must be >= 1");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());
+    hipFree(c->d_cache); hipFree(c->d_cclaim); hipFree(c->d_cstate);
+    c->d_cache = nullptr; c->d_cclaim = nullptr; c->d_cstate = nullptr;
+    const uint64_t slots = next_pow2(2 * capacity);
+    ORL_HIP(c, hipMalloc((void**)&c->d_cache, slots * sizeof(DirSlot)));
+    ORL_HIP(c, hipMalloc((void**)&c->d_cclaim, slots * 4));
+    ORL_HIP(c, hipMalloc((void**)&c->d_cstate, 32));
+    ORL_HIP(c, hipMemset(c->d_cache, 0, slots * sizeof(DirSlot)));
+    ORL_HIP(c, hipMemset(c->d_cclaim, 0xFF, slots * 4));
+    ORL_HIP(c, hipMemset(c->d_cstate, 0, 32));
+    c->cache_slots = slots;
+    c->cache_ub = c->cache_tombs_ub = 0;
+    set_cache_on(c, false);
+    return ORL_OK;
+}
+
+int orl_cache_clear(orl_ctx* c) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->cache_slots) return ORL_OK;
+    ORL_HIP(c, hipDeviceSynchronize());
+    ORL_HIP(c, hipMemset(c->d_cache, 0, c->cache_slots * sizeof(DirSlot)));
+    ORL_HIP(c, hipMemset(c->d_cstate, 0, 32));
+    c->cache_ub = c->cache_tombs_ub = 0;
+    set_cache_on(c, false);
+    return ORL_OK;
+}
+
+int orl_cache_add_or_update_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
+                                   size_t n, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->cache_slots) return fail(c, ORL_E_STATE, "directory cache not configured (orl_cache_config)");
+    if (n && (!d_keys || !d_acts || !d_silos)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    auto fits = [&](uint64_t cnt, uint64_t tombs) {
+        return (cnt + n) * 2 <= c->cache_slots && (cnt + tombs + n) * 8 <= c->cache_slots * 7;
+    };
+    if (!fits(c->cache_ub, c->cache_tombs_ub)) {  // exact counters (a sync), then the cache is full: the host evicts
+        ORL_HIP(c, hipDeviceSynchronize());
+        uint64_t st[3];
+        ORL_HIP(c, hipMemcpy(st, c->d_cstate, sizeof st, hipMemcpyDeviceToHost));
+        c->cache_ub = st[0];
+        c->cache_tombs_ub = st[1];
+        if (!fits(c->cache_ub, c->cache_tombs_ub))
+            return fail(c, ORL_E_CAPACITY, "directory cache full (%llu entries; remove or clear)", (unsigned long long)st[0]);
+    }
+    int r = sync_device_state(c);
+    if (r) return r;
+    set_cache_on(c, true);
+    if ((r = sync_device_state(c))) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_cache_update(c->d_cache, c->cache_slots - 1, c->d_cclaim, c->d_cstate, d_keys, d_acts, d_silos, n, c->cfg.n_act,
+                                c->n_silos, c->d_dslot, c->d_dflag, reinterpret_cast<uint32_t*>(c->d_cstate + 2), st);
+    if (e) return hipfail(c, (hipError_t)e, "cache update launch");
+    c->cache_ub += n;
+    return ORL_OK;
+}
+
+int orl_cache_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->cache_slots) return fail(c, ORL_E_STATE, "directory cache not configured (orl_cache_config)");
+    if (n && (!d_keys || !d_removed)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_dir_remove(c->d_cache, c->cache_slots - 1, c->d_cclaim, c->d_cstate, d_keys, n, c->d_dslot, d_removed, st);
+    if (e) return hipfail(c, (hipError_t)e, "cache remove launch");
+    c->cache_tombs_ub += n;
+    return ORL_OK;
+}
+
+int orl_cache_count(orl_ctx* c, uint64_t* n) {
+    if (!c || !n) return ORL_E_INVALID;
+    *n = 0;
+    if (!c->cache_slots) return ORL_OK;
+    ORL_HIP(c, hipDeviceSynchronize());
+    uint64_t st[3];
+    ORL_HIP(c, hipMemcpy(st, c->d_cstate, sizeof st, hipMemcpyDeviceToHost));
+    *n = st[0];
+    return ORL_OK;
+}
+
+// ---- f4: outbound queues, client buckets --------------------------------------------------------
+int orl_outbound_queues_device(orl_ctx* c, const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n, uint32_t n_senders,
+                               uint32_t* d_queue, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_msgs || !d_route || !d_queue)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n_senders == 0) return fail(c, ORL_E_INVALID, "n_senders must be >= 1");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    if (int r = sync_device_state(c)) return r;
+    int e = launch_outbound_queues(d_msgs, d_route, n, n_senders, c->d_silo_hash, c->d_silo_known, d_queue,
+                                   stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "outbound queues launch");
+    return ORL_OK;
+}
+
+int orl_client_buckets_device(orl_ctx* c, const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket,
+                              void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_msgs || !d_bucket)) return fail(c, ORL_E_INVALID, "null device buffer");
+    // above 2^30, ((key % mod) + mod) can pass int.MaxValue: the reference's checked((uint)key) then throws
+    if (n_buckets == 0 || n_buckets > (1u << 30)) return fail(c, ORL_E_INVALID, "n_buckets must be in [1, 2^30]");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    int e = launch_client_buckets(d_msgs, n, n_buckets, d_bucket, stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "client buckets launch");
     return ORL_OK;
 }
 

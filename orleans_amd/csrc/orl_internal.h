@@ -87,7 +87,8 @@ struct alignas(16) RouteParams {
     uint32_t policy;
     uint32_t n_active;
     uint32_t n_act;
-    uint32_t pad0[3];
+    uint32_t cache_on;                 // directory cache populated: probe it for remote owners
+    uint32_t pad0[2];
     uint64_t mem_tcd, mem_n0, mem_n1;  // Constants.SystemMembershipTableId
     uint64_t pad1;
 };
@@ -157,6 +158,15 @@ inline uint64_t max_segments(uint64_t n, int hb) {
     return (n + s - 1) / s + std::min<uint64_t>(1ull << hb, n);
 }
 
+// The directory partition table and the directory cache (AdaptiveGrainDirectoryCache) a route launch probes.
+// cache == nullptr / RouteParams.cache_on == 0: remote owners give ORL_ST_REMOTE_OWNER without a probe.
+struct DirView {
+    const DirSlot* dir;
+    uint64_t mask;
+    const DirSlot* cache;
+    uint64_t cmask;
+};
+
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
 // All return hipError_t as int; they only enqueue on `stream`.
 struct Scratch {
@@ -178,11 +188,11 @@ struct Scratch {
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
-int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
+int launch_route_bucket(const RouteParams* d_params, const DirView& dv,
                         const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
                         void* ev_route_begin, void* ev_route_end);
-int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask,
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv,
                                const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
                                const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
                                uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
@@ -194,6 +204,9 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
                       const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act,
                       uint32_t n_silos, uint32_t* d_slot, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status, uint32_t* d_err,
                       void* stream);
+int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                        const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
+                        uint8_t* d_flag, uint32_t* d_err, void* stream);
 int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                       size_t n, uint32_t* d_slot, uint8_t* d_removed, void* stream);
 int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots, uint32_t me, bool remove, uint64_t* d_cnt,
@@ -207,6 +220,10 @@ int launch_ring_owner(uint32_t kind, const RouteParams* d_params, const uint32_t
 int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32_t* d_vr_hash, const uint8_t* d_vr_silo,
                         uint32_t vr_n, const uint8_t* d_guids, size_t n, uint32_t n_queues, uint32_t me, bool excl_me,
                         uint32_t* d_queue, uint8_t* d_silo, void* stream);
+// f4: outbound queue per routed message; client gateway bucket per message.
+int launch_outbound_queues(const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n, uint32_t n_senders,
+                           const int32_t* d_silo_hash, const uint8_t* d_silo_known, uint32_t* d_queue, void* stream);
+int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

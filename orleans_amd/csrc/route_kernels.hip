@@ -112,11 +112,13 @@ __device__ __forceinline__ bool encode_wire(const u32x4& h0, const u32x4& h1, u3
 
 // Stages 1-3 for one message, split so a thread can keep several messages' directory probes in flight:
 //   route_head  stages 1-2 + every decision that needs no directory (returns the final route word, or
-//               kNeedProbe when the owner's partition is local and must be probed);
+//               kNeedProbe when the owner's partition is local and must be probed, or kNeedProbeCache when the
+//               owner is remote and the directory cache is on: LocalLookup's cache branch, :691-702);
 //   probe_slot  one 32-B slot compare (stage 3), repeated along the linear-probe chain;
 //   route_tail  IsValidSilo filter + placement of misses.
 // Together they mirror the oracle's route_one (Dispatcher.AddressMessage, Dispatcher.cs:555-579).
 constexpr uint32_t kNeedProbe = 0xFFFFFFFFu;
+constexpr uint32_t kNeedProbeCache = 0xFFFFFFFEu;
 
 __device__ __forceinline__ uint32_t route_head(const RouteParams& P, const Msg& m, bool excl_opt, uint32_t& h,
                                                uint32_t& owner, uint32_t& rf) {
@@ -148,7 +150,8 @@ __device__ __forceinline__ uint32_t route_head(const RouteParams& P, const Msg& 
         }
     }
     if (cat == ORL_CAT_KEYEXT_GRAIN) return pack_route(owner, 0xFFu, ORL_ST_KEYEXT_UNRESOLVED, rf);
-    if (!mask_bit(P.local, owner)) return pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, rf);
+    if (!mask_bit(P.local, owner))
+        return P.cache_on ? kNeedProbeCache : pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, rf);
     return kNeedProbe;
 }
 
@@ -167,13 +170,14 @@ __device__ __forceinline__ int probe_slot(const u32x4& a, const u32x4& b, const 
 }
 
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
-                                               bool found, uint32_t fact, uint32_t fsilo, uint32_t& act) {
+                                               bool found, uint32_t fact, uint32_t fsilo, uint32_t& act, bool via_cache) {
     const uint32_t me = m.meta & 0xFFu;
-    if (found && mask_bit(P.functional, fsilo)) {  // LookUpGrain filtered by IsValidSilo
+    if (found && mask_bit(P.functional, fsilo)) {  // LookUpGrain / cache LookUp, filtered by IsValidSilo
         act = fact;
-        return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u));
+        return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u) | (via_cache ? ORL_RF_CACHED : 0u));
     }
     act = ORL_NO_ACT;
+    if (via_cache) return pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, rf);  // cache miss: the FullLookup path
     if ((uint32_t)(m.tcd >> 56) == ORL_CAT_CLIENT) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
     uint32_t host;
     if (P.policy == ORL_POLICY_PREFER_LOCAL) host = me;
@@ -184,13 +188,16 @@ __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& 
 
 // Stages 1-3 for one message.  The linear-probe chain is continued by a flag loop (measured 13 % faster in
 // k_route than an early-return helper loop).
-__device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t mask,
-                                              const Msg& m, bool excl_opt, uint32_t& act) {
+__device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
+                                              const DirSlot* __restrict__ cache, uint64_t cmask, const Msg& m, bool excl_opt,
+                                              uint32_t& act) {
     uint32_t h, owner, rf;
     act = ORL_NO_ACT;
     const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
-    if (r != kNeedProbe) return r;
-    const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
+    if (r < kNeedProbeCache) return r;
+    const bool vc = r == kNeedProbeCache;
+    const u32x4* dir4 = reinterpret_cast<const u32x4*>(vc ? cache : dir);
+    const uint64_t mask = vc ? cmask : dmask;
     uint64_t slot = fmix32(h) & mask;
     uint32_t fact = 0, fsilo = 0;
     int st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
@@ -198,7 +205,7 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
         slot = (slot + 1) & mask;
         st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
     }
-    return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act);
+    return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, vc);
 }
 
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
@@ -247,7 +254,8 @@ struct RouteSmem {
 // WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
 template <int HB, bool WIRE>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
-                                                         uint64_t mask, const void* __restrict__ in, uint32_t n,
+                                                         uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
+                                                         const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
                                                          uint32_t bins, uint32_t shift, uint32_t items) {
@@ -257,7 +265,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     __syncthreads();
-    const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
     const uint32_t n_act = sm.P.n_act;
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
     for (uint32_t j = 0; j < items; ++j) {
@@ -265,11 +272,16 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         Msg m;
         if (e < n) m = WIRE ? load_wire(static_cast<const orl_wire_msg*>(in), e) : load_hdr(static_cast<const orl_msg_hdr*>(in), e);
         uint32_t h = 0, own = 0, rf = 0, r = 0;
-        uint64_t slot = 0;
+        uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
+        const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
         if (e < n) {
             r = route_head(sm.P, m, excl != 0, h, own, rf);
-            if (r == kNeedProbe) {
+            if (r >= kNeedProbeCache) {
+                if (r == kNeedProbeCache) {  // remote owner, directory cache on
+                    dir4 = reinterpret_cast<const u32x4*>(cache);
+                    mask = cmask;
+                }
                 slot = fmix32(h) & mask;
                 sa = dir4[2 * slot];
                 sb = dir4[2 * slot + 1];
@@ -277,7 +289,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         }
         int st = 3;
         uint32_t fact = 0, fsilo = 0;
-        if (r == kNeedProbe) st = probe_slot(sa, sb, m, fact, fsilo);
+        if (r >= kNeedProbeCache) st = probe_slot(sa, sb, m, fact, fsilo);
         for (uint64_t step = 0; st == 2 && step < mask; ++step) {
             slot = (slot + 1) & mask;
             sa = dir4[2 * slot];
@@ -286,7 +298,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         }
         if (e < n) {
             uint32_t act = ORL_NO_ACT, rr = r;
-            if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act);
+            if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
             route[e] = rr;
             act_out[e] = act;
             if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
@@ -944,7 +956,8 @@ struct FanSmem {
 
 template <int HB>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
-    const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask,
+    const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
+    uint64_t cmask,
     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
@@ -1012,7 +1025,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
-        route[e] = route_msg(sm.P, dir, mask, m, excl != 0, act);
+        route[e] = route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
         act_out[e] = act;
         if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
     }
@@ -1313,6 +1326,73 @@ constexpr uint32_t kSlotMask = 0x7FFFFFFFu;
 constexpr uint8_t kInsCandidate = 0xFE;  // probe outcome: joined / claimed a slot (resolved by k_dir_ins_resolve)
 constexpr uint32_t kRetryLimit = 1u << 22;
 
+// Find `k` on its chain or claim a slot for it (the probe of k_dir_ins_probe / k_cache_probe): returns 0 = an
+// equal FULL entry at *slot_out, 1 = joined or claimed the slot *slot_out (claim word atomicMin'ed with `tag`),
+// -1 = no free slot.  LAST_WINS (cache AddOrUpdate) also claims a FULL entry, so the batch's last writer updates it.
+template <bool LAST_WINS>
+__device__ __forceinline__ int find_or_claim(DirSlot* __restrict__ dir, uint64_t mask, uint32_t* __restrict__ claim,
+                                             const orl_grain_key& k, uint32_t tag, uint64_t& slot_out, bool& was_tomb_out) {
+    const uint64_t start = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
+    int outcome = -1;  // 0 = existing FULL entry, 1 = candidate for a claimed slot
+    uint64_t slot = start;
+    bool was_tomb = false;
+    for (uint32_t attempt = 0; outcome < 0 && attempt < kRetryLimit; ++attempt) {
+        // one attempt: walk the chain to its end (EMPTY), looking for the key and remembering the first
+        // reusable slot (tombstone or the EMPTY end); a slot another registration is still CLAIMING hides
+        // its key, so the attempt is abandoned and retried (its owner publishes within its own iteration)
+        uint64_t cur = start, free_slot = ~0ull;
+        uint32_t free_word = 0;
+        bool blocked = false, ended = false;
+        for (uint64_t step = 0; step <= mask && outcome < 0 && !blocked && !ended; ++step) {
+            const uint32_t v = __hip_atomic_load(slot_word28(dir, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t state = (v >> 8) & 0xFFu;
+            if (state == SLOT_EMPTY || state == SLOT_TOMB) {
+                if (free_slot == ~0ull) {
+                    free_slot = cur;
+                    free_word = v;
+                }
+                ended = state == SLOT_EMPTY;
+            } else if (state == SLOT_CLAIMING) {
+                blocked = true;
+            } else if (state == SLOT_CLAIMED) {
+                if (slot_key_eq(dir, cur, k, true)) {
+                    atomicMin(&claim[cur], tag);
+                    slot = cur;
+                    outcome = 1;
+                }
+            } else if (slot_key_eq(dir, cur, k, false)) {  // FULL
+                slot = cur;
+                outcome = 0;
+                if (LAST_WINS) atomicMin(&claim[cur], tag);  // an update of the present entry
+            }
+            cur = (cur + 1) & mask;
+        }
+        if (outcome >= 0) break;
+        if (blocked || free_slot == ~0ull) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t expect = free_word;
+        if (__hip_atomic_compare_exchange_strong(slot_word28(dir, free_slot), &expect, (uint32_t)SLOT_CLAIMING << 8,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            uint64_t* kw = reinterpret_cast<uint64_t*>(dir + free_slot);
+            __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key write-through before the state flips
+            __hip_atomic_store(slot_word28(dir, free_slot), (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            atomicMin(&claim[free_slot], tag);
+            slot = free_slot;
+            was_tomb = ((free_word >> 8) & 0xFFu) == SLOT_TOMB;
+            outcome = 1;
+        }  // else: another registration took that slot first: walk again
+    }
+    slot_out = slot;
+    was_tomb_out = was_tomb;
+    return outcome;
+}
+
 __global__ __launch_bounds__(256) void k_dir_ins_probe(const RouteParams* __restrict__ gp, DirSlot* __restrict__ dir, uint64_t mask,
                                                        uint32_t* __restrict__ claim, const orl_grain_key* __restrict__ keys,
                                                        const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
@@ -1337,61 +1417,9 @@ __global__ __launch_bounds__(256) void k_dir_ins_probe(const RouteParams* __rest
     }
     uint32_t out_slot = kSlotNone;
     if (st == kInsCandidate) {
-        const uint64_t start = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
-        int outcome = -1;  // 0 = existing FULL entry, 1 = candidate for a claimed slot
-        uint64_t slot = start;
+        uint64_t slot = 0;
         bool was_tomb = false;
-        for (uint32_t attempt = 0; outcome < 0 && attempt < kRetryLimit; ++attempt) {
-            // one attempt: walk the chain to its end (EMPTY), looking for the key and remembering the first
-            // reusable slot (tombstone or the EMPTY end); a slot another registration is still CLAIMING hides
-            // its key, so the attempt is abandoned and retried (its owner publishes within its own iteration)
-            uint64_t cur = start, free_slot = ~0ull;
-            uint32_t free_word = 0;
-            bool blocked = false, ended = false;
-            for (uint64_t step = 0; step <= mask && outcome < 0 && !blocked && !ended; ++step) {
-                const uint32_t v = __hip_atomic_load(slot_word28(dir, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t state = (v >> 8) & 0xFFu;
-                if (state == SLOT_EMPTY || state == SLOT_TOMB) {
-                    if (free_slot == ~0ull) {
-                        free_slot = cur;
-                        free_word = v;
-                    }
-                    ended = state == SLOT_EMPTY;
-                } else if (state == SLOT_CLAIMING) {
-                    blocked = true;
-                } else if (state == SLOT_CLAIMED) {
-                    if (slot_key_eq(dir, cur, k, true)) {
-                        atomicMin(&claim[cur], i);
-                        slot = cur;
-                        outcome = 1;
-                    }
-                } else if (slot_key_eq(dir, cur, k, false)) {  // FULL
-                    slot = cur;
-                    outcome = 0;
-                }
-                cur = (cur + 1) & mask;
-            }
-            if (outcome >= 0) break;
-            if (blocked || free_slot == ~0ull) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            uint32_t expect = free_word;
-            if (__hip_atomic_compare_exchange_strong(slot_word28(dir, free_slot), &expect, (uint32_t)SLOT_CLAIMING << 8,
-                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                uint64_t* kw = reinterpret_cast<uint64_t*>(dir + free_slot);
-                __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key write-through before the state flips
-                __hip_atomic_store(slot_word28(dir, free_slot), (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                atomicMin(&claim[free_slot], i);
-                slot = free_slot;
-                was_tomb = ((free_word >> 8) & 0xFFu) == SLOT_TOMB;
-                outcome = 1;
-            }  // else: another registration took that slot first: walk again
-        }
+        const int outcome = find_or_claim<false>(dir, mask, claim, k, i, slot, was_tomb);
         if (outcome < 0) {  // no free slot on the whole table (or a claim that never published)
             atomicOr(err, 1u);
             st = ORL_INS_UNSUPPORTED;
@@ -1440,6 +1468,52 @@ __global__ __launch_bounds__(256) void k_dir_ins_commit(DirSlot* __restrict__ di
     claim[slot] = kSlotNone;
     atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
     if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);  // tombstones - 1
+}
+
+// Directory cache AddOrUpdate (AdaptiveGrainDirectoryCache.AddOrUpdate; f4): the batch's LAST writer of a key
+// sets its entry (insert or update).  Claim tag = ~index, so atomicMin keeps the largest index.  Entries with an
+// activation handle >= n_act or a silo outside the table are skipped.
+__global__ __launch_bounds__(256) void k_cache_probe(DirSlot* __restrict__ cache, uint64_t mask, uint32_t* __restrict__ claim,
+                                                     const orl_grain_key* __restrict__ keys, const uint32_t* __restrict__ acts,
+                                                     const uint8_t* __restrict__ silos, uint32_t n, uint32_t n_act,
+                                                     uint32_t n_silos, uint32_t* __restrict__ slot_out, uint32_t* __restrict__ err) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    uint32_t out = kSlotNone;
+    if (acts[i] < n_act && silos[i] < n_silos) {
+        uint64_t slot = 0;
+        bool was_tomb = false;
+        if (find_or_claim<true>(cache, mask, claim, keys[i], ~i, slot, was_tomb) >= 0)
+            out = (uint32_t)slot | (was_tomb ? kSlotWasTomb : 0u);
+        else
+            atomicOr(err, 1u);
+    }
+    slot_out[i] = out;
+}
+
+__global__ __launch_bounds__(256) void k_cache_resolve(const uint32_t* __restrict__ claim, uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                       uint8_t* __restrict__ win) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t sl = slot_in[i];
+    win[i] = (sl != kSlotNone && claim[sl & kSlotMask] == ~i) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_cache_commit(DirSlot* __restrict__ cache, uint32_t* __restrict__ claim,
+                                                      const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos, uint32_t n,
+                                                      const uint32_t* __restrict__ slot_in, const uint8_t* __restrict__ win,
+                                                      uint64_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || !win[i]) return;
+    const uint32_t slot = slot_in[i] & kSlotMask;
+    const bool fresh = cache[slot].state == SLOT_CLAIMED;  // a new entry (else an update of a FULL one)
+    uint64_t* w24 = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(cache + slot) + 24);
+    *w24 = (uint64_t)acts[i] | ((uint64_t)silos[i] << 32) | ((uint64_t)SLOT_FULL << 40);
+    claim[slot] = kSlotNone;
+    if (fresh) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
+        if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);
+    }
 }
 
 // Unregister: the first removal of a key in batch order removes it (RemoveActivation on the entry; later ones
@@ -1668,6 +1742,39 @@ __global__ __launch_bounds__(256) void k_stream_queue(const RouteParams* __restr
 }
 
 // ---------------------------------------------------------------------------------------------------
+// f4: outbound queue selection (OutboundMessageQueue.SendMessage, OutboundMessageQueue.cs:75-150) and client
+// gateway buckets (ProxiedMessageCenter.cs:222 → UniqueIdentifier.GetHashCode_Modulo, UniqueIdentifier.cs:60-66).
+__global__ __launch_bounds__(256) void k_outbound_queues(const orl_msg_hdr* __restrict__ msgs, const uint32_t* __restrict__ route,
+                                                         uint32_t n, uint32_t n_senders, const int32_t* __restrict__ silo_hash,
+                                                         const uint8_t* __restrict__ silo_known, uint32_t* __restrict__ queue) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t meta = reinterpret_cast<const uint32_t*>(msgs + e)[6];  // sending_silo, category, flags, target_silo
+    const uint32_t host = (route[e] >> 8) & 0xFFu, me = meta & 0xFFu, cat = (meta >> 8) & 0xFFu;
+    uint32_t q;
+    if (host == 0xFFu) q = ORL_OUTQ_REJECT;                      // no target silo (:100-105)
+    else if (host == me) q = ORL_OUTQ_LOOPBACK;                   // shortcut to this silo (:113-119)
+    else if (cat == 0u) q = ORL_OUTQ_PING;                        // Message.Categories.Ping
+    else if (cat == 1u) q = ORL_OUTQ_SYSTEM;                      // Message.Categories.System
+    else if (!silo_known[host]) q = ORL_OUTQ_UNKNOWN_SILO;
+    else {
+        const int32_t h = silo_hash[host];
+        q = h == INT32_MIN ? ORL_OUTQ_OVERFLOW : (uint32_t)(h < 0 ? -h : h) % n_senders;  // Math.Abs(...) % senders.Length
+    }
+    queue[e] = q;
+}
+
+__global__ __launch_bounds__(256) void k_client_buckets(const orl_msg_hdr* __restrict__ msgs, uint32_t n, uint32_t n_buckets,
+                                                        uint32_t* __restrict__ bucket) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= n) return;
+    const Msg m = load_hdr(msgs, e);
+    const uint32_t u = ((m.meta >> 16) & ORL_HDR_HASH_VALID) ? m.aux : jenkins3(m.tcd, m.n0, m.n1);  // GetUniformHashCode
+    const int32_t key = (int32_t)u, mod = (int32_t)n_buckets;                                     // GetHashCode()
+    bucket[e] = (uint32_t)(((key % mod) + mod) % mod);                                             // C# % truncates as C does
+}
+
+// ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
@@ -1818,7 +1925,7 @@ int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* st
     return (int)hipGetLastError();
 }
 
-int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const void* d_in, bool wire,
+int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const void* d_in, bool wire,
                         size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                         uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
     hipStream_t st = (hipStream_t)stream;
@@ -1835,7 +1942,8 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
     const bool hist = buckets && rh.on;
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
-#define ORL_ROUTE(H, W) hipLaunchKernelGGL((k_route<H, W>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir, dir_mask, d_in, \
+#define ORL_ROUTE(H, W) hipLaunchKernelGGL((k_route<H, W>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask,     \
+                                           dv.cache, dv.cmask, d_in,                                                          \
                                            (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
     if (hist) {
         if (wire) ORL_ROUTE(kMaxDigitBits, true); else ORL_ROUTE(kMaxDigitBits, false);
@@ -1850,7 +1958,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint6
     return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st);
 }
 
-int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir, uint64_t dir_mask, const uint64_t* d_csr_off,
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const uint64_t* d_csr_off,
                                const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys, const uint32_t* d_pubs,
                                const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts, uint32_t n_act,
                                uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
@@ -1886,8 +1994,8 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirSlot* d_dir
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
 
-#define ORL_FAN(H, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, d_dir,   \
-                                                       dir_mask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
+#define ORL_FAN(H, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
+                                                       dv.mask, dv.cache, dv.cmask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
                                                        follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);
@@ -1927,6 +2035,19 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
     hipLaunchKernelGGL(k_dir_ins_resolve, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_wact,
                        d_wsilo);
     hipLaunchKernelGGL(k_dir_ins_commit, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_cnt);
+    return (int)hipGetLastError();
+}
+
+int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                        const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
+                        uint8_t* d_flag, uint32_t* d_err, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return 0;
+    const dim3 g(ceil_div(n, 256)), b(256);
+    hipLaunchKernelGGL(k_cache_probe, g, b, 0, st, d_cache, mask, d_claim, d_keys, d_acts, d_silos, (uint32_t)n, n_act, n_silos,
+                       d_slot, d_err);
+    hipLaunchKernelGGL(k_cache_resolve, g, b, 0, st, d_claim, (uint32_t)n, d_slot, d_flag);
+    hipLaunchKernelGGL(k_cache_commit, g, b, 0, st, d_cache, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_flag, d_cnt);
     return (int)hipGetLastError();
 }
 
@@ -1981,6 +2102,21 @@ int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32
     else
         hipLaunchKernelGGL(k_stream_queue<ORL_RING_VBUCKETS>, g, b, d_silo ? 5 * (size_t)vr_n + 16 : 0, st, d_params, d_vr_hash,
                            d_vr_silo, vr_n, gu, (uint32_t)n, n_queues, me, excl_me ? 1u : 0u, d_queue, d_silo);
+    return (int)hipGetLastError();
+}
+
+int launch_outbound_queues(const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n, uint32_t n_senders,
+                           const int32_t* d_silo_hash, const uint8_t* d_silo_known, uint32_t* d_queue, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_outbound_queues, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_msgs, d_route, (uint32_t)n,
+                       n_senders, d_silo_hash, d_silo_known, d_queue);
+    return (int)hipGetLastError();
+}
+
+int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_client_buckets, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_msgs, (uint32_t)n, n_buckets,
+                       d_bucket);
     return (int)hipGetLastError();
 }
 

@@ -387,6 +387,41 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_stream_queue_batch_device(self._ctx, int(kind), ptr(d_guids), int(n), int(n_queues),
                                                          int(me), int(opts), ptr(d_queue), ptr(d_silo), ptr(stream)))
 
+    # ---- directory cache ----
+    def cache_config(self, capacity: int) -> None:
+        """Allocate the device directory cache (AdaptiveGrainDirectoryCache) for `capacity` remote grains."""
+        self._ck(self._lib.orl_cache_config(self._ctx, int(capacity)))
+
+    def cache_clear(self) -> None:
+        self._ck(self._lib.orl_cache_clear(self._ctx))
+
+    def cache_add_or_update_device(self, d_keys, d_acts, d_silos, n: int, stream=None) -> None:
+        self._ck(self._lib.orl_cache_add_or_update_device(self._ctx, ptr(d_keys), ptr(d_acts), ptr(d_silos), int(n),
+                                                          ptr(stream)))
+
+    def cache_remove_device(self, d_keys, n: int, d_removed, stream=None) -> None:
+        """Cache invalidation (CACHE_INVALIDATION_HEADER, InsideGrainClient.cs:298-308)."""
+        self._ck(self._lib.orl_cache_remove_device(self._ctx, ptr(d_keys), int(n), ptr(d_removed), ptr(stream)))
+
+    def cache_count(self) -> int:
+        n = C.c_uint64()
+        self._ck(self._lib.orl_cache_count(self._ctx, C.byref(n)))
+        return n.value
+
+    # ---- outbound queues / client buckets (SURVEY §8(f) f4) ----
+    def set_silo_hash(self, silo: int, consistent_hash: int) -> None:
+        self._ck(self._lib.orl_silo_hash_set(self._ctx, int(silo), int(consistent_hash)))
+
+    def outbound_queues_device(self, d_msgs, d_route, n: int, n_senders: int, d_queue, stream=None) -> None:
+        """OutboundMessageQueue.SendMessage's queue per routed message (OutboundMessageQueue.cs:75-150)."""
+        self._ck(self._lib.orl_outbound_queues_device(self._ctx, ptr(d_msgs), ptr(d_route), int(n), int(n_senders),
+                                                      ptr(d_queue), ptr(stream)))
+
+    def client_buckets_device(self, d_msgs, n: int, n_buckets: int, d_bucket, stream=None) -> None:
+        """ProxiedMessageCenter's gateway bucket per message: TargetGrain.GetHashCode_Modulo(n_buckets)."""
+        self._ck(self._lib.orl_client_buckets_device(self._ctx, ptr(d_msgs), int(n), int(n_buckets), ptr(d_bucket),
+                                                     ptr(stream)))
+
     def compact_directory(self) -> None:
         """Rebuild the partition without tombstones."""
         self._ck(self._lib.orl_dir_compact(self._ctx))

@@ -701,3 +701,108 @@ def test_stream_reminder_rings_vs_oracle(torch):
         exp_s = np.array([vr.target(qh[q], 0, False) for q in exp_q], np.uint8)
         np.testing.assert_array_equal(d_s.cpu().numpy(), exp_s)
     eng.close()
+
+
+def test_outbound_queues_and_client_buckets_vs_oracle(torch):
+    """OutboundMessageQueue.SendMessage queue selection per routed message (reject, loopback,
+    ping / system senders, Math.Abs(hash) % senders incl. the int.MinValue overflow, unknown silo) and the client's
+    GetHashCode_Modulo gateway buckets (incl. KeyExt precomputed hashes), against the pure-Python restatement."""
+    t = torch
+    cl = W.default_cluster()
+    eng = GrainDirectoryEngine(n_act=4, dir_capacity=16, max_batch=1024, device=0)
+    eng.set_silos(12)
+    hashes = {s: int(cl.hashes[s]) for s in range(8)}
+    for s in range(8):
+        eng.add_server(s, hashes[s])
+    hashes[9] = -(1 << 31)   # Math.Abs(int.MinValue) overflows
+    hashes[10] = -12345
+    eng.set_silo_hash(9, hashes[9])
+    eng.set_silo_hash(10, hashes[10])  # silo 11: never given → unknown
+    rng = np.random.default_rng(11)
+    n = 50_000
+    msgs = W.uniform_messages(cl, 100_000, n, seed=8)
+    msgs["category"] = rng.integers(0, 3, n)
+    msgs["sending_silo"] = rng.integers(0, 12, n)
+    kx = rng.random(n) < 0.1
+    msgs["flags"][kx] |= L.HDR_HASH_VALID
+    msgs["aux"][kx] = rng.integers(0, 1 << 32, int(kx.sum()), dtype=np.uint64).astype(np.uint32)
+    host = rng.integers(0, 13, n)
+    host[host == 12] = 0xFF
+    route = (host.astype(np.uint32) << 8) | np.uint32(L.ST_HIT << 16)
+    d_m = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+    d_r = t.from_numpy(route.view(np.int32)).cuda()
+    d_q = t.empty(n, dtype=t.int32, device="cuda")
+    st = t.cuda.current_stream().cuda_stream
+    for ns in (1, 3, 8):
+        eng.outbound_queues_device(d_m, d_r, n, ns, d_q, stream=st)
+        t.cuda.synchronize()
+        exp = np.array([P.outbound_queue(int(host[i]), int(msgs["sending_silo"][i]), int(msgs["category"][i]), hashes, ns)
+                        for i in range(n)], np.uint32)
+        np.testing.assert_array_equal(d_q.cpu().numpy().view(np.uint32), exp)
+    uni = np.where(kx, msgs["aux"], W.jenkins3_np(msgs["tcd"], msgs["n0"], msgs["n1"])).astype(np.uint32)
+    for nb in (1, 7, 100, 1 << 30):
+        eng.client_buckets_device(d_m, n, nb, d_q, stream=st)
+        t.cuda.synchronize()
+        exp = np.array([P.client_bucket(int(u), nb) for u in uni], np.uint32)
+        np.testing.assert_array_equal(d_q.cpu().numpy().view(np.uint32), exp)
+    eng.close()
+
+
+def test_directory_cache_in_route_vs_oracle(torch):
+    """the device directory cache answers LocalLookup for remote-owned grains (HIT | CACHED, the
+    cached silo as host; entries on invalid silos filtered; misses stay REMOTE_OWNER), AddOrUpdate keeps the batch's
+    last writer, invalidation removes, and stage 4 buckets cached activations by their handle — all equal to the
+    oracle (C++ restatement + pyref.apply_directory_cache)."""
+    t = torch
+    cl = W.default_cluster()
+    local = [1, 1, 0, 0, 0, 0, 0, 0]
+    functional = [1, 1, 1, 1, 1, 1, 0, 1]
+    n_grains, n_act = 50_000, 60_000
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+    eng.set_silos(8, functional=functional, local=local)
+    o = cpu_ref.Oracle(8, functional=functional, local=local)
+    for s in range(8):
+        eng.add_server(s, int(cl.hashes[s]))
+        o.add_server(s, int(cl.hashes[s]))
+    keys, _, owner, _ = W.grain_population(cl, n_grains)
+    mine = np.nonzero(np.isin(owner, [0, 1]))[0]
+    eng.register_single_activation(keys[mine], mine.astype(np.uint32), owner[mine])
+    o.register(keys[mine], mine.astype(np.uint32), owner[mine])
+    eng.cache_config(40_000)
+    rng = np.random.default_rng(2)
+    remote = np.nonzero(~np.isin(owner, [0, 1]))[0]
+    cache = {}
+    st_ = t.cuda.current_stream().cuda_stream
+
+    def dev(a):
+        return t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+
+    msgs = W.uniform_messages(cl, n_grains, 200_000, seed=4)
+    kt = list(zip(msgs["tcd"].tolist(), msgs["n0"].tolist(), msgs["n1"].tolist()))
+    for rnd in range(3):
+        pick = rng.choice(remote, 20_000)   # duplicates within the batch: the last writer wins
+        acts = (50_000 + rng.integers(0, 10_000, len(pick))).astype(np.uint32)
+        silos = rng.integers(0, 8, len(pick)).astype(np.uint8)
+        eng.cache_add_or_update_device(dev(keys[pick]), dev(acts), dev(silos), len(pick), stream=st_)
+        for g, a, s in zip(pick.tolist(), acts.tolist(), silos.tolist()):
+            cache[(int(keys["tcd"][g]), int(keys["n0"][g]), int(keys["n1"][g]))] = (a, s)
+        inval = rng.choice(remote, 3000)
+        d_rm = t.empty(len(inval), dtype=t.uint8, device="cuda")
+        eng.cache_remove_device(dev(keys[inval]), len(inval), d_rm, stream=st_)
+        t.cuda.synchronize()
+        for g in inval.tolist():
+            cache.pop((int(keys["tcd"][g]), int(keys["n0"][g]), int(keys["n1"][g])), None)
+        assert eng.cache_count() == len(cache)
+        res = eng.address_messages(msgs)
+        r0, a0 = o.route(msgs)
+        r_ref, a_ref = P.apply_directory_cache(r0.tolist(), a0.tolist(), msgs["sending_silo"].tolist(), kt, cache,
+                                               functional)
+        np.testing.assert_array_equal(res.route, np.array(r_ref, np.uint32))
+        np.testing.assert_array_equal(res.act, np.array(a_ref, np.uint32))
+        o_ref, f_ref = o.bucket(np.array(a_ref, np.uint32), n_act)
+        np.testing.assert_array_equal(res.order, o_ref)
+        np.testing.assert_array_equal(res.offsets, f_ref)
+        assert ((res.route >> 24) & L.RF_CACHED).sum() > 1000
+    eng.cache_clear()
+    np.testing.assert_array_equal(eng.address_messages(msgs).route, o.route(msgs)[0])
+    eng.close()
