@@ -2,10 +2,10 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
-SRC = orleans_amd/csrc/route_kernels.hip orleans_amd/csrc/orl_api.cpp
+SRC = orleans_amd/csrc/route_kernels.hip orleans_amd/csrc/wire_codec.hip orleans_amd/csrc/orl_api.cpp
 HDR = include/orleans_route.h orleans_amd/csrc/orl_internal.h
 LIB = orleans_amd/liborleans_route.so
-OBJ = build/route_kernels.o build/orl_api.o
+OBJ = build/route_kernels.o build/wire_codec.o build/orl_api.o
 
 all: $(LIB) oracle
 
@@ -13,6 +13,10 @@ $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
 
 build/route_kernels.o: orleans_amd/csrc/route_kernels.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/wire_codec.o: orleans_amd/csrc/wire_codec.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

@@ -48,9 +48,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7, 8],
                     help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches; "
-                         "7 = stream / reminder ring leg (f3)")
+                         "7 = stream / reminder ring leg (f3); 8 = receive path leg (f2): frames -> headers -> route")
+    ap.add_argument("--frames", type=int, default=4 * 1024 * 1024, help="frames per step (config 8)")
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -73,8 +74,8 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if args.config in (4, 5, 6, 7):
-            raise SystemExit("--config 4/5/6/7 are single-GPU measurement legs")
+        if args.config in (4, 5, 6, 7, 8):
+            raise SystemExit("--config 4/5/6/7/8 are single-GPU measurement legs")
 
     if args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
@@ -84,6 +85,8 @@ def main():
         res = run_directory(args, torch)
     elif args.config == 7:
         res = run_rings(args, torch)
+    elif args.config == 8:
+        res = run_wire(args, torch)
     else:
         res = run_presence(args, torch)
     if world > 1:
@@ -444,6 +447,105 @@ def run_rings(args, torch):
                                     "unit": "GB/s", "frac": 5.0 * n / (out["vbuckets"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "traffic": None, "bytes_per_key": 5},
             "cpu_baseline": None}
+
+
+def run_wire(args, torch):
+    """Receive path: a receive buffer of back-to-back frames (config-2 addressing, 20% complete
+    addresses, 5% KeyExt targets, bodies 0-48 B) decoded into headers on the device, then routed + bucketed."""
+    from orleans_amd import _lib as L
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+
+    n, n_grains = args.frames, args.grains or (1 << 24)
+    cl = W.balanced_cluster()
+    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=n, device=0)
+    W.setup_engine(eng, cl)
+    W.register_silo_addresses(eng, cl)
+    keys, _, owner, reg = W.grain_population(cl, n_grains, 1.0)
+    W.register_population(eng, keys, owner, reg)
+    t0 = time.perf_counter()
+    buf, offs, exp = W.request_frames(cl, n_grains, n, complete_frac=0.2, keyext_frac=0.05)
+    log(f"wire: {n} frames, {len(buf) / 2**20:.0f} MiB built in {time.perf_counter() - t0:.1f} s")
+    hl = np.array([int.from_bytes(bytes(buf[int(o):int(o) + 4]), "little") for o in offs[:4096]])
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_hdr = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    d_st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    d_r = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_a = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_o = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_f = torch.empty(n_grains + 2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.Stream()  # the library launches on this stream; events are recorded on it too
+    st = stream.cuda_stream
+
+    def decode():
+        eng.decode_frames_device(d_buf, len(buf), d_off, n, d_hdr, d_st, d_bad, stream=st)
+
+    def decode_route():
+        decode()
+        eng.address_messages_device(d_hdr, n, d_r, d_a, d_o, d_f, stream=st)
+
+    decode()
+    torch.cuda.synchronize()
+    assert int(d_bad.item()) == 0, "synthetic frames must decode cleanly"
+    got = d_hdr[:4096].cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+    for f in ("tcd", "n1", "sending_silo", "flags", "target_silo"):
+        assert (got[f] == exp[f][:4096]).all(), f
+    out = {}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for name, fn in (("decode", decode), ("decode_route", decode_route)):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        out[name] = (time.perf_counter() - t0) * 1e3 / args.steps
+        out[name + "_event"] = ev[0].elapsed_time(ev[1]) / args.steps
+    # algorithmic bytes per decode: the 8-byte prefix + header of every frame, its offset (8), the record (32)
+    # and status (1) written; bodies are not touched
+    mean_hl = float(hl.mean())
+    alg = n * (8 + mean_hl + 8 + 32 + 1)
+    eng.close()
+    cpu = None
+    if not args.no_cpu:
+        cpu = wire_cpu_baseline(buf, offs, cl, args.cpu_wall)
+    log("wire: " + ", ".join(f"{k} {v:.3f} ms" for k, v in out.items()) + f" per {n} frames (mean header {mean_hl:.0f} B)")
+    ms = out["decode_route"]
+    return {"metric": "frames decoded+routed/sec", "value": n / (ms * 1e-3), "unit": "frames/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32 integer",
+            "data": "synthetic frames (request / response header dictionaries as SerializeMessageHeaders writes them)",
+            "config": {"workload": f"leg 8: {n} frames -> headers (device decode) -> route + bucket, "
+                                   f"{n_grains} registered grains"},
+            "ms": out, "decode_frames_per_s": n / (out["decode_event"] * 1e-3),
+            "roofline": {"bound": "hbm", "kernel": "k_decode_frames", "achieved": alg / (out["decode_event"] * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (out["decode_event"] * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_frame": 8 + mean_hl + 41},
+            "cpu_baseline": cpu}
+
+
+def wire_cpu_baseline(buf, offs, cl, target_wall):
+    """oracle/wire_codec.decode_frames (pure Python, 1 core) on a bounded prefix of the same buffer."""
+    from oracle import wire_codec as WC
+    from orleans_amd import workloads as W
+    idx = {(cl.silo_ip16(s), W.PORT, cl.gens[s]): s for s in range(cl.n_silos)}
+    raw = bytes(buf[:int(offs[min(len(offs) - 1, 200_000)])])
+    n = 2000
+    while True:
+        t0 = time.perf_counter()
+        WC.decode_frames(raw, [int(o) for o in offs[:n]], idx)
+        dt = time.perf_counter() - t0
+        if dt > target_wall or n >= 200_000:
+            break
+        n = min(200_000, int(n * max(2.0, target_wall / max(dt, 1e-3))))
+    return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} frames of the same buffer through oracle/wire_codec.decode_frames (Python)"}
 
 
 # ---- config 5: Presence heartbeats, small batches, hipGraph --------------------------------------------

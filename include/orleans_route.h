@@ -320,6 +320,38 @@ int orl_outbound_queues_device(orl_ctx* ctx, const orl_msg_hdr* d_msgs, const ui
 int orl_client_buckets_device(orl_ctx* ctx, const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket,
                               void* stream);
 
+/* ---- message header wire codec ------------------------------------------------
+ * Received frames decoded on the device into the orl_msg_hdr records the route kernels read.  A frame is
+ * Message.Serialize_Impl's output (src/Orleans/Messaging/Message.cs:915-951): int32 header length, int32 body
+ * length, the header bytes of SerializationManager.SerializeMessageHeaders (SerializationManager.cs:1692-1770),
+ * the body.  The caller gives each frame's byte offset (the decode offsets IncomingMessageBuffer.TryDecodeMessage
+ * walks, IncomingMessageBuffer.cs:94-135); the header is parsed as DeserializeMessageHeaders does
+ * (:1773-1853, BinaryTokenStreamReader.TryReadSimpleType :489-582), every value validated as the reference reader
+ * validates it, and the routing fields read as the Message getters read them (Message.cs:149, 199-255, 650-666):
+ *   target        TARGET_GRAIN (GrainId; a KeyExt grain also gets aux = its uniform hash, ORL_HDR_HASH_VALID)
+ *   sending_silo  SENDING_SILO's index in the silo address table, or sender_override (< 255) for every frame
+ *   category      CATEGORY (default Ping)
+ *   flags         ORL_HDR_ADDRESS_COMPLETE when TARGET_SILO and TARGET_ACTIVATION are set (target_silo = index)
+ * d_status[i] (one byte per frame) gives ORL_DEC_*; a non-OK frame's record is all zero and counts in *d_n_bad
+ * (device u32, optional; the call zeroes it).  d_bytes must be 4-byte aligned; nbytes is its valid length.
+ * The device decoder hands these to the host (ORL_DEC_UNSUPPORTED): SpecifiedType values (registered
+ * serializers), a header dictionary nested in a header value, local-kind DateTime values (the result depends on
+ * the host time zone), and a TARGET_GRAIN KeyExt that is not strict UTF-8 (its hash re-encodes the decoded
+ * string).  Where the reference reader or getter throws: ORL_DEC_MALFORMED. */
+#define ORL_DEC_OK 0u
+#define ORL_DEC_UNSUPPORTED 1u
+#define ORL_DEC_MALFORMED 2u
+#define ORL_DEC_UNKNOWN_SILO 3u  /* SENDING_SILO (or TARGET_SILO of a complete address) not in the table */
+#define ORL_DEC_NO_TARGET 4u     /* TargetGrain null (absent, null or not a GrainId) */
+#define ORL_DEC_NO_SENDER 5u     /* SendingSilo null and no sender_override */
+#define ORL_SENDER_FROM_HEADER 0xFFu
+/* Silo address table: the serialized SiloAddress (16 IP bytes as BinaryTokenStreamWriter.Write(IPAddress) writes
+ * them — IPv4 as 12 zero bytes + 4 — port, generation) of silo index `silo` (< 255).  ip16 NULL removes it. */
+int orl_silo_address_set(orl_ctx* ctx, uint32_t silo, const uint8_t* ip16, int32_t port, int32_t generation);
+int orl_decode_frames_device(orl_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_frame_offsets,
+                             size_t n, uint32_t sender_override, orl_msg_hdr* d_out, uint8_t* d_status, uint32_t* d_n_bad,
+                             void* stream);
+
 /* ---- multi-GPU exchange support --------------------------------------------
  * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is
  * null / system target / complete stay on the sending rank (dest = my_rank).  Writes the partitioned

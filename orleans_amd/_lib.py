@@ -51,6 +51,8 @@ RF_CACHED = 0x08
 RING_CONSISTENT, RING_VBUCKETS = 0, 1
 OUTQ_LOOPBACK, OUTQ_PING, OUTQ_SYSTEM, OUTQ_REJECT, OUTQ_OVERFLOW, OUTQ_UNKNOWN_SILO = (
     0xFFFFFFF0, 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3, 0xFFFFFFF4, 0xFFFFFFF5)
+DEC_OK, DEC_UNSUPPORTED, DEC_MALFORMED, DEC_UNKNOWN_SILO, DEC_NO_TARGET, DEC_NO_SENDER = 0, 1, 2, 3, 4, 5
+SENDER_FROM_HEADER = 0xFF
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -114,6 +116,8 @@ _SIGS = {
     "orl_silo_hash_set": (C.c_int, [_P, C.c_uint32, C.c_int32]),
     "orl_outbound_queues_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint32, _P, _P]),
     "orl_client_buckets_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P]),
+    "orl_silo_address_set": (C.c_int, [_P, C.c_uint32, _P, C.c_int32, C.c_int32]),
+    "orl_decode_frames_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
     "orl_cache_config": (C.c_int, [_P, C.c_uint64]),
     "orl_cache_clear": (C.c_int, [_P]),
     "orl_cache_add_or_update_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),

@@ -212,6 +212,11 @@ struct orl_ctx {
     uint32_t vr_n_dev = 0;
     uint32_t* d_vr_hash = nullptr;
     uint8_t* d_vr_silo = nullptr;
+    // f2: serialized SiloAddress -> silo index for the wire decoder
+    uint32_t silo_addr[256][6] = {};
+    uint8_t silo_addr_known[256] = {};
+    bool silo_addr_dirty = true;
+    SiloAddrEntry* d_silo_tab = nullptr;
     // timing: 4 events per recorded batch (call begin, route begin, route end, call end)
     bool timing = false;
     std::vector<hipEvent_t> tev;
@@ -316,6 +321,19 @@ int sync_device_state(orl_ctx* c) {
         c->vr_n_dev = (uint32_t)h.size();
         c->vr_dirty = false;
     }
+    if (c->silo_addr_dirty) {
+        SiloAddrEntry tab[kSiloAddrSlots];
+        for (auto& e : tab) { std::memset(&e, 0, sizeof e); e.silo = 0xFFu; }
+        for (uint32_t s = 0; s < 255; ++s) {
+            if (!c->silo_addr_known[s]) continue;
+            uint32_t i = silo_addr_slot(c->silo_addr[s]);
+            while (tab[i].silo != 0xFFu) i = (i + 1) & (kSiloAddrSlots - 1);
+            std::memcpy(tab[i].w, c->silo_addr[s], sizeof tab[i].w);
+            tab[i].silo = s;
+        }
+        ORL_HIP(c, hipMemcpy(c->d_silo_tab, tab, sizeof tab, hipMemcpyHostToDevice));
+        c->silo_addr_dirty = false;
+    }
     if (c->dir_dirty) {
         if (c->count == 0 && c->tombs == 0)  // an empty partition: no 32 B/slot upload
             ORL_HIP(c, hipMemset(c->d_table, 0, c->table.size() * sizeof(DirSlot)));
@@ -409,7 +427,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -467,6 +485,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
             return bail(e, "hipMalloc(vring silos)");
         if ((e = hipMalloc((void**)&c->d_silo_hash, 1024)) != hipSuccess) return bail(e, "hipMalloc(silo hashes)");
         if ((e = hipMalloc((void**)&c->d_silo_known, 256)) != hipSuccess) return bail(e, "hipMalloc(silo known)");
+        if ((e = hipMalloc((void**)&c->d_silo_tab, kSiloAddrSlots * sizeof(SiloAddrEntry))) != hipSuccess)
+            return bail(e, "hipMalloc(silo addresses)");
         if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
         if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
@@ -1079,7 +1099,7 @@ int orl_cache_config(orl_ctx* c, uint64_t capacity) {
     if (capacity == 0) return fail(c, ORL_E_INVALID, "capacity must be >= 1");
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     ORL_HIP(c, hipDeviceSynchronize());
-    hipFree(c->d_cache); hipFree(c->d_cclaim); hipFree(c->d_cstate);
+    (void)hipFree(c->d_cache); (void)hipFree(c->d_cclaim); (void)hipFree(c->d_cstate);
     c->d_cache = nullptr; c->d_cclaim = nullptr; c->d_cstate = nullptr;
     const uint64_t slots = next_pow2(2 * capacity);
     ORL_HIP(c, hipMalloc((void**)&c->d_cache, slots * sizeof(DirSlot)));
@@ -1182,6 +1202,43 @@ int orl_client_buckets_device(orl_ctx* c, const orl_msg_hdr* d_msgs, size_t n, u
     if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
     int e = launch_client_buckets(d_msgs, n, n_buckets, d_bucket, stream ? stream : c->stream);
     if (e) return hipfail(c, (hipError_t)e, "client buckets launch");
+    return ORL_OK;
+}
+
+// ---- f2: wire codec ---------------------------------------------------------------------------------
+int orl_silo_address_set(orl_ctx* c, uint32_t silo, const uint8_t* ip16, int32_t port, int32_t generation) {
+    if (!c) return ORL_E_INVALID;
+    if (silo >= 255) return fail(c, ORL_E_INVALID, "silo index %u out of range (< 255)", silo);
+    if (!ip16) {
+        c->silo_addr_known[silo] = 0;
+        c->silo_addr_dirty = true;
+        return ORL_OK;
+    }
+    if (port < 0 || port > 65535) return fail(c, ORL_E_INVALID, "port %d out of range", port);
+    uint32_t w[6];
+    std::memcpy(w, ip16, 16);
+    w[4] = (uint32_t)port;
+    w[5] = (uint32_t)generation;
+    for (uint32_t s = 0; s < 255; ++s)
+        if (s != silo && c->silo_addr_known[s] && std::memcmp(c->silo_addr[s], w, sizeof w) == 0)
+            return fail(c, ORL_E_INVALID, "address already belongs to silo %u", s);
+    std::memcpy(c->silo_addr[silo], w, sizeof w);
+    c->silo_addr_known[silo] = 1;
+    c->silo_addr_dirty = true;
+    return ORL_OK;
+}
+
+int orl_decode_frames_device(orl_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_frame_offsets, size_t n,
+                             uint32_t sender_override, orl_msg_hdr* d_out, uint8_t* d_status, uint32_t* d_n_bad, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_bytes || !d_frame_offsets || !d_out || !d_status)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if ((uintptr_t)d_bytes & 3u) return fail(c, ORL_E_INVALID, "frame buffer must be 4-byte aligned");
+    if (sender_override > ORL_SENDER_FROM_HEADER) return fail(c, ORL_E_INVALID, "sender_override must be < 255 or 0xFF");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    if (int r = sync_device_state(c)) return r;
+    int e = launch_decode_frames(d_bytes, nbytes, d_frame_offsets, n, sender_override, c->d_silo_tab, d_out, d_status,
+                                 d_n_bad, stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "decode frames launch");
     return ORL_OK;
 }
 

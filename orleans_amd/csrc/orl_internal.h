@@ -74,6 +74,23 @@ __host__ __device__ inline uint32_t jenkins3(uint64_t u1, uint64_t u2, uint64_t 
     return c;
 }
 
+// ---- f2: SiloAddress -> silo index (wire decoder) ----------------------------------------------------
+// The serialized form of a SiloAddress (BinaryTokenStreamWriter.Write(SiloAddress), :482-486): 16 IP bytes,
+// int32 port, int32 generation = six LE words.  SiloAddress.Equals compares endpoint + generation
+// (SiloAddress.cs:246-250) and the writer is canonical, so equal addresses have equal words.  Open addressing,
+// linear probing, 512 entries for at most 255 silos (load <= 1/2); silo 0xFF marks an empty entry.
+constexpr uint32_t kSiloAddrSlots = 512;
+struct alignas(32) SiloAddrEntry {
+    uint32_t w[6];
+    uint32_t silo;
+    uint32_t pad;
+};
+__host__ __device__ inline uint32_t silo_addr_slot(const uint32_t w[6]) {
+    uint32_t h = 0x811C9DC5u;
+    for (int i = 0; i < 6; ++i) h = fmix32(h ^ w[i]) * 0x9E3779B1u;
+    return fmix32(h) & (kSiloAddrSlots - 1u);
+}
+
 // ---- everything a route launch needs besides the messages (device copy, staged into LDS) ------------
 struct alignas(16) RouteParams {
     int32_t ring_hash[ORL_MAX_RING];   // membershipRingList, ascending signed hash
@@ -224,6 +241,10 @@ int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32
 int launch_outbound_queues(const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n, uint32_t n_senders,
                            const int32_t* d_silo_hash, const uint8_t* d_silo_known, uint32_t* d_queue, void* stream);
 int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket, void* stream);
+// f2: received frames -> orl_msg_hdr (wire_codec.hip).  d_bytes 4-byte aligned.
+int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
+                         uint32_t sender_override, const SiloAddrEntry* d_silo_tab, orl_msg_hdr* d_out,
+                         uint8_t* d_status, uint32_t* d_n_bad, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

@@ -1,0 +1,547 @@
+// wire_codec.hip — f2: received message frames -> the orl_msg_hdr records the route kernels read (gfx950).
+//
+// Reference (paths relative to randa1/orleans):
+//   framing    Message.Serialize_Impl (src/Orleans/Messaging/Message.cs:915-951): int32 header length, int32 body
+//              length, header bytes, body bytes; IncomingMessageBuffer.TryDecodeMessage (IncomingMessageBuffer.cs:
+//              94-135) walks the frames — the host hands us the frame offsets it found.
+//   headers    SerializationManager.DeserializeMessageHeaders (SerializationManager.cs:1773-1853) over
+//              BinaryTokenStreamReader.TryReadSimpleType (BinaryTokenStreamReader.cs:489-582).
+//   getters    Message.Category / TargetSilo / SendingSilo / TargetGrain / TargetActivation / TargetAddress
+//              (Message.cs:149, 199-231, 251-255; GetScalarHeader / GetSimpleHeader :650-666).
+// The oracle is oracle/wire_codec.py (decode_frames); statuses and their precedence are defined there.
+//
+// One lane per frame.  Each lane walks its own header sequentially; bytes come from 4-byte aligned word
+// loads joined with v_alignbyte (a lane's consecutive reads hit the same L1/L2 lines), so no byte-granular
+// global loads and no reads beyond the aligned word that holds a frame's last byte.  Byte/integer work only.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "orl_internal.h"
+
+namespace orl {
+
+namespace {
+
+// SerializationTokenType (SerializationTokenType.cs:30-109)
+enum : uint32_t {
+    T_NULL = 0, T_TRUE = 3, T_FALSE = 4, T_INT = 11, T_SHORT = 12, T_LONG = 13, T_SBYTE = 14, T_UINT = 15,
+    T_USHORT = 16, T_ULONG = 17, T_BYTE = 18, T_FLOAT = 19, T_DOUBLE = 20, T_DECIMAL = 21, T_STRING = 22,
+    T_CHAR = 23, T_GUID = 24, T_DATE = 25, T_TIMESPAN = 26, T_IPADDR = 27, T_IPEP = 28, T_OBJECT = 29,
+    T_GRAIN = 40, T_ACT = 41, T_SILO = 42, T_ACTADDR = 43, T_CORR = 44, T_DICT = 50, T_LIST = 51,
+    T_SPECIFIED = 97,
+};
+// Message.Header values the routing path reads (Message.cs:29-70)
+enum : uint32_t { H_CATEGORY = 3, H_SENDING_SILO = 20, H_TARGET_ACTIVATION = 22, H_TARGET_GRAIN = 23, H_TARGET_SILO = 24 };
+
+constexpr uint64_t kMaxTicks = 3155378975999999999ull;  // DateTime.MaxValue.Ticks
+
+// Byte sources: positions are absolute buffer offsets; word(i) returns aligned word i of the buffer.
+struct GlobalSrc {  // the receive buffer in HBM
+    const uint32_t* __restrict__ w;
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return w[i]; }
+};
+struct LdsSrc {     // one frame staged in LDS: row[k] = buffer word base + k
+    const uint32_t* row;
+    uint64_t base;
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return row[(uint32_t)(i - base)]; }
+};
+
+// 4 bytes at p (little endian).  Caller guarantees p + 4 <= a frame end <= nbytes, so the second word holds
+// byte p+3 and is inside the buffer's (or the staged row's) last word at worst.
+template <class S>
+__device__ __forceinline__ uint32_t ld32(const S& w, uint64_t p) {
+    const uint64_t wi = p >> 2;
+    const uint32_t sh = (uint32_t)(p & 3u);
+    const uint32_t lo = w.word(wi);
+    if (sh == 0) return lo;
+    return __builtin_amdgcn_alignbyte(w.word(wi + 1), lo, sh);  // v_alignbyte: ({hi, lo} >> 8 * sh)[31:0]
+}
+template <class S>
+__device__ __forceinline__ uint32_t ld8(const S& w, uint64_t p) {
+    return (w.word(p >> 2) >> ((uint32_t)(p & 3u) * 8u)) & 0xFFu;
+}
+template <class S>
+__device__ __forceinline__ uint64_t ld64(const S& w, uint64_t p) {
+    return (uint64_t)ld32(w, p) | ((uint64_t)ld32(w, p + 4) << 32);
+}
+
+// string.IsNullOrWhiteSpace over the UTF-8 bytes [p, p+len): whitespace-only iff the bytes split into encodings
+// of Char.IsWhiteSpace code points (U+0009-000D, 0020, 0085, 00A0, 1680, 2000-200A, 2028, 2029, 202F, 205F,
+// 3000).  Any other byte decodes to a non-space char or to U+FFFD.
+template <class S>
+__device__ bool all_whitespace(const S& w, uint64_t p, uint64_t len) {
+    const uint64_t e = p + len;
+    while (p < e) {
+        const uint32_t b0 = ld8(w, p);
+        if (b0 == 0x20u || (b0 >= 0x09u && b0 <= 0x0Du)) { p += 1; continue; }
+        if (b0 == 0xC2u && p + 2 <= e) {
+            const uint32_t b1 = ld8(w, p + 1);
+            if (b1 == 0x85u || b1 == 0xA0u) { p += 2; continue; }
+            return false;
+        }
+        if ((b0 == 0xE1u || b0 == 0xE2u || b0 == 0xE3u) && p + 3 <= e) {
+            const uint32_t b1 = ld8(w, p + 1), b2 = ld8(w, p + 2);
+            const uint32_t cp = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
+            const bool cont = (b1 & 0xC0u) == 0x80u && (b2 & 0xC0u) == 0x80u;
+            const bool ws = cp == 0x1680u || (cp >= 0x2000u && cp <= 0x200Au) || cp == 0x2028u || cp == 0x2029u ||
+                            cp == 0x202Fu || cp == 0x205Fu || cp == 0x3000u;
+            if (cont && ws) { p += 3; continue; }
+            return false;
+        }
+        return false;
+    }
+    return true;
+}
+
+// Strict UTF-8 (RFC 3629: no overlongs, no surrogates, <= U+10FFFF) — the byte strings .NET's decoder maps to
+// themselves when re-encoded.
+template <class S>
+__device__ bool strict_utf8(const S& w, uint64_t p, uint64_t len) {
+    const uint64_t e = p + len;
+    while (p < e) {
+        const uint32_t b0 = ld8(w, p);
+        if (b0 < 0x80u) { p += 1; continue; }
+        uint32_t n, lo = 0x80u, hi = 0xBFu;
+        if (b0 >= 0xC2u && b0 <= 0xDFu) n = 1;
+        else if (b0 >= 0xE0u && b0 <= 0xEFu) { n = 2; if (b0 == 0xE0u) lo = 0xA0u; if (b0 == 0xEDu) hi = 0x9Fu; }
+        else if (b0 >= 0xF0u && b0 <= 0xF4u) { n = 3; if (b0 == 0xF0u) lo = 0x90u; if (b0 == 0xF4u) hi = 0x8Fu; }
+        else return false;
+        if (p + 1 + n > e) return false;
+        const uint32_t b1 = ld8(w, p + 1);
+        if (b1 < lo || b1 > hi) return false;
+        for (uint32_t j = 2; j <= n; ++j)
+            if ((ld8(w, p + j) & 0xC0u) != 0x80u) return false;
+        p += 1 + n;
+    }
+    return true;
+}
+
+// JenkinsHash.ComputeHash(byte[]) (JenkinsHash.cs:68-115) over [p, p+len).
+template <class S>
+__device__ uint32_t jenkins_stream(const S& w, uint64_t p, uint32_t len) {
+    uint32_t a = 0x9e3779b9u, b = 0x9e3779b9u, c = 0u;
+    uint32_t i = 0;
+    for (; i + 12u <= len; i += 12u) {
+        a += ld32(w, p + i);
+        b += ld32(w, p + i + 4);
+        c += ld32(w, p + i + 8);
+        ORL_MIX(a, b, c);
+    }
+    c += len;
+    const uint32_t t = len - i;  // 0..11 tail bytes: 0-3 -> a, 4-7 -> b, 8-10 -> c << 8
+    for (uint32_t j = 0; j < t; ++j) {
+        const uint32_t by = ld8(w, p + i + j);
+        if (j < 4) a += by << (8u * j);
+        else if (j < 8) b += by << (8u * (j - 4u));
+        else c += by << (8u * (j - 7u));
+    }
+    ORL_MIX(a, b, c);
+    return c;
+}
+
+// ReadUniqueKey (:424-431) + UniqueKey.ValidateKeyExt (UniqueKey.cs:328-350).  Advances p; returns a status.
+template <class S>
+__device__ __forceinline__ uint32_t skip_unique_key(const S& w, uint64_t end, uint64_t& p) {
+    if (p + 28 > end) return ORL_DEC_MALFORMED;
+    const uint32_t cat = ld32(w, p + 20) >> 24;  // top byte of TypeCodeData
+    const int32_t len = (int32_t)ld32(w, p + 24);
+    p += 28;
+    if (len == -1) return cat == 6u ? ORL_DEC_MALFORMED : ORL_DEC_OK;  // KeyExt grain needs an extension
+    if (len < 0 || p + (uint64_t)len > end) return ORL_DEC_MALFORMED;
+    if (cat != 6u) return ORL_DEC_MALFORMED;                             // extension on a non-KeyExt key
+    if (all_whitespace(w, p, (uint64_t)len)) return ORL_DEC_MALFORMED;
+    p += (uint64_t)len;
+    return ORL_DEC_OK;
+}
+
+template <class S>
+__device__ __forceinline__ bool port_ok(const S& w, uint64_t p) {
+    return ld32(w, p) <= 65535u;  // new IPEndPoint(addr, port): 0 <= port <= 65535
+}
+
+// One header value (DeserializeMessageHeaderHelper :1833-1853), starting at its token.  Lists are flattened
+// with a pending-value counter (a list only adds values), so nesting depth costs no state.
+template <class S>
+__device__ uint32_t skip_value(const S& w, uint64_t end, uint64_t& p) {
+    uint64_t pending = 1;
+    while (pending) {
+        --pending;
+        if (p >= end) return ORL_DEC_MALFORMED;
+        const uint32_t t = ld8(w, p);
+        p += 1;
+        uint64_t sz = 0;
+        switch (t) {
+        case T_NULL: case T_TRUE: case T_FALSE: case T_OBJECT: sz = 0; break;
+        case T_SBYTE: case T_BYTE: sz = 1; break;
+        case T_SHORT: case T_USHORT: sz = 2; break;
+        case T_INT: case T_UINT: case T_FLOAT: sz = 4; break;
+        case T_LONG: case T_ULONG: case T_DOUBLE: case T_TIMESPAN: case T_CORR: sz = 8; break;
+        case T_GUID: case T_IPADDR: sz = 16; break;
+        case T_CHAR:  // Convert.ToChar(short) throws for a negative short
+            if (p + 2 > end) return ORL_DEC_MALFORMED;
+            if (ld8(w, p + 1) & 0x80u) return ORL_DEC_MALFORMED;
+            sz = 2;
+            break;
+        case T_DECIMAL: {  // new decimal(int[]): flags = sign | scale<<16, scale <= 28
+            if (p + 16 > end) return ORL_DEC_MALFORMED;
+            const uint32_t f = ld32(w, p + 12);
+            if ((f & 0x7F00FFFFu) || ((f >> 16) & 0xFFu) > 28u) return ORL_DEC_MALFORMED;
+            sz = 16;
+            break;
+        }
+        case T_DATE: {  // DateTime.FromBinary: local kinds depend on the host time zone
+            if (p + 8 > end) return ORL_DEC_MALFORMED;
+            const uint64_t v = ld64(w, p);
+            if (v >> 63) return ORL_DEC_UNSUPPORTED;
+            if ((v & 0x3FFFFFFFFFFFFFFFull) > kMaxTicks) return ORL_DEC_MALFORMED;
+            sz = 8;
+            break;
+        }
+        case T_IPEP:
+            if (p + 20 > end || !port_ok(w, p + 16)) return ORL_DEC_MALFORMED;
+            sz = 20;
+            break;
+        case T_SILO:
+            if (p + 24 > end || !port_ok(w, p + 16)) return ORL_DEC_MALFORMED;
+            sz = 24;
+            break;
+        case T_STRING: {
+            if (p + 4 > end) return ORL_DEC_MALFORMED;
+            const int32_t len = (int32_t)ld32(w, p);
+            if (len < -1) return ORL_DEC_MALFORMED;
+            sz = 4 + (len > 0 ? (uint64_t)len : 0);
+            break;
+        }
+        case T_GRAIN: case T_ACT: {
+            const uint32_t st = skip_unique_key(w, end, p);
+            if (st) return st;
+            continue;
+        }
+        case T_ACTADDR: {
+            if (p + 24 > end || !port_ok(w, p + 16)) return ORL_DEC_MALFORMED;
+            p += 24;
+            uint32_t st = skip_unique_key(w, end, p);
+            if (!st) st = skip_unique_key(w, end, p);
+            if (st) return st;
+            continue;
+        }
+        case T_LIST: {
+            if (p + 4 > end) return ORL_DEC_MALFORMED;
+            const int32_t cnt = (int32_t)ld32(w, p);
+            if (cnt < 0) return ORL_DEC_MALFORMED;
+            pending += (uint64_t)cnt;
+            sz = 4;
+            break;
+        }
+        case T_DICT: return ORL_DEC_UNSUPPORTED;       // nested header dictionary: host path
+        case T_SPECIFIED: return ORL_DEC_UNSUPPORTED;  // registered serializer: host path
+        default: return ORL_DEC_MALFORMED;             // "Unexpected token ... parsing message headers"
+        }
+        if (p + sz > end) return ORL_DEC_MALFORMED;
+        p += sz;
+    }
+    return ORL_DEC_OK;
+}
+
+template <class S>
+__device__ uint32_t silo_lookup(const SiloAddrEntry* __restrict__ tab, const S& w, uint64_t p) {
+    uint32_t a[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a[i] = ld32(w, p + 4u * i);
+    uint32_t s = silo_addr_slot(a);
+    for (uint32_t probe = 0; probe < kSiloAddrSlots; ++probe) {
+        const SiloAddrEntry& e = tab[s];
+        if (e.silo == 0xFFu) return 0xFFu;
+        if (e.w[0] == a[0] && e.w[1] == a[1] && e.w[2] == a[2] && e.w[3] == a[3] && e.w[4] == a[4] && e.w[5] == a[5])
+            return e.silo;
+        s = (s + 1u) & (kSiloAddrSlots - 1u);
+    }
+    return 0xFFu;
+}
+
+// Token classes for the common-case entry loop: the fixed byte count after the token plus what else the reader
+// checks.  Rare or nested tokens (CLS_SLOW) go through skip_value, which restates every reader rule.
+enum : uint32_t {
+    CLS_SIZE = 63u,
+    CLS_STR = 1u << 6,    // + max(int32 length at +0, 0); length < -1 throws
+    CLS_KEY = 1u << 7,    // UniqueKey: + max(int32 length at +24, 0); ValidateKeyExt on the category byte at +23
+    CLS_PORT = 1u << 8,   // int32 port at +16 must be in [0, 65535]
+    CLS_DATE = 1u << 9,   // DateTime.FromBinary rules
+    CLS_SLOW = 1u << 10,
+};
+__device__ uint32_t token_class(uint32_t t) {
+    switch (t) {
+    case T_NULL: case T_TRUE: case T_FALSE: case T_OBJECT: return 0;
+    case T_SBYTE: case T_BYTE: return 1;
+    case T_SHORT: case T_USHORT: return 2;
+    case T_INT: case T_UINT: case T_FLOAT: return 4;
+    case T_LONG: case T_ULONG: case T_DOUBLE: case T_TIMESPAN: case T_CORR: return 8;
+    case T_GUID: case T_IPADDR: return 16;
+    case T_IPEP: return 20 | CLS_PORT;
+    case T_SILO: return 24 | CLS_PORT;
+    case T_STRING: return 4 | CLS_STR;
+    case T_GRAIN: case T_ACT: return 28 | CLS_KEY;
+    case T_DATE: return 8 | CLS_DATE;
+    default: return CLS_SLOW;  // char, decimal, activation address, list, nested dict, SpecifiedType, invalid
+    }
+}
+
+// One header value starting at its token p - 1 (token tok, class cls): the common-case form of skip_value.
+template <class S>
+__device__ __forceinline__ uint32_t skip_value_fast(const S& w, uint64_t end, uint32_t cls, uint64_t& p) {
+    if (cls & CLS_SLOW) {
+        p -= 1;
+        return skip_value(w, end, p);
+    }
+    uint64_t sz = cls & CLS_SIZE;
+    if (p + sz > end) return ORL_DEC_MALFORMED;
+    uint32_t st = ORL_DEC_OK;
+    if (cls & (CLS_STR | CLS_KEY)) {
+        const uint64_t lp = (cls & CLS_KEY) ? p + 24 : p;
+        const int32_t len = (int32_t)ld32(w, lp);
+        if (cls & CLS_KEY) {
+            const uint32_t cat = ld8(w, p + 23);
+            if (cat == 6u) {  // KeyExt grain: a non-blank extension (UniqueKey.cs:328-345)
+                if (len < 1 || p + 28 + (uint64_t)len > end) st = ORL_DEC_MALFORMED;
+                else if (all_whitespace(w, p + 28, (uint64_t)len)) st = ORL_DEC_MALFORMED;
+            } else if (len != -1) {
+                st = ORL_DEC_MALFORMED;  // a length < -1 throws in ReadString; >= 0 in ValidateKeyExt
+            }
+        } else if (len < -1) {
+            st = ORL_DEC_MALFORMED;
+        }
+        sz += len > 0 ? (uint64_t)len : 0;
+    }
+    if ((cls & CLS_PORT) && ld32(w, p + 16) > 65535u) st = ORL_DEC_MALFORMED;
+    if (cls & CLS_DATE) {
+        const uint64_t v = ld64(w, p);
+        if (v >> 63) st = ORL_DEC_UNSUPPORTED;
+        else if ((v & 0x3FFFFFFFFFFFFFFFull) > kMaxTicks) st = ORL_DEC_MALFORMED;
+    }
+    if (!st && p + sz > end) st = ORL_DEC_MALFORMED;
+    p += sz;
+    return st;
+}
+
+// One frame's header [p, end) (frame validated by the caller) -> status + the two 16-byte halves of its record.
+template <class S>
+__device__ uint32_t decode_header(const S& w, uint64_t p, uint64_t end, uint32_t sender_override,
+                                  const SiloAddrEntry* __restrict__ tab, const uint16_t* lut, uint4& r0, uint4& r1) {
+    uint32_t st = ORL_DEC_OK;
+    uint32_t cat_v = 0, cat_st = 0;           // 0 absent, 1 Int, 2 other type (cast fails)
+    uint32_t ts_st = 0, ss_st = 0;            // 0 absent / null, 1 SiloAddress, 2 other type
+    uint64_t ts_p = 0, ss_p = 0, tg_p = 0;
+    bool tg = false, ta = false;
+    // DeserializeMessageHeaders: StringObjDict, int32 count, count x (byte key, value); duplicate keys throw.
+    if (p + 5 > end || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
+    int32_t count = 0;
+    if (!st) {
+        count = (int32_t)ld32(w, p + 1);
+        p += 5;
+        if (count < 0) st = ORL_DEC_MALFORMED;
+    }
+    uint64_t seen0 = 0, seen1 = 0, seen2 = 0, seen3 = 0;
+    for (int32_t e = 0; !st && e < count; ++e) {
+        if (p + 2 > end) { st = ORL_DEC_MALFORMED; break; }
+        const uint32_t kt = ld32(w, p - 2) >> 16;  // key, token: p >= frame + 10, so p - 2 is in the frame
+        const uint32_t key = kt & 0xFFu;
+        const uint32_t tok = (kt >> 8) & 0xFFu;
+        const uint64_t vp = p + 2;  // first byte after the value token
+        p = vp;
+        st = skip_value_fast(w, end, lut[tok], p);
+        if (st) break;
+        const uint32_t q = key >> 6;
+        const uint64_t bit = 1ull << (key & 63u);
+        const uint64_t cur = q == 0 ? seen0 : q == 1 ? seen1 : q == 2 ? seen2 : seen3;
+        if (cur & bit) { st = ORL_DEC_MALFORMED; break; }
+        seen0 |= q == 0 ? bit : 0; seen1 |= q == 1 ? bit : 0; seen2 |= q == 2 ? bit : 0; seen3 |= q == 3 ? bit : 0;
+        switch (key) {
+        case H_CATEGORY: cat_st = tok == T_INT ? 1u : 2u; if (tok == T_INT) cat_v = ld32(w, vp); break;
+        case H_TARGET_SILO: ts_st = tok == T_SILO ? 1u : tok == T_NULL ? 0u : 2u; ts_p = vp; break;
+        case H_SENDING_SILO: ss_st = tok == T_SILO ? 1u : tok == T_NULL ? 0u : 2u; ss_p = vp; break;
+        case H_TARGET_GRAIN: tg = tok == T_GRAIN; tg_p = vp; break;
+        case H_TARGET_ACTIVATION: ta = tok == T_ACT; break;
+        default: break;
+        }
+    }
+    // the getters, in the order the oracle defines (oracle/wire_codec.py decode_for_route)
+    uint32_t sending = sender_override, target_silo = 0, flags = 0, aux = 0;
+    uint64_t tcd = 0, n0 = 0, n1 = 0;
+    if (!st && (cat_st == 2 || (cat_st == 1 && cat_v > 255u))) st = ORL_DEC_MALFORMED;
+    if (!st && ts_st == 2) st = ORL_DEC_MALFORMED;
+    if (!st && sender_override == ORL_SENDER_FROM_HEADER) {
+        if (ss_st == 2) st = ORL_DEC_MALFORMED;
+        else if (ss_st == 0) st = ORL_DEC_NO_SENDER;
+        else if ((sending = silo_lookup(tab, w, ss_p)) == 0xFFu) st = ORL_DEC_UNKNOWN_SILO;
+    }
+    if (!st && !tg) st = ORL_DEC_NO_TARGET;
+    if (!st) {
+        n0 = ld64(w, tg_p);
+        n1 = ld64(w, tg_p + 8);
+        tcd = ld64(w, tg_p + 16);
+        if ((tcd >> 56) == 6u) {  // KeyExt: uniform hash over Write(UniqueKey) (UniqueKey.cs:288-294)
+            const uint32_t len = ld32(w, tg_p + 24);
+            if (!strict_utf8(w, tg_p + 28, len)) st = ORL_DEC_UNSUPPORTED;
+            else {
+                aux = jenkins_stream(w, tg_p, 28u + len);
+                flags |= ORL_HDR_HASH_VALID;
+            }
+        }
+    }
+    if (!st && ta && ts_st == 1) {
+        if ((target_silo = silo_lookup(tab, w, ts_p)) == 0xFFu) st = ORL_DEC_UNKNOWN_SILO;
+        else flags |= ORL_HDR_ADDRESS_COMPLETE;
+    }
+    if (st) {
+        r0 = make_uint4(0, 0, 0, 0);
+        r1 = make_uint4(0, 0, 0, 0);
+    } else {
+        r0 = make_uint4((uint32_t)tcd, (uint32_t)(tcd >> 32), (uint32_t)n0, (uint32_t)(n0 >> 32));
+        r1 = make_uint4((uint32_t)n1, (uint32_t)(n1 >> 32),
+                        (sending & 0xFFu) | (cat_v << 8) | (flags << 16) | ((target_silo & 0xFFu) << 24), aux);
+    }
+    return st;
+}
+
+__device__ __forceinline__ void write_record(uint32_t i, uint32_t st, const uint4& r0, const uint4& r1, uint4* __restrict__ out,
+                                             uint8_t* __restrict__ status, uint32_t* __restrict__ n_bad) {
+    if (st && n_bad) atomicAdd(n_bad, 1u);
+    out[2ull * i] = r0;
+    out[2ull * i + 1] = r1;
+    status[i] = (uint8_t)st;
+}
+
+// Frame i's prefix checks (IncomingMessageBuffer.cs:94-135): the 8-byte lengths inside the buffer, both lengths
+// >= 0, header + body inside the buffer.  Returns the header end (absolute) or 0 when malformed.
+template <class S>
+__device__ __forceinline__ uint64_t frame_end(const S& w, uint64_t off, uint64_t nbytes) {
+    if (off > nbytes || nbytes - off < 8) return 0;
+    const int32_t hl = (int32_t)ld32(w, off), bl = (int32_t)ld32(w, off + 4);
+    if (hl < 0 || bl < 0 || (uint64_t)hl + (uint64_t)bl > nbytes - off - 8) return 0;
+    return off + 8 + (uint64_t)hl;
+}
+
+// Simple form: one lane per frame, parsing straight from HBM through L1/L2.  Used for small batches.
+__global__ __launch_bounds__(256) void k_decode_frames(const uint32_t* __restrict__ buf, uint64_t nbytes,
+                                                       const uint64_t* __restrict__ offs, uint32_t n, uint32_t sender_override,
+                                                       const SiloAddrEntry* __restrict__ tab, uint4* __restrict__ out,
+                                                       uint8_t* __restrict__ status, uint32_t* __restrict__ n_bad) {
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GlobalSrc g{buf};
+    const uint64_t off = offs[i];
+    const uint64_t end = frame_end(g, off, nbytes);
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+    const uint32_t st = end ? decode_header(g, off + 8, end, sender_override, tab, lut, r0, r1) : ORL_DEC_MALFORMED;
+    write_record(i, st, r0, r1, out, status, n_bad);
+}
+
+// Pipelined form.  A persistent wave walks 64-frame chunks.  For every frame of a chunk it loads the 64-word
+// (256-byte) window that starts at the frame's first aligned word — one coalesced load per frame, issued for the
+// NEXT chunk while the current chunk is parsed, so the HBM latency hides behind the parse — then copies the
+// window into the frame's LDS row and parses it there: one pass over the header bytes instead of the dozens of
+// L2 requests per frame that lanes parsing 64 different frames through a 32-KB L1 cost.  Rows are 65 words
+// apart, so lanes reading the same relative word hit distinct banks.  A header that does not fit its window is
+// parsed straight from HBM.  Window loads are clamped to the buffer's last word.
+constexpr uint32_t kRowWords = 64;
+constexpr uint32_t kRowStride = kRowWords + 1;
+constexpr size_t kPipeMinFrames = 1u << 16;  // below this the simple form fills the chip better
+
+__device__ __forceinline__ void load_windows(const uint32_t* __restrict__ buf, uint64_t last_word, uint64_t off,
+                                             uint32_t lane, uint32_t (&v)[64]) {
+    const uint32_t w_lo = (uint32_t)(off >> 2), w_hi = (uint32_t)(off >> 34);
+#pragma unroll
+    for (uint32_t j = 0; j < 64; ++j) {
+        // frame j's first word, broadcast from lane j into scalar registers
+        const uint64_t w0 = (uint64_t)__builtin_amdgcn_readlane(w_lo, j) | ((uint64_t)__builtin_amdgcn_readlane(w_hi, j) << 32);
+        const uint64_t wi = w0 + lane;
+        v[j] = buf[wi < last_word ? wi : last_word];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __restrict__ buf, uint64_t nbytes,
+                                                            const uint64_t* __restrict__ offs, uint32_t n,
+                                                            uint32_t sender_override, const SiloAddrEntry* __restrict__ tab,
+                                                            uint4* __restrict__ out, uint8_t* __restrict__ status,
+                                                            uint32_t* __restrict__ n_bad) {
+    __shared__ uint32_t rows[4][64 * kRowStride];
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t n_chunks = (n + 63) / 64;
+    const uint32_t stride = gridDim.x * 4;
+    uint32_t c = blockIdx.x * 4 + wv;
+    if (c >= n_chunks) return;  // wave-uniform: the kernel has no block-wide barrier after this point
+    const uint64_t last_word = (nbytes + 3) / 4 - 1;  // launcher guarantees nbytes >= 8
+    const GlobalSrc g{buf};
+    uint32_t* my = rows[wv];
+    auto frame_off = [&](uint32_t chunk) -> uint64_t {
+        const uint32_t i = chunk * 64 + lane;
+        return chunk < n_chunks && i < n ? offs[i] : ~0ull;
+    };
+    uint64_t off = frame_off(c);
+    uint32_t v[64];
+    load_windows(buf, last_word, off == ~0ull ? 0 : off, lane, v);
+    uint64_t off_next = frame_off(c + stride);
+    while (true) {
+#pragma unroll
+        for (uint32_t j = 0; j < 64; ++j) my[j * kRowStride + lane] = v[j];
+        const uint32_t cn = c + stride;
+        const uint64_t off_nn = frame_off(cn + stride);
+        if (cn < n_chunks) load_windows(buf, last_word, off_next == ~0ull ? 0 : off_next, lane, v);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t i = c * 64 + lane;
+        if (i < n) {
+            const LdsSrc l{my + lane * kRowStride, off >> 2};
+            uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+            uint32_t st = ORL_DEC_MALFORMED;
+            const uint64_t end = frame_end(l, off, nbytes);  // the first 8 bytes always lie in the window
+            if (end) {
+                if ((end + 3) / 4 - off / 4 <= kRowWords)
+                    st = decode_header(l, off + 8, end, sender_override, tab, lut, r0, r1);
+                else
+                    st = decode_header(g, off + 8, end, sender_override, tab, lut, r0, r1);
+            }
+            write_record(i, st, r0, r1, out, status, n_bad);
+        }
+        if (cn >= n_chunks) break;
+        __builtin_amdgcn_wave_barrier();  // the rows are rewritten next iteration
+        c = cn;
+        off = off_next;
+        off_next = off_nn;
+    }
+}
+
+}  // namespace
+
+int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
+                         uint32_t sender_override, const SiloAddrEntry* d_silo_tab, orl_msg_hdr* d_out,
+                         uint8_t* d_status, uint32_t* d_n_bad, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (d_n_bad) {
+        const hipError_t e = hipMemsetAsync(d_n_bad, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    if (n == 0) return 0;
+    static const int mode = [] { const char* e = getenv("ORL_DECODE_MODE"); return e ? atoi(e) : 1; }();
+    if (mode == 1 && n >= kPipeMinFrames && nbytes >= 8) {
+        // persistent: 2 workgroups (66.5 KB LDS each) per CU
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t chunks = (uint32_t)((n + 63) / 64);
+        const uint32_t blocks = std::min<uint32_t>((uint32_t)cus * 2u, (chunks + 3) / 4);
+        hipLaunchKernelGGL(k_decode_frames_pipe, dim3(blocks), dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets,
+                           (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
+    } else {
+        hipLaunchKernelGGL(k_decode_frames, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, (const uint32_t*)d_bytes,
+                           nbytes, d_offsets, (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace orl

@@ -422,6 +422,26 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_client_buckets_device(self._ctx, ptr(d_msgs), int(n), int(n_buckets), ptr(d_bucket),
                                                      ptr(stream)))
 
+    def set_silo_address(self, silo: int, ip16: Optional[bytes], port: int = 0, generation: int = 0) -> None:
+        """Silo address table of the wire decoder: serialized SiloAddress (16 IP bytes, port, generation) of
+        silo index `silo`; ip16 None removes it."""
+        if ip16 is None:
+            self._ck(self._lib.orl_silo_address_set(self._ctx, int(silo), None, 0, 0))
+            return
+        b = bytes(ip16)
+        if len(b) != 16:
+            raise ValueError("ip16 must be 16 bytes")
+        buf = (C.c_uint8 * 16).from_buffer_copy(b)
+        self._ck(self._lib.orl_silo_address_set(self._ctx, int(silo), buf, int(port), int(generation)))
+
+    def decode_frames_device(self, d_bytes, nbytes: int, d_offsets, n: int, d_out, d_status, d_n_bad=None,
+                             sender_override: int = L.SENDER_FROM_HEADER, stream=None) -> None:
+        """Received frames -> orl_msg_hdr records + one ORL_DEC_* status byte per frame (device buffers;
+        d_bytes 4-byte aligned).  Reference: Message.Serialize_Impl framing + DeserializeMessageHeaders."""
+        self._ck(self._lib.orl_decode_frames_device(self._ctx, ptr(d_bytes), int(nbytes), ptr(d_offsets), int(n),
+                                                    int(sender_override), ptr(d_out), ptr(d_status), ptr(d_n_bad),
+                                                    ptr(stream)))
+
     def compact_directory(self) -> None:
         """Rebuild the partition without tombstones."""
         self._ck(self._lib.orl_dir_compact(self._ctx))

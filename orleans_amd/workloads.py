@@ -90,6 +90,11 @@ class Cluster:
     ring_hash: np.ndarray     # int32, membershipRingList order
     ring_silo: np.ndarray     # uint8
     type_code: int
+    gens: Tuple[int, ...] = ()  # generation per silo index (SiloAddress 10.0.0.{s+1}:PORT@gen)
+
+    def silo_ip16(self, s: int) -> bytes:
+        """Serialized IPv4 address of silo s (12 zero bytes + 4, BinaryTokenStreamWriter.cs:455-469)."""
+        return bytes(12) + bytes([10, 0, 0, s + 1])
 
     def owner_of(self, uniform: np.ndarray) -> np.ndarray:
         """CalculateTargetSilo for running silos (no exclusion): predecessor-or-equal in signed order, wrap."""
@@ -112,7 +117,7 @@ def default_cluster(n_silos: int = N_SILOS, generations=None) -> Cluster:
         idx = max([i for i, (rh, _) in enumerate(ring) if rh < h], default=-1)
         ring.insert(idx + 1, (h, s))
     return Cluster(n_silos, hashes, np.array([h for h, _ in ring], np.int32), np.array([s for _, s in ring], np.uint8),
-                   calc_id_hash(CHIRPER_ACCOUNT_CLASS))
+                   calc_id_hash(CHIRPER_ACCOUNT_CLASS), tuple(gens))
 
 
 def setup_engine(eng, cl: Cluster, local_silos: Optional[np.ndarray] = None, seed: int = 0) -> None:
@@ -292,3 +297,158 @@ def heartbeat_batch(pr: Presence, cl: Cluster, n_hb: int, batch: int, seed: int 
     m["sending_silo"] = (s % np.uint64(cl.n_silos)).astype(np.uint8)
     m["category"] = 2
     return g.astype(np.uint32), m
+
+
+# ---- f2: received frames (Message.Serialize_Impl layout) --------------------------------------------------
+# A typical request's header dictionary as InsideRuntimeClient.SendRequestMessage / Message.CreateMessage fill it
+# (src/Orleans/Runtime/InsideRuntimeClient.cs, src/Orleans/Messaging/Message.cs): category, direction,
+# correlation id, interface / method ids, sending silo / grain / activation, target grain, expiration; a
+# response-style frame also carries TARGET_SILO + TARGET_ACTIVATION (a complete address).  Serialized per
+# SerializationManager.SerializeMessageHeaders (token StringObjDict, count, byte key + token + value).
+_H = dict(CATEGORY=3, CORRELATION_ID=4, DIRECTION=6, EXPIRATION=7, INTERFACE_ID=9, METHOD_ID=10,
+          SENDING_ACTIVATION=18, SENDING_GRAIN=19, SENDING_SILO=20, TARGET_ACTIVATION=22, TARGET_GRAIN=23,
+          TARGET_SILO=24)
+_T_INT, _T_DATE, _T_STRDICT, _T_GRAIN, _T_ACT, _T_SILO, _T_CORR = 11, 25, 50, 40, 41, 42, 44
+
+
+class _FrameTemplate:
+    """One header shape: frame bytes with placeholders, and the offsets of the per-message fields."""
+
+    def __init__(self, complete: bool, ext_len: int):
+        b = bytearray(8)  # int32 header length, int32 body length
+        at = {}
+
+        def entry(key, tok):
+            b.append(_H[key])
+            b.append(tok)
+
+        def field(name, n):
+            at[name] = len(b)
+            b.extend(bytes(n))
+
+        def i32(v):
+            b.extend(int(v).to_bytes(4, "little", signed=True))
+
+        b.append(_T_STRDICT)
+        i32(12 if complete else 10)
+        entry("CATEGORY", _T_INT); i32(2)                       # Categories.Application
+        entry("DIRECTION", _T_INT); i32(0)                      # Directions.Request
+        entry("CORRELATION_ID", _T_CORR); field("corr", 8)
+        entry("INTERFACE_ID", _T_INT); field("iface", 4)
+        entry("METHOD_ID", _T_INT); field("method", 4)
+        entry("SENDING_SILO", _T_SILO); field("ss", 24)
+        entry("SENDING_GRAIN", _T_GRAIN); field("sg", 24); i32(-1)
+        entry("SENDING_ACTIVATION", _T_ACT); field("sa", 24); i32(-1)
+        entry("TARGET_GRAIN", _T_GRAIN); field("tg", 24)
+        if ext_len:
+            i32(ext_len); field("ext", ext_len)
+        else:
+            i32(-1)
+        entry("EXPIRATION", _T_DATE); field("exp", 8)
+        if complete:
+            entry("TARGET_SILO", _T_SILO); field("ts", 24)
+            entry("TARGET_ACTIVATION", _T_ACT); field("ta", 24); i32(-1)
+        self.hl = len(b) - 8
+        b[0:4] = self.hl.to_bytes(4, "little")
+        self.bytes = np.frombuffer(bytes(b), np.uint8)
+        self.at = at
+
+
+def _put(rows: np.ndarray, pos: int, vals: np.ndarray, dtype: str) -> None:
+    v = np.ascontiguousarray(vals.astype(dtype))
+    rows[:, pos:pos + v.dtype.itemsize] = v.view(np.uint8).reshape(len(v), v.dtype.itemsize)
+
+
+def _silo_words(cl: Cluster, silo: np.ndarray) -> np.ndarray:
+    tab = np.zeros((cl.n_silos, 24), np.uint8)
+    for s in range(cl.n_silos):
+        tab[s] = np.frombuffer(cl.silo_ip16(s) + PORT.to_bytes(4, "little") +
+                               int(cl.gens[s] if cl.gens else GENERATION).to_bytes(4, "little", signed=True), np.uint8)
+    return tab[silo]
+
+
+def request_frames(cl: Cluster, n_grains: int, n_frames: int, seed: int = SEED_C2, complete_frac: float = 0.0,
+                   keyext_frac: float = 0.0, ext_lens=(11, 29), max_body: int = 48, chunk: int = 1 << 16):
+    """n_frames back-to-back frames (one receive buffer) addressed like config 2 (target ~ Uniform[0, n_grains),
+    sender ~ uniform silo) with `complete_frac` response-style complete addresses and `keyext_frac` KeyExt target
+    grains (ASCII extensions of the given lengths).  Returns (buffer u8 padded to 4 bytes, frame offsets u64,
+    expected headers MSG_DTYPE — aux left 0: the KeyExt hash is the decoder's to compute)."""
+    r = [stream(seed ^ k, 0, n_frames) for k in (0x11, 0x22, 0x33, 0x44, 0x55, 0x66)]
+    tgt = r[0] % np.uint64(n_grains)
+    sender = (r[1] % np.uint64(cl.n_silos)).astype(np.int64)
+    u = (r[2] >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    complete = u < complete_frac
+    u2 = (r[3] >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    ext_cls = np.where(u2 < keyext_frac, 1 + (r[3] % np.uint64(len(ext_lens))).astype(np.int64), 0)
+    body = ((r[4] % np.uint64(max_body // 8 + 1)) * np.uint64(8)).astype(np.int64) if max_body else np.zeros(n_frames, np.int64)
+    tsilo = (r[5] % np.uint64(cl.n_silos)).astype(np.int64)
+    shapes = {}
+    for c in (False, True):
+        for e in range(len(ext_lens) + 1):
+            shapes[(c, e)] = _FrameTemplate(c, ext_lens[e - 1] if e else 0)
+    shape_id = complete.astype(np.int64) * (len(ext_lens) + 1) + ext_cls
+    hl = np.array([shapes[(c, e)].hl for c in (False, True) for e in range(len(ext_lens) + 1)], np.int64)[shape_id]
+    size = 8 + hl + body
+    offs = np.zeros(n_frames, np.uint64)
+    offs[1:] = np.cumsum(size[:-1]).astype(np.uint64)
+    total = int(size.sum())
+    buf = np.zeros((total + 3) // 4 * 4, np.uint8)
+    grain_tcd = np.uint64(((L.CAT_GRAIN << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF)
+    keyext_tcd = np.uint64(((6 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF)
+    act_tcd = np.uint64(((L.CAT_GRAIN << 56)) & 0xFFFFFFFFFFFFFFFF)
+    exp = np.full(n_frames, (1 << 62) | 638000000000000000, np.int64)  # a UTC DateTime.ToBinary
+    exp = exp + (r[2] % np.uint64(10_000_000)).astype(np.int64)
+    sw = _silo_words(cl, sender)
+    tw = _silo_words(cl, tsilo)
+    for (c, e), tpl in shapes.items():
+        sel = np.nonzero(shape_id == (int(c) * (len(ext_lens) + 1) + e))[0]
+        for lo in range(0, len(sel), chunk):
+            idx = sel[lo:lo + chunk]
+            k = len(idx)
+            rows = np.tile(tpl.bytes, (k, 1))
+            _put(rows, 4, body[idx], "<i4")
+            _put(rows, tpl.at["corr"], r[4][idx] >> np.uint64(1), "<u8")
+            _put(rows, tpl.at["iface"], np.full(k, cl.type_code, np.int64), "<i4")
+            _put(rows, tpl.at["method"], (r[5][idx] >> np.uint64(40)) % np.uint64(7), "<i4")
+            rows[:, tpl.at["ss"]:tpl.at["ss"] + 24] = sw[idx]
+            sg = np.zeros((k, 3), np.uint64)
+            sg[:, 1] = r[1][idx] >> np.uint64(8)
+            sg[:, 2] = grain_tcd
+            rows[:, tpl.at["sg"]:tpl.at["sg"] + 24] = sg.view(np.uint8).reshape(k, 24)
+            sa = np.zeros((k, 3), np.uint64)
+            sa[:, 0] = r[2][idx]
+            sa[:, 1] = r[3][idx]
+            sa[:, 2] = act_tcd
+            rows[:, tpl.at["sa"]:tpl.at["sa"] + 24] = sa.view(np.uint8).reshape(k, 24)
+            tg = np.zeros((k, 3), np.uint64)
+            tg[:, 1] = tgt[idx]
+            tg[:, 2] = keyext_tcd if e else grain_tcd
+            rows[:, tpl.at["tg"]:tpl.at["tg"] + 24] = tg.view(np.uint8).reshape(k, 24)
+            if e:
+                n_ext = ext_lens[e - 1]
+                letters = stream(seed ^ 0x77, int(lo), k * n_ext).reshape(k, n_ext) % np.uint64(26) + np.uint64(97)
+                rows[:, tpl.at["ext"]:tpl.at["ext"] + n_ext] = letters.astype(np.uint8)
+            _put(rows, tpl.at["exp"], exp[idx], "<i8")
+            if c:
+                rows[:, tpl.at["ts"]:tpl.at["ts"] + 24] = tw[idx]
+                ta = np.zeros((k, 3), np.uint64)
+                ta[:, 0] = r[0][idx]
+                ta[:, 1] = r[5][idx]
+                ta[:, 2] = act_tcd
+                rows[:, tpl.at["ta"]:tpl.at["ta"] + 24] = ta.view(np.uint8).reshape(k, 24)
+            L_ = rows.shape[1]
+            buf[(offs[idx].astype(np.int64)[:, None] + np.arange(L_)[None, :]).ravel()] = rows.ravel()
+    exp_m = np.zeros(n_frames, L.MSG_DTYPE)
+    exp_m["tcd"] = np.where(ext_cls > 0, keyext_tcd, grain_tcd)
+    exp_m["n1"] = tgt
+    exp_m["sending_silo"] = sender.astype(np.uint8)
+    exp_m["category"] = 2
+    exp_m["flags"] = np.where(complete, L.HDR_ADDRESS_COMPLETE, 0) | np.where(ext_cls > 0, L.HDR_HASH_VALID, 0)
+    exp_m["target_silo"] = np.where(complete, tsilo, 0).astype(np.uint8)
+    return buf, offs, exp_m
+
+
+def register_silo_addresses(eng, cl: Cluster) -> None:
+    """The decoder's silo address table for the synthetic cluster."""
+    for s in range(cl.n_silos):
+        eng.set_silo_address(s, cl.silo_ip16(s), PORT, int(cl.gens[s] if cl.gens else GENERATION))

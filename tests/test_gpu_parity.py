@@ -806,3 +806,100 @@ def test_directory_cache_in_route_vs_oracle(torch):
     eng.cache_clear()
     np.testing.assert_array_equal(eng.address_messages(msgs).route, o.route(msgs)[0])
     eng.close()
+
+
+def _decode_on_device(t, eng, buf, nbytes, offs, sender_override=L.SENDER_FROM_HEADER):
+    d_buf = t.from_numpy(buf).cuda()
+    d_off = t.from_numpy(offs.view(np.int64)).cuda()
+    n = len(offs)
+    d_out = t.empty((n, 32), dtype=t.uint8, device="cuda")
+    d_st = t.empty(n, dtype=t.uint8, device="cuda")
+    d_bad = t.empty(1, dtype=t.int32, device="cuda")
+    eng.decode_frames_device(d_buf, nbytes, d_off, n, d_out, d_st, d_bad, sender_override=sender_override,
+                             stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    return d_st.cpu().numpy(), d_out.cpu().numpy().reshape(-1).view(L.MSG_DTYPE), int(d_bad.cpu()[0]), d_out
+
+
+def test_decode_frames_vs_oracle(torch):
+    """received frames -> orl_msg_hdr on the device, status and record bit-exact against
+    oracle/wire_codec.py over (a) one frame per decoder rule, (b) random header dictionaries using every value
+    type the reference header reader accepts, (c) random truncations / byte flips / garbage lengths of those, at
+    every start alignment, with and without a sender override; then a small batch (the simple kernel)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import wire_corpus as C
+    t = torch
+    eng = GrainDirectoryEngine(n_act=16, dir_capacity=16, max_batch=1024, device=0)
+    eng.set_silos(8)
+    for s in range(8):
+        eng.set_silo_address(s, *C.silo_addr(s))
+    typed = C.typed_corpus(4000, seed=21)
+    frames = C.edge_corpus() + typed + C.mutate(typed, 8000, seed=22)
+    frames = frames * 6  # > 64k frames: the launcher's pipelined (LDS-staged) kernel; gaps differ per copy
+    buf, offs, nbytes = C.pack(frames)
+    for so in (L.SENDER_FROM_HEADER, 3):
+        st, m, n_bad, _ = _decode_on_device(t, eng, buf, nbytes, offs, so)
+        st_ref, m_ref = C.oracle_decode(buf, nbytes, offs, so)
+        bad = np.nonzero(st != st_ref)[0]
+        assert len(bad) == 0, (so, bad[:10], st[bad[:10]], st_ref[bad[:10]])
+        np.testing.assert_array_equal(m.view(np.uint8), m_ref.view(np.uint8))
+        assert n_bad == int((st_ref != 0).sum())
+        assert len(set(st_ref.tolist())) == (6 if so == L.SENDER_FROM_HEADER else 5)  # every status exercised
+    small = C.edge_corpus() + typed[:500]
+    sb, so_, snb = C.pack(small, seed=5)
+    st, m, _, _ = _decode_on_device(t, eng, sb, snb, so_)
+    st_ref, m_ref = C.oracle_decode(sb, snb, so_)
+    np.testing.assert_array_equal(st, st_ref)
+    np.testing.assert_array_equal(m.view(np.uint8), m_ref.view(np.uint8))
+    # a silo address removed from the table -> UNKNOWN_SILO for its senders
+    eng.set_silo_address(1, None)
+    st, _, _, _ = _decode_on_device(t, eng, buf, nbytes, offs)
+    st_ref, _ = C.oracle_decode(buf, nbytes, offs)
+    idx = {k: v for k, v in C.silo_index().items() if v != 1}
+    from oracle import wire_codec as WC
+    exp = [d.status for d in WC.decode_frames(bytes(buf[:nbytes]), [int(o) for o in offs], idx)]
+    np.testing.assert_array_equal(st, np.array(exp, np.uint8))
+    assert (st == 3).sum() > (st_ref == 3).sum()
+    eng.close()
+
+
+def test_decode_generator_frames_then_route(torch):
+    """f2 feeding stages 1-4: synthetic request / response frames (complete addresses, KeyExt targets) decoded on
+    the device equal the oracle's decode, and routing the decoded records equals routing the expected headers
+    (KeyExt aux = pyref.uniform_hash)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import wire_corpus as C
+    from oracle import wire_codec as WC
+    t = torch
+    cl = W.balanced_cluster()
+    n_grains, n = 200_000, 120_000
+    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=1 << 18, device=0)
+    W.setup_engine(eng, cl)
+    W.register_silo_addresses(eng, cl)
+    keys, _, owner, reg = W.grain_population(cl, n_grains, 0.8)
+    W.register_population(eng, keys, owner, reg)
+    buf, offs, exp = W.request_frames(cl, n_grains, n, seed=77, complete_frac=0.2, keyext_frac=0.1)
+    st, m, n_bad, d_out = _decode_on_device(t, eng, buf, len(buf), offs)
+    assert n_bad == 0 and (st == 0).all()
+    for f in ("tcd", "n0", "n1", "sending_silo", "category", "flags", "target_silo"):
+        np.testing.assert_array_equal(m[f], exp[f], err_msg=f)
+    kx = np.nonzero(exp["flags"] & L.HDR_HASH_VALID)[0]
+    assert len(kx) > 1000
+    idx = {(cl.silo_ip16(s), W.PORT, cl.gens[s]): s for s in range(cl.n_silos)}
+    for i in kx[:300].tolist():
+        o = int(offs[i])
+        hl = int.from_bytes(bytes(buf[o:o + 4]), "little")
+        d = WC.decode_for_route(bytes(buf[o + 8:o + 8 + hl]), idx)
+        assert d.status == 0 and d.aux == int(m["aux"][i])
+    exp["aux"] = m["aux"]
+    d_r = t.empty(n, dtype=t.int32, device="cuda")
+    d_a = t.empty(n, dtype=t.int32, device="cuda")
+    eng.address_messages_device(d_out, n, d_r, d_a, stream=t.cuda.current_stream().cuda_stream, opts=L.OPT_NO_BUCKETS)
+    t.cuda.synchronize()
+    ref = eng.address_messages(exp)
+    np.testing.assert_array_equal(d_r.cpu().numpy().view(np.uint32), ref.route)
+    np.testing.assert_array_equal(d_a.cpu().numpy().view(np.uint32), ref.act)
+    assert ((ref.route >> 16) & 0xFF == L.ST_ADDRESS_COMPLETE).sum() > 10_000
+    eng.close()
