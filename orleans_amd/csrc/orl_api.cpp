@@ -217,6 +217,7 @@ struct orl_ctx {
     uint8_t silo_addr_known[256] = {};
     bool silo_addr_dirty = true;
     SiloAddrEntry* d_silo_tab = nullptr;
+    uint32_t* d_decode_flag = nullptr;
     // timing: 4 events per recorded batch (call begin, route begin, route end, call end)
     bool timing = false;
     std::vector<hipEvent_t> tev;
@@ -427,7 +428,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -487,6 +488,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_silo_known, 256)) != hipSuccess) return bail(e, "hipMalloc(silo known)");
         if ((e = hipMalloc((void**)&c->d_silo_tab, kSiloAddrSlots * sizeof(SiloAddrEntry))) != hipSuccess)
             return bail(e, "hipMalloc(silo addresses)");
+        if ((e = hipMalloc((void**)&c->d_decode_flag, 4)) != hipSuccess) return bail(e, "hipMalloc(decode flag)");
         if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
         if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
@@ -1237,7 +1239,7 @@ int orl_decode_frames_device(orl_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
     if (int r = sync_device_state(c)) return r;
     int e = launch_decode_frames(d_bytes, nbytes, d_frame_offsets, n, sender_override, c->d_silo_tab, d_out, d_status,
-                                 d_n_bad, stream ? stream : c->stream);
+                                 d_n_bad, c->d_decode_flag, stream ? stream : c->stream);
     if (e) return hipfail(c, (hipError_t)e, "decode frames launch");
     return ORL_OK;
 }

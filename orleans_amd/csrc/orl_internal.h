@@ -241,10 +241,10 @@ int launch_stream_queue(uint32_t kind, const RouteParams* d_params, const uint32
 int launch_outbound_queues(const orl_msg_hdr* d_msgs, const uint32_t* d_route, size_t n, uint32_t n_senders,
                            const int32_t* d_silo_hash, const uint8_t* d_silo_known, uint32_t* d_queue, void* stream);
 int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_buckets, uint32_t* d_bucket, void* stream);
-// f2: received frames -> orl_msg_hdr (wire_codec.hip).  d_bytes 4-byte aligned.
+// f2: received frames -> orl_msg_hdr (wire_codec.hip).  d_bytes 4-byte aligned; d_flag: one device word of scratch.
 int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
                          uint32_t sender_override, const SiloAddrEntry* d_silo_tab, orl_msg_hdr* d_out,
-                         uint8_t* d_status, uint32_t* d_n_bad, void* stream);
+                         uint8_t* d_status, uint32_t* d_n_bad, uint32_t* d_flag, void* stream);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

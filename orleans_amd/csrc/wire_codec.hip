@@ -10,12 +10,10 @@
 //              (Message.cs:149, 199-231, 251-255; GetScalarHeader / GetSimpleHeader :650-666).
 // The oracle is oracle/wire_codec.py (decode_frames); statuses and their precedence are defined there.
 //
-// One lane per frame.  Each lane walks its own header sequentially; bytes come from 4-byte aligned word
-// loads joined with v_alignbyte (a lane's consecutive reads hit the same L1/L2 lines), so no byte-granular
-// global loads and no reads beyond the aligned word that holds a frame's last byte.  Byte/integer work only.
+// One lane per frame: each lane walks its own header sequentially.  Bytes come from 4-byte aligned words joined
+// with v_alignbyte (no byte-granular loads, no read beyond the aligned word that holds a frame's last byte).
+// Large batches stage every frame's header window in LDS first (k_decode_frames_pipe).  Byte/integer work only.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "orl_internal.h"
 
@@ -36,33 +34,39 @@ enum : uint32_t { H_CATEGORY = 3, H_SENDING_SILO = 20, H_TARGET_ACTIVATION = 22,
 
 constexpr uint64_t kMaxTicks = 3155378975999999999ull;  // DateTime.MaxValue.Ticks
 
-// Byte sources: positions are absolute buffer offsets; word(i) returns aligned word i of the buffer.
-struct GlobalSrc {  // the receive buffer in HBM
+// Byte sources.  GlobalSrc: positions are absolute 64-bit buffer offsets; word reads are clamped to `last`, the
+// word holding the current frame's last byte, so any read is inside the frame's words.  LdsSrc: one frame staged in
+// an LDS row, positions are 32-bit offsets from the row start (the frame's first aligned word); a row has a spare
+// word after its 64, so the second word of a read is always readable.  Both read 4 bytes with two word loads and
+// v_alignbyte and no branch: ({hi, lo} >> 8 * (p & 3))[31:0].
+struct GlobalSrc {
+    using P = uint64_t;
     const uint32_t* __restrict__ w;
-    __device__ __forceinline__ uint32_t word(uint64_t i) const { return w[i]; }
+    uint64_t last;
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return w[i < last ? i : last]; }
+    __device__ __forceinline__ uint32_t ld32(uint64_t p) const {
+        const uint64_t wi = p >> 2;
+        return __builtin_amdgcn_alignbyte(word(wi + 1), word(wi), (uint32_t)(p & 3u));
+    }
 };
-struct LdsSrc {     // one frame staged in LDS: row[k] = buffer word base + k
+struct LdsSrc {
+    using P = uint32_t;
     const uint32_t* row;
-    uint64_t base;
-    __device__ __forceinline__ uint32_t word(uint64_t i) const { return row[(uint32_t)(i - base)]; }
+    __device__ __forceinline__ uint32_t word(uint32_t i) const { return row[i]; }
+    __device__ __forceinline__ uint32_t ld32(uint32_t p) const {
+        const uint32_t wi = p >> 2;
+        return __builtin_amdgcn_alignbyte(row[wi + 1], row[wi], p & 3u);
+    }
 };
 
-// 4 bytes at p (little endian).  Caller guarantees p + 4 <= a frame end <= nbytes, so the second word holds
-// byte p+3 and is inside the buffer's (or the staged row's) last word at worst.
 template <class S>
-__device__ __forceinline__ uint32_t ld32(const S& w, uint64_t p) {
-    const uint64_t wi = p >> 2;
-    const uint32_t sh = (uint32_t)(p & 3u);
-    const uint32_t lo = w.word(wi);
-    if (sh == 0) return lo;
-    return __builtin_amdgcn_alignbyte(w.word(wi + 1), lo, sh);  // v_alignbyte: ({hi, lo} >> 8 * sh)[31:0]
-}
+__device__ __forceinline__ uint32_t ld32(const S& w, typename S::P p) { return w.ld32(p); }
 template <class S>
-__device__ __forceinline__ uint32_t ld8(const S& w, uint64_t p) {
+__device__ __forceinline__ uint32_t ld8(const S& w, typename S::P p) {
     return (w.word(p >> 2) >> ((uint32_t)(p & 3u) * 8u)) & 0xFFu;
 }
 template <class S>
-__device__ __forceinline__ uint64_t ld64(const S& w, uint64_t p) {
+__device__ __forceinline__ uint64_t ld64(const S& w, typename S::P p) {
     return (uint64_t)ld32(w, p) | ((uint64_t)ld32(w, p + 4) << 32);
 }
 
@@ -70,8 +74,8 @@ __device__ __forceinline__ uint64_t ld64(const S& w, uint64_t p) {
 // of Char.IsWhiteSpace code points (U+0009-000D, 0020, 0085, 00A0, 1680, 2000-200A, 2028, 2029, 202F, 205F,
 // 3000).  Any other byte decodes to a non-space char or to U+FFFD.
 template <class S>
-__device__ bool all_whitespace(const S& w, uint64_t p, uint64_t len) {
-    const uint64_t e = p + len;
+__device__ bool all_whitespace(const S& w, typename S::P p, typename S::P len) {
+    const typename S::P e = p + len;
     while (p < e) {
         const uint32_t b0 = ld8(w, p);
         if (b0 == 0x20u || (b0 >= 0x09u && b0 <= 0x0Du)) { p += 1; continue; }
@@ -97,9 +101,10 @@ __device__ bool all_whitespace(const S& w, uint64_t p, uint64_t len) {
 // Strict UTF-8 (RFC 3629: no overlongs, no surrogates, <= U+10FFFF) — the byte strings .NET's decoder maps to
 // themselves when re-encoded.
 template <class S>
-__device__ bool strict_utf8(const S& w, uint64_t p, uint64_t len) {
-    const uint64_t e = p + len;
+__device__ bool strict_utf8(const S& w, typename S::P p, typename S::P len) {
+    const typename S::P e = p + len;
     while (p < e) {
+        if (p + 4 <= e && (ld32(w, p) & 0x80808080u) == 0) { p += 4; continue; }  // four ASCII bytes
         const uint32_t b0 = ld8(w, p);
         if (b0 < 0x80u) { p += 1; continue; }
         uint32_t n, lo = 0x80u, hi = 0xBFu;
@@ -119,7 +124,7 @@ __device__ bool strict_utf8(const S& w, uint64_t p, uint64_t len) {
 
 // JenkinsHash.ComputeHash(byte[]) (JenkinsHash.cs:68-115) over [p, p+len).
 template <class S>
-__device__ uint32_t jenkins_stream(const S& w, uint64_t p, uint32_t len) {
+__device__ uint32_t jenkins_stream(const S& w, typename S::P p, uint32_t len) {
     uint32_t a = 0x9e3779b9u, b = 0x9e3779b9u, c = 0u;
     uint32_t i = 0;
     for (; i + 12u <= len; i += 12u) {
@@ -130,47 +135,45 @@ __device__ uint32_t jenkins_stream(const S& w, uint64_t p, uint32_t len) {
     }
     c += len;
     const uint32_t t = len - i;  // 0..11 tail bytes: 0-3 -> a, 4-7 -> b, 8-10 -> c << 8
-    for (uint32_t j = 0; j < t; ++j) {
-        const uint32_t by = ld8(w, p + i + j);
-        if (j < 4) a += by << (8u * j);
-        else if (j < 8) b += by << (8u * (j - 4u));
-        else c += by << (8u * (j - 7u));
-    }
+    auto mask = [](uint32_t k) { return k >= 4 ? 0xFFFFFFFFu : (1u << (8u * k)) - 1u; };
+    a += ld32(w, p + i) & mask(t);
+    b += ld32(w, p + i + 4) & mask(t > 4 ? t - 4 : 0);
+    c += (ld32(w, p + i + 8) & mask(t > 8 ? t - 8 : 0)) << 8;
     ORL_MIX(a, b, c);
     return c;
 }
 
 // ReadUniqueKey (:424-431) + UniqueKey.ValidateKeyExt (UniqueKey.cs:328-350).  Advances p; returns a status.
 template <class S>
-__device__ __forceinline__ uint32_t skip_unique_key(const S& w, uint64_t end, uint64_t& p) {
+__device__ __forceinline__ uint32_t skip_unique_key(const S& w, typename S::P end, typename S::P& p) {
     if (p + 28 > end) return ORL_DEC_MALFORMED;
     const uint32_t cat = ld32(w, p + 20) >> 24;  // top byte of TypeCodeData
     const int32_t len = (int32_t)ld32(w, p + 24);
     p += 28;
     if (len == -1) return cat == 6u ? ORL_DEC_MALFORMED : ORL_DEC_OK;  // KeyExt grain needs an extension
-    if (len < 0 || p + (uint64_t)len > end) return ORL_DEC_MALFORMED;
+    if (len < 0 || p + (typename S::P)len > end) return ORL_DEC_MALFORMED;
     if (cat != 6u) return ORL_DEC_MALFORMED;                             // extension on a non-KeyExt key
-    if (all_whitespace(w, p, (uint64_t)len)) return ORL_DEC_MALFORMED;
-    p += (uint64_t)len;
+    if (all_whitespace(w, p, (typename S::P)len)) return ORL_DEC_MALFORMED;
+    p += (typename S::P)len;
     return ORL_DEC_OK;
 }
 
 template <class S>
-__device__ __forceinline__ bool port_ok(const S& w, uint64_t p) {
+__device__ __forceinline__ bool port_ok(const S& w, typename S::P p) {
     return ld32(w, p) <= 65535u;  // new IPEndPoint(addr, port): 0 <= port <= 65535
 }
 
 // One header value (DeserializeMessageHeaderHelper :1833-1853), starting at its token.  Lists are flattened
 // with a pending-value counter (a list only adds values), so nesting depth costs no state.
 template <class S>
-__device__ uint32_t skip_value(const S& w, uint64_t end, uint64_t& p) {
+__device__ uint32_t skip_value(const S& w, typename S::P end, typename S::P& p) {
     uint64_t pending = 1;
     while (pending) {
         --pending;
         if (p >= end) return ORL_DEC_MALFORMED;
         const uint32_t t = ld8(w, p);
         p += 1;
-        uint64_t sz = 0;
+        typename S::P sz = 0;
         switch (t) {
         case T_NULL: case T_TRUE: case T_FALSE: case T_OBJECT: sz = 0; break;
         case T_SBYTE: case T_BYTE: sz = 1; break;
@@ -210,7 +213,7 @@ __device__ uint32_t skip_value(const S& w, uint64_t end, uint64_t& p) {
             if (p + 4 > end) return ORL_DEC_MALFORMED;
             const int32_t len = (int32_t)ld32(w, p);
             if (len < -1) return ORL_DEC_MALFORMED;
-            sz = 4 + (len > 0 ? (uint64_t)len : 0);
+            sz = 4 + (len > 0 ? (typename S::P)len : 0);
             break;
         }
         case T_GRAIN: case T_ACT: {
@@ -245,7 +248,7 @@ __device__ uint32_t skip_value(const S& w, uint64_t end, uint64_t& p) {
 }
 
 template <class S>
-__device__ uint32_t silo_lookup(const SiloAddrEntry* __restrict__ tab, const S& w, uint64_t p) {
+__device__ uint32_t silo_lookup(const SiloAddrEntry* __restrict__ tab, const S& w, typename S::P p) {
     uint32_t a[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) a[i] = ld32(w, p + 4u * i);
@@ -287,88 +290,98 @@ __device__ uint32_t token_class(uint32_t t) {
     }
 }
 
-// One header value starting at its token p - 1 (token tok, class cls): the common-case form of skip_value.
+// One header value whose token (class cls) sits at p - 1: the common-case form of skip_value, branch-free except
+// for the rare classes.  The speculative reads (a length at +0 or +24, a port at +16, a DateTime at +0) are
+// issued together at positions clamped into the header, and only the ones the class needs are used.
 template <class S>
-__device__ __forceinline__ uint32_t skip_value_fast(const S& w, uint64_t end, uint32_t cls, uint64_t& p) {
+__device__ __forceinline__ uint32_t skip_value_fast(const S& w, typename S::P end, uint32_t cls, typename S::P& p) {
+    using P = typename S::P;
     if (cls & CLS_SLOW) {
         p -= 1;
         return skip_value(w, end, p);
     }
-    uint64_t sz = cls & CLS_SIZE;
-    if (p + sz > end) return ORL_DEC_MALFORMED;
-    uint32_t st = ORL_DEC_OK;
-    if (cls & (CLS_STR | CLS_KEY)) {
-        const uint64_t lp = (cls & CLS_KEY) ? p + 24 : p;
-        const int32_t len = (int32_t)ld32(w, lp);
-        if (cls & CLS_KEY) {
-            const uint32_t cat = ld8(w, p + 23);
-            if (cat == 6u) {  // KeyExt grain: a non-blank extension (UniqueKey.cs:328-345)
-                if (len < 1 || p + 28 + (uint64_t)len > end) st = ORL_DEC_MALFORMED;
-                else if (all_whitespace(w, p + 28, (uint64_t)len)) st = ORL_DEC_MALFORMED;
-            } else if (len != -1) {
-                st = ORL_DEC_MALFORMED;  // a length < -1 throws in ReadString; >= 0 in ValidateKeyExt
-            }
-        } else if (len < -1) {
-            st = ORL_DEC_MALFORMED;
-        }
-        sz += len > 0 ? (uint64_t)len : 0;
-    }
-    if ((cls & CLS_PORT) && ld32(w, p + 16) > 65535u) st = ORL_DEC_MALFORMED;
+    const P lim = end - 4;  // the header holds >= 4 bytes before p (intro + count), so lim >= 0
+    auto at = [&](P q) { return q < lim ? q : lim; };
+    const uint32_t r0 = ld32(w, at(p)), r4 = ld32(w, at(p + 4)), r16 = ld32(w, at(p + 16)), r20 = ld32(w, at(p + 20)),
+                   r24 = ld32(w, at(p + 24));
+    const P fixed = cls & CLS_SIZE;
+    const bool fits = fixed <= end - p;
+    const bool is_key = cls & CLS_KEY, is_str = cls & CLS_STR;
+    const int32_t len = (int32_t)(is_key ? r24 : r0);
+    const bool keyext = (r20 >> 24) == 6u;  // category byte of TypeCodeData (key at p: N0, N1, TCD)
+    bool bad = (is_str && len < -1) || (is_key && (keyext ? len < 1 : len != -1)) || ((cls & CLS_PORT) && r16 > 65535u);
+    bool unsup = false;
     if (cls & CLS_DATE) {
-        const uint64_t v = ld64(w, p);
-        if (v >> 63) st = ORL_DEC_UNSUPPORTED;
-        else if ((v & 0x3FFFFFFFFFFFFFFFull) > kMaxTicks) st = ORL_DEC_MALFORMED;
+        const uint64_t v = (uint64_t)r0 | ((uint64_t)r4 << 32);
+        unsup = (v >> 63) != 0;
+        bad = bad || (v & 0x3FFFFFFFFFFFFFFFull) > kMaxTicks;
     }
-    if (!st && p + sz > end) st = ORL_DEC_MALFORMED;
+    const P var = (is_str || is_key) && len > 0 ? (P)len : 0;
+    const P sz = fixed + var;
+    const bool fits_all = fits && var <= end - p - fixed;
+    uint32_t st = !fits ? ORL_DEC_MALFORMED : unsup ? ORL_DEC_UNSUPPORTED : (bad || !fits_all) ? ORL_DEC_MALFORMED : ORL_DEC_OK;
+    // KeyExt grain: the extension must not be blank (UniqueKey.cs:328-345) — rare, so a branch
+    if (!st && is_key && keyext && all_whitespace(w, p + 28, var)) st = ORL_DEC_MALFORMED;
     p += sz;
     return st;
 }
 
 // One frame's header [p, end) (frame validated by the caller) -> status + the two 16-byte halves of its record.
 template <class S>
-__device__ uint32_t decode_header(const S& w, uint64_t p, uint64_t end, uint32_t sender_override,
+__device__ uint32_t decode_header(const S& w, typename S::P p, typename S::P end, uint32_t sender_override,
                                   const SiloAddrEntry* __restrict__ tab, const uint16_t* lut, uint4& r0, uint4& r1) {
     uint32_t st = ORL_DEC_OK;
     uint32_t cat_v = 0, cat_st = 0;           // 0 absent, 1 Int, 2 other type (cast fails)
     uint32_t ts_st = 0, ss_st = 0;            // 0 absent / null, 1 SiloAddress, 2 other type
-    uint64_t ts_p = 0, ss_p = 0, tg_p = 0;
+    typename S::P ts_p = 0, ss_p = 0, tg_p = 0;
     bool tg = false, ta = false;
     // DeserializeMessageHeaders: StringObjDict, int32 count, count x (byte key, value); duplicate keys throw.
-    if (p + 5 > end || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
+    if (5 > end - p || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
     int32_t count = 0;
     if (!st) {
         count = (int32_t)ld32(w, p + 1);
         p += 5;
         if (count < 0) st = ORL_DEC_MALFORMED;
     }
-    uint64_t seen0 = 0, seen1 = 0, seen2 = 0, seen3 = 0;
+    // duplicate keys: a 32-bit mask for keys < 32 (every Message.Header value); larger keys (legal bytes, never
+    // written by the reference) take the rare path through a 256-bit mask
+    uint32_t seen = 0;
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     for (int32_t e = 0; !st && e < count; ++e) {
-        if (p + 2 > end) { st = ORL_DEC_MALFORMED; break; }
+        if (2 > end - p) { st = ORL_DEC_MALFORMED; break; }
         const uint32_t kt = ld32(w, p - 2) >> 16;  // key, token: p >= frame + 10, so p - 2 is in the frame
         const uint32_t key = kt & 0xFFu;
         const uint32_t tok = (kt >> 8) & 0xFFu;
-        const uint64_t vp = p + 2;  // first byte after the value token
+        const typename S::P vp = p + 2;  // first byte after the value token
         p = vp;
         st = skip_value_fast(w, end, lut[tok], p);
         if (st) break;
-        const uint32_t q = key >> 6;
-        const uint64_t bit = 1ull << (key & 63u);
-        const uint64_t cur = q == 0 ? seen0 : q == 1 ? seen1 : q == 2 ? seen2 : seen3;
-        if (cur & bit) { st = ORL_DEC_MALFORMED; break; }
-        seen0 |= q == 0 ? bit : 0; seen1 |= q == 1 ? bit : 0; seen2 |= q == 2 ? bit : 0; seen3 |= q == 3 ? bit : 0;
-        switch (key) {
-        case H_CATEGORY: cat_st = tok == T_INT ? 1u : 2u; if (tok == T_INT) cat_v = ld32(w, vp); break;
-        case H_TARGET_SILO: ts_st = tok == T_SILO ? 1u : tok == T_NULL ? 0u : 2u; ts_p = vp; break;
-        case H_SENDING_SILO: ss_st = tok == T_SILO ? 1u : tok == T_NULL ? 0u : 2u; ss_p = vp; break;
-        case H_TARGET_GRAIN: tg = tok == T_GRAIN; tg_p = vp; break;
-        case H_TARGET_ACTIVATION: ta = tok == T_ACT; break;
-        default: break;
+        bool dup;
+        if (key < 32u) {
+            const uint32_t bit = 1u << key;
+            dup = (seen & bit) != 0;
+            seen |= bit;
+        } else {
+            const uint32_t q = key >> 6;
+            const uint64_t bit = 1ull << (key & 63u);
+            dup = ((q == 0 ? h0 : q == 1 ? h1 : q == 2 ? h2 : h3) & bit) != 0;
+            h0 |= q == 0 ? bit : 0; h1 |= q == 1 ? bit : 0; h2 |= q == 2 ? bit : 0; h3 |= q == 3 ? bit : 0;
         }
+        if (dup) { st = ORL_DEC_MALFORMED; break; }
+        // captures, as selects
+        const bool is_int = tok == T_INT, is_silo = tok == T_SILO, is_null = tok == T_NULL;
+        const uint32_t sst = is_silo ? 1u : is_null ? 0u : 2u;
+        if (key == H_CATEGORY) { cat_st = is_int ? 1u : 2u; cat_v = ld32(w, vp); }
+        if (key == H_TARGET_SILO) { ts_st = sst; ts_p = vp; }
+        if (key == H_SENDING_SILO) { ss_st = sst; ss_p = vp; }
+        if (key == H_TARGET_GRAIN) { tg = tok == T_GRAIN; tg_p = vp; }
+        if (key == H_TARGET_ACTIVATION) ta = tok == T_ACT;
     }
     // the getters, in the order the oracle defines (oracle/wire_codec.py decode_for_route)
     uint32_t sending = sender_override, target_silo = 0, flags = 0, aux = 0;
     uint64_t tcd = 0, n0 = 0, n1 = 0;
-    if (!st && (cat_st == 2 || (cat_st == 1 && cat_v > 255u))) st = ORL_DEC_MALFORMED;
+    if (cat_st != 1) cat_v = 0;
+    if (!st && (cat_st == 2 || cat_v > 255u)) st = ORL_DEC_MALFORMED;
     if (!st && ts_st == 2) st = ORL_DEC_MALFORMED;
     if (!st && sender_override == ORL_SENDER_FROM_HEADER) {
         if (ss_st == 2) st = ORL_DEC_MALFORMED;
@@ -404,25 +417,16 @@ __device__ uint32_t decode_header(const S& w, uint64_t p, uint64_t end, uint32_t
     return st;
 }
 
-__device__ __forceinline__ void write_record(uint32_t i, uint32_t st, const uint4& r0, const uint4& r1, uint4* __restrict__ out,
-                                             uint8_t* __restrict__ status, uint32_t* __restrict__ n_bad) {
-    if (st && n_bad) atomicAdd(n_bad, 1u);
-    out[2ull * i] = r0;
-    out[2ull * i + 1] = r1;
-    status[i] = (uint8_t)st;
+// Frame prefix checks (IncomingMessageBuffer.cs:94-135): the 8-byte lengths inside the buffer, both lengths >= 0,
+// header + body inside the buffer.  hl / bl are the two int32 lengths.
+__device__ __forceinline__ bool frame_ok(uint64_t off, uint64_t nbytes, int32_t hl, int32_t bl) {
+    return hl >= 0 && bl >= 0 && (uint64_t)hl + (uint64_t)bl <= nbytes - off - 8;
 }
+__device__ __forceinline__ bool prefix_in_buffer(uint64_t off, uint64_t nbytes) { return off <= nbytes && nbytes - off >= 8; }
 
-// Frame i's prefix checks (IncomingMessageBuffer.cs:94-135): the 8-byte lengths inside the buffer, both lengths
-// >= 0, header + body inside the buffer.  Returns the header end (absolute) or 0 when malformed.
-template <class S>
-__device__ __forceinline__ uint64_t frame_end(const S& w, uint64_t off, uint64_t nbytes) {
-    if (off > nbytes || nbytes - off < 8) return 0;
-    const int32_t hl = (int32_t)ld32(w, off), bl = (int32_t)ld32(w, off + 4);
-    if (hl < 0 || bl < 0 || (uint64_t)hl + (uint64_t)bl > nbytes - off - 8) return 0;
-    return off + 8 + (uint64_t)hl;
-}
+constexpr uint32_t kDeferred = 0xFEu;  // pipelined kernel: header longer than its window, left to k_decode_deferred
 
-// Simple form: one lane per frame, parsing straight from HBM through L1/L2.  Used for small batches.
+// Simple form: one lane per frame, parsing straight from HBM through L1/L2 (small batches).
 __global__ __launch_bounds__(256) void k_decode_frames(const uint32_t* __restrict__ buf, uint64_t nbytes,
                                                        const uint64_t* __restrict__ offs, uint32_t n, uint32_t sender_override,
                                                        const SiloAddrEntry* __restrict__ tab, uint4* __restrict__ out,
@@ -432,23 +436,90 @@ __global__ __launch_bounds__(256) void k_decode_frames(const uint32_t* __restric
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const GlobalSrc g{buf};
     const uint64_t off = offs[i];
-    const uint64_t end = frame_end(g, off, nbytes);
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
-    const uint32_t st = end ? decode_header(g, off + 8, end, sender_override, tab, lut, r0, r1) : ORL_DEC_MALFORMED;
-    write_record(i, st, r0, r1, out, status, n_bad);
+    uint32_t st = ORL_DEC_MALFORMED;
+    if (prefix_in_buffer(off, nbytes)) {
+        const GlobalSrc pre{buf, (off + 7) >> 2};
+        const int32_t hl = (int32_t)ld32(pre, off), bl = (int32_t)ld32(pre, off + 4);
+        if (frame_ok(off, nbytes, hl, bl)) {
+            const uint64_t end = off + 8 + (uint64_t)hl;
+            st = decode_header(GlobalSrc{buf, (end - 1) >> 2}, off + 8, end, sender_override, tab, lut, r0, r1);
+        }
+    }
+    if (st && n_bad) atomicAdd(n_bad, 1u);
+    out[2ull * i] = r0;
+    out[2ull * i + 1] = r1;
+    status[i] = (uint8_t)st;
+}
+
+// Fallback for the frames the pipelined kernel could not finish (a header longer than kHeldWords words, or more
+// than 64 long headers in one wave's share): a no-op unless the kernel raised *any_deferred.  Each wave ballots
+// its 64 statuses; for every deferred frame the whole wave copies the frame (prefix + header, up to kLongWords words)
+// into the wave's LDS buffer with coalesced loads, and that frame's lane parses it from LDS.  Headers beyond
+// kLongWords words are parsed from HBM.
+constexpr uint32_t kLongWords = 1024;
+
+__global__ __launch_bounds__(256) void k_decode_deferred(const uint32_t* __restrict__ buf, uint64_t nbytes,
+                                                         const uint64_t* __restrict__ offs, uint32_t n, uint32_t sender_override,
+                                                         const SiloAddrEntry* __restrict__ tab, uint4* __restrict__ out,
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ n_bad,
+                                                         const uint32_t* __restrict__ any_deferred) {
+    if (*any_deferred == 0) return;  // the pipelined kernel finished every frame itself
+    __shared__ uint32_t big[4][kLongWords];
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool mine = i < n && status[i] == kDeferred;
+    uint64_t todo = __ballot(mine);
+    if (!todo) return;  // wave-uniform; no block barrier follows
+    const uint64_t off = mine ? offs[i] : 0;
+    const int32_t hl = mine ? (int32_t)ld32(GlobalSrc{buf, (off + 7) >> 2}, off) : 0;  // validated by the pipelined kernel
+    const uint32_t w_lo = (uint32_t)(off >> 2), w_hi = (uint32_t)(off >> 34);
+    const uint32_t words = (uint32_t)(((off & 3u) + 8u + (uint64_t)hl + 3u) / 4u);
+    uint32_t* row = big[wv];
+    while (todo) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane(words, j);
+        if (nw <= kLongWords) {
+            const uint64_t w0 = (uint64_t)__builtin_amdgcn_readlane(w_lo, j) | ((uint64_t)__builtin_amdgcn_readlane(w_hi, j) << 32);
+            for (uint32_t k = lane; k < nw; k += 64) row[k] = buf[w0 + k];
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (lane == j) {
+            uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+            uint32_t st;
+            const uint32_t q0 = (uint32_t)(off & 3u);
+            if (nw <= kLongWords)
+                st = decode_header(LdsSrc{row}, q0 + 8, q0 + 8 + (uint32_t)hl, sender_override, tab, lut, r0, r1);
+            else
+                st = decode_header(GlobalSrc{buf, (off + 7 + (uint64_t)hl) >> 2}, off + 8, off + 8 + (uint64_t)hl, sender_override,
+                                   tab, lut, r0, r1);
+            if (st && n_bad) atomicAdd(n_bad, 1u);
+            out[2ull * i] = r0;
+            out[2ull * i + 1] = r1;
+            status[i] = (uint8_t)st;
+        }
+        __builtin_amdgcn_wave_barrier();  // the buffer is rewritten for the next frame
+    }
 }
 
 // Pipelined form.  A persistent wave walks 64-frame chunks.  For every frame of a chunk it loads the 64-word
 // (256-byte) window that starts at the frame's first aligned word — one coalesced load per frame, issued for the
 // NEXT chunk while the current chunk is parsed, so the HBM latency hides behind the parse — then copies the
-// window into the frame's LDS row and parses it there: one pass over the header bytes instead of the dozens of
-// L2 requests per frame that lanes parsing 64 different frames through a 32-KB L1 cost.  Rows are 65 words
-// apart, so lanes reading the same relative word hit distinct banks.  A header that does not fit its window is
-// parsed straight from HBM.  Window loads are clamped to the buffer's last word.
+// window into the frame's LDS row and parses it there with 32-bit positions: one pass over the header bytes
+// instead of the dozens of L2 requests per frame that lanes parsing 64 different frames through a 32-KB L1 cost.
+// Rows are 65 words apart, so lanes reading the same relative word hit distinct banks.  Window loads are
+// clamped to the buffer's last word.  A header that does not fit its window is held in a per-wave list and, after
+// the wave's last chunk, parsed 16 at a time from kHeldWords-word LDS rows; beyond that it is left to
+// k_decode_deferred (status kDeferred, *any_deferred = 1).
 constexpr uint32_t kRowWords = 64;
 constexpr uint32_t kRowStride = kRowWords + 1;
+constexpr uint32_t kHeldWords = 64 * kRowStride / 16;  // 260 words per held frame, 16 at a time
+constexpr uint32_t kHeldMax = 64;
 constexpr size_t kPipeMinFrames = 1u << 16;  // below this the simple form fills the chip better
 
 __device__ __forceinline__ void load_windows(const uint32_t* __restrict__ buf, uint64_t last_word, uint64_t off,
@@ -467,10 +538,13 @@ __global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __re
                                                             const uint64_t* __restrict__ offs, uint32_t n,
                                                             uint32_t sender_override, const SiloAddrEntry* __restrict__ tab,
                                                             uint4* __restrict__ out, uint8_t* __restrict__ status,
-                                                            uint32_t* __restrict__ n_bad) {
+                                                            uint32_t* __restrict__ n_bad, uint32_t* __restrict__ any_deferred) {
     __shared__ uint32_t rows[4][64 * kRowStride];
+    __shared__ uint32_t held[4][kHeldMax];
+    __shared__ uint32_t n_held[4];
     __shared__ uint16_t lut[256];
     lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    if ((threadIdx.x & 63u) == 0) n_held[threadIdx.x >> 6] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t n_chunks = (n + 63) / 64;
@@ -478,11 +552,21 @@ __global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __re
     uint32_t c = blockIdx.x * 4 + wv;
     if (c >= n_chunks) return;  // wave-uniform: the kernel has no block-wide barrier after this point
     const uint64_t last_word = (nbytes + 3) / 4 - 1;  // launcher guarantees nbytes >= 8
-    const GlobalSrc g{buf};
     uint32_t* my = rows[wv];
+    const LdsSrc l{my + lane * kRowStride};
     auto frame_off = [&](uint32_t chunk) -> uint64_t {
         const uint32_t i = chunk * 64 + lane;
         return chunk < n_chunks && i < n ? offs[i] : ~0ull;
+    };
+    auto finish = [&](uint32_t i, uint32_t st, const uint4& r0, const uint4& r1) {
+        if (st == kDeferred) {
+            *any_deferred = 1u;
+        } else {
+            if (st && n_bad) atomicAdd(n_bad, 1u);
+            out[2ull * i] = r0;
+            out[2ull * i + 1] = r1;
+        }
+        status[i] = (uint8_t)st;
     };
     uint64_t off = frame_off(c);
     uint32_t v[64];
@@ -497,17 +581,23 @@ __global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __re
         __builtin_amdgcn_wave_barrier();
         const uint32_t i = c * 64 + lane;
         if (i < n) {
-            const LdsSrc l{my + lane * kRowStride, off >> 2};
             uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
             uint32_t st = ORL_DEC_MALFORMED;
-            const uint64_t end = frame_end(l, off, nbytes);  // the first 8 bytes always lie in the window
-            if (end) {
-                if ((end + 3) / 4 - off / 4 <= kRowWords)
-                    st = decode_header(l, off + 8, end, sender_override, tab, lut, r0, r1);
-                else
-                    st = decode_header(g, off + 8, end, sender_override, tab, lut, r0, r1);
+            bool hold = false;
+            if (prefix_in_buffer(off, nbytes)) {
+                const uint32_t q0 = (uint32_t)(off & 3u);  // the frame's first byte in its row
+                const int32_t hl = (int32_t)ld32(l, q0), bl = (int32_t)ld32(l, q0 + 4);
+                if (frame_ok(off, nbytes, hl, bl)) {
+                    if ((uint64_t)hl <= kRowWords * 4 - 8 - q0) {
+                        st = decode_header(l, q0 + 8, q0 + 8 + (uint32_t)hl, sender_override, tab, lut, r0, r1);
+                    } else {
+                        const uint32_t k = atomicAdd(&n_held[wv], 1u);
+                        if (k < kHeldMax) { held[wv][k] = i; hold = true; }
+                        else st = kDeferred;
+                    }
+                }
             }
-            write_record(i, st, r0, r1, out, status, n_bad);
+            if (!hold) finish(i, st, r0, r1);
         }
         if (cn >= n_chunks) break;
         __builtin_amdgcn_wave_barrier();  // the rows are rewritten next iteration
@@ -515,31 +605,65 @@ __global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __re
         off = off_next;
         off_next = off_nn;
     }
+    // the held long headers, 16 at a time
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nh = min(n_held[wv], kHeldMax);
+    for (uint32_t b = 0; b < nh; b += 16) {
+        const uint32_t m = min(16u, nh - b);
+        const bool act = lane < m;
+        const uint32_t fi = act ? held[wv][b + lane] : 0;
+        const uint64_t foff = act ? offs[fi] : 0;
+        const int32_t fhl = act ? (int32_t)ld32(GlobalSrc{buf, (foff + 7) >> 2}, foff) : 0;  // checked in the loop
+        const uint32_t fw = (uint32_t)(((foff & 3u) + 8u + (uint64_t)fhl + 3u) / 4u);
+        const uint32_t w_lo = (uint32_t)(foff >> 2), w_hi = (uint32_t)(foff >> 34);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane(fw, k);
+            if (nw > kHeldWords) continue;
+            const uint64_t w0 = (uint64_t)__builtin_amdgcn_readlane(w_lo, k) | ((uint64_t)__builtin_amdgcn_readlane(w_hi, k) << 32);
+            for (uint32_t t = lane; t < nw; t += 64) my[k * kHeldWords + t] = buf[w0 + t];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (act) {
+            uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+            uint32_t st = kDeferred;
+            if (fw <= kHeldWords) {
+                const uint32_t q0 = (uint32_t)(foff & 3u);
+                st = decode_header(LdsSrc{my + lane * kHeldWords}, q0 + 8, q0 + 8 + (uint32_t)fhl, sender_override, tab, lut, r0, r1);
+            }
+            finish(fi, st, r0, r1);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 }  // namespace
 
 int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
                          uint32_t sender_override, const SiloAddrEntry* d_silo_tab, orl_msg_hdr* d_out,
-                         uint8_t* d_status, uint32_t* d_n_bad, void* stream) {
+                         uint8_t* d_status, uint32_t* d_n_bad, uint32_t* d_flag, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (d_n_bad) {
         const hipError_t e = hipMemsetAsync(d_n_bad, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return (int)e;
     }
     if (n == 0) return 0;
-    static const int mode = [] { const char* e = getenv("ORL_DECODE_MODE"); return e ? atoi(e) : 1; }();
-    if (mode == 1 && n >= kPipeMinFrames && nbytes >= 8) {
-        // persistent: 2 workgroups (66.5 KB LDS each) per CU
+    const dim3 grid((uint32_t)((n + 255) / 256));
+    if (n >= kPipeMinFrames && nbytes >= 8) {
+        // persistent: 2 workgroups (66.5 KB LDS each) per CU; then the deferred long headers
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const uint32_t chunks = (uint32_t)((n + 63) / 64);
         const uint32_t blocks = std::min<uint32_t>((uint32_t)cus * 2u, (chunks + 3) / 4);
+        const hipError_t e = hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL(k_decode_frames_pipe, dim3(blocks), dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets,
-                           (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
+                           (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad, d_flag);
+        hipLaunchKernelGGL(k_decode_deferred, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets,
+                           (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad, (const uint32_t*)d_flag);
     } else {
-        hipLaunchKernelGGL(k_decode_frames, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, (const uint32_t*)d_bytes,
-                           nbytes, d_offsets, (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
+        hipLaunchKernelGGL(k_decode_frames, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets,
+                           (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
     }
     return (int)hipGetLastError();
 }

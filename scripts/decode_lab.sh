@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/dlab}
 mkdir -p $OUT
-for v in 0 1; do  # 0 = simple kernel, 1 = auto (pipelined above 64k frames)
+for v in ${MODES:-1}; do
   echo "=== ORL_DECODE_MODE=$v"
   ORL_DECODE_MODE=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k decode --timeout 240 --timeout-method thread > $OUT/tests_$v.log 2>&1
   rc=$?; tail -1 $OUT/tests_$v.log; [ $rc = 0 ] || exit $rc
@@ -14,6 +14,6 @@ for v in 0 1; do  # 0 = simple kernel, 1 = auto (pipelined above 64k frames)
 import csv,glob
 for f in glob.glob('$OUT/trace_$v/**/*kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        if 'decode' in r['Name']: print(r['Name'][:50], r['Calls'], float(r['AverageNs'])/1e3, 'us')
+        if 'decode' in r['Name'] or 'k_route' in r['Name']: print(r['Name'][:50], r['Calls'], float(r['AverageNs'])/1e3, 'us')
 "
 done
