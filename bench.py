@@ -486,6 +486,28 @@ def run_wire(args, torch):
         decode()
         eng.address_messages_device(d_hdr, n, d_r, d_a, d_o, d_f, stream=st)
 
+    # emit: the routed frames re-serialized with SetTargetPlacement (ActivationId key per activation handle)
+    akeys = np.zeros(n_grains, L.KEY_DTYPE)
+    akeys["n0"] = np.arange(n_grains, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    akeys["n1"] = np.arange(n_grains, dtype=np.uint64)
+    d_akeys = torch.from_numpy(akeys.view(np.uint8)).cuda()
+    eng_types = [(cl.type_code, "Orleans.Samples.Chirper.Grains.ChirperAccount")]
+    for code, name in eng_types:
+        eng.set_grain_type(code, name)
+    out_cap = len(buf) + n * (L.STAMP_MAX_GROWTH + 64)
+    d_sout = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
+    d_soff = torch.empty(n, dtype=torch.int64, device="cuda")
+    d_stot = torch.empty(1, dtype=torch.int64, device="cuda")
+    d_sst = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+    def stamp():
+        eng.stamp_frames_device(d_buf, len(buf), d_off, n, d_r, d_a, d_akeys, n_grains, None, d_sout, out_cap, d_soff,
+                                d_stot, d_sst, stream=st)
+
+    def receive_route_emit():
+        decode_route()
+        stamp()
+
     decode()
     torch.cuda.synchronize()
     assert int(d_bad.item()) == 0, "synthetic frames must decode cleanly"
@@ -494,7 +516,14 @@ def run_wire(args, torch):
         assert (got[f] == exp[f][:4096]).all(), f
     out = {}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    for name, fn in (("decode", decode), ("decode_route", decode_route)):
+    decode_route()
+    stamp()
+    torch.cuda.synchronize()
+    sst = np.bincount(d_sst.cpu().numpy(), minlength=6)
+    log(f"wire: stamp statuses {sst.tolist()} (OK, COMPLETE, SKIPPED, UNSUPPORTED, MALFORMED, OVERFLOW), "
+        f"{int(d_stot.item()) / 2**20:.0f} MiB out")
+    for name, fn in (("decode", decode), ("decode_route", decode_route), ("stamp", stamp),
+                     ("decode_route_stamp", receive_route_emit)):
         for _ in range(max(args.warmup, 1)):
             fn()
         torch.cuda.synchronize()
@@ -515,13 +544,13 @@ def run_wire(args, torch):
     if not args.no_cpu:
         cpu = wire_cpu_baseline(buf, offs, cl, args.cpu_wall)
     log("wire: " + ", ".join(f"{k} {v:.3f} ms" for k, v in out.items()) + f" per {n} frames (mean header {mean_hl:.0f} B)")
-    ms = out["decode_route"]
-    return {"metric": "frames decoded+routed/sec", "value": n / (ms * 1e-3), "unit": "frames/s", "n_gpus": 1,
+    ms = out["decode_route_stamp"]
+    return {"metric": "frames decoded+routed+re-serialized/sec", "value": n / (ms * 1e-3), "unit": "frames/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32 integer",
             "data": "synthetic frames (request / response header dictionaries as SerializeMessageHeaders writes them)",
-            "config": {"workload": f"leg 8: {n} frames -> headers (device decode) -> route + bucket, "
-                                   f"{n_grains} registered grains"},
+            "config": {"workload": f"leg 8: {n} frames -> headers (device decode) -> route + bucket -> frames "
+                                   f"re-serialized with the placement (SetTargetPlacement), {n_grains} registered grains"},
             "ms": out, "decode_frames_per_s": n / (out["decode_event"] * 1e-3),
             "roofline": {"bound": "hbm", "kernel": "k_decode_frames", "achieved": alg / (out["decode_event"] * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

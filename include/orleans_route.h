@@ -351,6 +351,34 @@ int orl_silo_address_set(orl_ctx* ctx, uint32_t silo, const uint8_t* ip16, int32
 int orl_decode_frames_device(orl_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_frame_offsets,
                              size_t n, uint32_t sender_override, orl_msg_hdr* d_out, uint8_t* d_status, uint32_t* d_n_bad,
                              void* stream);
+/* Emit: the routed frames re-serialized with the placement applied — Dispatcher.AddressMessage →
+ * Message.SetTargetPlacement (src/OrleansRuntime/Core/Dispatcher.cs:555-579, src/Orleans/Messaging/Message.cs:
+ * 1079-1096) → Message.Serialize_Impl (:915-951).  For route status HIT the placement is
+ * PlacementResult.IdentifySelection (activation d_act_keys[d_act[i]] = its ActivationId key, host silo); for
+ * NEW_PLACEMENT it is SpecifyCreation (host silo, ActivationId d_new_act_keys[i] — ActivationId.NewId() is the
+ * caller's —, the grain class of the target's type code from orl_grain_type_set).  The header dictionary is
+ * updated as .NET's Dictionary does: PRIOR_MESSAGE_ID / PRIOR_MESSAGE_TIMES removed on a new placement or an
+ * activation change (free-list slots, reused last-removed first by the keys added next), TARGET_ACTIVATION and
+ * TARGET_SILO set (in place if present), and on a new placement IS_NEW_PLACEMENT = true and NEW_GRAIN_TYPE.
+ * Other frames are copied unchanged (status says why).  Output frame i starts at d_out_offsets[i] (4-byte aligned,
+ * back to back in frame order, padding between frames); *d_out_total = the aligned end; frames that do not fit
+ * out_cap are not written (ORL_STAMP_OVERFLOW).  A frame's output never exceeds its input by more than
+ * ORL_STAMP_MAX_GROWTH + the longest grain class name.  d_out 4-byte aligned; d_new_act_keys may be NULL when
+ * no message is a new placement. */
+#define ORL_STAMP_OK 0u
+#define ORL_STAMP_COMPLETE 1u     /* TargetAddress already complete: unchanged (Dispatcher.cs:557-558) */
+#define ORL_STAMP_SKIPPED 2u      /* route status other than HIT / NEW_PLACEMENT: unchanged, host path */
+#define ORL_STAMP_UNSUPPORTED 3u  /* header needs the managed serializer, a string is not byte-canonical (not
+                                     strict UTF-8), an unknown grain type / activation handle: unchanged */
+#define ORL_STAMP_MALFORMED 4u    /* the reference throws (undecodable header; a TARGET_ACTIVATION that is not an
+                                     ActivationId); an invalid frame prefix emits nothing */
+#define ORL_STAMP_OVERFLOW 5u     /* past out_cap: not written */
+#define ORL_STAMP_MAX_GROWTH 72u
+int orl_grain_type_set(orl_ctx* ctx, int32_t type_code, const char* class_name_utf8, size_t len);  /* len 0: remove */
+int orl_stamp_frames_device(orl_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_frame_offsets,
+                            size_t n, const uint32_t* d_route, const uint32_t* d_act, const orl_grain_key* d_act_keys,
+                            uint32_t n_act_keys, const orl_grain_key* d_new_act_keys, uint8_t* d_out, uint64_t out_cap,
+                            uint64_t* d_out_offsets, uint64_t* d_out_total, uint8_t* d_status, void* stream);
 
 /* ---- multi-GPU exchange support --------------------------------------------
  * Stages 1-2 + stable partition by destination rank (rank_of_silo[owner]).  Messages whose owner is

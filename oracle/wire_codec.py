@@ -71,7 +71,7 @@ SENDER_FROM_HEADER = 0xFF
 
 # ---------------------------------------------------------------------------------------
 # values: ("null",) ("bool", b) ("int", v) ("uint", v) ("short", v) ("ushort", v) ("long", v) ("ulong", v)
-# ("byte", v) ("sbyte", v) ("float", f) ("double", f) ("decimal", bytes16) ("string", s|None) ("char", u16)
+# ("byte", v) ("sbyte", v) ("float", f) ("double", f) ("floatbits", u32) ("doublebits", u64) ("decimal", bytes16) ("string", s|None) ("char", u16)
 # ("guid", bytes16) ("date", i64 binary) ("timespan", i64) ("ip", bytes16) ("ipep", bytes16, port)
 # ("object",) ("grain", Key) ("act", Key) ("silo", SiloAddr) ("actaddr", SiloAddr|None, Key, Key|None)
 # ("corr", i64) ("list", [values]) ("dict", [(key, value)]) ("specified", raw bytes after the token)
@@ -117,6 +117,7 @@ class HeaderWriter:
         fixed = {"int": (T_INT, "<i"), "uint": (T_UINT, "<I"), "short": (T_SHORT, "<h"), "ushort": (T_USHORT, "<H"),
                  "long": (T_LONG, "<q"), "ulong": (T_ULONG, "<Q"), "byte": (T_BYTE, "<B"), "sbyte": (T_SBYTE, "<b"),
                  "float": (T_FLOAT, "<f"), "double": (T_DOUBLE, "<d"), "char": (T_CHAR, "<H"),
+                 "floatbits": (T_FLOAT, "<I"), "doublebits": (T_DOUBLE, "<Q"),
                  "date": (T_DATE, "<Q"), "timespan": (T_TIMESPAN, "<q"), "corr": (T_CORR, "<q")}
         if kind in fixed:
             t, f = fixed[kind]
@@ -271,9 +272,11 @@ def _read_value(r: _Reader, depth: int = 0):
         return ("bool", t == T_TRUE)
     if t == T_OBJECT:
         return ("object",)
+    # floats keep their bits (BitConverter.ToSingle / GetBytes round-trip every pattern, signalling NaNs too;
+    # Python's float32 unpack would quiet them)
     fixed = {T_INT: ("int", "<i"), T_UINT: ("uint", "<I"), T_SHORT: ("short", "<h"), T_USHORT: ("ushort", "<H"),
              T_LONG: ("long", "<q"), T_ULONG: ("ulong", "<Q"), T_BYTE: ("byte", "<B"), T_SBYTE: ("sbyte", "<b"),
-             T_FLOAT: ("float", "<f"), T_DOUBLE: ("double", "<d"), T_TIMESPAN: ("timespan", "<q"),
+             T_FLOAT: ("floatbits", "<I"), T_DOUBLE: ("doublebits", "<Q"), T_TIMESPAN: ("timespan", "<q"),
              T_CORR: ("corr", "<q")}
     if t in fixed:
         kind, f = fixed[t]
@@ -333,7 +336,12 @@ def _read_value(r: _Reader, depth: int = 0):
 
 def parse_headers(hdr: bytes) -> Dict[int, tuple]:
     """DeserializeMessageHeaders (:1773-1831): intro token, int32 count, count x (byte key, value);
-    Dictionary.Add throws on a duplicate key."""
+    Dictionary.Add throws on a duplicate key.  Bytes after the dictionary are not read."""
+    return parse_headers_end(hdr)[0]
+
+
+def parse_headers_end(hdr: bytes):
+    """parse_headers + the offset one past the dictionary's last byte."""
     r = _Reader(hdr)
     if r.u8() != T_DICT:
         raise DecodeError(DEC_MALFORMED, "introductory token is not StringObjDict")
@@ -347,7 +355,7 @@ def parse_headers(hdr: bytes) -> Dict[int, tuple]:
         if k in out:
             raise DecodeError(DEC_MALFORMED, "duplicate header key")
         out[k] = v
-    return out
+    return out, r.p
 
 
 @dataclass
@@ -426,4 +434,149 @@ def decode_frames(buf: bytes, offsets: Sequence[int], silo_index: Dict[SiloAddr,
             out.append(Decoded(DEC_MALFORMED))
             continue
         out.append(decode_for_route(buf[off + 8:off + 8 + hl], silo_index, sender_override))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# emit: SetTargetPlacement on a received header dictionary, re-serialized
+# ---------------------------------------------------------------------------------------
+H_NEW_GRAIN_TYPE = 11
+H_IS_NEW_PLACEMENT = 21
+H_PRIOR_MESSAGE_ID = 28
+H_PRIOR_MESSAGE_TIMES = 29
+
+STAMP_OK = 0          # SetTargetPlacement applied
+STAMP_COMPLETE = 1    # TargetAddress already complete: frame copied unchanged (Dispatcher.cs:557-558)
+STAMP_SKIPPED = 2     # route status other than HIT / NEW_PLACEMENT: copied unchanged, host path
+STAMP_UNSUPPORTED = 3 # header not decodable on the device, or not byte-canonical (a non-UTF-8 string), or no grain type
+STAMP_MALFORMED = 4   # the reference throws (undecodable header, or a present non-ActivationId TARGET_ACTIVATION)
+
+
+class NetDictionary:
+    """System.Collections.Generic.Dictionary<K,V> insertion / removal order as .NET Framework 4.5 keeps it:
+    entries array in insertion order; Remove pushes the entry on a LIFO free list; Add takes the free list head
+    (or appends); enumeration walks the entries array skipping free entries."""
+
+    def __init__(self, items):
+        self.entries = [[k, v] for k, v in items]
+        self.free = []                 # stack of free entry indices
+
+    def index(self, k):
+        for i, e in enumerate(self.entries):
+            if e is not None and e[0] == k:
+                return i
+        return -1
+
+    def contains(self, k):
+        return self.index(k) >= 0
+
+    def get(self, k):
+        i = self.index(k)
+        return None if i < 0 else self.entries[i][1]
+
+    def remove(self, k):
+        i = self.index(k)
+        if i >= 0:
+            self.entries[i] = None
+            self.free.append(i)
+
+    def set(self, k, v):               # headers[tag] = value
+        i = self.index(k)
+        if i >= 0:
+            self.entries[i][1] = v
+        elif self.free:
+            self.entries[self.free.pop()] = [k, v]
+        else:
+            self.entries.append([k, v])
+
+    def items(self):
+        return [(e[0], e[1]) for e in self.entries if e is not None]
+
+
+def _strict_canonical(dict_bytes: bytes, parsed) -> bool:
+    """Byte-exact canonicality of the dictionary: re-serializing the parsed values gives its bytes back (false
+    for a string or KeyExt that is not strict UTF-8: .NET decodes it with U+FFFD and re-encodes that)."""
+    return serialize_headers([(k, _writer_form(v)) for k, v in parsed.items()]) == dict_bytes
+
+
+def _writer_form(v):
+    if v[0] == "grain":
+        return ("grain", v[1])
+    if v[0] == "list":
+        return ("list", [_writer_form(x) for x in v[1]])
+    return v
+
+
+def stamp_frame(frame_hdr: bytes, body: bytes, route: int, act_key: Optional[Key], new_act_key: Optional[Key],
+                silo_addr_of: Dict[int, SiloAddr], grain_type_of: Dict[int, str]):
+    """One outgoing frame after routing -> (status, frame bytes).  Message.SetTargetPlacement
+    (Message.cs:1079-1096) with PlacementResult (Orleans/Placement/PlacementResult.cs:45-72): HIT ->
+    IdentifySelection(activation, host silo); NEW_PLACEMENT -> SpecifyCreation(host silo, grain type of the
+    target's type code) with the caller's new ActivationId.  Every other status leaves the frame unchanged."""
+    st_route = (route >> 16) & 0xFF
+    host = (route >> 8) & 0xFF
+    unchanged = struct.pack("<ii", len(frame_hdr), len(body)) + frame_hdr + body
+    try:
+        parsed, dict_end = parse_headers_end(frame_hdr)
+    except DecodeError as e:
+        return (STAMP_UNSUPPORTED if e.status == DEC_UNSUPPORTED else STAMP_MALFORMED), unchanged
+    if st_route == 3:  # ST_ADDRESS_COMPLETE
+        return STAMP_COMPLETE, unchanged
+    if st_route not in (0, 1):
+        return STAMP_SKIPPED, unchanged
+    if not _strict_canonical(frame_hdr[:dict_end], parsed):  # bytes after the dictionary are dropped, as
+        return STAMP_UNSUPPORTED, unchanged                   # SerializeMessageHeaders writes the dictionary only
+    new_placement = st_route == 1
+    if host not in silo_addr_of:
+        return STAMP_UNSUPPORTED, unchanged
+    activation = new_act_key if new_placement else act_key
+    d = NetDictionary(parsed.items())
+    grain_type = None
+    if new_placement:
+        tg = d.get(H_TARGET_GRAIN)
+        type_code = (tg[1].tcd & 0xFFFFFFFF) if tg is not None and tg[0] == "grain" else None
+        if type_code is None or type_code not in grain_type_of:
+            return STAMP_UNSUPPORTED, unchanged
+        grain_type = grain_type_of[type_code]
+        if new_act_key is None:
+            return STAMP_UNSUPPORTED, unchanged
+    elif act_key is None:
+        return STAMP_UNSUPPORTED, unchanged
+    if d.contains(H_TARGET_ACTIVATION):
+        cur = d.get(H_TARGET_ACTIVATION)
+        if cur[0] != "act":
+            return STAMP_MALFORMED, unchanged  # null.Equals(...) in SetTargetPlacement
+        differs = cur[1] != activation
+    else:
+        differs = False
+    if new_placement or differs:
+        d.remove(H_PRIOR_MESSAGE_ID)
+        d.remove(H_PRIOR_MESSAGE_TIMES)
+    d.set(H_TARGET_ACTIVATION, ("act", activation))
+    d.set(H_TARGET_SILO, ("silo", silo_addr_of[host]))
+    if new_placement:
+        d.set(H_IS_NEW_PLACEMENT, ("bool", True))
+        d.set(H_NEW_GRAIN_TYPE, ("string", grain_type))
+    hdr = serialize_headers([(k, _writer_form(v)) for k, v in d.items()])
+    return STAMP_OK, struct.pack("<ii", len(hdr), len(body)) + hdr + body
+
+
+def stamp_frames(buf: bytes, offsets: Sequence[int], routes, acts, act_keys: Sequence[Key], new_act_keys,
+                 silo_addr_of: Dict[int, SiloAddr], grain_type_of: Dict[int, str]):
+    """orl_stamp_frames_device: per frame (status, output bytes); an invalid prefix emits nothing (MALFORMED)."""
+    out = []
+    for i, off in enumerate(offsets):
+        if off + LENGTH_HEADER_SIZE > len(buf):
+            out.append((STAMP_MALFORMED, b""))
+            continue
+        hl, bl = struct.unpack("<ii", buf[off:off + 8])
+        if hl < 0 or bl < 0 or off + 8 + hl + bl > len(buf):
+            out.append((STAMP_MALFORMED, b""))
+            continue
+        hdr = buf[off + 8:off + 8 + hl]
+        body = buf[off + 8 + hl:off + 8 + hl + bl]
+        a = int(acts[i])
+        ak = act_keys[a] if a < len(act_keys) else None
+        nk = new_act_keys[i] if new_act_keys is not None else None
+        out.append(stamp_frame(hdr, body, int(routes[i]), ak, nk, silo_addr_of, grain_type_of))
     return out

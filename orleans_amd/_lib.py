@@ -53,6 +53,8 @@ OUTQ_LOOPBACK, OUTQ_PING, OUTQ_SYSTEM, OUTQ_REJECT, OUTQ_OVERFLOW, OUTQ_UNKNOWN_
     0xFFFFFFF0, 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3, 0xFFFFFFF4, 0xFFFFFFF5)
 DEC_OK, DEC_UNSUPPORTED, DEC_MALFORMED, DEC_UNKNOWN_SILO, DEC_NO_TARGET, DEC_NO_SENDER = 0, 1, 2, 3, 4, 5
 SENDER_FROM_HEADER = 0xFF
+STAMP_OK, STAMP_COMPLETE, STAMP_SKIPPED, STAMP_UNSUPPORTED, STAMP_MALFORMED, STAMP_OVERFLOW = 0, 1, 2, 3, 4, 5
+STAMP_MAX_GROWTH = 72
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -118,6 +120,9 @@ _SIGS = {
     "orl_client_buckets_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P]),
     "orl_silo_address_set": (C.c_int, [_P, C.c_uint32, _P, C.c_int32, C.c_int32]),
     "orl_decode_frames_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
+    "orl_grain_type_set": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_size_t]),
+    "orl_stamp_frames_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_size_t, _P, _P, _P, C.c_uint32, _P, _P, C.c_uint64,
+                                          _P, _P, _P, _P]),
     "orl_cache_config": (C.c_int, [_P, C.c_uint64]),
     "orl_cache_clear": (C.c_int, [_P]),
     "orl_cache_add_or_update_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),

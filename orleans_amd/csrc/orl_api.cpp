@@ -218,6 +218,15 @@ struct orl_ctx {
     bool silo_addr_dirty = true;
     SiloAddrEntry* d_silo_tab = nullptr;
     uint32_t* d_decode_flag = nullptr;
+    uint32_t* d_silo_words = nullptr;  // [256][6] serialized SiloAddress by silo index (stamp)
+    // f2 emit: grain class names by type code, and the stamp's scratch
+    std::map<int32_t, std::string> grain_types;
+    bool gt_dirty = true;
+    GrainTypeEntry* d_gt = nullptr;
+    uint8_t* d_gt_blob = nullptr;
+    uint64_t* d_stamp_sizes = nullptr;
+    void* d_stamp_temp = nullptr;
+    size_t stamp_cap = 0, stamp_temp_bytes = 0;
     // timing: 4 events per recorded batch (call begin, route begin, route end, call end)
     bool timing = false;
     std::vector<hipEvent_t> tev;
@@ -333,7 +342,21 @@ int sync_device_state(orl_ctx* c) {
             tab[i].silo = s;
         }
         ORL_HIP(c, hipMemcpy(c->d_silo_tab, tab, sizeof tab, hipMemcpyHostToDevice));
+        ORL_HIP(c, hipMemcpy(c->d_silo_words, c->silo_addr, sizeof c->silo_addr, hipMemcpyHostToDevice));
         c->silo_addr_dirty = false;
+    }
+    if (c->gt_dirty) {
+        std::vector<GrainTypeEntry> tab(kGrainTypeSlots, GrainTypeEntry{0, 0, 0, 0});
+        std::vector<uint8_t> blob;
+        for (const auto& kv : c->grain_types) {
+            uint32_t i = fmix32((uint32_t)kv.first) & (kGrainTypeSlots - 1);
+            while (tab[i].used) i = (i + 1) & (kGrainTypeSlots - 1);
+            tab[i] = GrainTypeEntry{kv.first, (uint32_t)blob.size(), (uint32_t)kv.second.size(), 1};
+            blob.insert(blob.end(), kv.second.begin(), kv.second.end());
+        }
+        ORL_HIP(c, hipMemcpy(c->d_gt, tab.data(), tab.size() * sizeof(GrainTypeEntry), hipMemcpyHostToDevice));
+        if (!blob.empty()) ORL_HIP(c, hipMemcpy(c->d_gt_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+        c->gt_dirty = false;
     }
     if (c->dir_dirty) {
         if (c->count == 0 && c->tombs == 0)  // an empty partition: no 32 B/slot upload
@@ -428,7 +451,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag);
+    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -489,6 +512,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_silo_tab, kSiloAddrSlots * sizeof(SiloAddrEntry))) != hipSuccess)
             return bail(e, "hipMalloc(silo addresses)");
         if ((e = hipMalloc((void**)&c->d_decode_flag, 4)) != hipSuccess) return bail(e, "hipMalloc(decode flag)");
+        if ((e = hipMalloc((void**)&c->d_silo_words, 256 * 24)) != hipSuccess) return bail(e, "hipMalloc(silo words)");
+        if ((e = hipMalloc((void**)&c->d_gt, kGrainTypeSlots * sizeof(GrainTypeEntry))) != hipSuccess)
+            return bail(e, "hipMalloc(grain types)");
+        if ((e = hipMalloc((void**)&c->d_gt_blob, kGrainTypeBlob)) != hipSuccess) return bail(e, "hipMalloc(grain type names)");
         if ((e = hipMalloc((void**)&c->d_dirstate, 32)) != hipSuccess) return bail(e, "hipMalloc(dirstate)");
         if ((e = hipMemset(c->d_dirstate, 0, 32)) != hipSuccess) return bail(e, "hipMemset(dirstate)");
         if ((e = hipMalloc((void**)&c->d_params, sizeof(RouteParams))) != hipSuccess) return bail(e, "hipMalloc(params)");
@@ -1241,6 +1268,55 @@ int orl_decode_frames_device(orl_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     int e = launch_decode_frames(d_bytes, nbytes, d_frame_offsets, n, sender_override, c->d_silo_tab, d_out, d_status,
                                  d_n_bad, c->d_decode_flag, stream ? stream : c->stream);
     if (e) return hipfail(c, (hipError_t)e, "decode frames launch");
+    return ORL_OK;
+}
+
+int orl_grain_type_set(orl_ctx* c, int32_t type_code, const char* utf8, size_t len) {
+    if (!c) return ORL_E_INVALID;
+    if (len == 0 || !utf8) {
+        c->grain_types.erase(type_code);
+        c->gt_dirty = true;
+        return ORL_OK;
+    }
+    size_t total = len;
+    for (const auto& kv : c->grain_types)
+        if (kv.first != type_code) total += kv.second.size();
+    if (total > kGrainTypeBlob) return fail(c, ORL_E_CAPACITY, "grain type names exceed %u bytes", kGrainTypeBlob);
+    if (c->grain_types.size() >= kGrainTypeSlots / 2 && !c->grain_types.count(type_code))
+        return fail(c, ORL_E_CAPACITY, "more than %u grain types", kGrainTypeSlots / 2);
+    c->grain_types[type_code] = std::string(utf8, len);
+    c->gt_dirty = true;
+    return ORL_OK;
+}
+
+int orl_stamp_frames_device(orl_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_frame_offsets, size_t n,
+                            const uint32_t* d_route, const uint32_t* d_act, const orl_grain_key* d_act_keys, uint32_t n_act_keys,
+                            const orl_grain_key* d_new_act_keys, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_offsets,
+                            uint64_t* d_out_total, uint8_t* d_status, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!d_out_total) return fail(c, ORL_E_INVALID, "null total pointer");
+    if (n && (!d_bytes || !d_frame_offsets || !d_route || !d_act || !d_out || !d_out_offsets || !d_status))
+        return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n_act_keys && !d_act_keys) return fail(c, ORL_E_INVALID, "null activation key table");
+    if (((uintptr_t)d_bytes & 3u) || ((uintptr_t)d_out & 3u)) return fail(c, ORL_E_INVALID, "frame buffers must be 4-byte aligned");
+    if (n > 0xFFFFFFFFull) return fail(c, ORL_E_CAPACITY, "batch too large");
+    if (int r = sync_device_state(c)) return r;
+    if (n > c->stamp_cap) {  // scratch grows to the largest batch seen (a synchronising allocation, once)
+        if (c->d_stamp_sizes) (void)hipFree(c->d_stamp_sizes);
+        if (c->d_stamp_temp) (void)hipFree(c->d_stamp_temp);
+        c->d_stamp_sizes = nullptr;
+        c->d_stamp_temp = nullptr;
+        c->stamp_cap = 0;
+        const size_t tb = stamp_scan_temp_bytes(n);
+        ORL_HIP(c, hipMalloc((void**)&c->d_stamp_sizes, n * sizeof(uint64_t)));
+        ORL_HIP(c, hipMalloc(&c->d_stamp_temp, std::max<size_t>(tb, 16)));
+        c->stamp_cap = n;
+        c->stamp_temp_bytes = std::max<size_t>(tb, 16);
+    }
+    int e = launch_stamp_frames(d_bytes, nbytes, d_frame_offsets, n, d_route, d_act, d_act_keys, n_act_keys, d_new_act_keys,
+                                c->d_gt, c->d_gt_blob, c->d_silo_words, c->d_stamp_sizes, c->d_stamp_temp, c->stamp_temp_bytes,
+                                d_out, out_cap, d_out_offsets, d_out_total, d_status, stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "stamp frames launch");
     return ORL_OK;
 }
 

@@ -91,6 +91,14 @@ __host__ __device__ inline uint32_t silo_addr_slot(const uint32_t w[6]) {
     return fmix32(h) & (kSiloAddrSlots - 1u);
 }
 
+// ---- f2 emit: grain class name per type code (PlacementResult.GrainType for new placements) ---------------
+constexpr uint32_t kGrainTypeSlots = 1024;
+constexpr uint32_t kGrainTypeBlob = 1u << 16;
+struct GrainTypeEntry {
+    int32_t code;
+    uint32_t off, len, used;
+};
+
 // ---- everything a route launch needs besides the messages (device copy, staged into LDS) ------------
 struct alignas(16) RouteParams {
     int32_t ring_hash[ORL_MAX_RING];   // membershipRingList, ascending signed hash
@@ -245,6 +253,14 @@ int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_bucket
 int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
                          uint32_t sender_override, const SiloAddrEntry* d_silo_tab, orl_msg_hdr* d_out,
                          uint8_t* d_status, uint32_t* d_n_bad, uint32_t* d_flag, void* stream);
+// f2 emit (wire_codec.hip): SetTargetPlacement on routed frames.  d_sizes: n u64 of scratch; d_temp: the scan's
+// temporary storage of stamp_scan_temp_bytes(n) bytes.
+int launch_stamp_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n, const uint32_t* d_route,
+                        const uint32_t* d_act, const orl_grain_key* d_act_keys, uint32_t n_act_keys,
+                        const orl_grain_key* d_new_act_keys, const GrainTypeEntry* d_gt, const uint8_t* d_gt_blob,
+                        const uint32_t* d_silo_words, uint64_t* d_sizes, void* d_temp, size_t temp_bytes, uint8_t* d_out,
+                        uint64_t out_cap, uint64_t* d_out_offsets, uint64_t* d_out_total, uint8_t* d_status, void* stream);
+size_t stamp_scan_temp_bytes(size_t n);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,

@@ -15,6 +15,8 @@
 // Large batches stage every frame's header window in LDS first (k_decode_frames_pipe).  Byte/integer work only.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "orl_internal.h"
 
 namespace orl {
@@ -144,8 +146,8 @@ __device__ uint32_t jenkins_stream(const S& w, typename S::P p, uint32_t len) {
 }
 
 // ReadUniqueKey (:424-431) + UniqueKey.ValidateKeyExt (UniqueKey.cs:328-350).  Advances p; returns a status.
-template <class S>
-__device__ __forceinline__ uint32_t skip_unique_key(const S& w, typename S::P end, typename S::P& p) {
+template <bool CANON = false, class S>
+__device__ __forceinline__ uint32_t skip_unique_key(const S& w, typename S::P end, typename S::P& p, bool* noncanon = nullptr) {
     if (p + 28 > end) return ORL_DEC_MALFORMED;
     const uint32_t cat = ld32(w, p + 20) >> 24;  // top byte of TypeCodeData
     const int32_t len = (int32_t)ld32(w, p + 24);
@@ -154,6 +156,7 @@ __device__ __forceinline__ uint32_t skip_unique_key(const S& w, typename S::P en
     if (len < 0 || p + (typename S::P)len > end) return ORL_DEC_MALFORMED;
     if (cat != 6u) return ORL_DEC_MALFORMED;                             // extension on a non-KeyExt key
     if (all_whitespace(w, p, (typename S::P)len)) return ORL_DEC_MALFORMED;
+    if (CANON && !strict_utf8(w, p, (typename S::P)len)) *noncanon = true;
     p += (typename S::P)len;
     return ORL_DEC_OK;
 }
@@ -165,8 +168,10 @@ __device__ __forceinline__ bool port_ok(const S& w, typename S::P p) {
 
 // One header value (DeserializeMessageHeaderHelper :1833-1853), starting at its token.  Lists are flattened
 // with a pending-value counter (a list only adds values), so nesting depth costs no state.
-template <class S>
-__device__ uint32_t skip_value(const S& w, typename S::P end, typename S::P& p) {
+// CANON (the stamp path): also flag, in *noncanon, a string or KeyExt that is not strict UTF-8 — re-serializing it
+// would not give its bytes back.
+template <bool CANON = false, class S>
+__device__ uint32_t skip_value(const S& w, typename S::P end, typename S::P& p, bool* noncanon = nullptr) {
     uint64_t pending = 1;
     while (pending) {
         --pending;
@@ -214,18 +219,19 @@ __device__ uint32_t skip_value(const S& w, typename S::P end, typename S::P& p) 
             const int32_t len = (int32_t)ld32(w, p);
             if (len < -1) return ORL_DEC_MALFORMED;
             sz = 4 + (len > 0 ? (typename S::P)len : 0);
+            if (CANON && len > 0 && p + sz <= end && !strict_utf8(w, p + 4, (typename S::P)len)) *noncanon = true;
             break;
         }
         case T_GRAIN: case T_ACT: {
-            const uint32_t st = skip_unique_key(w, end, p);
+            const uint32_t st = skip_unique_key<CANON>(w, end, p, noncanon);
             if (st) return st;
             continue;
         }
         case T_ACTADDR: {
             if (p + 24 > end || !port_ok(w, p + 16)) return ORL_DEC_MALFORMED;
             p += 24;
-            uint32_t st = skip_unique_key(w, end, p);
-            if (!st) st = skip_unique_key(w, end, p);
+            uint32_t st = skip_unique_key<CANON>(w, end, p, noncanon);
+            if (!st) st = skip_unique_key<CANON>(w, end, p, noncanon);
             if (st) return st;
             continue;
         }
@@ -293,12 +299,13 @@ __device__ uint32_t token_class(uint32_t t) {
 // One header value whose token (class cls) sits at p - 1: the common-case form of skip_value, branch-free except
 // for the rare classes.  The speculative reads (a length at +0 or +24, a port at +16, a DateTime at +0) are
 // issued together at positions clamped into the header, and only the ones the class needs are used.
-template <class S>
-__device__ __forceinline__ uint32_t skip_value_fast(const S& w, typename S::P end, uint32_t cls, typename S::P& p) {
+template <bool CANON = false, class S>
+__device__ __forceinline__ uint32_t skip_value_fast(const S& w, typename S::P end, uint32_t cls, typename S::P& p,
+                                                    bool* noncanon = nullptr) {
     using P = typename S::P;
     if (cls & CLS_SLOW) {
         p -= 1;
-        return skip_value(w, end, p);
+        return skip_value<CANON>(w, end, p, noncanon);
     }
     const P lim = end - 4;  // the header holds >= 4 bytes before p (intro + count), so lim >= 0
     auto at = [&](P q) { return q < lim ? q : lim; };
@@ -322,6 +329,7 @@ __device__ __forceinline__ uint32_t skip_value_fast(const S& w, typename S::P en
     uint32_t st = !fits ? ORL_DEC_MALFORMED : unsup ? ORL_DEC_UNSUPPORTED : (bad || !fits_all) ? ORL_DEC_MALFORMED : ORL_DEC_OK;
     // KeyExt grain: the extension must not be blank (UniqueKey.cs:328-345) — rare, so a branch
     if (!st && is_key && keyext && all_whitespace(w, p + 28, var)) st = ORL_DEC_MALFORMED;
+    if (CANON && !st && var > 0 && !strict_utf8(w, p + (is_key ? 28 : 4), var)) *noncanon = true;
     p += sz;
     return st;
 }
@@ -637,6 +645,309 @@ __global__ __launch_bounds__(256) void k_decode_frames_pipe(const uint32_t* __re
     }
 }
 
+// ---- f2 emit: SetTargetPlacement on routed frames (orl_stamp_frames_device) ----------------------------------
+// Message.SetTargetPlacement (Message.cs:1079-1096) on the header dictionary DeserializeMessageHeaders built
+// (entries in wire order, no free slots), then SerializeMessageHeaders: PRIOR_MESSAGE_ID / _TIMES removed on a new
+// placement or an activation change (Dictionary.Remove pushes the entry on a LIFO free list), TARGET_ACTIVATION
+// and TARGET_SILO set (an existing key keeps its position; a new key takes the free-list head, else is appended),
+// and on a new placement IS_NEW_PLACEMENT = true and NEW_GRAIN_TYPE.  The oracle is wire_codec.stamp_frame.
+enum : uint32_t { H_NEW_GRAIN_TYPE = 11, H_IS_NEW_PLACEMENT = 21, H_PRIOR_ID = 28, H_PRIOR_TIMES = 29 };
+enum : uint32_t { NE_KEEP = 0, NE_REMOVE = 1, NE_ACT = 2, NE_SILO = 3, NE_ISNEW = 4, NE_GTYPE = 5 };
+constexpr uint32_t kSpecials = 6;  // 28, 29, 22, 24, 21, 11
+
+struct StampPlan {
+    uint32_t st;
+    uint64_t hdr, end;      // header start / end (absolute)
+    uint64_t dict_end;      // one past the dictionary's last byte (bytes after it are not re-serialized)
+    uint64_t hl_new;        // new header length
+    int32_t count_new;
+    // the special entries present in the header: [start, end) of the whole entry (key byte .. value end)
+    uint64_t s_start[kSpecials], s_end[kSpecials];
+    uint32_t present;       // bit k: special k present
+    uint32_t kind[kSpecials];
+    uint32_t app;           // appended kinds, 4 bits each, first in the low nibble
+    uint32_t n_app;
+    uint64_t act_tcd, act_n0, act_n1;
+    uint32_t host, gt_off, gt_len;
+};
+
+__device__ __forceinline__ uint32_t special_index(uint32_t key) {
+    return key == H_PRIOR_ID ? 0u : key == H_PRIOR_TIMES ? 1u : key == H_TARGET_ACTIVATION ? 2u
+         : key == H_TARGET_SILO ? 3u : key == H_IS_NEW_PLACEMENT ? 4u : key == H_NEW_GRAIN_TYPE ? 5u : kSpecials;
+}
+
+__device__ __forceinline__ uint32_t new_entry_len(uint32_t kind, uint32_t gt_len) {
+    return kind == NE_ACT ? 30u : kind == NE_SILO ? 26u : kind == NE_ISNEW ? 2u : kind == NE_GTYPE ? 6u + gt_len : 0u;
+}
+
+__device__ bool grain_type_lookup(const GrainTypeEntry* __restrict__ gt, uint32_t code, uint32_t& off, uint32_t& len) {
+    uint32_t s = fmix32(code) & (kGrainTypeSlots - 1u);
+    for (uint32_t probe = 0; probe < kGrainTypeSlots; ++probe) {
+        const GrainTypeEntry e = gt[s];
+        if (!e.used) return false;
+        if ((uint32_t)e.code == code) { off = e.off; len = e.len; return true; }
+        s = (s + 1u) & (kGrainTypeSlots - 1u);
+    }
+    return false;
+}
+
+// Frame i -> plan.  Statuses in the order of wire_codec.stamp_frames.
+__device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbytes, uint64_t off, uint32_t route, uint32_t act,
+                                uint64_t i, const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
+                                const orl_grain_key* __restrict__ new_act_keys, const GrainTypeEntry* __restrict__ gt,
+                                const uint32_t* __restrict__ silo_words, const uint16_t* lut) {
+    StampPlan P;
+    P.st = ORL_STAMP_MALFORMED;
+    P.present = 0;
+    P.app = 0;
+    P.n_app = 0;
+    P.hdr = P.end = 0;
+    P.hl_new = 0;
+    P.count_new = 0;
+    if (!prefix_in_buffer(off, nbytes)) return P;
+    const GlobalSrc pre{buf, (off + 7) >> 2};
+    const int32_t hl = (int32_t)ld32(pre, off), bl = (int32_t)ld32(pre, off + 4);
+    if (!frame_ok(off, nbytes, hl, bl)) return P;
+    P.hdr = off + 8;
+    P.end = P.hdr + (uint64_t)hl;
+    P.hl_new = (uint64_t)hl;
+    const GlobalSrc w{buf, (P.end - 1) >> 2};
+    // structural parse (DeserializeMessageHeaders), recording the special entries
+    uint64_t p = P.hdr;
+    uint32_t st = ORL_DEC_OK;
+    bool noncanon = false;
+    uint32_t tok22 = 0;
+    uint64_t v22 = 0;
+    int32_t count = 0;
+    if (5 > P.end - p || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
+    if (!st) {
+        count = (int32_t)ld32(w, p + 1);
+        p += 5;
+        if (count < 0) st = ORL_DEC_MALFORMED;
+    }
+    uint32_t seen = 0;
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    for (int32_t e = 0; !st && e < count; ++e) {
+        if (2 > P.end - p) { st = ORL_DEC_MALFORMED; break; }
+        const uint64_t es = p;
+        const uint32_t key = ld8(w, p), tok = ld8(w, p + 1);
+        p += 2;
+        st = skip_value_fast<true>(w, P.end, lut[tok], p, &noncanon);
+        if (st) break;
+        bool dup;
+        if (key < 32u) {
+            dup = (seen >> key) & 1u;
+            seen |= 1u << key;
+        } else {
+            const uint32_t q = key >> 6;
+            const uint64_t bit = 1ull << (key & 63u);
+            dup = ((q == 0 ? h0 : q == 1 ? h1 : q == 2 ? h2 : h3) & bit) != 0;
+            h0 |= q == 0 ? bit : 0; h1 |= q == 1 ? bit : 0; h2 |= q == 2 ? bit : 0; h3 |= q == 3 ? bit : 0;
+        }
+        if (dup) { st = ORL_DEC_MALFORMED; break; }
+        const uint32_t k = special_index(key);
+        if (k < kSpecials) {
+            P.present |= 1u << k;
+            P.s_start[k] = es;
+            P.s_end[k] = p;
+            if (k == 2) { tok22 = tok; v22 = es + 2; }
+        }
+    }
+    if (st) {
+        P.st = st == ORL_DEC_UNSUPPORTED ? ORL_STAMP_UNSUPPORTED : ORL_STAMP_MALFORMED;
+        return P;
+    }
+    P.dict_end = p;
+    const uint32_t rst = (route >> 16) & 0xFFu;
+    if (rst == ORL_ST_ADDRESS_COMPLETE) { P.st = ORL_STAMP_COMPLETE; return P; }
+    if (rst != ORL_ST_HIT && rst != ORL_ST_NEW_PLACEMENT) { P.st = ORL_STAMP_SKIPPED; return P; }
+    if (noncanon) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
+    const bool np = rst == ORL_ST_NEW_PLACEMENT;
+    P.host = (route >> 8) & 0xFFu;
+    P.gt_off = P.gt_len = 0;
+    {   // the host silo's address must be known (orl_silo_address_set); SiloAddress.Zero never is a silo
+        uint32_t any = 0;
+        for (uint32_t k = 0; k < 6; ++k) any |= silo_words[P.host * 6 + k];
+        if (!any) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
+    }
+    if (np) {
+        // SpecifyCreation(silo, strategy, context.GetGrainTypeName(grain)): the target's type code
+        // (TARGET_GRAIN was parsed above; routing needs it, so it is a GrainId here)
+        uint32_t code = 0;
+        // find TARGET_GRAIN again: it is not a special entry; scan for it (rare path: new placements)
+        uint64_t q = P.hdr + 5;
+        bool found = false;
+        for (int32_t e = 0; e < count; ++e) {
+            const uint32_t key = ld8(w, q), tok = ld8(w, q + 1);
+            if (key == H_TARGET_GRAIN && tok == T_GRAIN) { code = ld32(w, q + 2 + 16); found = true; break; }
+            q += 2;
+            (void)skip_value_fast(w, P.end, lut[tok], q);
+        }
+        if (!found || !grain_type_lookup(gt, code, P.gt_off, P.gt_len)) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
+        if (!new_act_keys) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
+        const orl_grain_key a = new_act_keys[i];
+        P.act_tcd = a.type_code_data; P.act_n0 = a.n0; P.act_n1 = a.n1;
+    } else {
+        if (act >= n_act_keys) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
+        const orl_grain_key a = act_keys[act];
+        P.act_tcd = a.type_code_data; P.act_n0 = a.n0; P.act_n1 = a.n1;
+    }
+    bool differs = false;
+    if (P.present & 4u) {
+        if (tok22 != T_ACT) { P.st = ORL_STAMP_MALFORMED; return P; }  // null.Equals(...) in SetTargetPlacement
+        differs = ld64(w, v22) != P.act_n0 || ld64(w, v22 + 8) != P.act_n1 || ld64(w, v22 + 16) != P.act_tcd ||
+                  (int32_t)ld32(w, v22 + 24) != -1;
+    }
+    // the dictionary updates
+    for (uint32_t k = 0; k < kSpecials; ++k) P.kind[k] = NE_KEEP;
+    uint32_t fstack = 0, nfree = 0;  // free-list: entry indices 0 (PRIOR_ID) / 1 (PRIOR_TIMES), top = last pushed
+    int32_t cnt = count;
+    if (np || differs) {
+        if (P.present & 1u) { P.kind[0] = NE_REMOVE; fstack = (fstack << 2) | 0u; ++nfree; --cnt; }
+        if (P.present & 2u) { P.kind[1] = NE_REMOVE; fstack = (fstack << 2) | 1u; ++nfree; --cnt; }
+        // (the free list holds at most these two; its head is the last removed)
+    }
+    auto set = [&](uint32_t k, uint32_t kind) {
+        if (P.present & (1u << k)) { P.kind[k] = kind; return; }
+        ++cnt;
+        if (nfree) {
+            if ((fstack & 3u) == 0) P.kind[0] = kind;
+            else P.kind[1] = kind;
+            fstack >>= 2;
+            --nfree;
+            return;
+        }
+        P.app |= kind << (4u * P.n_app);
+        ++P.n_app;
+    };
+    set(2, NE_ACT);
+    set(3, NE_SILO);
+    if (np) {
+        set(4, NE_ISNEW);
+        set(5, NE_GTYPE);
+    }
+    // new header length
+    int64_t hl_new = (int64_t)(P.dict_end - P.hdr);
+    for (uint32_t k = 0; k < kSpecials; ++k)
+        if ((P.present >> k) & 1u && P.kind[k] != NE_KEEP)
+            hl_new += (int64_t)new_entry_len(P.kind[k], P.gt_len) - (int64_t)(P.s_end[k] - P.s_start[k]);
+    for (uint32_t a = 0; a < P.n_app; ++a) hl_new += new_entry_len((P.app >> (4u * a)) & 15u, P.gt_len);
+    P.hl_new = (uint64_t)hl_new;
+    P.count_new = cnt;
+    P.st = ORL_STAMP_OK;
+    return P;
+}
+
+// Output words of one frame.  The frame's output starts 4-byte aligned and owns its words up to its aligned end.
+struct WordWriter {
+    uint32_t* dst;
+    uint64_t acc = 0;
+    uint32_t nacc = 0;  // bytes pending in acc (0..3)
+    __device__ __forceinline__ void put32(uint32_t v) {
+        acc |= (uint64_t)v << (8u * nacc);
+        *dst++ = (uint32_t)acc;
+        acc >>= 32;
+    }
+    __device__ __forceinline__ void put8(uint32_t b) {
+        acc |= (uint64_t)(b & 0xFFu) << (8u * nacc);
+        if (++nacc == 4) { *dst++ = (uint32_t)acc; acc = 0; nacc = 0; }
+    }
+    __device__ __forceinline__ void put64(uint64_t v) { put32((uint32_t)v); put32((uint32_t)(v >> 32)); }
+    __device__ __forceinline__ void flush() { if (nacc) *dst++ = (uint32_t)acc; }
+    __device__ void copy(const GlobalSrc& s, uint64_t p, uint64_t len) {
+        for (; len >= 4; len -= 4, p += 4) put32(ld32(s, p));
+        for (; len; --len, ++p) put8(ld8(s, p));
+    }
+};
+
+__device__ void emit_entry(WordWriter& o, uint32_t kind, const StampPlan& P, const uint32_t* __restrict__ silo_words,
+                           const uint8_t* __restrict__ gt_blob) {
+    switch (kind) {
+    case NE_ACT:
+        o.put8(H_TARGET_ACTIVATION); o.put8(T_ACT);
+        o.put64(P.act_n0); o.put64(P.act_n1); o.put64(P.act_tcd); o.put32(0xFFFFFFFFu);
+        break;
+    case NE_SILO:
+        o.put8(H_TARGET_SILO); o.put8(T_SILO);
+        for (uint32_t k = 0; k < 6; ++k) o.put32(silo_words[P.host * 6 + k]);
+        break;
+    case NE_ISNEW:
+        o.put8(H_IS_NEW_PLACEMENT); o.put8(T_TRUE);
+        break;
+    case NE_GTYPE:
+        o.put8(H_NEW_GRAIN_TYPE); o.put8(T_STRING); o.put32(P.gt_len);
+        for (uint32_t k = 0; k < P.gt_len; ++k) o.put8(gt_blob[P.gt_off + k]);
+        break;
+    default: break;
+    }
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_stamp(const uint32_t* __restrict__ buf, uint64_t nbytes, const uint64_t* __restrict__ offs,
+                                               uint32_t n, const uint32_t* __restrict__ route, const uint32_t* __restrict__ act,
+                                               const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
+                                               const orl_grain_key* __restrict__ new_act_keys, const GrainTypeEntry* __restrict__ gt,
+                                               const uint8_t* __restrict__ gt_blob, const uint32_t* __restrict__ silo_words,
+                                               uint64_t* __restrict__ sizes, const uint64_t* __restrict__ out_offs,
+                                               uint32_t* __restrict__ out, uint64_t out_cap, uint8_t* __restrict__ status) {
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t off = offs[i];
+    const StampPlan P = stamp_plan(buf, nbytes, off, route[i], act[i], i, act_keys, n_act_keys, new_act_keys, gt, silo_words, lut);
+    const uint64_t bl = P.end ? (uint64_t)ld32(GlobalSrc{buf, (off + 7) >> 2}, off + 4) : 0;
+    const uint64_t size = P.end == 0 ? 0 : 8 + (P.st == ORL_STAMP_OK ? P.hl_new : P.end - P.hdr) + bl;
+    if (!WRITE) {
+        sizes[i] = (size + 3) & ~3ull;
+        return;
+    }
+    uint32_t st = P.st;
+    const uint64_t o = out_offs[i], asz = (size + 3) & ~3ull;
+    if (size && (o > out_cap || asz > out_cap - o)) st = ORL_STAMP_OVERFLOW;
+    status[i] = (uint8_t)st;
+    if (size == 0 || st == ORL_STAMP_OVERFLOW) return;
+    const GlobalSrc g{buf, (P.end + bl + 3) / 4 - 1};
+    WordWriter wr{out + o / 4};
+    if (P.st != ORL_STAMP_OK) {  // unchanged copy
+        wr.copy(g, off, size);
+        wr.flush();
+        return;
+    }
+    wr.put32((uint32_t)P.hl_new);
+    wr.put32((uint32_t)bl);
+    wr.put8(T_DICT);
+    wr.put32((uint32_t)P.count_new);
+    // original entries in order, the special ones replaced / removed
+    uint64_t pos = P.hdr + 5;
+    while (true) {  // the next special entry at or after pos (selects only: no dynamic indexing)
+        uint64_t ns = ~0ull, ne = 0;
+        uint32_t nkind = NE_KEEP;
+#pragma unroll
+        for (uint32_t k = 0; k < kSpecials; ++k) {
+            const bool take = ((P.present >> k) & 1u) && P.s_start[k] >= pos && P.s_start[k] < ns;
+            ns = take ? P.s_start[k] : ns;
+            ne = take ? P.s_end[k] : ne;
+            nkind = take ? P.kind[k] : nkind;
+        }
+        if (ns == ~0ull) break;
+        wr.copy(g, pos, ns - pos);
+        if (nkind == NE_KEEP) wr.copy(g, ns, ne - ns);
+        else emit_entry(wr, nkind, P, silo_words, gt_blob);
+        pos = ne;
+    }
+    wr.copy(g, pos, P.dict_end - pos);
+    for (uint32_t a = 0; a < P.n_app; ++a) emit_entry(wr, (P.app >> (4u * a)) & 15u, P, silo_words, gt_blob);
+    wr.copy(g, P.end, bl);
+    wr.flush();
+}
+
+__global__ void k_stamp_total(const uint64_t* __restrict__ sizes, const uint64_t* __restrict__ offs, uint32_t n,
+                              uint64_t* __restrict__ total) {
+    *total = n ? offs[n - 1] + sizes[n - 1] : 0;
+}
+
 }  // namespace
 
 int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n,
@@ -666,6 +977,39 @@ int launch_decode_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t
                            (uint32_t)n, sender_override, d_silo_tab, (uint4*)d_out, d_status, d_n_bad);
     }
     return (int)hipGetLastError();
+}
+
+}  // namespace orl
+
+namespace orl {
+
+int launch_stamp_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_offsets, size_t n, const uint32_t* d_route,
+                        const uint32_t* d_act, const orl_grain_key* d_act_keys, uint32_t n_act_keys,
+                        const orl_grain_key* d_new_act_keys, const GrainTypeEntry* d_gt, const uint8_t* d_gt_blob,
+                        const uint32_t* d_silo_words, uint64_t* d_sizes, void* d_temp, size_t temp_bytes, uint8_t* d_out,
+                        uint64_t out_cap, uint64_t* d_out_offsets, uint64_t* d_out_total, uint8_t* d_status, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return (int)hipMemsetAsync(d_out_total, 0, sizeof(uint64_t), st);
+    const dim3 grid((uint32_t)((n + 255) / 256));
+    hipLaunchKernelGGL(k_stamp<false>, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets, (uint32_t)n, d_route,
+                       d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                       (const uint64_t*)nullptr, (uint32_t*)nullptr, out_cap, d_status);
+    size_t tb = temp_bytes;
+    hipError_t e = rocprim::exclusive_scan(d_temp, tb, d_sizes, d_out_offsets, (uint64_t)0, n, rocprim::plus<uint64_t>(), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_stamp_total, dim3(1), dim3(1), 0, st, (const uint64_t*)d_sizes, (const uint64_t*)d_out_offsets,
+                       (uint32_t)n, d_out_total);
+    hipLaunchKernelGGL(k_stamp<true>, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets, (uint32_t)n, d_route,
+                       d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                       (const uint64_t*)d_out_offsets, (uint32_t*)d_out, out_cap, d_status);
+    return (int)hipGetLastError();
+}
+
+size_t stamp_scan_temp_bytes(size_t n) {
+    size_t tb = 0;
+    (void)rocprim::exclusive_scan(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, n,
+                                  rocprim::plus<uint64_t>(), (hipStream_t)0);
+    return tb;
 }
 
 }  // namespace orl

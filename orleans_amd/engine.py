@@ -442,6 +442,21 @@ class GrainDirectoryEngine:
                                                     int(sender_override), ptr(d_out), ptr(d_status), ptr(d_n_bad),
                                                     ptr(stream)))
 
+    def set_grain_type(self, type_code: int, class_name: Optional[str]) -> None:
+        """Grain class name of a type code (PlacementResult.GrainType of new placements); None removes it."""
+        b = b"" if class_name is None else class_name.encode("utf-8")
+        self._ck(self._lib.orl_grain_type_set(self._ctx, C.c_int32(int(type_code) & 0xFFFFFFFF).value, b, len(b)))
+
+    def stamp_frames_device(self, d_bytes, nbytes: int, d_offsets, n: int, d_route, d_act, d_act_keys, n_act_keys: int,
+                            d_new_act_keys, d_out, out_cap: int, d_out_offsets, d_out_total, d_status,
+                            stream=None) -> None:
+        """Routed frames re-serialized with Message.SetTargetPlacement applied (device buffers; one ORL_STAMP_*
+        status byte per frame; output frame i at d_out_offsets[i], 4-byte aligned)."""
+        self._ck(self._lib.orl_stamp_frames_device(self._ctx, ptr(d_bytes), int(nbytes), ptr(d_offsets), int(n), ptr(d_route),
+                                                   ptr(d_act), ptr(d_act_keys), int(n_act_keys), ptr(d_new_act_keys),
+                                                   ptr(d_out), int(out_cap), ptr(d_out_offsets), ptr(d_out_total),
+                                                   ptr(d_status), ptr(stream)))
+
     def compact_directory(self) -> None:
         """Rebuild the partition without tombstones."""
         self._ck(self._lib.orl_dir_compact(self._ctx))

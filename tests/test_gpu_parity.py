@@ -903,3 +903,104 @@ def test_decode_generator_frames_then_route(torch):
     np.testing.assert_array_equal(d_a.cpu().numpy().view(np.uint32), ref.act)
     assert ((ref.route >> 16) & 0xFF == L.ST_ADDRESS_COMPLETE).sum() > 10_000
     eng.close()
+
+
+def test_stamp_frames_vs_oracle(torch):
+    """f2 emit: routed frames re-serialized with Message.SetTargetPlacement applied (.NET Dictionary slot reuse,
+    PRIOR_MESSAGE_* removal, IS_NEW_PLACEMENT / NEW_GRAIN_TYPE on new placements, unchanged copies with a status
+    for everything else), byte-exact against oracle/wire_codec.stamp_frames: random typed headers, the rule
+    corpus, random mutations and generator frames, at every start alignment; output offsets = the scan of the
+    4-byte-aligned output sizes; the out_cap overflow rule."""
+    import random
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import wire_corpus as C
+    from oracle import wire_codec as WC
+    from oracle.pyref import Key
+    t = torch
+    rng = random.Random(31)
+    eng = GrainDirectoryEngine(n_act=16, dir_capacity=16, max_batch=1024, device=0)
+    eng.set_silos(8)
+    for s in range(8):
+        eng.set_silo_address(s, *C.silo_addr(s))
+    typed = C.typed_corpus(3000, seed=41)
+    cl = W.balanced_cluster()
+    gbuf, goffs, _ = W.request_frames(cl, 1000, 1500, seed=5, complete_frac=0.3, keyext_frac=0.1)
+    gen = [bytes(gbuf[int(o):int(goffs[k + 1]) if k + 1 < len(goffs) else len(gbuf)]) for k, o in enumerate(goffs)]
+    gen = [g[:8 + int.from_bytes(g[:4], "little") + int.from_bytes(g[4:8], "little")] for g in gen]
+    frames = C.edge_corpus() + typed + C.mutate(typed, 2000, seed=42) + gen
+    rng.shuffle(frames)
+    buf, offs, nbytes = C.pack(frames, seed=43)
+    n = len(frames)
+    # grain types for some target type codes
+    codes = set()
+    for f in frames:
+        try:
+            h = WC.parse_headers(f[8:8 + int.from_bytes(f[:4], "little", signed=True)])
+        except Exception:
+            continue
+        tg = h.get(WC.H_TARGET_GRAIN)
+        if tg is not None and tg[0] == "grain":
+            codes.add(tg[1].tcd & 0xFFFFFFFF)
+    codes = sorted(codes)
+    rng.shuffle(codes)
+    grain_types = {c: "Grains.Type%d.%s" % (c, "é" * (c % 3)) for c in codes[:400]}
+    for c, name in grain_types.items():
+        eng.set_grain_type(c, name)
+    statuses = [0, 0, 0, 1, 1, 3, 8, 2]
+    route = np.array([(rng.choice(statuses) << 16) | (rng.randrange(10) << 8) for _ in range(n)], np.uint32)
+    n_keys = 500
+    act = np.array([rng.randrange(n_keys + 20) for _ in range(n)], np.uint32)
+    act_keys = [Key(rng.choice([0, 3 << 56]), rng.getrandbits(64), rng.getrandbits(64), None) for _ in range(n_keys)]
+    new_keys = [Key(0, rng.getrandbits(64), rng.getrandbits(64), None) for _ in range(n)]
+    # a frame that already targets the activation it routes to (no PRIOR_MESSAGE_* removal)
+    kd = np.zeros(n_keys, L.KEY_DTYPE)
+    kd["tcd"], kd["n0"], kd["n1"] = [k.tcd for k in act_keys], [k.n0 for k in act_keys], [k.n1 for k in act_keys]
+    nd = np.zeros(n, L.KEY_DTYPE)
+    nd["tcd"], nd["n0"], nd["n1"] = [k.tcd for k in new_keys], [k.n0 for k in new_keys], [k.n1 for k in new_keys]
+    silo_of = {s: C.silo_addr(s) for s in range(8)}
+    ref = WC.stamp_frames(bytes(buf[:nbytes]), [int(o) for o in offs], route, act, act_keys, new_keys, silo_of, grain_types)
+    st_ref = np.array([r[0] for r in ref], np.uint8)
+    sizes = np.array([(len(r[1]) + 3) // 4 * 4 for r in ref], np.uint64)
+    off_ref = np.zeros(n, np.uint64)
+    off_ref[1:] = np.cumsum(sizes)[:-1]
+    total_ref = int(sizes.sum())
+    assert len(set(st_ref.tolist())) == 5, np.unique(st_ref, return_counts=True)
+
+    d_buf = t.from_numpy(buf).cuda()
+    d_off = t.from_numpy(offs.view(np.int64)).cuda()
+    d_route = t.from_numpy(route.view(np.int32)).cuda()
+    d_act = t.from_numpy(act.view(np.int32)).cuda()
+    d_keys = t.from_numpy(kd.view(np.uint8)).cuda()
+    d_new = t.from_numpy(nd.view(np.uint8)).cuda()
+    cap = int(nbytes) + n * (L.STAMP_MAX_GROWTH + 64)
+    d_out = t.zeros(cap, dtype=t.uint8, device="cuda")
+    d_ooff = t.empty(n, dtype=t.int64, device="cuda")
+    d_tot = t.empty(1, dtype=t.int64, device="cuda")
+    d_st = t.empty(n, dtype=t.uint8, device="cuda")
+    stream = t.cuda.current_stream().cuda_stream
+    eng.stamp_frames_device(d_buf, nbytes, d_off, n, d_route, d_act, d_keys, n_keys, d_new, d_out, cap, d_ooff, d_tot,
+                            d_st, stream=stream)
+    t.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    bad = np.nonzero(st != st_ref)[0]
+    assert len(bad) == 0, (bad[:8], st[bad[:8]], st_ref[bad[:8]])
+    np.testing.assert_array_equal(d_ooff.cpu().numpy().view(np.uint64), off_ref)
+    assert int(d_tot.cpu()[0]) == total_ref
+    out = d_out.cpu().numpy()
+    for i, (s_, b) in enumerate(ref):
+        o = int(off_ref[i])
+        assert bytes(out[o:o + len(b)]) == b, (i, s_)
+    assert (st_ref == WC.STAMP_OK).sum() > 1000
+    # out_cap too small: frames past it are not written (ORL_STAMP_OVERFLOW), earlier ones are
+    cap2 = int(off_ref[n // 2])
+    d_out2 = t.zeros(cap2 + 64, dtype=t.uint8, device="cuda")
+    eng.stamp_frames_device(d_buf, nbytes, d_off, n, d_route, d_act, d_keys, n_keys, d_new, d_out2, cap2, d_ooff, d_tot,
+                            d_st, stream=stream)
+    t.cuda.synchronize()
+    st2 = d_st.cpu().numpy()
+    fits = off_ref + sizes <= cap2
+    np.testing.assert_array_equal(st2[fits], st_ref[fits])
+    assert (st2[~fits & (sizes > 0)] == L.STAMP_OVERFLOW).all()
+    assert not d_out2[cap2:].any()
+    eng.close()

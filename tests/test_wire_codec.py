@@ -121,3 +121,75 @@ def test_generator_frames_decode_to_the_expected_headers(complete_frac, keyext_f
     if keyext_frac:
         assert any(d.flags & P.HDR_HASH_VALID for d in dec)
         assert any(d.flags & P.HDR_ADDRESS_COMPLETE for d in dec)
+
+
+# ---- emit: SetTargetPlacement + .NET Dictionary order --------------------------------------------------------
+def _route(status, host=4):
+    return (status << 16) | (host << 8)
+
+
+def _stamp_items(items, status, act_key, new_key=None, grain_types=None):
+    hdr = W.serialize_headers(items)
+    st, fr = W.stamp_frame(hdr, b"BODY", _route(status), act_key, new_key,
+                           {s: C.silo_addr(s) for s in range(8)}, grain_types or {})
+    if st != W.STAMP_OK:
+        return st, None
+    hl = struct.unpack("<i", fr[:4])[0]
+    assert fr[8 + hl:] == b"BODY"
+    return st, list(W.parse_headers(fr[8:8 + hl]).items())
+
+
+def test_stamp_new_placement_reuses_freed_slots_lifo():
+    tg = P.key_from_long(77, 1234)
+    items = [(W.H_CATEGORY, ("int", 2)), (W.H_PRIOR_MESSAGE_ID, ("corr", 5)), (W.H_TARGET_GRAIN, ("grain", tg)),
+             (W.H_PRIOR_MESSAGE_TIMES, ("int", 3)), (W.H_SENDING_SILO, ("silo", C.silo_addr(1)))]
+    new_act = P.Key(0, 11, 22, None)
+    st, out = _stamp_items(items, 1, None, new_act, {1234: "My.Grain"})
+    assert st == W.STAMP_OK
+    # removed PRIOR_ID (index 1) then PRIOR_TIMES (index 3): TARGET_ACTIVATION takes 3, TARGET_SILO takes 1
+    assert [k for k, _ in out] == [W.H_CATEGORY, W.H_TARGET_SILO, W.H_TARGET_GRAIN, W.H_TARGET_ACTIVATION,
+                                   W.H_SENDING_SILO, W.H_IS_NEW_PLACEMENT, W.H_NEW_GRAIN_TYPE]
+    d = dict(out)
+    assert d[W.H_TARGET_ACTIVATION] == ("act", new_act) and d[W.H_TARGET_SILO] == ("silo", C.silo_addr(4))
+    assert d[W.H_IS_NEW_PLACEMENT] == ("bool", True) and d[W.H_NEW_GRAIN_TYPE] == ("string", "My.Grain")
+
+
+def test_stamp_hit_same_activation_keeps_prior_headers():
+    tg = P.key_from_long(77, 1234)
+    act = P.Key(0, 5, 6, None)
+    items = [(W.H_TARGET_ACTIVATION, ("act", act)), (W.H_PRIOR_MESSAGE_ID, ("corr", 5)), (W.H_TARGET_GRAIN, ("grain", tg))]
+    st, out = _stamp_items(items, 0, act)
+    assert st == W.STAMP_OK
+    assert [k for k, _ in out] == [W.H_TARGET_ACTIVATION, W.H_PRIOR_MESSAGE_ID, W.H_TARGET_GRAIN, W.H_TARGET_SILO]
+    # a different activation drops PRIOR_MESSAGE_ID; TARGET_SILO then takes its slot
+    st, out = _stamp_items(items, 0, P.Key(0, 5, 7, None))
+    assert [k for k, _ in out] == [W.H_TARGET_ACTIVATION, W.H_TARGET_SILO, W.H_TARGET_GRAIN]
+
+
+def test_stamp_statuses():
+    tg = P.key_from_long(77, 1234)
+    base = [(W.H_TARGET_GRAIN, ("grain", tg))]
+    act = P.Key(0, 5, 6, None)
+    assert _stamp_items(base, 3, act)[0] == W.STAMP_COMPLETE
+    assert _stamp_items(base, 8, act)[0] == W.STAMP_SKIPPED
+    assert _stamp_items(base, 1, None, act, {})[0] == W.STAMP_UNSUPPORTED          # no grain type
+    assert _stamp_items(base + [(W.H_TARGET_ACTIVATION, ("null",))], 0, act)[0] == W.STAMP_MALFORMED
+    assert _stamp_items(base + [(5, ("specified", b"x"))], 0, act)[0] == W.STAMP_UNSUPPORTED
+    # a string that is not strict UTF-8 would not re-serialize to its bytes
+    hdr = bytearray(W.serialize_headers(base + [(5, ("string", "abcd"))]))
+    hdr[hdr.index(b"abcd")] = 0xC3
+    st, fr = W.stamp_frame(bytes(hdr), b"", _route(0), act, None, {4: C.silo_addr(4)}, {})
+    assert st == W.STAMP_UNSUPPORTED and fr[8:] == bytes(hdr)
+    # unknown host silo
+    st, _ = W.stamp_frame(W.serialize_headers(base), b"", _route(0, host=9), act, None, {4: C.silo_addr(4)}, {})
+    assert st == W.STAMP_UNSUPPORTED
+
+
+def test_stamped_frame_decodes_as_complete_address():
+    tg = P.key_from_long(77, 1234)
+    items = [(W.H_CATEGORY, ("int", 2)), (W.H_SENDING_SILO, ("silo", C.silo_addr(1))), (W.H_TARGET_GRAIN, ("grain", tg))]
+    st, fr = W.stamp_frame(W.serialize_headers(items), b"", _route(0, host=6), P.Key(0, 1, 2, None), None,
+                           {s: C.silo_addr(s) for s in range(8)}, {})
+    assert st == W.STAMP_OK
+    d = W.decode_frames(fr, [0], C.silo_index())[0]
+    assert d.status == W.DEC_OK and d.flags == P.HDR_ADDRESS_COMPLETE and d.target_silo == 6
