@@ -1308,7 +1308,7 @@ int orl_stamp_frames_device(orl_ctx* c, const uint8_t* d_bytes, uint64_t nbytes,
         c->d_stamp_temp = nullptr;
         c->stamp_cap = 0;
         const size_t tb = stamp_scan_temp_bytes(n);
-        ORL_HIP(c, hipMalloc((void**)&c->d_stamp_sizes, n * sizeof(uint64_t)));
+        ORL_HIP(c, hipMalloc((void**)&c->d_stamp_sizes, (n + 1) * sizeof(uint64_t)));  // + the deferral flag
         ORL_HIP(c, hipMalloc(&c->d_stamp_temp, std::max<size_t>(tb, 16)));
         c->stamp_cap = n;
         c->stamp_temp_bytes = std::max<size_t>(tb, 16);

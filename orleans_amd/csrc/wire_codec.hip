@@ -691,35 +691,33 @@ __device__ bool grain_type_lookup(const GrainTypeEntry* __restrict__ gt, uint32_
     return false;
 }
 
-// Frame i -> plan.  Statuses in the order of wire_codec.stamp_frames.
-__device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbytes, uint64_t off, uint32_t route, uint32_t act,
-                                uint64_t i, const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
+// One frame's header [hdr, end) (prefix already validated) -> plan.  Statuses in the order of
+// wire_codec.stamp_frames.
+template <class S>
+__device__ StampPlan stamp_plan(const S& w, typename S::P hdr, typename S::P end, uint32_t route, uint32_t act, uint64_t i,
+                                const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
                                 const orl_grain_key* __restrict__ new_act_keys, const GrainTypeEntry* __restrict__ gt,
                                 const uint32_t* __restrict__ silo_words, const uint16_t* lut) {
+    using P_t = typename S::P;
     StampPlan P;
     P.st = ORL_STAMP_MALFORMED;
     P.present = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSpecials; ++j) P.s_start[j] = P.s_end[j] = 0;
     P.app = 0;
     P.n_app = 0;
-    P.hdr = P.end = 0;
-    P.hl_new = 0;
+    P.hdr = hdr;
+    P.end = end;
+    P.hl_new = end - hdr;
     P.count_new = 0;
-    if (!prefix_in_buffer(off, nbytes)) return P;
-    const GlobalSrc pre{buf, (off + 7) >> 2};
-    const int32_t hl = (int32_t)ld32(pre, off), bl = (int32_t)ld32(pre, off + 4);
-    if (!frame_ok(off, nbytes, hl, bl)) return P;
-    P.hdr = off + 8;
-    P.end = P.hdr + (uint64_t)hl;
-    P.hl_new = (uint64_t)hl;
-    const GlobalSrc w{buf, (P.end - 1) >> 2};
     // structural parse (DeserializeMessageHeaders), recording the special entries
-    uint64_t p = P.hdr;
+    P_t p = hdr;
     uint32_t st = ORL_DEC_OK;
     bool noncanon = false;
     uint32_t tok22 = 0;
-    uint64_t v22 = 0;
+    P_t v22 = 0;
     int32_t count = 0;
-    if (5 > P.end - p || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
+    if (5 > end - p || ld8(w, p) != T_DICT) st = ORL_DEC_MALFORMED;
     if (!st) {
         count = (int32_t)ld32(w, p + 1);
         p += 5;
@@ -728,11 +726,12 @@ __device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbyte
     uint32_t seen = 0;
     uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     for (int32_t e = 0; !st && e < count; ++e) {
-        if (2 > P.end - p) { st = ORL_DEC_MALFORMED; break; }
-        const uint64_t es = p;
-        const uint32_t key = ld8(w, p), tok = ld8(w, p + 1);
+        if (2 > end - p) { st = ORL_DEC_MALFORMED; break; }
+        const P_t es = p;
+        const uint32_t kt = ld32(w, p - 2) >> 16;  // key, token: p >= frame + 10
+        const uint32_t key = kt & 0xFFu, tok = (kt >> 8) & 0xFFu;
         p += 2;
-        st = skip_value_fast<true>(w, P.end, lut[tok], p, &noncanon);
+        st = skip_value_fast<true>(w, end, lut[tok], p, &noncanon);
         if (st) break;
         bool dup;
         if (key < 32u) {
@@ -746,10 +745,13 @@ __device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbyte
         }
         if (dup) { st = ORL_DEC_MALFORMED; break; }
         const uint32_t k = special_index(key);
-        if (k < kSpecials) {
+        if (k < kSpecials) {  // unrolled: the struct's arrays stay in registers
             P.present |= 1u << k;
-            P.s_start[k] = es;
-            P.s_end[k] = p;
+#pragma unroll
+            for (uint32_t j = 0; j < kSpecials; ++j) {
+                P.s_start[j] = j == k ? es : P.s_start[j];
+                P.s_end[j] = j == k ? p : P.s_end[j];
+            }
             if (k == 2) { tok22 = tok; v22 = es + 2; }
         }
     }
@@ -775,13 +777,13 @@ __device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbyte
         // (TARGET_GRAIN was parsed above; routing needs it, so it is a GrainId here)
         uint32_t code = 0;
         // find TARGET_GRAIN again: it is not a special entry; scan for it (rare path: new placements)
-        uint64_t q = P.hdr + 5;
+        P_t q = hdr + 5;
         bool found = false;
         for (int32_t e = 0; e < count; ++e) {
             const uint32_t key = ld8(w, q), tok = ld8(w, q + 1);
             if (key == H_TARGET_GRAIN && tok == T_GRAIN) { code = ld32(w, q + 2 + 16); found = true; break; }
             q += 2;
-            (void)skip_value_fast(w, P.end, lut[tok], q);
+            (void)skip_value_fast(w, end, lut[tok], q);
         }
         if (!found || !grain_type_lookup(gt, code, P.gt_off, P.gt_len)) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
         if (!new_act_keys) { P.st = ORL_STAMP_UNSUPPORTED; return P; }
@@ -799,6 +801,7 @@ __device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbyte
                   (int32_t)ld32(w, v22 + 24) != -1;
     }
     // the dictionary updates
+#pragma unroll
     for (uint32_t k = 0; k < kSpecials; ++k) P.kind[k] = NE_KEEP;
     uint32_t fstack = 0, nfree = 0;  // free-list: entry indices 0 (PRIOR_ID) / 1 (PRIOR_TIMES), top = last pushed
     int32_t cnt = count;
@@ -828,6 +831,8 @@ __device__ StampPlan stamp_plan(const uint32_t* __restrict__ buf, uint64_t nbyte
     }
     // new header length
     int64_t hl_new = (int64_t)(P.dict_end - P.hdr);
+    (void)P_t(0);
+#pragma unroll
     for (uint32_t k = 0; k < kSpecials; ++k)
         if ((P.present >> k) & 1u && P.kind[k] != NE_KEEP)
             hl_new += (int64_t)new_entry_len(P.kind[k], P.gt_len) - (int64_t)(P.s_end[k] - P.s_start[k]);
@@ -854,7 +859,15 @@ struct WordWriter {
     }
     __device__ __forceinline__ void put64(uint64_t v) { put32((uint32_t)v); put32((uint32_t)(v >> 32)); }
     __device__ __forceinline__ void flush() { if (nacc) *dst++ = (uint32_t)acc; }
-    __device__ void copy(const GlobalSrc& s, uint64_t p, uint64_t len) {
+    template <class S>
+    __device__ void copy(const S& s, typename S::P p, typename S::P len) {
+        for (; len >= 32; len -= 32, p += 32) {  // eight words in flight before the first store
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) v[k] = ld32(s, p + 4 * k);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) put32(v[k]);
+        }
         for (; len >= 4; len -= 4, p += 4) put32(ld32(s, p));
         for (; len; --len, ++p) put8(ld8(s, p));
     }
@@ -882,44 +895,16 @@ __device__ void emit_entry(WordWriter& o, uint32_t kind, const StampPlan& P, con
     }
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(256) void k_stamp(const uint32_t* __restrict__ buf, uint64_t nbytes, const uint64_t* __restrict__ offs,
-                                               uint32_t n, const uint32_t* __restrict__ route, const uint32_t* __restrict__ act,
-                                               const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
-                                               const orl_grain_key* __restrict__ new_act_keys, const GrainTypeEntry* __restrict__ gt,
-                                               const uint8_t* __restrict__ gt_blob, const uint32_t* __restrict__ silo_words,
-                                               uint64_t* __restrict__ sizes, const uint64_t* __restrict__ out_offs,
-                                               uint32_t* __restrict__ out, uint64_t out_cap, uint8_t* __restrict__ status) {
-    __shared__ uint16_t lut[256];
-    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
-    __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t off = offs[i];
-    const StampPlan P = stamp_plan(buf, nbytes, off, route[i], act[i], i, act_keys, n_act_keys, new_act_keys, gt, silo_words, lut);
-    const uint64_t bl = P.end ? (uint64_t)ld32(GlobalSrc{buf, (off + 7) >> 2}, off + 4) : 0;
-    const uint64_t size = P.end == 0 ? 0 : 8 + (P.st == ORL_STAMP_OK ? P.hl_new : P.end - P.hdr) + bl;
-    if (!WRITE) {
-        sizes[i] = (size + 3) & ~3ull;
-        return;
-    }
-    uint32_t st = P.st;
-    const uint64_t o = out_offs[i], asz = (size + 3) & ~3ull;
-    if (size && (o > out_cap || asz > out_cap - o)) st = ORL_STAMP_OVERFLOW;
-    status[i] = (uint8_t)st;
-    if (size == 0 || st == ORL_STAMP_OVERFLOW) return;
-    const GlobalSrc g{buf, (P.end + bl + 3) / 4 - 1};
-    WordWriter wr{out + o / 4};
-    if (P.st != ORL_STAMP_OK) {  // unchanged copy
-        wr.copy(g, off, size);
-        wr.flush();
-        return;
-    }
+// The stamped frame: prefix, dictionary with the special entries replaced / removed and the new ones appended,
+// then the body (copied from HBM at body_pos).
+template <class S>
+__device__ void write_stamped(WordWriter& wr, const S& w, const StampPlan& P, const GlobalSrc& g, uint64_t body_pos,
+                              uint64_t bl, const uint32_t* __restrict__ silo_words, const uint8_t* __restrict__ gt_blob) {
+    using P_t = typename S::P;
     wr.put32((uint32_t)P.hl_new);
     wr.put32((uint32_t)bl);
     wr.put8(T_DICT);
     wr.put32((uint32_t)P.count_new);
-    // original entries in order, the special ones replaced / removed
     uint64_t pos = P.hdr + 5;
     while (true) {  // the next special entry at or after pos (selects only: no dynamic indexing)
         uint64_t ns = ~0ull, ne = 0;
@@ -932,15 +917,153 @@ __global__ __launch_bounds__(256) void k_stamp(const uint32_t* __restrict__ buf,
             nkind = take ? P.kind[k] : nkind;
         }
         if (ns == ~0ull) break;
-        wr.copy(g, pos, ns - pos);
-        if (nkind == NE_KEEP) wr.copy(g, ns, ne - ns);
+        wr.copy(w, (P_t)pos, (P_t)(ns - pos));
+        if (nkind == NE_KEEP) wr.copy(w, (P_t)ns, (P_t)(ne - ns));
         else emit_entry(wr, nkind, P, silo_words, gt_blob);
         pos = ne;
     }
-    wr.copy(g, pos, P.dict_end - pos);
+    wr.copy(w, (P_t)pos, (P_t)(P.dict_end - pos));
     for (uint32_t a = 0; a < P.n_app; ++a) emit_entry(wr, (P.app >> (4u * a)) & 15u, P, silo_words, gt_blob);
-    wr.copy(g, P.end, bl);
+    wr.copy(g, body_pos, bl);
     wr.flush();
+}
+
+// Size (WRITE = false) and write passes for one frame whose prefix is (hl, bl) at off, parsed from w at hdr.
+template <bool WRITE, class S>
+__device__ __forceinline__ void stamp_one(const S& w, typename S::P hdr, uint32_t i, uint64_t off, int32_t hl, int32_t bl,
+                                          const uint32_t* __restrict__ buf, const uint32_t* __restrict__ route,
+                                          const uint32_t* __restrict__ act, const orl_grain_key* __restrict__ act_keys,
+                                          uint32_t n_act_keys, const orl_grain_key* __restrict__ new_act_keys,
+                                          const GrainTypeEntry* __restrict__ gt, const uint8_t* __restrict__ gt_blob,
+                                          const uint32_t* __restrict__ silo_words, uint64_t* __restrict__ sizes,
+                                          const uint64_t* __restrict__ out_offs, uint32_t* __restrict__ out, uint64_t out_cap,
+                                          uint8_t* __restrict__ status, const uint16_t* lut) {
+    const StampPlan P = stamp_plan(w, hdr, hdr + (typename S::P)hl, route[i], act[i], i, act_keys, n_act_keys, new_act_keys,
+                                   gt, silo_words, lut);
+    const uint64_t size = 8 + (P.st == ORL_STAMP_OK ? P.hl_new : (uint64_t)hl) + (uint64_t)bl;
+    if (!WRITE) {
+        sizes[i] = (size + 3) & ~3ull;
+        return;
+    }
+    uint32_t st = P.st;
+    const uint64_t o = out_offs[i], asz = (size + 3) & ~3ull;
+    if (o > out_cap || asz > out_cap - o) st = ORL_STAMP_OVERFLOW;
+    status[i] = (uint8_t)st;
+    if (st == ORL_STAMP_OVERFLOW) return;
+    const GlobalSrc g{buf, (off + 8 + (uint64_t)hl + (uint64_t)bl + 3) / 4 - 1};
+    WordWriter wr{out + o / 4};
+    if (P.st != ORL_STAMP_OK) {  // unchanged copy
+        wr.copy(g, off, size);
+        wr.flush();
+        return;
+    }
+    write_stamped(wr, w, P, g, off + 8 + (uint64_t)hl, (uint64_t)bl, silo_words, gt_blob);
+}
+
+// Simple form (small batches, and the frames the pipelined form defers when *any_deferred): one lane per frame
+// parsing from HBM.  An invalid prefix emits nothing.
+template <bool WRITE, bool DEFERRED>
+__global__ __launch_bounds__(256) void k_stamp(const uint32_t* __restrict__ buf, uint64_t nbytes, const uint64_t* __restrict__ offs,
+                                               uint32_t n, const uint32_t* __restrict__ route, const uint32_t* __restrict__ act,
+                                               const orl_grain_key* __restrict__ act_keys, uint32_t n_act_keys,
+                                               const orl_grain_key* __restrict__ new_act_keys, const GrainTypeEntry* __restrict__ gt,
+                                               const uint8_t* __restrict__ gt_blob, const uint32_t* __restrict__ silo_words,
+                                               uint64_t* __restrict__ sizes, const uint64_t* __restrict__ out_offs,
+                                               uint32_t* __restrict__ out, uint64_t out_cap, uint8_t* __restrict__ status,
+                                               const uint32_t* __restrict__ any_deferred) {
+    if (DEFERRED && *any_deferred == 0) return;
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (DEFERRED && status[i] != kDeferred) return;
+    const uint64_t off = offs[i];
+    int32_t hl = -1, bl = -1;
+    if (prefix_in_buffer(off, nbytes)) {
+        const GlobalSrc pre{buf, (off + 7) >> 2};
+        hl = (int32_t)ld32(pre, off);
+        bl = (int32_t)ld32(pre, off + 4);
+    }
+    if (!prefix_in_buffer(off, nbytes) || !frame_ok(off, nbytes, hl, bl)) {
+        if (WRITE) status[i] = ORL_STAMP_MALFORMED;
+        else sizes[i] = 0;
+        return;
+    }
+    const uint64_t end = off + 8 + (uint64_t)hl;
+    stamp_one<WRITE>(GlobalSrc{buf, (end - 1) >> 2}, off + 8, i, off, hl, bl, buf, route, act, act_keys, n_act_keys,
+                     new_act_keys, gt, gt_blob, silo_words, sizes, out_offs, out, out_cap, status, lut);
+}
+
+// Pipelined form (the decoder's k_decode_frames_pipe scheme): persistent waves stage every frame's 256-byte
+// header window in LDS, prefetching the next chunk's windows during the current chunk, and plan / write from LDS
+// with 32-bit positions; frames whose header does not fit are left to k_stamp<., true> (status kDeferred in the
+// size pass, *any_deferred = 1).  Outputs are written per lane (4-byte aligned frame starts).
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_stamp_pipe(const uint32_t* __restrict__ buf, uint64_t nbytes,
+                                                    const uint64_t* __restrict__ offs, uint32_t n, const uint32_t* __restrict__ route,
+                                                    const uint32_t* __restrict__ act, const orl_grain_key* __restrict__ act_keys,
+                                                    uint32_t n_act_keys, const orl_grain_key* __restrict__ new_act_keys,
+                                                    const GrainTypeEntry* __restrict__ gt, const uint8_t* __restrict__ gt_blob,
+                                                    const uint32_t* __restrict__ silo_words, uint64_t* __restrict__ sizes,
+                                                    const uint64_t* __restrict__ out_offs, uint32_t* __restrict__ out,
+                                                    uint64_t out_cap, uint8_t* __restrict__ status, uint32_t* __restrict__ any_deferred) {
+    __shared__ uint32_t rows[4][64 * kRowStride];
+    __shared__ uint16_t lut[256];
+    lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t n_chunks = (n + 63) / 64;
+    const uint32_t stride = gridDim.x * 4;
+    uint32_t c = blockIdx.x * 4 + wv;
+    if (c >= n_chunks) return;  // wave-uniform; no block barrier follows
+    const uint64_t last_word = (nbytes + 3) / 4 - 1;  // launcher guarantees nbytes >= 8
+    uint32_t* my = rows[wv];
+    const LdsSrc l{my + lane * kRowStride};
+    auto frame_off = [&](uint32_t chunk) -> uint64_t {
+        const uint32_t i = chunk * 64 + lane;
+        return chunk < n_chunks && i < n ? offs[i] : ~0ull;
+    };
+    uint64_t off = frame_off(c);
+    uint32_t v[64];
+    load_windows(buf, last_word, off == ~0ull ? 0 : off, lane, v);
+    uint64_t off_next = frame_off(c + stride);
+    while (true) {
+#pragma unroll
+        for (uint32_t j = 0; j < 64; ++j) my[j * kRowStride + lane] = v[j];
+        const uint32_t cn = c + stride;
+        const uint64_t off_nn = frame_off(cn + stride);
+        if (cn < n_chunks) load_windows(buf, last_word, off_next == ~0ull ? 0 : off_next, lane, v);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t i = c * 64 + lane;
+        if (i < n) {
+            if (!prefix_in_buffer(off, nbytes)) {
+                if (WRITE) status[i] = ORL_STAMP_MALFORMED;
+                else sizes[i] = 0;
+            } else {
+                const uint32_t q0 = (uint32_t)(off & 3u);
+                const int32_t hl = (int32_t)ld32(l, q0), bl = (int32_t)ld32(l, q0 + 4);
+                if (!frame_ok(off, nbytes, hl, bl)) {
+                    if (WRITE) status[i] = ORL_STAMP_MALFORMED;
+                    else sizes[i] = 0;
+                } else if ((uint64_t)hl > kRowWords * 4 - 8 - q0) {
+                    if (!WRITE) {  // left to k_stamp<., true>
+                        status[i] = kDeferred;
+                        *any_deferred = 1u;
+                    }
+                } else {
+                    if (!WRITE) status[i] = 0;
+                    stamp_one<WRITE>(l, q0 + 8, i, off, hl, bl, buf, route, act, act_keys, n_act_keys, new_act_keys, gt,
+                                     gt_blob, silo_words, sizes, out_offs, out, out_cap, status, lut);
+                }
+            }
+        }
+        if (cn >= n_chunks) break;
+        __builtin_amdgcn_wave_barrier();  // the rows are rewritten next iteration
+        c = cn;
+        off = off_next;
+        off_next = off_nn;
+    }
 }
 
 __global__ void k_stamp_total(const uint64_t* __restrict__ sizes, const uint64_t* __restrict__ offs, uint32_t n,
@@ -991,17 +1114,50 @@ int launch_stamp_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t*
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) return (int)hipMemsetAsync(d_out_total, 0, sizeof(uint64_t), st);
     const dim3 grid((uint32_t)((n + 255) / 256));
-    hipLaunchKernelGGL(k_stamp<false>, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets, (uint32_t)n, d_route,
-                       d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
-                       (const uint64_t*)nullptr, (uint32_t*)nullptr, out_cap, d_status);
+    const uint32_t* buf = (const uint32_t*)d_bytes;
+    uint32_t* out = (uint32_t*)d_out;
+    uint32_t* flag = (uint32_t*)(d_sizes + n);  // d_sizes holds n + 1 words: the last one is the deferral flag
+    const bool pipe = n >= kPipeMinFrames && nbytes >= 8;
+    uint32_t blocks = 0;
+    if (pipe) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        blocks = std::min<uint32_t>((uint32_t)cus * 2u, (uint32_t)(((n + 63) / 64 + 3) / 4));
+        const hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    // pass 1: output sizes
+    if (pipe) {
+        hipLaunchKernelGGL(k_stamp_pipe<false>, dim3(blocks), dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route,
+                           d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)nullptr, out, out_cap, d_status, flag);
+        hipLaunchKernelGGL((k_stamp<false, true>), grid, dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route, d_act,
+                           d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)nullptr, out, out_cap, d_status, (const uint32_t*)flag);
+    } else {
+        hipLaunchKernelGGL((k_stamp<false, false>), grid, dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route, d_act,
+                           d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)nullptr, out, out_cap, d_status, (const uint32_t*)flag);
+    }
+    // output offsets = exclusive scan of the 4-byte-aligned sizes
     size_t tb = temp_bytes;
     hipError_t e = rocprim::exclusive_scan(d_temp, tb, d_sizes, d_out_offsets, (uint64_t)0, n, rocprim::plus<uint64_t>(), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_stamp_total, dim3(1), dim3(1), 0, st, (const uint64_t*)d_sizes, (const uint64_t*)d_out_offsets,
                        (uint32_t)n, d_out_total);
-    hipLaunchKernelGGL(k_stamp<true>, grid, dim3(256), 0, st, (const uint32_t*)d_bytes, nbytes, d_offsets, (uint32_t)n, d_route,
-                       d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
-                       (const uint64_t*)d_out_offsets, (uint32_t*)d_out, out_cap, d_status);
+    // pass 2: write
+    if (pipe) {
+        hipLaunchKernelGGL(k_stamp_pipe<true>, dim3(blocks), dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route,
+                           d_act, d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)d_out_offsets, out, out_cap, d_status, flag);
+        hipLaunchKernelGGL((k_stamp<true, true>), grid, dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route, d_act,
+                           d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)d_out_offsets, out, out_cap, d_status, (const uint32_t*)flag);
+    } else {
+        hipLaunchKernelGGL((k_stamp<true, false>), grid, dim3(256), 0, st, buf, nbytes, d_offsets, (uint32_t)n, d_route, d_act,
+                           d_act_keys, n_act_keys, d_new_act_keys, d_gt, d_gt_blob, d_silo_words, d_sizes,
+                           (const uint64_t*)d_out_offsets, out, out_cap, d_status, (const uint32_t*)flag);
+    }
     return (int)hipGetLastError();
 }
 
