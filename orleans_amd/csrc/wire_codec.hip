@@ -1009,8 +1009,11 @@ __global__ __launch_bounds__(256) void k_stamp_pipe(const uint32_t* __restrict__
                                                     const uint64_t* __restrict__ out_offs, uint32_t* __restrict__ out,
                                                     uint64_t out_cap, uint8_t* __restrict__ status, uint32_t* __restrict__ any_deferred) {
     __shared__ uint32_t rows[4][64 * kRowStride];
+    __shared__ uint32_t held[4][kHeldMax];
+    __shared__ uint32_t n_held[4];
     __shared__ uint16_t lut[256];
     lut[threadIdx.x] = (uint16_t)token_class(threadIdx.x);
+    if ((threadIdx.x & 63u) == 0) n_held[threadIdx.x >> 6] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t n_chunks = (n + 63) / 64;
@@ -1047,7 +1050,10 @@ __global__ __launch_bounds__(256) void k_stamp_pipe(const uint32_t* __restrict__
                     if (WRITE) status[i] = ORL_STAMP_MALFORMED;
                     else sizes[i] = 0;
                 } else if ((uint64_t)hl > kRowWords * 4 - 8 - q0) {
-                    if (!WRITE) {  // left to k_stamp<., true>
+                    const uint32_t k = atomicAdd(&n_held[wv], 1u);
+                    if (k < kHeldMax) {
+                        held[wv][k] = i;
+                    } else if (!WRITE) {  // left to k_stamp<., true>
                         status[i] = kDeferred;
                         *any_deferred = 1u;
                     }
@@ -1063,6 +1069,40 @@ __global__ __launch_bounds__(256) void k_stamp_pipe(const uint32_t* __restrict__
         c = cn;
         off = off_next;
         off_next = off_nn;
+    }
+    // the held long headers, 16 at a time from kHeldWords-word rows (the same frames in both passes: the
+    // held / deferred split depends only on the frame and its chunk's wave)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nh = min(n_held[wv], kHeldMax);
+    for (uint32_t b = 0; b < nh; b += 16) {
+        const uint32_t m = min(16u, nh - b);
+        const bool act_ = lane < m;
+        const uint32_t fi = act_ ? held[wv][b + lane] : 0;
+        const uint64_t foff = act_ ? offs[fi] : 0;
+        const GlobalSrc pre{buf, (foff + 7) >> 2};
+        const int32_t fhl = act_ ? (int32_t)ld32(pre, foff) : 0, fbl = act_ ? (int32_t)ld32(pre, foff + 4) : 0;
+        const uint32_t fw = (uint32_t)(((foff & 3u) + 8u + (uint64_t)fhl + 3u) / 4u);
+        const uint32_t w_lo = (uint32_t)(foff >> 2), w_hi = (uint32_t)(foff >> 34);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane(fw, k);
+            if (nw > kHeldWords) continue;
+            const uint64_t w0 = (uint64_t)__builtin_amdgcn_readlane(w_lo, k) | ((uint64_t)__builtin_amdgcn_readlane(w_hi, k) << 32);
+            for (uint32_t t = lane; t < nw; t += 64) my[k * kHeldWords + t] = buf[w0 + t];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (act_) {
+            if (fw <= kHeldWords) {
+                if (!WRITE) status[fi] = 0;
+                stamp_one<WRITE>(LdsSrc{my + lane * kHeldWords}, (uint32_t)(foff & 3u) + 8, fi, foff, fhl, fbl, buf, route, act,
+                                 act_keys, n_act_keys, new_act_keys, gt, gt_blob, silo_words, sizes, out_offs, out, out_cap,
+                                 status, lut);
+            } else if (!WRITE) {
+                status[fi] = kDeferred;
+                *any_deferred = 1u;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
