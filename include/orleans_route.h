@@ -209,6 +209,24 @@ int orl_dir_remove_device(orl_ctx* ctx, const orl_grain_key* d_keys, size_t n, u
 #define ORL_SPLIT_REMOVE 0x1u
 int orl_dir_split_device(orl_ctx* ctx, uint32_t me, uint32_t flags, orl_grain_key* d_keys, uint32_t* d_acts, uint8_t* d_silos,
                          uint64_t cap, uint64_t* d_n_out, void* stream);
+/* Merge of a partition copy (GrainDirectoryHandoffManager.ProcessSiloRemoveEvent,
+ * GrainDirectoryHandoffManager.cs:141-168 → GrainDirectoryPartition.Merge, GrainDirectoryPartition.cs:366-383):
+ * when a silo leaves, its successor merges the copy of the removed silo's partition it holds.  An absent grain is
+ * added as is (Merge checks neither ownership nor silo validity); for a grain present on both sides GrainInfo.Merge
+ * (:158-183) keeps the activation with the smaller ActivationId — UniqueKey.CompareTo order (TypeCodeData, N0, N1),
+ * d_act_keys[handle] = the ActivationId key of each activation handle — and the other is reported in
+ * d_dropped_act / d_dropped_silo (for Catalog.DeleteActivations on its silo; ORL_NO_ACT otherwise).  The copy is a
+ * dictionary: a key repeated within the batch is ORL_MERGE_DUPLICATE after its first occurrence.  Capacity rules
+ * as orl_dir_insert_single_device. */
+#define ORL_MERGE_INSERTED 0u
+#define ORL_MERGE_KEPT 1u         /* present; ours has the smaller ActivationId: the incoming one is dropped */
+#define ORL_MERGE_REPLACED 2u     /* present; the incoming one is smaller: ours is dropped and replaced */
+#define ORL_MERGE_SAME 3u         /* present with the same ActivationId */
+#define ORL_MERGE_DUPLICATE 4u
+#define ORL_MERGE_UNSUPPORTED 5u  /* KeyExt grain, out-of-range handle or silo */
+int orl_dir_merge_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n,
+                         const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint8_t* d_status, uint32_t* d_dropped_act,
+                         uint8_t* d_dropped_silo, void* stream);
 /* Rebuild the partition without tombstones (GrainDirectoryPartition keeps a Dictionary: no tombstones there;
  * long-running silos call this when orl_dir_insert_single_device reports ORL_E_CAPACITY with tombstones). */
 int orl_dir_compact(orl_ctx* ctx);

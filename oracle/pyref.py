@@ -304,6 +304,8 @@ INS_REMOTE_OWNER = 3
 INS_OWNER_NULL = 4
 INS_UNSUPPORTED = 5
 
+MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+
 
 class Partition:
     """Dictionary<GrainId, GrainInfo> restricted to single-activation grains
@@ -331,6 +333,39 @@ class Partition:
     def remove(self, key: Key) -> bool:
         """RemoveGrain :310-318 / RemoveActivation(force) for a single-activation grain."""
         return self.data.pop(self._k(key), None) is not None
+
+    def merge(self, entries, act_key_of) -> List[Tuple[int, int, int]]:
+        """GrainDirectoryPartition.Merge(other) (GrainDirectoryPartition.cs:366-383) with `other` given as
+        (Key, act, silo) entries in its enumeration order: an absent grain is added; a present one goes through
+        GrainInfo.Merge (:158-183): the other's activation is added unless the same ActivationId is present, then
+        the single-activation grain keeps the smallest ActivationId (OrderBy key: UniqueKey.CompareTo =
+        (TypeCodeData, N0, N1)) and drops the rest.  act_key_of(handle) -> (tcd, n0, n1).  A grain repeated in
+        `entries` is not a dictionary: MERGE_DUPLICATE after the first.  Returns per entry (status, dropped act,
+        dropped silo)."""
+        out, seen = [], set()
+        for key, act, silo in entries:
+            k = self._k(key)
+            if key.category == CAT_KEYEXT_GRAIN:
+                out.append((MERGE_UNSUPPORTED, NO_ACT, NULL_SILO))
+                continue
+            if k in seen:
+                out.append((MERGE_DUPLICATE, NO_ACT, NULL_SILO))
+                continue
+            seen.add(k)
+            if k not in self.data:
+                self.data[k] = (act, silo)
+                out.append((MERGE_INSERTED, NO_ACT, NULL_SILO))
+                continue
+            a_old, s_old = self.data[k]
+            ko, kn = act_key_of(a_old), act_key_of(act)
+            if ko == kn:
+                out.append((MERGE_SAME, NO_ACT, NULL_SILO))
+            elif kn < ko:
+                self.data[k] = (act, silo)
+                out.append((MERGE_REPLACED, a_old, s_old))
+            else:
+                out.append((MERGE_KEPT, act, silo))
+        return out
 
     def lookup(self, key: Key, view: SiloView) -> Optional[Tuple[int, int]]:
         """LookUpGrain :326-344 filtered by IsValidSilo (:337-340): returns (act, silo) or None."""

@@ -55,6 +55,7 @@ DEC_OK, DEC_UNSUPPORTED, DEC_MALFORMED, DEC_UNKNOWN_SILO, DEC_NO_TARGET, DEC_NO_
 SENDER_FROM_HEADER = 0xFF
 STAMP_OK, STAMP_COMPLETE, STAMP_SKIPPED, STAMP_UNSUPPORTED, STAMP_MALFORMED, STAMP_OVERFLOW = 0, 1, 2, 3, 4, 5
 STAMP_MAX_GROWTH = 72
+MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -121,6 +122,7 @@ _SIGS = {
     "orl_silo_address_set": (C.c_int, [_P, C.c_uint32, _P, C.c_int32, C.c_int32]),
     "orl_decode_frames_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
     "orl_grain_type_set": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_size_t]),
+    "orl_dir_merge_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, C.c_uint32, _P, _P, _P, _P]),
     "orl_stamp_frames_device": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_size_t, _P, _P, _P, C.c_uint32, _P, _P, C.c_uint64,
                                           _P, _P, _P, _P]),
     "orl_cache_config": (C.c_int, [_P, C.c_uint64]),

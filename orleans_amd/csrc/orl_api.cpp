@@ -972,6 +972,34 @@ int orl_dir_insert_single_device(orl_ctx* c, const orl_grain_key* d_keys, const 
     return ORL_OK;
 }
 
+int orl_dir_merge_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n,
+                         const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint8_t* d_status, uint32_t* d_dropped_act,
+                         uint8_t* d_dropped_silo, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_keys || !d_acts || !d_silos || !d_status || !d_act_keys)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
+    int r = sync_device_state(c);
+    if (r) return r;
+    auto fits = [&](uint64_t cnt, uint64_t tombs) {
+        return (cnt + n) * 2 <= c->table.size() && (cnt + tombs + n) * 8 <= c->table.size() * 7;
+    };
+    if (!fits(c->count_ub, c->tombs_ub)) {
+        if ((r = refresh_counts(c))) return r;
+        if (!fits(c->count_ub, c->tombs_ub))
+            return fail(c, ORL_E_CAPACITY, "directory full (%llu entries + %llu tombstones + batch %zu)",
+                        (unsigned long long)c->count_ub, (unsigned long long)c->tombs_ub, n);
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_dir_merge(c->d_table, c->mask, c->d_claim, c->d_dirstate, d_keys, d_acts, d_silos, n, c->cfg.n_act, c->n_silos,
+                             d_act_keys, n_act_keys, c->d_dslot, d_status, d_dropped_act, d_dropped_silo,
+                             reinterpret_cast<uint32_t*>(c->d_dirstate + 2), st);
+    if (e) return hipfail(c, (hipError_t)e, "directory merge launch");
+    c->count_ub += n;
+    c->mirror_stale = true;
+    return ORL_OK;
+}
+
 int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uint8_t* d_removed, void* stream) {
     if (!c) return ORL_E_INVALID;
     if (n && (!d_keys || !d_removed)) return fail(c, ORL_E_INVALID, "null device buffer");

@@ -232,6 +232,10 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
 int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                         const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
                         uint8_t* d_flag, uint32_t* d_err, void* stream);
+int launch_dir_merge(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                     const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos,
+                     const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint32_t* d_slot, uint8_t* d_status,
+                     uint32_t* d_dropped_act, uint8_t* d_dropped_silo, uint32_t* d_err, void* stream);
 int launch_dir_remove(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                       size_t n, uint32_t* d_slot, uint8_t* d_removed, void* stream);
 int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots, uint32_t me, bool remove, uint64_t* d_cnt,

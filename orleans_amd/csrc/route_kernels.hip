@@ -1516,6 +1516,107 @@ __global__ __launch_bounds__(256) void k_cache_commit(DirSlot* __restrict__ cach
     }
 }
 
+// Merge of a partition copy (GrainDirectoryPartition.Merge, GrainDirectoryPartition.cs:366-383, on
+// ProcessSiloRemoveEvent, GrainDirectoryHandoffManager.cs:141-168): an absent grain is added as is; for a grain
+// present on both sides GrainInfo.Merge (:158-183) keeps, of the single-activation grain's activations, the one
+// with the smallest ActivationId (UniqueKey.CompareTo: TypeCodeData, N0, N1 unsigned) and the other is dropped
+// (reported for Catalog.DeleteActivations).  A copy is a dictionary: a key appearing twice in one batch gets
+// ORL_MERGE_DUPLICATE (only the first is applied).  probe (find or claim; FULL entries claimed too, so the first
+// batch entry of a key owns it) → resolve (compare ActivationIds) → commit.
+__device__ __forceinline__ bool act_key_less(const orl_grain_key& a, const orl_grain_key& b) {
+    return a.type_code_data != b.type_code_data ? a.type_code_data < b.type_code_data
+         : a.n0 != b.n0 ? a.n0 < b.n0 : a.n1 < b.n1;
+}
+__device__ __forceinline__ bool act_key_eq(const orl_grain_key& a, const orl_grain_key& b) {
+    return a.type_code_data == b.type_code_data && a.n0 == b.n0 && a.n1 == b.n1;
+}
+
+__global__ __launch_bounds__(256) void k_dir_merge_probe(DirSlot* __restrict__ dir, uint64_t mask, uint32_t* __restrict__ claim,
+                                                         const orl_grain_key* __restrict__ keys, const uint32_t* __restrict__ acts,
+                                                         const uint8_t* __restrict__ silos, uint32_t n, uint32_t n_act,
+                                                         uint32_t n_silos, uint32_t n_act_keys, uint32_t* __restrict__ slot_out,
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ err) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const orl_grain_key k = keys[i];
+    const uint32_t cat = (uint32_t)(k.type_code_data >> 56);
+    uint32_t out = kSlotNone;
+    uint8_t st = kInsCandidate;
+    if (acts[i] >= n_act || acts[i] >= n_act_keys || silos[i] >= n_silos || cat == ORL_CAT_KEYEXT_GRAIN) {
+        st = ORL_MERGE_UNSUPPORTED;
+    } else {
+        uint64_t slot = 0;
+        bool was_tomb = false;
+        const int outcome = find_or_claim<true>(dir, mask, claim, k, i, slot, was_tomb);
+        if (outcome < 0) {
+            atomicOr(err, 1u);
+            st = ORL_MERGE_UNSUPPORTED;
+        } else {
+            out = (uint32_t)slot | (was_tomb ? kSlotWasTomb : 0u);
+            st = outcome == 0 ? (uint8_t)ORL_MERGE_KEPT : kInsCandidate;  // resolved below
+        }
+    }
+    slot_out[i] = out;
+    status[i] = st;
+}
+
+__global__ __launch_bounds__(256) void k_dir_merge_resolve(const DirSlot* __restrict__ dir, const uint32_t* __restrict__ claim,
+                                                           const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                           const orl_grain_key* __restrict__ act_keys, uint32_t n,
+                                                           const uint32_t* __restrict__ slot_in, uint8_t* __restrict__ status,
+                                                           uint32_t* __restrict__ dropped_act, uint8_t* __restrict__ dropped_silo) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    uint8_t st = status[i];
+    uint32_t da = ORL_NO_ACT;
+    uint8_t ds = (uint8_t)ORL_NULL_SILO;
+    if (st != ORL_MERGE_UNSUPPORTED) {
+        const uint32_t slot = slot_in[i] & kSlotMask;
+        if (claim[slot] != i) {
+            st = ORL_MERGE_DUPLICATE;
+        } else if (st == kInsCandidate) {
+            st = ORL_MERGE_INSERTED;
+        } else {  // present on both sides: keep the smaller ActivationId
+            const uint32_t a_old = dir[slot].act;
+            const orl_grain_key ko = act_keys[a_old], kn = act_keys[acts[i]];
+            if (act_key_eq(ko, kn)) {
+                st = ORL_MERGE_SAME;
+            } else if (act_key_less(kn, ko)) {
+                st = ORL_MERGE_REPLACED;
+                da = a_old;
+                ds = dir[slot].silo;
+            } else {
+                st = ORL_MERGE_KEPT;
+                da = acts[i];
+                ds = silos[i];
+            }
+        }
+    }
+    status[i] = st;
+    if (dropped_act) dropped_act[i] = da;
+    if (dropped_silo) dropped_silo[i] = ds;
+}
+
+__global__ __launch_bounds__(256) void k_dir_merge_commit(DirSlot* __restrict__ dir, uint32_t* __restrict__ claim,
+                                                          const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                          uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                          const uint8_t* __restrict__ status, uint64_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t st = status[i];
+    if (st == ORL_MERGE_UNSUPPORTED || st == ORL_MERGE_DUPLICATE) return;
+    const uint32_t slot = slot_in[i] & kSlotMask;
+    if (st == ORL_MERGE_INSERTED || st == ORL_MERGE_REPLACED) {
+        uint64_t* w24 = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(dir + slot) + 24);
+        *w24 = (uint64_t)acts[i] | ((uint64_t)silos[i] << 32) | ((uint64_t)SLOT_FULL << 40);
+    }
+    if (st == ORL_MERGE_INSERTED) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
+        if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);
+    }
+    claim[slot] = kSlotNone;  // this entry owned the slot's claim (duplicates returned above)
+}
+
 // Unregister: the first removal of a key in batch order removes it (RemoveActivation on the entry; later ones
 // find nothing).  probe → atomicMin on the entry's claim word; resolve; commit (FULL → TOMB).
 __global__ __launch_bounds__(256) void k_dir_rm_probe(const DirSlot* __restrict__ dir, uint64_t mask, uint32_t* __restrict__ claim,
@@ -2035,6 +2136,21 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
     hipLaunchKernelGGL(k_dir_ins_resolve, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_wact,
                        d_wsilo);
     hipLaunchKernelGGL(k_dir_ins_commit, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_cnt);
+    return (int)hipGetLastError();
+}
+
+int launch_dir_merge(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
+                     const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos,
+                     const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint32_t* d_slot, uint8_t* d_status,
+                     uint32_t* d_dropped_act, uint8_t* d_dropped_silo, uint32_t* d_err, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return 0;
+    const dim3 g(ceil_div(n, 256)), b(256);
+    hipLaunchKernelGGL(k_dir_merge_probe, g, b, 0, st, d_dir, dir_mask, d_claim, d_keys, d_acts, d_silos, (uint32_t)n, n_act,
+                       n_silos, n_act_keys, d_slot, d_status, d_err);
+    hipLaunchKernelGGL(k_dir_merge_resolve, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, d_act_keys, (uint32_t)n, d_slot,
+                       d_status, d_dropped_act, d_dropped_silo);
+    hipLaunchKernelGGL(k_dir_merge_commit, g, b, 0, st, d_dir, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_cnt);
     return (int)hipGetLastError();
 }
 

@@ -442,6 +442,14 @@ class GrainDirectoryEngine:
                                                     int(sender_override), ptr(d_out), ptr(d_status), ptr(d_n_bad),
                                                     ptr(stream)))
 
+    def merge_directory_device(self, d_keys, d_acts, d_silos, n: int, d_act_keys, n_act_keys: int, d_status,
+                               d_dropped_act=None, d_dropped_silo=None, stream=None) -> None:
+        """GrainDirectoryPartition.Merge of a partition copy (ProcessSiloRemoveEvent): absent grains added, present
+        ones keep the smaller ActivationId (d_act_keys[handle]); the dropped activation is reported per entry."""
+        self._ck(self._lib.orl_dir_merge_device(self._ctx, ptr(d_keys), ptr(d_acts), ptr(d_silos), int(n), ptr(d_act_keys),
+                                                int(n_act_keys), ptr(d_status), ptr(d_dropped_act), ptr(d_dropped_silo),
+                                                ptr(stream)))
+
     def set_grain_type(self, type_code: int, class_name: Optional[str]) -> None:
         """Grain class name of a type code (PlacementResult.GrainType of new placements); None removes it."""
         b = b"" if class_name is None else class_name.encode("utf-8")

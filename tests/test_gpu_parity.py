@@ -1032,3 +1032,92 @@ def test_stamp_frames_vs_oracle(torch):
     assert (st2[~fits & (sizes > 0)] == L.STAMP_OVERFLOW).all()
     assert not d_out2[cap2:].any()
     eng.close()
+
+
+def test_device_directory_merge_on_silo_remove(torch):
+    """ProcessSiloRemoveEvent's GrainDirectoryPartition.Merge of a removed silo's partition copy on
+    the device == pyref.Partition.merge: absent grains added; present grains keep the smaller ActivationId
+    (UniqueKey.CompareTo order over the handles' ActivationId keys, incl. ties in TypeCodeData / N0) and report
+    the dropped activation; same ActivationId kept; duplicates within the copy; unsupported entries; then the
+    whole table read back against the oracle partition."""
+    t = torch
+    from oracle.pyref import Partition, Key
+    rng = np.random.default_rng(17)
+    cl = W.default_cluster()
+    n_grains, n_act = 40_000, 30_000
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=2 * n_grains, max_batch=1 << 18, device=0)
+    eng.set_silos(8)
+    for s in range(8):
+        eng.add_server(s, int(cl.hashes[s]))
+    keys_all, _, owner, _ = W.grain_population(cl, n_grains)
+    # our partition: the first half of the grains, any silo (the host path registers without an owner check here:
+    # a silo holding its own partition and the copy it merges)
+    ours = np.arange(n_grains // 2)
+    acts0 = rng.integers(0, n_act, len(ours)).astype(np.uint32)
+    silos0 = rng.integers(0, 8, len(ours)).astype(np.uint8)
+    part = Partition()
+    st0 = np.zeros(len(ours), np.uint8)
+    # register through the device merge itself into an empty table (all INSERTED) — also a test of that path
+    n_keys = n_act
+    ak = np.zeros(n_keys, L.KEY_DTYPE)
+    ak["tcd"] = rng.integers(0, 3, n_keys).astype(np.uint64)          # ties in TypeCodeData ...
+    ak["n0"] = rng.integers(0, 4, n_keys).astype(np.uint64)           # ... and in N0
+    ak["n1"] = rng.integers(0, 1 << 62, n_keys, dtype=np.uint64)
+    ak[7] = ak[8]                                                     # two handles, one ActivationId
+    akey = lambda a: (int(ak["tcd"][a]), int(ak["n0"][a]), int(ak["n1"][a]))
+
+    def dev(a):
+        return t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+
+    d_ak = dev(ak)
+    st_ = t.cuda.current_stream().cuda_stream
+
+    def merge(keys, acts, silos):
+        m = len(keys)
+        d_st = t.empty(m, dtype=t.uint8, device="cuda")
+        d_da = t.empty(m, dtype=t.int32, device="cuda")
+        d_ds = t.empty(m, dtype=t.uint8, device="cuda")
+        eng.merge_directory_device(dev(keys), dev(acts), dev(silos), m, d_ak, n_keys, d_st, d_da, d_ds, stream=st_)
+        t.cuda.synchronize()
+        return d_st.cpu().numpy(), d_da.cpu().numpy().view(np.uint32), d_ds.cpu().numpy()
+
+    k0 = keys_all[ours]
+    st, da, ds = merge(k0, acts0, silos0)
+    exp = part.merge([(Key(int(k["tcd"]), int(k["n0"]), int(k["n1"])), int(a), int(s)) for k, a, s in zip(k0, acts0, silos0)], akey)
+    np.testing.assert_array_equal(st, [e[0] for e in exp])
+    assert (st == L.MERGE_INSERTED).all()
+    # the removed silo's copy: half overlapping our grains, half new, duplicates, same activations, bad entries
+    m = 30_000
+    pick = rng.integers(n_grains // 4, n_grains, m)
+    keys = keys_all[pick].copy()
+    acts = rng.integers(0, n_act, m).astype(np.uint32)
+    same = rng.random(m) < 0.1
+    cur_act = {int(i): int(a) for i, a in zip(ours, acts0)}
+    for j in np.nonzero(same)[0]:
+        if int(pick[j]) in cur_act:
+            acts[j] = cur_act[int(pick[j])]
+    acts[5] = 8 if int(pick[5]) in cur_act and cur_act[int(pick[5])] == 7 else acts[5]
+    silos = rng.integers(0, 8, m).astype(np.uint8)
+    bad = np.zeros(m, bool)
+    bad[::501] = True
+    acts[::501] = n_act + 3                                           # out-of-range handle
+    keys[250]["tcd"] = (np.uint64(L.CAT_KEYEXT_GRAIN) << np.uint64(56)) | np.uint64(5)
+    bad[250] = True
+    st, da, ds = merge(keys, acts, silos)
+    good = np.nonzero(~bad)[0]
+    exp = part.merge([(Key(int(keys["tcd"][j]), int(keys["n0"][j]), int(keys["n1"][j])), int(acts[j]), int(silos[j]))
+                      for j in good], akey)
+    assert (st[bad] == L.MERGE_UNSUPPORTED).all()
+    np.testing.assert_array_equal(st[good], [e[0] for e in exp])
+    np.testing.assert_array_equal(da[good], [e[1] for e in exp])
+    np.testing.assert_array_equal(ds[good], [e[2] for e in exp])
+    for code in (L.MERGE_INSERTED, L.MERGE_KEPT, L.MERGE_REPLACED, L.MERGE_SAME, L.MERGE_DUPLICATE):
+        assert (st == code).sum() > 50, code
+    # the table after the merge
+    a, s = eng.lookup_host(keys_all)
+    for g in range(n_grains):
+        k = keys_all[g]
+        r = part.data.get((int(k["tcd"]), int(k["n0"]), int(k["n1"]), None))
+        assert (int(a[g]), int(s[g])) == (r if r is not None else (L.NO_ACT, 0xFF)), g
+    assert eng.directory_count() == len(part.data)
+    eng.close()
