@@ -539,6 +539,12 @@ def run_wire(args, torch):
     # and status (1) written; bodies are not touched
     mean_hl = float(hl.mean())
     alg = n * (8 + mean_hl + 8 + 32 + 1)
+    traffic = None  # measured HBM bytes per launch (profiles/r01_leg8_decode_pmc.json), for this batch size only
+    tj = os.path.join(ROOT, "profiles", "r01_leg8_decode_pmc.json")
+    if os.path.exists(tj):
+        rec = json.load(open(tj))
+        if rec.get("frames_per_launch") == n:
+            traffic = rec.get("hbm_bytes_per_launch")
     eng.close()
     cpu = None
     if not args.no_cpu:
@@ -554,7 +560,7 @@ def run_wire(args, torch):
             "ms": out, "decode_frames_per_s": n / (out["decode_event"] * 1e-3),
             "roofline": {"bound": "hbm", "kernel": "k_decode_frames", "achieved": alg / (out["decode_event"] * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alg / (out["decode_event"] * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "frac": alg / (out["decode_event"] * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_frame": 8 + mean_hl + 41},
             "cpu_baseline": cpu}
 
