@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -176,6 +177,9 @@ struct orl_ctx {
     uint64_t count_ub = 0, tombs_ub = 0;  // upper bounds while the mirror is stale (capacity checks without a sync)
     // device state
     DirSlot* d_table = nullptr;
+    ProbeSlot* d_probe = nullptr;    // compact probe table of d_table (ProbeSlot, orl_internal.h)
+    bool probe_valid = false;        // d_probe mirrors d_table (set by the host upload, cleared by device mutations)
+    bool probe_off = false;          // ORL_NO_PROBE16=1: always probe the 32-B table (A/B measurements)
     uint32_t* d_claim = nullptr;     // per-slot claim word of the device insert/remove kernels (0xFFFFFFFF at rest)
     uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
     uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
@@ -284,10 +288,14 @@ uint32_t host_owner(const orl_ctx* c, const orl_grain_key& k, uint32_t me, bool 
 void rebuild_params(orl_ctx* c) {
     RouteParams& P = c->hp;
     const uint64_t mt = P.mem_tcd, m0 = P.mem_n0, m1 = P.mem_n1;
-    const uint32_t cache_on = P.cache_on;
+    const uint32_t cache_on = P.cache_on, npt = P.n_probe_types;
+    uint64_t ptcd[kProbeTypes];
+    std::memcpy(ptcd, P.probe_tcd, sizeof ptcd);
     std::memset(&P, 0, sizeof P);
     P.mem_tcd = mt; P.mem_n0 = m0; P.mem_n1 = m1;
     P.cache_on = cache_on;
+    P.n_probe_types = npt;
+    std::memcpy(P.probe_tcd, ptcd, sizeof ptcd);
     P.ring_n = (uint32_t)c->ring.size();
     for (size_t i = 0; i < c->ring.size(); ++i) {
         P.ring_hash[i] = c->ring[i].first;
@@ -306,12 +314,51 @@ void rebuild_params(orl_ctx* c) {
     c->params_dirty = true;
 }
 
+// Compact probe table from the host mirror: valid when every FULL slot is a long-key grain (N0 = 0) of at most
+// kProbeTypes TypeCodeData values.  Slot i of d_probe describes slot i of d_table, so chains are identical.
+int upload_probe(orl_ctx* c) {
+    c->probe_valid = false;
+    if (c->probe_off) return ORL_OK;
+    uint64_t types[kProbeTypes];
+    uint32_t nt = 0;
+    if (c->count == 0 && c->tombs == 0) {  // empty partition: every probe slot EMPTY
+        ORL_HIP(c, hipMemset(c->d_probe, 0, c->table.size() * sizeof(ProbeSlot)));
+        c->hp.n_probe_types = 0;
+        c->params_dirty = true;
+        c->probe_valid = true;
+        return ORL_OK;
+    }
+    for (const DirSlot& d : c->table) {
+        if (d.state != SLOT_FULL) continue;
+        if (d.n0 != 0) return ORL_OK;
+        uint32_t t = 0;
+        while (t < nt && types[t] != d.tcd) ++t;
+        if (t == nt) {
+            if (nt == kProbeTypes) return ORL_OK;
+            types[nt++] = d.tcd;
+        }
+    }
+    std::vector<ProbeSlot> pt(c->table.size());
+    for (size_t i = 0; i < c->table.size(); ++i) {
+        const DirSlot& d = c->table[i];
+        uint32_t t = 0;
+        if (d.state == SLOT_FULL)
+            while (types[t] != d.tcd) ++t;
+        // EMPTY ends a chain, FULL is compared, every other state (tombstone) is stepped over
+        const uint32_t state = d.state == SLOT_EMPTY ? SLOT_EMPTY : d.state == SLOT_FULL ? SLOT_FULL : SLOT_TOMB;
+        pt[i] = ProbeSlot{d.state == SLOT_FULL ? d.n1 : 0, d.state == SLOT_FULL ? d.act : 0,
+                          state | ((uint32_t)(d.state == SLOT_FULL ? d.silo : 0) << 8) | (t << 16)};
+    }
+    ORL_HIP(c, hipMemcpy(c->d_probe, pt.data(), pt.size() * sizeof(ProbeSlot), hipMemcpyHostToDevice));
+    c->hp.n_probe_types = nt;
+    std::memcpy(c->hp.probe_tcd, types, nt * sizeof(uint64_t));
+    c->params_dirty = true;
+    c->probe_valid = true;
+    return ORL_OK;
+}
+
 int sync_device_state(orl_ctx* c) {
     if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
-    if (c->params_dirty) {
-        ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
-        c->params_dirty = false;
-    }
     if (c->silo_hash_dirty) {
         ORL_HIP(c, hipMemcpy(c->d_silo_hash, c->silo_hash, sizeof c->silo_hash, hipMemcpyHostToDevice));
         ORL_HIP(c, hipMemcpy(c->d_silo_known, c->silo_known, sizeof c->silo_known, hipMemcpyHostToDevice));
@@ -368,12 +415,18 @@ int sync_device_state(orl_ctx* c) {
         c->dir_dirty = false;
         c->count_ub = c->count;
         c->tombs_ub = c->tombs;
+        if (int r = upload_probe(c)) return r;
+    }
+    if (c->params_dirty) {  // last: upload_probe sets the probe type list
+        ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
+        c->params_dirty = false;
     }
     return ORL_OK;
 }
 
 DirView dir_view(const orl_ctx* c) {
-    return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0};
+    return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
+                   c->probe_valid ? c->d_probe : nullptr};
 }
 
 void set_cache_on(orl_ctx* c, bool on) {
@@ -451,7 +504,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
+    f(c->d_table); f(c->d_probe); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -501,6 +554,9 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
         if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
+        if ((e = hipMalloc((void**)&c->d_probe, slots * sizeof(ProbeSlot))) != hipSuccess) return bail(e, "hipMalloc(probe table)");
+        const char* np = getenv("ORL_NO_PROBE16");
+        c->probe_off = np && np[0] == '1';
         if ((e = hipMalloc((void**)&c->d_claim, slots * 4)) != hipSuccess) return bail(e, "hipMalloc(claim)");
         if ((e = hipMemset(c->d_claim, 0xFF, slots * 4)) != hipSuccess) return bail(e, "hipMemset(claim)");
         if ((e = hipMalloc((void**)&c->d_vr_hash, ORL_MAX_SILOS * ORL_MAX_VBUCKETS_PER_SILO * 4)) != hipSuccess)
@@ -969,6 +1025,7 @@ int orl_dir_insert_single_device(orl_ctx* c, const orl_grain_key* d_keys, const 
     if (e) return hipfail(c, (hipError_t)e, "directory insert launch");
     c->count_ub += n;
     c->mirror_stale = true;
+    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
     return ORL_OK;
 }
 
@@ -997,6 +1054,7 @@ int orl_dir_merge_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t
     if (e) return hipfail(c, (hipError_t)e, "directory merge launch");
     c->count_ub += n;
     c->mirror_stale = true;
+    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
     return ORL_OK;
 }
 
@@ -1011,6 +1069,7 @@ int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uin
     if (e) return hipfail(c, (hipError_t)e, "directory remove launch");
     c->tombs_ub += n;
     c->mirror_stale = true;
+    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
     return ORL_OK;
 }
 
@@ -1029,7 +1088,10 @@ int orl_dir_split_device(orl_ctx* c, uint32_t me, uint32_t flags, orl_grain_key*
     int e = launch_dir_split(c->d_params, c->d_table, c->table.size(), me, remove, c->d_dirstate, d_keys, d_acts, d_silos, cap,
                              d_n_out, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "directory split launch");
-    if (remove) c->mirror_stale = true;  // tombstones: the upper bounds stay valid (entries + tombstones unchanged)
+    if (remove) {
+        c->mirror_stale = true;
+        c->probe_valid = false;
+    }  // tombstones: the upper bounds stay valid (entries + tombstones unchanged)
     return ORL_OK;
 }
 

@@ -33,6 +33,19 @@ struct alignas(32) DirSlot {
 };
 static_assert(sizeof(DirSlot) == 32, "slot must be 32 bytes");
 
+// Compact probe table: a 16-B copy of every slot of the partition at the same index (same chains), kept when
+// every FULL slot holds a long-key grain (N0 = 0) whose TypeCodeData is one of <= kProbeTypes values listed in
+// RouteParams.probe_tcd.  The key is then exactly (probe_tcd[tidx], 0, n1), so a probe compares n1 and the
+// type index: half the bytes per probe and half the table footprint (32 MB instead of 64 MB at config 2),
+// which is what the route kernel's random-probe rate depends on.  w = state | silo << 8 | tidx << 16.
+constexpr uint32_t kProbeTypes = 8;
+struct alignas(16) ProbeSlot {
+    uint64_t n1;
+    uint32_t act;
+    uint32_t w;
+};
+static_assert(sizeof(ProbeSlot) == 16, "probe slot must be 16 bytes");
+
 // Probe start: murmur3 fmix32 of the Jenkins uniform hash.  The uniform hash alone would do for one
 // silo, but a GPU that holds only some ring ranges sees hashes confined to those ranges; fmix32 is a
 // bijection that spreads any range over the whole table.
@@ -113,9 +126,11 @@ struct alignas(16) RouteParams {
     uint32_t n_active;
     uint32_t n_act;
     uint32_t cache_on;                 // directory cache populated: probe it for remote owners
-    uint32_t pad0[2];
+    uint32_t n_probe_types;            // entries of probe_tcd (compact probe table)
+    uint32_t pad0;
     uint64_t mem_tcd, mem_n0, mem_n1;  // Constants.SystemMembershipTableId
     uint64_t pad1;
+    uint64_t probe_tcd[kProbeTypes];   // TypeCodeData of type index i in ProbeSlot.w
 };
 static_assert(sizeof(RouteParams) % 16 == 0, "params must be 16-B granular");
 
@@ -185,11 +200,13 @@ inline uint64_t max_segments(uint64_t n, int hb) {
 
 // The directory partition table and the directory cache (AdaptiveGrainDirectoryCache) a route launch probes.
 // cache == nullptr / RouteParams.cache_on == 0: remote owners give ORL_ST_REMOTE_OWNER without a probe.
+// probe != nullptr: the compact probe table of `dir` is current and the route kernel probes it instead.
 struct DirView {
     const DirSlot* dir;
     uint64_t mask;
     const DirSlot* cache;
     uint64_t cmask;
+    const ProbeSlot* probe = nullptr;
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------

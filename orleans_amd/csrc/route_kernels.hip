@@ -169,6 +169,28 @@ __device__ __forceinline__ int probe_slot(const u32x4& a, const u32x4& b, const 
     return 2;
 }
 
+// Compact probe table (ProbeSlot): mk = the message's type index (kNoType when the message cannot equal any
+// FULL slot: N0 != 0 or a TypeCodeData not in probe_tcd; such a message misses without a probe).
+constexpr uint32_t kNoType = 0xFFu;
+__device__ __forceinline__ uint32_t probe_type(const RouteParams& P, const Msg& m) {
+    uint32_t mk = kNoType;
+    if (m.n0 == 0)
+        for (uint32_t i = 0; i < P.n_probe_types; ++i)
+            if (P.probe_tcd[i] == m.tcd) mk = i;
+    return mk;
+}
+
+__device__ __forceinline__ int probe_slot16(const u32x4& q, uint64_t n1, uint32_t mk, uint32_t& act, uint32_t& silo) {
+    const uint32_t state = q.w & 0xFFu;
+    if (state == SLOT_EMPTY) return 1;
+    if (state == SLOT_FULL && (q.w >> 16) == mk && q.x == (uint32_t)n1 && q.y == (uint32_t)(n1 >> 32)) {
+        act = q.z;
+        silo = (q.w >> 8) & 0xFFu;
+        return 0;
+    }
+    return 2;
+}
+
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
                                                bool found, uint32_t fact, uint32_t fsilo, uint32_t& act, bool via_cache) {
     const uint32_t me = m.meta & 0xFFu;
@@ -252,9 +274,11 @@ struct RouteSmem {
 };
 
 // WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
-template <int HB, bool WIRE>
+// P16: local-owner probes read the compact probe table `probe` (16-B slots, same indices) instead of `dir`.
+template <int HB, bool WIRE, bool P16>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
+                                                         const ProbeSlot* __restrict__ probe,
                                                          const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
@@ -275,6 +299,36 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
         const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
+        if (P16) {
+            // Local owner: chain walk over the 16-B probe table.  A remote owner with the cache on walks the
+            // 32-B cache table (route_msg).  Same decisions as the 32-B path (the probe table mirrors `dir`).
+            uint32_t mk = kNoType;
+            if (e < n) {
+                r = route_head(sm.P, m, excl != 0, h, own, rf);
+                if (r == kNeedProbe) {
+                    mk = probe_type(sm.P, m);
+                    slot = fmix32(h) & dmask;
+                    if (mk != kNoType) sa = reinterpret_cast<const u32x4*>(probe)[slot];
+                }
+            }
+            int st = 3;
+            uint32_t fact = 0, fsilo = 0;
+            if (r == kNeedProbe) st = mk == kNoType ? 1 : probe_slot16(sa, m.n1, mk, fact, fsilo);
+            for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
+                slot = (slot + 1) & dmask;
+                sa = reinterpret_cast<const u32x4*>(probe)[slot];
+                st = probe_slot16(sa, m.n1, mk, fact, fsilo);
+            }
+            if (e < n) {
+                uint32_t act = ORL_NO_ACT, rr = r;
+                if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
+                else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                route[e] = rr;
+                act_out[e] = act;
+                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+            }
+            continue;
+        }
         if (e < n) {
             r = route_head(sm.P, m, excl != 0, h, own, rf);
             if (r >= kNeedProbeCache) {
@@ -2043,14 +2097,16 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const bool hist = buckets && rh.on;
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
-#define ORL_ROUTE(H, W) hipLaunchKernelGGL((k_route<H, W>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask,     \
-                                           dv.cache, dv.cmask, d_in,                                                          \
-                                           (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
-    if (hist) {
-        if (wire) ORL_ROUTE(kMaxDigitBits, true); else ORL_ROUTE(kMaxDigitBits, false);
+#define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
+                                              dv.mask, dv.cache, dv.cmask, dv.probe, d_in,                                     \
+                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
+#define ORL_ROUTE_W(H, Q) do { if (wire) ORL_ROUTE(H, true, Q); else ORL_ROUTE(H, false, Q); } while (0)
+    if (dv.probe) {
+        if (hist) ORL_ROUTE_W(kMaxDigitBits, true); else ORL_ROUTE_W(0, true);
     } else {
-        if (wire) ORL_ROUTE(0, true); else ORL_ROUTE(0, false);
+        if (hist) ORL_ROUTE_W(kMaxDigitBits, false); else ORL_ROUTE_W(0, false);
     }
+#undef ORL_ROUTE_W
 #undef ORL_ROUTE
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();

@@ -1121,3 +1121,65 @@ def test_device_directory_merge_on_silo_remove(torch):
         assert (int(a[g]), int(s[g])) == (r if r is not None else (L.NO_ACT, 0xFF)), g
     assert eng.directory_count() == len(part.data)
     eng.close()
+
+
+def _mixed_type_setup(n_types, guid_frac, seed):
+    """A partition of long-key grains of `n_types` type codes (plus Guid keys with probability guid_frac), a tenth
+    of them unregistered again (tombstones), and messages that also name unregistered keys, unknown type codes,
+    N0 != 0 and registered N1 values under another type code."""
+    n_silos, n = 8, 20_000
+    cl = W.default_cluster(n_silos)
+    rng = np.random.default_rng(seed)
+    tcs = (L.CAT_GRAIN << 56) + (rng.integers(-2**31, 2**31, n_types).astype(np.int64).astype(np.uint64)
+                                  & np.uint64(0x00FFFFFFFFFFFFFF))
+    keys = np.zeros(n, L.KEY_DTYPE)
+    keys["tcd"] = tcs[rng.integers(0, n_types, n)]
+    keys["n1"] = rng.permutation(n * 4)[:n].astype(np.uint64)
+    g = rng.random(n) < guid_frac
+    keys["n0"][g] = rng.integers(1, 2**63, int(g.sum()), dtype=np.int64).astype(np.uint64)
+    acts = np.arange(n, dtype=np.uint32)
+    silos = rng.integers(0, n_silos, n).astype(np.uint8)
+    msgs = np.zeros(200_000, L.MSG_DTYPE)
+    pick = rng.integers(0, n, len(msgs))
+    msgs["tcd"], msgs["n0"], msgs["n1"] = keys["tcd"][pick], keys["n0"][pick], keys["n1"][pick]
+    r = rng.random(len(msgs))
+    msgs["n1"][r < 0.05] += np.uint64(n * 4)                         # never registered
+    msgs["tcd"][(r >= 0.05) & (r < 0.08)] ^= np.uint64(0x5A5A)        # unknown type code, registered N1
+    msgs["n0"][(r >= 0.08) & (r < 0.10)] ^= np.uint64(1)              # N0 flipped
+    msgs["tcd"][(r >= 0.10) & (r < 0.13)] = tcs[0]                     # N1 of another type under type 0
+    msgs["sending_silo"] = rng.integers(0, n_silos, len(msgs)).astype(np.uint8)
+    return cl, keys, acts, silos, msgs, rng
+
+
+@pytest.mark.parametrize("n_types,guid_frac", [(1, 0.0), (8, 0.0), (9, 0.0), (3, 0.01)])
+def test_compact_probe_table_vs_full_table(torch, monkeypatch, n_types, guid_frac):
+    """The 16-B probe table (<= 8 long-key type codes: probe_tcd) and the 32-B table route identically, and both
+    match the oracle, with tombstones, misses, foreign type codes and N0 != 0 keys; 9 types or a Guid key fall
+    back to the 32-B table."""
+    cl, keys, acts, silos, msgs, rng = _mixed_type_setup(n_types, guid_frac, seed=n_types * 31 + int(guid_frac * 100))
+    o = cpu_ref.Oracle(8, seed=0)
+    outs = []
+    for off in ("0", "1"):
+        monkeypatch.setenv("ORL_NO_PROBE16", off)
+        eng = GrainDirectoryEngine(n_act=len(keys), dir_capacity=len(keys), max_batch=1 << 20, device=0)
+        eng.set_silos(8, seed=0)
+        for s in range(8):
+            eng.add_server(s, int(cl.hashes[s]))
+            if off == "0":
+                o.add_server(s, int(cl.hashes[s]))
+        eng.register_single_activation(keys, acts, silos)
+        gone = keys[rng.permutation(len(keys))[: len(keys) // 10]] if off == "0" else gone
+        np.testing.assert_array_equal(eng.unregister(gone), np.ones(len(gone), np.uint8))
+        if off == "0":
+            o.register(keys, acts, silos)
+            o.unregister(gone)
+        res = eng.address_messages(msgs)
+        outs.append((res.route.copy(), res.act.copy(), res.order.copy(), res.offsets.copy()))
+        eng.close()
+    r, a = o.route(msgs)
+    np.testing.assert_array_equal(outs[0][0], r)
+    np.testing.assert_array_equal(outs[0][1], a)
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(x, y)
+    hit = (r >> 16) & 0xFF
+    assert (hit == L.ST_HIT).sum() > 100_000 and (hit == L.ST_NEW_PLACEMENT).sum() > 20_000
