@@ -230,6 +230,30 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
     return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, vc);
 }
 
+// route_msg over the compact probe table for local owners (remote owners with the cache on: route_msg).
+__device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
+                                                const ProbeSlot* __restrict__ probe, const DirSlot* __restrict__ cache,
+                                                uint64_t cmask, const Msg& m, bool excl_opt, uint32_t& act) {
+    uint32_t h, owner, rf;
+    act = ORL_NO_ACT;
+    const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
+    if (r < kNeedProbeCache) return r;
+    if (r == kNeedProbeCache) return route_msg(P, dir, dmask, cache, cmask, m, excl_opt, act);
+    const uint32_t mk = probe_type(P, m);
+    uint32_t fact = 0, fsilo = 0;
+    int st = 1;
+    if (mk != kNoType) {
+        const u32x4* p4 = reinterpret_cast<const u32x4*>(probe);
+        uint64_t slot = fmix32(h) & dmask;
+        st = probe_slot16(p4[slot], m.n1, mk, fact, fsilo);
+        for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
+            slot = (slot + 1) & dmask;
+            st = probe_slot16(p4[slot], m.n1, mk, fact, fsilo);
+        }
+    }
+    return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, false);
+}
+
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
 
 // Stable rank of this lane's digit among the wave's earlier elements with the same digit: one returning LDS
@@ -1008,10 +1032,10 @@ struct FanSmem {
     uint32_t prange[2];
 };
 
-template <int HB>
+template <int HB, bool P16>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
-    uint64_t cmask,
+    uint64_t cmask, const ProbeSlot* __restrict__ probe,
     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
@@ -1079,7 +1103,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
-        route[e] = route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
+        route[e] = P16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
+                       : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
         act_out[e] = act;
         if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
     }
@@ -2151,13 +2176,15 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
 
-#define ORL_FAN(H, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
-                                                       dv.mask, dv.cache, dv.cmask, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
+#define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe) ORL_FAN_(H, true, TH, BINS, SHIFT); else ORL_FAN_(H, false, TH, BINS, SHIFT); } while (0)
+#define ORL_FAN_(H, Q, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
+                                                       dv.mask, dv.cache, dv.cmask, dv.probe, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
                                                        follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);
     else ORL_FAN(0, nullptr, 1u, 0u);
 #undef ORL_FAN
+#undef ORL_FAN_
     if (ev_route_end) (void)hipEventRecord((hipEvent_t)ev_route_end, st);
     int e = (int)hipGetLastError();
     if (e || !buckets) return e;
