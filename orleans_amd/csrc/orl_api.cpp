@@ -180,6 +180,9 @@ struct orl_ctx {
     ProbeSlot* d_probe = nullptr;    // compact probe table of d_table (ProbeSlot, orl_internal.h)
     bool probe_valid = false;        // d_probe mirrors d_table (set by the host upload, cleared by device mutations)
     bool probe_off = false;          // ORL_NO_PROBE16=1: always probe the 32-B table (A/B measurements)
+    bool probe_dev = false;          // d_probe was built on the device: validity in *d_probe_bad
+    bool probe_dev_stale = false;    // device mutations since: rebuild before the next route launch
+    uint32_t* d_probe_bad = nullptr;
     uint32_t* d_claim = nullptr;     // per-slot claim word of the device insert/remove kernels (0xFFFFFFFF at rest)
     uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
     uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
@@ -317,7 +320,7 @@ void rebuild_params(orl_ctx* c) {
 // Compact probe table from the host mirror: valid when every FULL slot is a long-key grain (N0 = 0) of at most
 // kProbeTypes TypeCodeData values.  Slot i of d_probe describes slot i of d_table, so chains are identical.
 int upload_probe(orl_ctx* c) {
-    c->probe_valid = false;
+    c->probe_valid = c->probe_dev = c->probe_dev_stale = false;
     if (c->probe_off) return ORL_OK;
     uint64_t types[kProbeTypes];
     uint32_t nt = 0;
@@ -426,7 +429,23 @@ int sync_device_state(orl_ctx* c) {
 
 DirView dir_view(const orl_ctx* c) {
     return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
-                   c->probe_valid ? c->d_probe : nullptr};
+                   (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr};
+}
+
+// After a device mutation of the partition: the probe table no longer mirrors it.  When it held a type list,
+// the next route launch rebuilds it on the device (prepare_probe); the route kernels check the build's flag.
+void probe_after_device_mutation(orl_ctx* c) {
+    if ((c->probe_valid || c->probe_dev) && c->hp.n_probe_types > 0) c->probe_dev_stale = true;
+    c->probe_valid = c->probe_dev = false;
+}
+
+int prepare_probe(orl_ctx* c, hipStream_t st) {
+    if (!c->probe_dev_stale) return ORL_OK;
+    int e = launch_probe_build(c->d_table, c->table.size(), c->d_params, c->d_probe, c->d_probe_bad, st);
+    if (e) return hipfail(c, (hipError_t)e, "probe table build launch");
+    c->probe_dev_stale = false;
+    c->probe_dev = true;
+    return ORL_OK;
 }
 
 void set_cache_on(orl_ctx* c, bool on) {
@@ -504,7 +523,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
+    f(c->d_table); f(c->d_probe); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -555,6 +574,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
         if ((e = hipMalloc((void**)&c->d_probe, slots * sizeof(ProbeSlot))) != hipSuccess) return bail(e, "hipMalloc(probe table)");
+        if ((e = hipMalloc((void**)&c->d_probe_bad, 4)) != hipSuccess) return bail(e, "hipMalloc(probe flag)");
         const char* np = getenv("ORL_NO_PROBE16");
         c->probe_off = np && np[0] == '1';
         if ((e = hipMalloc((void**)&c->d_claim, slots * 4)) != hipSuccess) return bail(e, "hipMalloc(claim)");
@@ -834,6 +854,7 @@ int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts,
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     hipEvent_t* ev = nullptr;
     if (c->timing && n > 0 && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
+    if ((r = prepare_probe(c, st))) return r;
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
     int e = launch_route_bucket(c->d_params, dir_view(c), d_in, wire, n, opts, c->cfg.n_act, d_route, d_act, d_order,
                                 d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
@@ -897,6 +918,7 @@ int fanout_impl(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     hipEvent_t* ev = nullptr;
     if (c->timing && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
+    if ((r = prepare_probe(c, st))) return r;
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
     int e = launch_fanout_route_bucket(c->d_params, dir_view(c), d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub,
                                        follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
@@ -1025,7 +1047,7 @@ int orl_dir_insert_single_device(orl_ctx* c, const orl_grain_key* d_keys, const 
     if (e) return hipfail(c, (hipError_t)e, "directory insert launch");
     c->count_ub += n;
     c->mirror_stale = true;
-    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
+    probe_after_device_mutation(c);
     return ORL_OK;
 }
 
@@ -1054,7 +1076,7 @@ int orl_dir_merge_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t
     if (e) return hipfail(c, (hipError_t)e, "directory merge launch");
     c->count_ub += n;
     c->mirror_stale = true;
-    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
+    probe_after_device_mutation(c);
     return ORL_OK;
 }
 
@@ -1069,7 +1091,7 @@ int orl_dir_remove_device(orl_ctx* c, const orl_grain_key* d_keys, size_t n, uin
     if (e) return hipfail(c, (hipError_t)e, "directory remove launch");
     c->tombs_ub += n;
     c->mirror_stale = true;
-    c->probe_valid = false;  // the probe table is rebuilt by the next host upload
+    probe_after_device_mutation(c);
     return ORL_OK;
 }
 
@@ -1090,7 +1112,7 @@ int orl_dir_split_device(orl_ctx* c, uint32_t me, uint32_t flags, orl_grain_key*
     if (e) return hipfail(c, (hipError_t)e, "directory split launch");
     if (remove) {
         c->mirror_stale = true;
-        c->probe_valid = false;
+        probe_after_device_mutation(c);
     }  // tombstones: the upper bounds stay valid (entries + tombstones unchanged)
     return ORL_OK;
 }

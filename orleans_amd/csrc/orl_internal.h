@@ -207,6 +207,7 @@ struct DirView {
     const DirSlot* cache;
     uint64_t cmask;
     const ProbeSlot* probe = nullptr;
+    const uint32_t* probe_bad = nullptr;  // device-built probe table: nonzero = a key did not fit, probe `dir`
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
@@ -230,6 +231,10 @@ struct Scratch {
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
+// Compact probe table from the device partition (after device mutations), with the type list in d_params;
+// *d_bad = 1 when a FULL slot is not a long key of a listed type.
+int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* d_params, ProbeSlot* d_probe,
+                       uint32_t* d_bad, void* stream);
 int launch_route_bucket(const RouteParams* d_params, const DirView& dv,
                         const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,

@@ -276,6 +276,40 @@ __device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t 
 __device__ __forceinline__ uint32_t packed_get(const uint32_t* row, uint32_t d) { return (row[d >> 1] >> ((d & 1u) << 4)) & 0xFFFFu; }
 
 // ---------------------------------------------------------------------------------------------------
+// Compact probe table of the device partition (ProbeSlot, orl_internal.h): slot i from DirSlot i, type index from
+// the host's list in RouteParams.probe_tcd.  A FULL slot that is not a long key of a listed type sets *bad (the
+// route kernels then probe the 32-B table).
+__global__ __launch_bounds__(256) void k_probe_build(const DirSlot* __restrict__ dir, uint64_t slots,
+                                                     const RouteParams* __restrict__ gp, ProbeSlot* __restrict__ probe,
+                                                     uint32_t* __restrict__ bad) {
+    __shared__ uint64_t types[kProbeTypes];
+    __shared__ uint32_t nt;
+    if (threadIdx.x < kProbeTypes) types[threadIdx.x] = gp->probe_tcd[threadIdx.x];
+    if (threadIdx.x == 0) nt = gp->n_probe_types;
+    __syncthreads();
+    const uint32_t ntypes = nt;
+    bool miss = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256u) {
+        const u32x4* d4 = reinterpret_cast<const u32x4*>(dir + i);
+        const u32x4 a = d4[0], b = d4[1];
+        const uint32_t st = (b.w >> 8) & 0xFFu;
+        const uint64_t tcd = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        uint32_t t = 0;
+        u32x4 q = {0u, 0u, 0u, st == SLOT_EMPTY ? (uint32_t)SLOT_EMPTY : (uint32_t)SLOT_TOMB};
+        if (st == SLOT_FULL) {
+            while (t < ntypes && types[t] != tcd) ++t;
+            if (t == ntypes || (a.z | a.w) != 0u) {
+                miss = true;
+                t = 0;
+            }
+            q = u32x4{b.x, b.y, b.z, (uint32_t)SLOT_FULL | ((b.w & 0xFFu) << 8) | (t << 16)};
+        }
+        reinterpret_cast<u32x4*>(probe)[i] = q;
+    }
+    if (miss) atomicOr(bad, 1u);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // stage 1 alone
 __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -303,6 +337,7 @@ template <int HB, bool WIRE, bool P16>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
+                                                         const uint32_t* __restrict__ probe_bad,
                                                          const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
@@ -314,6 +349,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
+    const bool use16 = P16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
@@ -323,7 +359,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
         const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
-        if (P16) {
+        if (use16) {
             // Local owner: chain walk over the 16-B probe table.  A remote owner with the cache on walks the
             // 32-B cache table (route_msg).  Same decisions as the 32-B path (the probe table mirrors `dir`).
             uint32_t mk = kNoType;
@@ -1035,7 +1071,7 @@ struct FanSmem {
 template <int HB, bool P16>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
-    uint64_t cmask, const ProbeSlot* __restrict__ probe,
+    uint64_t cmask, const ProbeSlot* __restrict__ probe, const uint32_t* __restrict__ probe_bad,
     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
@@ -1066,6 +1102,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
+    const bool use16 = P16 && (probe_bad == nullptr || *probe_bad == 0u);
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads + threadIdx.x;
         if (e >= n) break;
@@ -1103,7 +1140,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
-        route[e] = P16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
+        route[e] = use16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
                        : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
         act_out[e] = act;
         if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
@@ -2105,6 +2142,16 @@ int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* st
     return (int)hipGetLastError();
 }
 
+int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* d_params, ProbeSlot* d_probe,
+                       uint32_t* d_bad, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    int e = (int)hipMemsetAsync(d_bad, 0, 4, st);
+    if (e) return e;
+    const uint64_t blocks = std::min<uint64_t>((slots + 255) / 256, 256ull * 64ull);
+    hipLaunchKernelGGL(k_probe_build, dim3((uint32_t)blocks), dim3(256), 0, st, d_dir, slots, d_params, d_probe, d_bad);
+    return (int)hipGetLastError();
+}
+
 int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const void* d_in, bool wire,
                         size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                         uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
@@ -2123,7 +2170,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
-                                              dv.mask, dv.cache, dv.cmask, dv.probe, d_in,                                     \
+                                              dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
 #define ORL_ROUTE_W(H, Q) do { if (wire) ORL_ROUTE(H, true, Q); else ORL_ROUTE(H, false, Q); } while (0)
     if (dv.probe) {
@@ -2178,7 +2225,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
 
 #define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe) ORL_FAN_(H, true, TH, BINS, SHIFT); else ORL_FAN_(H, false, TH, BINS, SHIFT); } while (0)
 #define ORL_FAN_(H, Q, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
-                                                       dv.mask, dv.cache, dv.cmask, dv.probe, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
+                                                       dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
                                                        follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);

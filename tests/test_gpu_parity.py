@@ -1183,3 +1183,69 @@ def test_compact_probe_table_vs_full_table(torch, monkeypatch, n_types, guid_fra
         np.testing.assert_array_equal(x, y)
     hit = (r >> 16) & 0xFF
     assert (hit == L.ST_HIT).sum() > 100_000 and (hit == L.ST_NEW_PLACEMENT).sum() > 20_000
+
+
+def test_probe_table_rebuilt_after_device_mutations(torch, monkeypatch):
+    """After device registrations / unregistrations (f1) the compact probe table is rebuilt on the device from the
+    host's type list; routing matches the oracle and the 32-B table.  A device-registered Guid key (N0 != 0) does
+    not fit the probe table: the build flags it and the route kernels fall back to the 32-B table."""
+    t = torch
+    cl = W.default_cluster()
+    n_grains, n_act = 40_000, 40_000
+    keys_all, _, owner, _ = W.grain_population(cl, n_grains)
+    rng = np.random.default_rng(3)
+    host_part = rng.permutation(n_grains)[:10_000]
+    dev_part = rng.integers(0, n_grains, 30_000)
+    rm = keys_all[rng.integers(0, n_grains, 8_000)]
+    guid = keys_all[:64].copy()
+    guid["n0"] = rng.integers(1, 2**63, 64, dtype=np.int64).astype(np.uint64)
+    msgs = W.uniform_messages(cl, n_grains, 200_000, seed=4)
+    gm = np.zeros(64, L.MSG_DTYPE)
+    gm["tcd"], gm["n0"], gm["n1"] = guid["tcd"], guid["n0"], guid["n1"]
+    msgs2 = np.concatenate([msgs, gm])
+
+    def dev(a):
+        return t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+
+    o = cpu_ref.Oracle(8, seed=0)
+    for s in range(8):
+        o.add_server(s, int(cl.hashes[s]))
+    o.register(keys_all[host_part], host_part.astype(np.uint32), owner[host_part])
+    o.register(keys_all[dev_part], dev_part.astype(np.uint32), owner[dev_part])
+    o.unregister(rm)
+    ref1 = o.route(msgs)
+    o.register(guid, np.arange(64, dtype=np.uint32), owner[:64])
+    ref2 = o.route(msgs2)
+    outs = []
+    for off in ("0", "1"):
+        monkeypatch.setenv("ORL_NO_PROBE16", off)
+        eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+        eng.set_silos(8, seed=0)
+        for s in range(8):
+            eng.add_server(s, int(cl.hashes[s]))
+        eng.register_single_activation(keys_all[host_part], host_part.astype(np.uint32), owner[host_part])
+        st_ = t.cuda.current_stream().cuda_stream
+        m = len(dev_part)
+        d_st = t.empty(m, dtype=t.uint8, device="cuda")
+        d_wa = t.empty(m, dtype=t.int32, device="cuda")
+        d_ws = t.empty(m, dtype=t.uint8, device="cuda")
+        eng.register_single_activation_device(dev(keys_all[dev_part]), dev(dev_part.astype(np.uint32)),
+                                              dev(owner[dev_part]), m, d_st, d_wa, d_ws, stream=st_)
+        d_rm = t.empty(len(rm), dtype=t.uint8, device="cuda")
+        eng.unregister_device(dev(rm), len(rm), d_rm, stream=st_)
+        t.cuda.synchronize()
+        res = eng.address_messages(msgs)
+        np.testing.assert_array_equal(res.route, ref1[0])
+        np.testing.assert_array_equal(res.act, ref1[1])
+        outs.append((res.route.copy(), res.act.copy(), res.order.copy()))
+        d_st2 = t.empty(64, dtype=t.uint8, device="cuda")
+        eng.register_single_activation_device(dev(guid), dev(np.arange(64, dtype=np.uint32)), dev(owner[:64]), 64,
+                                              d_st2, d_wa[:64], d_ws[:64], stream=st_)
+        t.cuda.synchronize()
+        res2 = eng.address_messages(msgs2)
+        np.testing.assert_array_equal(res2.route, ref2[0])
+        np.testing.assert_array_equal(res2.act, ref2[1])
+        eng.close()
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(x, y)
+    assert ((ref2[0][-64:] >> 16) & 0xFF == L.ST_HIT).all()
