@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7, 8],
                     help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches; "
                          "7 = stream / reminder ring leg (f3); 8 = receive path leg (f2): frames -> headers -> route")
+    ap.add_argument("--c5-contexts", type=int, default=1, choices=[1, 2],
+                    help="config 5: routing contexts/streams per step (2: game messages and fan-out concurrently)")
     ap.add_argument("--frames", type=int, default=4 * 1024 * 1024, help="frames per step (config 8)")
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
@@ -599,6 +601,14 @@ def run_presence(args, torch):
     eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan, device=0)
     W.setup_engine(eng, cl)
     W.register_population(eng, all_keys, owner, np.ones(n_keys, bool))
+    # --c5-contexts 2: the game messages and the player fan-out of a step are independent, so they run concurrently on
+    # two routing contexts (each with its own scratch and a copy of the partition) and two streams, forked and
+    # joined inside the step; a 64k-message batch alone fills only a few dozen workgroups.
+    eng2 = eng
+    if args.c5_contexts > 1:
+        eng2 = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan, device=0)
+        W.setup_engine(eng2, cl)
+        W.register_population(eng2, all_keys, owner, np.ones(n_keys, bool))
     n_sets = 8
     batches = [W.heartbeat_batch(pr, cl, n_hb, b) for b in range(n_sets)]
     dev = "cuda"
@@ -615,13 +625,19 @@ def run_presence(args, torch):
     poff = torch.empty(n_hb + 1, dtype=torch.int64, device=dev)
     s = torch.cuda.Stream()
     sp = s.cuda_stream
+    s2 = torch.cuda.Stream() if eng2 is not eng else s
+    sp2 = s2.cuda_stream
 
     def one(i):
+        if s2 is not s:
+            s2.wait_stream(s)  # fork
         # 1 game message per heartbeat (PresenceGrain.Heartbeat → GameGrain.UpdateGameStatus) ...
         eng.address_messages_device(d_msgs[i], n_hb, o1[0], o1[1], o1[2], off1, stream=sp)
         # ... + the 8-way player fan-out (GameGrain.UpdateGameStatus → PlayerGrain.JoinGame/LeaveGame)
-        eng.fanout_keys_device(d_off, d_tgt, d_pkeys, d_games[i], d_gsilo[i], n_hb, poff, o2[0], o2[1], o2[2], off2,
-                               stream=sp, total=n_fan)
+        eng2.fanout_keys_device(d_off, d_tgt, d_pkeys, d_games[i], d_gsilo[i], n_hb, poff, o2[0], o2[1], o2[2], off2,
+                                stream=sp2, total=n_fan)
+        if s2 is not s:
+            s.wait_stream(s2)  # join: the step ends on s
 
     per_step = n_hb + n_fan
     log("config 5: warmup")
@@ -681,6 +697,8 @@ def run_presence(args, torch):
     lat_graph = lat_run(lambda i: graphs[i % n_sets].replay(), steps)
     thr_graph = thr_run(lambda i: graphs[i % n_sets].replay(), steps)
     eng.close()
+    if eng2 is not eng:
+        eng2.close()
     value = per_step * steps / thr_graph
     log(f"config 5: eager {thr_eager * 1e3 / steps:.3f} ms/step (p50 {np.percentile(lat_eager, 50):.3f}, "
         f"p99 {np.percentile(lat_eager, 99):.3f} ms); graph {thr_graph * 1e3 / steps:.3f} ms/step "
@@ -691,7 +709,7 @@ def run_presence(args, torch):
             "data": "synthetic (seeded Guids; config 5 of SURVEY §8(d))",
             "config": {"workload": f"config5: {n_games} Guid-keyed games x {per_game} players, {n_hb} heartbeats per "
                                    f"step = {n_hb} game + {n_fan} player messages, stages 1-5, hipGraph replay",
-                       "messages_per_step": per_step},
+                       "messages_per_step": per_step, "routing_contexts": args.c5_contexts},
             "latency_ms": {"eager_p50": float(np.percentile(lat_eager, 50)),
                            "eager_p99": float(np.percentile(lat_eager, 99)),
                            "graph_p50": float(np.percentile(lat_graph, 50)),
