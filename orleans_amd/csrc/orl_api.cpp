@@ -181,6 +181,8 @@ struct orl_ctx {
     bool probe_valid = false;        // d_probe mirrors d_table (set by the host upload, cleared by device mutations)
     bool probe_off = false;          // ORL_NO_PROBE16=1: always probe the 32-B table (A/B measurements)
     bool probe_dev = false;          // d_probe was built on the device: validity in *d_probe_bad
+    uint32_t probe_w = 16;           // slot bytes of d_probe: 16 (ProbeSlot) or 8 (one type, 32-bit N1, 24-bit handles)
+    bool probe8_off = false;         // ORL_NO_PROBE8=1: never the 8-B form (A/B measurements)
     bool probe_dev_stale = false;    // device mutations since: rebuild before the next route launch
     uint32_t* d_probe_bad = nullptr;
     uint32_t* d_claim = nullptr;     // per-slot claim word of the device insert/remove kernels (0xFFFFFFFF at rest)
@@ -321,6 +323,7 @@ void rebuild_params(orl_ctx* c) {
 // kProbeTypes TypeCodeData values.  Slot i of d_probe describes slot i of d_table, so chains are identical.
 int upload_probe(orl_ctx* c) {
     c->probe_valid = c->probe_dev = c->probe_dev_stale = false;
+    c->probe_w = 16;
     if (c->probe_off) return ORL_OK;
     uint64_t types[kProbeTypes];
     uint32_t nt = 0;
@@ -340,6 +343,26 @@ int upload_probe(orl_ctx* c) {
             if (nt == kProbeTypes) return ORL_OK;
             types[nt++] = d.tcd;
         }
+    }
+    bool fit8 = nt == 1 && !c->probe8_off;
+    for (size_t i = 0; fit8 && i < c->table.size(); ++i) {
+        const DirSlot& d = c->table[i];
+        if (d.state == SLOT_FULL && (d.n1 >= kProbe8Tomb || d.act >= (1u << 24))) fit8 = false;
+    }
+    if (fit8) {  // 8-B form: {(uint32_t)N1, act | silo << 24}, EMPTY / TOMB as reserved keys
+        std::vector<uint32_t> p8(2 * c->table.size());
+        for (size_t i = 0; i < c->table.size(); ++i) {
+            const DirSlot& d = c->table[i];
+            p8[2 * i] = d.state == SLOT_FULL ? (uint32_t)d.n1 : d.state == SLOT_EMPTY ? kProbe8Empty : kProbe8Tomb;
+            p8[2 * i + 1] = d.state == SLOT_FULL ? (d.act | ((uint32_t)d.silo << 24)) : 0u;
+        }
+        ORL_HIP(c, hipMemcpy(c->d_probe, p8.data(), p8.size() * 4, hipMemcpyHostToDevice));
+        c->hp.n_probe_types = nt;
+        c->hp.probe_tcd[0] = types[0];
+        c->params_dirty = true;
+        c->probe_valid = true;
+        c->probe_w = 8;
+        return ORL_OK;
     }
     std::vector<ProbeSlot> pt(c->table.size());
     for (size_t i = 0; i < c->table.size(); ++i) {
@@ -429,7 +452,8 @@ int sync_device_state(orl_ctx* c) {
 
 DirView dir_view(const orl_ctx* c) {
     return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
-                   (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr};
+                   (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr,
+                   c->probe_w};
 }
 
 // After a device mutation of the partition: the probe table no longer mirrors it.  When it held a type list,
@@ -445,6 +469,7 @@ int prepare_probe(orl_ctx* c, hipStream_t st) {
     if (e) return hipfail(c, (hipError_t)e, "probe table build launch");
     c->probe_dev_stale = false;
     c->probe_dev = true;
+    c->probe_w = 16;  // the device rebuild writes the 16-B form
     return ORL_OK;
 }
 
@@ -577,6 +602,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_probe_bad, 4)) != hipSuccess) return bail(e, "hipMalloc(probe flag)");
         const char* np = getenv("ORL_NO_PROBE16");
         c->probe_off = np && np[0] == '1';
+        const char* np8 = getenv("ORL_NO_PROBE8");
+        c->probe8_off = np8 && np8[0] == '1';
         if ((e = hipMalloc((void**)&c->d_claim, slots * 4)) != hipSuccess) return bail(e, "hipMalloc(claim)");
         if ((e = hipMemset(c->d_claim, 0xFF, slots * 4)) != hipSuccess) return bail(e, "hipMemset(claim)");
         if ((e = hipMalloc((void**)&c->d_vr_hash, ORL_MAX_SILOS * ORL_MAX_VBUCKETS_PER_SILO * 4)) != hipSuccess)

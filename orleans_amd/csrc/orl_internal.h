@@ -45,6 +45,11 @@ struct alignas(16) ProbeSlot {
     uint32_t w;
 };
 static_assert(sizeof(ProbeSlot) == 16, "probe slot must be 16 bytes");
+// 8-B form of the probe table ({key, value} u32 pairs) when additionally there is ONE type, every FULL N1 is below
+// kProbe8Tomb and every FULL activation handle is below 2^24: key = (uint32_t)N1 (kProbe8Empty / kProbe8Tomb mark
+// empty slots and tombstones), value = act | silo << 24.  16 MB at config 2.
+constexpr uint32_t kProbe8Empty = 0xFFFFFFFFu;
+constexpr uint32_t kProbe8Tomb = 0xFFFFFFFEu;
 
 // Probe start: murmur3 fmix32 of the Jenkins uniform hash.  The uniform hash alone would do for one
 // silo, but a GPU that holds only some ring ranges sees hashes confined to those ranges; fmix32 is a
@@ -208,6 +213,7 @@ struct DirView {
     uint64_t cmask;
     const ProbeSlot* probe = nullptr;
     const uint32_t* probe_bad = nullptr;  // device-built probe table: nonzero = a key did not fit, probe `dir`
+    uint32_t probe_w = 16;                // slot bytes of `probe`: 16 (ProbeSlot) or 8 (u32 key/value pairs)
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------

@@ -191,6 +191,22 @@ __device__ __forceinline__ int probe_slot16(const u32x4& q, uint64_t n1, uint32_
     return 2;
 }
 
+// 8-B probe table: kb = (uint32_t)N1, only when the message can equal a FULL slot (N0 = 0, the one listed
+// type, N1 < kProbe8Tomb).
+__device__ __forceinline__ bool probe8_key(const RouteParams& P, const Msg& m) {
+    return m.n0 == 0 && m.tcd == P.probe_tcd[0] && m.n1 < (uint64_t)kProbe8Tomb;
+}
+
+__device__ __forceinline__ int probe_slot8(const uint2& q, uint32_t kb, uint32_t& act, uint32_t& silo) {
+    if (q.x == kProbe8Empty) return 1;
+    if (q.x == kb) {
+        act = q.y & 0xFFFFFFu;
+        silo = q.y >> 24;
+        return 0;
+    }
+    return 2;
+}
+
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
                                                bool found, uint32_t fact, uint32_t fsilo, uint32_t& act, bool via_cache) {
     const uint32_t me = m.meta & 0xFFu;
@@ -231,6 +247,7 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
 }
 
 // route_msg over the compact probe table for local owners (remote owners with the cache on: route_msg).
+template <int PW>
 __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
                                                 const ProbeSlot* __restrict__ probe, const DirSlot* __restrict__ cache,
                                                 uint64_t cmask, const Msg& m, bool excl_opt, uint32_t& act) {
@@ -239,9 +256,22 @@ __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirS
     const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
     if (r < kNeedProbeCache) return r;
     if (r == kNeedProbeCache) return route_msg(P, dir, dmask, cache, cmask, m, excl_opt, act);
-    const uint32_t mk = probe_type(P, m);
     uint32_t fact = 0, fsilo = 0;
     int st = 1;
+    if (PW == 8) {
+        if (probe8_key(P, m)) {
+            const uint2* p8 = reinterpret_cast<const uint2*>(probe);
+            const uint32_t kb = (uint32_t)m.n1;
+            uint64_t slot = fmix32(h) & dmask;
+            st = probe_slot8(p8[slot], kb, fact, fsilo);
+            for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
+                slot = (slot + 1) & dmask;
+                st = probe_slot8(p8[slot], kb, fact, fsilo);
+            }
+        }
+        return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, false);
+    }
+    const uint32_t mk = probe_type(P, m);
     if (mk != kNoType) {
         const u32x4* p4 = reinterpret_cast<const u32x4*>(probe);
         uint64_t slot = fmix32(h) & dmask;
@@ -332,8 +362,9 @@ struct RouteSmem {
 };
 
 // WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
-// P16: local-owner probes read the compact probe table `probe` (16-B slots, same indices) instead of `dir`.
-template <int HB, bool WIRE, bool P16>
+// PW: local-owner probes read the compact probe table `probe` (PW = 16: ProbeSlot, 8: u32 key/value pairs; same
+// indices) instead of `dir` (PW = 0).
+template <int HB, bool WIRE, int PW>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
@@ -349,7 +380,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
-    const bool use16 = P16 && (probe_bad == nullptr || *probe_bad == 0u);
+    const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
@@ -359,6 +390,36 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
         const u32x4* dir4 = reinterpret_cast<const u32x4*>(dir);
+        if (PW == 8) {  // same walk over the 8-B table (host-built only: no flag)
+            bool can = false;
+            uint2 q;
+            if (e < n) {
+                r = route_head(sm.P, m, excl != 0, h, own, rf);
+                if (r == kNeedProbe) {
+                    can = probe8_key(sm.P, m);
+                    slot = fmix32(h) & dmask;
+                    if (can) q = reinterpret_cast<const uint2*>(probe)[slot];
+                }
+            }
+            const uint32_t kb = (uint32_t)m.n1;
+            int st = 3;
+            uint32_t fact = 0, fsilo = 0;
+            if (r == kNeedProbe) st = can ? probe_slot8(q, kb, fact, fsilo) : 1;
+            for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
+                slot = (slot + 1) & dmask;
+                q = reinterpret_cast<const uint2*>(probe)[slot];
+                st = probe_slot8(q, kb, fact, fsilo);
+            }
+            if (e < n) {
+                uint32_t act = ORL_NO_ACT, rr = r;
+                if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
+                else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                route[e] = rr;
+                act_out[e] = act;
+                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+            }
+            continue;
+        }
         if (use16) {
             // Local owner: chain walk over the 16-B probe table.  A remote owner with the cache on walks the
             // 32-B cache table (route_msg).  Same decisions as the 32-B path (the probe table mirrors `dir`).
@@ -1068,7 +1129,7 @@ struct FanSmem {
     uint32_t prange[2];
 };
 
-template <int HB, bool P16>
+template <int HB, int PW>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
     uint64_t cmask, const ProbeSlot* __restrict__ probe, const uint32_t* __restrict__ probe_bad,
@@ -1102,7 +1163,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
-    const bool use16 = P16 && (probe_bad == nullptr || *probe_bad == 0u);
+    const bool use16 = PW != 0 && (probe_bad == nullptr || *probe_bad == 0u);
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads + threadIdx.x;
         if (e >= n) break;
@@ -1140,7 +1201,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
-        route[e] = use16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
+        route[e] = use16 ? route_msg16<PW>(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
                        : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
         act_out[e] = act;
         if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
@@ -2173,10 +2234,12 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
 #define ORL_ROUTE_W(H, Q) do { if (wire) ORL_ROUTE(H, true, Q); else ORL_ROUTE(H, false, Q); } while (0)
-    if (dv.probe) {
-        if (hist) ORL_ROUTE_W(kMaxDigitBits, true); else ORL_ROUTE_W(0, true);
+    if (dv.probe && dv.probe_w == 8) {
+        if (hist) ORL_ROUTE_W(kMaxDigitBits, 8); else ORL_ROUTE_W(0, 8);
+    } else if (dv.probe) {
+        if (hist) ORL_ROUTE_W(kMaxDigitBits, 16); else ORL_ROUTE_W(0, 16);
     } else {
-        if (hist) ORL_ROUTE_W(kMaxDigitBits, false); else ORL_ROUTE_W(0, false);
+        if (hist) ORL_ROUTE_W(kMaxDigitBits, 0); else ORL_ROUTE_W(0, 0);
     }
 #undef ORL_ROUTE_W
 #undef ORL_ROUTE
@@ -2223,7 +2286,8 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
 
-#define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe) ORL_FAN_(H, true, TH, BINS, SHIFT); else ORL_FAN_(H, false, TH, BINS, SHIFT); } while (0)
+#define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe && dv.probe_w == 8) ORL_FAN_(H, 8, TH, BINS, SHIFT); \
+                                          else if (dv.probe) ORL_FAN_(H, 16, TH, BINS, SHIFT); else ORL_FAN_(H, 0, TH, BINS, SHIFT); } while (0)
 #define ORL_FAN_(H, Q, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
                                                        dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
                                                        follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \

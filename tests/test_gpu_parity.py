@@ -1147,6 +1147,7 @@ def _mixed_type_setup(n_types, guid_frac, seed):
     msgs["tcd"][(r >= 0.05) & (r < 0.08)] ^= np.uint64(0x5A5A)        # unknown type code, registered N1
     msgs["n0"][(r >= 0.08) & (r < 0.10)] ^= np.uint64(1)              # N0 flipped
     msgs["tcd"][(r >= 0.10) & (r < 0.13)] = tcs[0]                     # N1 of another type under type 0
+    msgs["n1"][(r >= 0.13) & (r < 0.15)] += np.uint64(1 << 32)        # low 32 bits of a registered N1
     msgs["sending_silo"] = rng.integers(0, n_silos, len(msgs)).astype(np.uint8)
     return cl, keys, acts, silos, msgs, rng
 
@@ -1155,12 +1156,14 @@ def _mixed_type_setup(n_types, guid_frac, seed):
 def test_compact_probe_table_vs_full_table(torch, monkeypatch, n_types, guid_frac):
     """The 16-B probe table (<= 8 long-key type codes: probe_tcd) and the 32-B table route identically, and both
     match the oracle, with tombstones, misses, foreign type codes and N0 != 0 keys; 9 types or a Guid key fall
-    back to the 32-B table."""
+    back to the 32-B table.  One type with 32-bit N1 values and small handles takes the 8-B form (N1 values whose
+    low 32 bits name a registered grain must still miss)."""
     cl, keys, acts, silos, msgs, rng = _mixed_type_setup(n_types, guid_frac, seed=n_types * 31 + int(guid_frac * 100))
     o = cpu_ref.Oracle(8, seed=0)
     outs = []
-    for off in ("0", "1"):
-        monkeypatch.setenv("ORL_NO_PROBE16", off)
+    for off in ("0", "1", "8"):
+        monkeypatch.setenv("ORL_NO_PROBE16", "1" if off == "1" else "0")
+        monkeypatch.setenv("ORL_NO_PROBE8", "1" if off == "8" else "0")
         eng = GrainDirectoryEngine(n_act=len(keys), dir_capacity=len(keys), max_batch=1 << 20, device=0)
         eng.set_silos(8, seed=0)
         for s in range(8):
@@ -1179,8 +1182,9 @@ def test_compact_probe_table_vs_full_table(torch, monkeypatch, n_types, guid_fra
     r, a = o.route(msgs)
     np.testing.assert_array_equal(outs[0][0], r)
     np.testing.assert_array_equal(outs[0][1], a)
-    for x, y in zip(outs[0], outs[1]):
-        np.testing.assert_array_equal(x, y)
+    for o2 in outs[1:]:
+        for x, y in zip(outs[0], o2):
+            np.testing.assert_array_equal(x, y)
     hit = (r >> 16) & 0xFF
     assert (hit == L.ST_HIT).sum() > 100_000 and (hit == L.ST_NEW_PLACEMENT).sum() > 20_000
 
