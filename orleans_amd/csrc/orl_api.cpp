@@ -181,7 +181,8 @@ struct orl_ctx {
     bool probe_valid = false;        // d_probe mirrors d_table (set by the host upload, cleared by device mutations)
     bool probe_off = false;          // ORL_NO_PROBE16=1: always probe the 32-B table (A/B measurements)
     bool probe_dev = false;          // d_probe was built on the device: validity in *d_probe_bad
-    uint32_t probe_w = 16;           // slot bytes of d_probe: 16 (ProbeSlot) or 8 (one type, 32-bit N1, 24-bit handles)
+    uint2* d_probe8 = nullptr;       // 8-B form of the probe table (one type, 32-bit N1, 24-bit handles)
+    bool probe8_valid = false;       // d_probe8 mirrors d_table (host upload only)
     bool probe8_off = false;         // ORL_NO_PROBE8=1: never the 8-B form (A/B measurements)
     bool probe_dev_stale = false;    // device mutations since: rebuild before the next route launch
     uint32_t* d_probe_bad = nullptr;
@@ -322,8 +323,7 @@ void rebuild_params(orl_ctx* c) {
 // Compact probe table from the host mirror: valid when every FULL slot is a long-key grain (N0 = 0) of at most
 // kProbeTypes TypeCodeData values.  Slot i of d_probe describes slot i of d_table, so chains are identical.
 int upload_probe(orl_ctx* c) {
-    c->probe_valid = c->probe_dev = c->probe_dev_stale = false;
-    c->probe_w = 16;
+    c->probe_valid = c->probe_dev = c->probe_dev_stale = c->probe8_valid = false;
     if (c->probe_off) return ORL_OK;
     uint64_t types[kProbeTypes];
     uint32_t nt = 0;
@@ -356,13 +356,8 @@ int upload_probe(orl_ctx* c) {
             p8[2 * i] = d.state == SLOT_FULL ? (uint32_t)d.n1 : d.state == SLOT_EMPTY ? kProbe8Empty : kProbe8Tomb;
             p8[2 * i + 1] = d.state == SLOT_FULL ? (d.act | ((uint32_t)d.silo << 24)) : 0u;
         }
-        ORL_HIP(c, hipMemcpy(c->d_probe, p8.data(), p8.size() * 4, hipMemcpyHostToDevice));
-        c->hp.n_probe_types = nt;
-        c->hp.probe_tcd[0] = types[0];
-        c->params_dirty = true;
-        c->probe_valid = true;
-        c->probe_w = 8;
-        return ORL_OK;
+        ORL_HIP(c, hipMemcpy(c->d_probe8, p8.data(), p8.size() * 4, hipMemcpyHostToDevice));
+        c->probe8_valid = true;  // the 16-B form below is built too (the fan-out kernel reads it)
     }
     std::vector<ProbeSlot> pt(c->table.size());
     for (size_t i = 0; i < c->table.size(); ++i) {
@@ -453,14 +448,14 @@ int sync_device_state(orl_ctx* c) {
 DirView dir_view(const orl_ctx* c) {
     return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
                    (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr,
-                   c->probe_w};
+                   c->probe8_valid ? c->d_probe8 : nullptr};
 }
 
 // After a device mutation of the partition: the probe table no longer mirrors it.  When it held a type list,
 // the next route launch rebuilds it on the device (prepare_probe); the route kernels check the build's flag.
 void probe_after_device_mutation(orl_ctx* c) {
     if ((c->probe_valid || c->probe_dev) && c->hp.n_probe_types > 0) c->probe_dev_stale = true;
-    c->probe_valid = c->probe_dev = false;
+    c->probe_valid = c->probe_dev = c->probe8_valid = false;
 }
 
 int prepare_probe(orl_ctx* c, hipStream_t st) {
@@ -469,7 +464,6 @@ int prepare_probe(orl_ctx* c, hipStream_t st) {
     if (e) return hipfail(c, (hipError_t)e, "probe table build launch");
     c->probe_dev_stale = false;
     c->probe_dev = true;
-    c->probe_w = 16;  // the device rebuild writes the 16-B form
     return ORL_OK;
 }
 
@@ -548,7 +542,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
+    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -600,6 +594,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
         if ((e = hipMalloc((void**)&c->d_probe, slots * sizeof(ProbeSlot))) != hipSuccess) return bail(e, "hipMalloc(probe table)");
         if ((e = hipMalloc((void**)&c->d_probe_bad, 4)) != hipSuccess) return bail(e, "hipMalloc(probe flag)");
+        if ((e = hipMalloc((void**)&c->d_probe8, slots * 8)) != hipSuccess) return bail(e, "hipMalloc(probe table 8)");
         const char* np = getenv("ORL_NO_PROBE16");
         c->probe_off = np && np[0] == '1';
         const char* np8 = getenv("ORL_NO_PROBE8");

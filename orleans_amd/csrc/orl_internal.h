@@ -213,7 +213,7 @@ struct DirView {
     uint64_t cmask;
     const ProbeSlot* probe = nullptr;
     const uint32_t* probe_bad = nullptr;  // device-built probe table: nonzero = a key did not fit, probe `dir`
-    uint32_t probe_w = 16;                // slot bytes of `probe`: 16 (ProbeSlot) or 8 (u32 key/value pairs)
+    const void* probe8 = nullptr;         // 8-B form of `probe` ({u32 key, u32 value} pairs) when the keys fit it
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
