@@ -247,7 +247,7 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
 }
 
 // route_msg over the compact probe table for local owners (remote owners with the cache on: route_msg).
-template <int PW>
+// (the fan-out kernel reads the 16-B form; see launch_fanout_route_bucket)
 __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
                                                 const ProbeSlot* __restrict__ probe, const DirSlot* __restrict__ cache,
                                                 uint64_t cmask, const Msg& m, bool excl_opt, uint32_t& act) {
@@ -258,19 +258,6 @@ __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirS
     if (r == kNeedProbeCache) return route_msg(P, dir, dmask, cache, cmask, m, excl_opt, act);
     uint32_t fact = 0, fsilo = 0;
     int st = 1;
-    if (PW == 8) {
-        if (probe8_key(P, m)) {
-            const uint2* p8 = reinterpret_cast<const uint2*>(probe);
-            const uint32_t kb = (uint32_t)m.n1;
-            uint64_t slot = fmix32(h) & dmask;
-            st = probe_slot8(p8[slot], kb, fact, fsilo);
-            for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
-                slot = (slot + 1) & dmask;
-                st = probe_slot8(p8[slot], kb, fact, fsilo);
-            }
-        }
-        return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, false);
-    }
     const uint32_t mk = probe_type(P, m);
     if (mk != kNoType) {
         const u32x4* p4 = reinterpret_cast<const u32x4*>(probe);
@@ -1201,7 +1188,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
         m.aux = 0;
         uint32_t act;
-        route[e] = use16 ? route_msg16<PW>(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
+        route[e] = use16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
                        : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
         act_out[e] = act;
         if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
