@@ -107,6 +107,7 @@ typedef struct orl_wire_msg {
 #define ORL_ST_CLIENT_UNREGISTERED 6u  /* client grain miss (KeyNotFoundException, PlacementDirectorsManager.cs:75-81) */
 #define ORL_ST_KEYEXT_UNRESOLVED 7u    /* KeyExt grain: owner computed, partition lookup left to host */
 #define ORL_ST_REMOTE_OWNER 8u         /* owner's partition not held by this context (cache/FullLookup path) */
+#define ORL_ST_PAST_TOTAL 9u           /* fan-out with an overstated ORL_OPT_TOTAL_GIVEN: no message at this index */
 
 #define ORL_RF_NEW_PLACEMENT 0x01u
 #define ORL_RF_LOOPBACK 0x02u          /* target silo == sending silo (OutboundMessageQueue.cs:113-119) */
@@ -432,6 +433,15 @@ int orl_sync(orl_ctx* ctx);
  * kernels (stage 4) and the whole call with HIP events on the submission stream (no host sync per batch;
  * up to ORL_TIMING_SLOTS batches are kept).  orl_set_timing(ctx, 1) clears the record.
  * orl_timing_summary waits for the last recorded batch and returns the per-batch averages in ms. */
+/* Context state, as the next route launch sees it (pending host-side changes are uploaded first).
+ *   ORL_Q_PROBE_FORM    directory form k_route probes: 8 / 16 (compact copies built by the host upload), 17 (16-B copy
+ *                       rebuilt on the device after device mutations, checked by its flag), 32 (the full 32-B table)
+ *   ORL_Q_FULL_UPLOADS  whole-partition uploads so far; ORL_Q_SLOT_PATCHES in-place uploads of host-changed slots */
+#define ORL_Q_PROBE_FORM 1u
+#define ORL_Q_FULL_UPLOADS 2u
+#define ORL_Q_SLOT_PATCHES 3u
+int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
+
 #define ORL_TIMING_SLOTS 256u
 int orl_set_timing(orl_ctx* ctx, int enable);
 int orl_timing_summary(const orl_ctx* ctx, uint32_t* n_batches, float* route_kernel_ms, float* bucket_ms,

@@ -35,6 +35,7 @@ ST_NO_SEED = 5
 ST_CLIENT_UNREGISTERED = 6
 ST_KEYEXT_UNRESOLVED = 7
 ST_REMOTE_OWNER = 8
+ST_PAST_TOTAL = 9
 
 RF_NEW_PLACEMENT = 0x01
 RF_LOOPBACK = 0x02
@@ -56,6 +57,8 @@ SENDER_FROM_HEADER = 0xFF
 STAMP_OK, STAMP_COMPLETE, STAMP_SKIPPED, STAMP_UNSUPPORTED, STAMP_MALFORMED, STAMP_OVERFLOW = 0, 1, 2, 3, 4, 5
 STAMP_MAX_GROWTH = 72
 MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+
+Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES = 1, 2, 3
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -131,6 +134,7 @@ _SIGS = {
     "orl_cache_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_cache_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_sync": (C.c_int, [_P]),
+    "orl_ctx_query": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint64)]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),

@@ -172,7 +172,12 @@ struct orl_ctx {
     // directory partition mirror
     std::vector<DirSlot> table;
     uint64_t mask = 0, count = 0, tombs = 0;
-    bool dir_dirty = true;
+    bool dir_dirty = true;           // the whole table must be uploaded (and the probe tables rebuilt)
+    std::vector<uint32_t> dirty_slots;  // else: host-changed slots since the last upload, patched in place
+    std::vector<uint8_t> slot_marked;   // dirty_slots membership (one byte per slot, allocated on first use)
+    void* d_patch_data = nullptr;       // device staging of a slot patch (grows to the largest patch)
+    size_t patch_cap = 0;
+    uint64_t n_full_uploads = 0, n_patches = 0;
     bool mirror_stale = false;       // device mutations since the mirror was last downloaded
     uint64_t count_ub = 0, tombs_ub = 0;  // upper bounds while the mirror is stale (capacity checks without a sync)
     // device state
@@ -320,6 +325,19 @@ void rebuild_params(orl_ctx* c) {
     c->params_dirty = true;
 }
 
+// Probe-table forms of one directory slot (ProbeSlot, orl_internal.h).  t = the slot's type index.
+ProbeSlot probe16_of(const DirSlot& d, uint32_t t) {
+    // EMPTY ends a chain, FULL is compared, every other state (tombstone) is stepped over
+    const uint32_t state = d.state == SLOT_EMPTY ? SLOT_EMPTY : d.state == SLOT_FULL ? SLOT_FULL : SLOT_TOMB;
+    if (d.state != SLOT_FULL) return ProbeSlot{0, 0, state};
+    return ProbeSlot{d.n1, d.act, state | ((uint32_t)d.silo << 8) | (t << 16)};
+}
+uint2 probe8_of(const DirSlot& d) {  // {(uint32_t)N1, act | silo << 24}, EMPTY / TOMB as reserved keys
+    if (d.state == SLOT_FULL) return make_uint2((uint32_t)d.n1, d.act | ((uint32_t)d.silo << 24));
+    return make_uint2(d.state == SLOT_EMPTY ? kProbe8Empty : kProbe8Tomb, 0u);
+}
+bool fits8(const DirSlot& d) { return d.state != SLOT_FULL || (d.n1 < kProbe8Tomb && d.act < (1u << 24)); }
+
 // Compact probe table from the host mirror: valid when every FULL slot is a long-key grain (N0 = 0) of at most
 // kProbeTypes TypeCodeData values.  Slot i of d_probe describes slot i of d_table, so chains are identical.
 int upload_probe(orl_ctx* c) {
@@ -345,18 +363,11 @@ int upload_probe(orl_ctx* c) {
         }
     }
     bool fit8 = nt == 1 && !c->probe8_off;
-    for (size_t i = 0; fit8 && i < c->table.size(); ++i) {
-        const DirSlot& d = c->table[i];
-        if (d.state == SLOT_FULL && (d.n1 >= kProbe8Tomb || d.act >= (1u << 24))) fit8 = false;
-    }
-    if (fit8) {  // 8-B form: {(uint32_t)N1, act | silo << 24}, EMPTY / TOMB as reserved keys
-        std::vector<uint32_t> p8(2 * c->table.size());
-        for (size_t i = 0; i < c->table.size(); ++i) {
-            const DirSlot& d = c->table[i];
-            p8[2 * i] = d.state == SLOT_FULL ? (uint32_t)d.n1 : d.state == SLOT_EMPTY ? kProbe8Empty : kProbe8Tomb;
-            p8[2 * i + 1] = d.state == SLOT_FULL ? (d.act | ((uint32_t)d.silo << 24)) : 0u;
-        }
-        ORL_HIP(c, hipMemcpy(c->d_probe8, p8.data(), p8.size() * 4, hipMemcpyHostToDevice));
+    for (size_t i = 0; fit8 && i < c->table.size(); ++i) fit8 = fits8(c->table[i]);
+    if (fit8) {
+        std::vector<uint2> p8(c->table.size());
+        for (size_t i = 0; i < c->table.size(); ++i) p8[i] = probe8_of(c->table[i]);
+        ORL_HIP(c, hipMemcpy(c->d_probe8, p8.data(), p8.size() * 8, hipMemcpyHostToDevice));
         c->probe8_valid = true;  // the 16-B form below is built too (the fan-out kernel reads it)
     }
     std::vector<ProbeSlot> pt(c->table.size());
@@ -365,10 +376,7 @@ int upload_probe(orl_ctx* c) {
         uint32_t t = 0;
         if (d.state == SLOT_FULL)
             while (types[t] != d.tcd) ++t;
-        // EMPTY ends a chain, FULL is compared, every other state (tombstone) is stepped over
-        const uint32_t state = d.state == SLOT_EMPTY ? SLOT_EMPTY : d.state == SLOT_FULL ? SLOT_FULL : SLOT_TOMB;
-        pt[i] = ProbeSlot{d.state == SLOT_FULL ? d.n1 : 0, d.state == SLOT_FULL ? d.act : 0,
-                          state | ((uint32_t)(d.state == SLOT_FULL ? d.silo : 0) << 8) | (t << 16)};
+        pt[i] = probe16_of(d, t);
     }
     ORL_HIP(c, hipMemcpy(c->d_probe, pt.data(), pt.size() * sizeof(ProbeSlot), hipMemcpyHostToDevice));
     c->hp.n_probe_types = nt;
@@ -378,8 +386,112 @@ int upload_probe(orl_ctx* c) {
     return ORL_OK;
 }
 
+// A host-side change of directory slot i (registration / unregistration through the host mirror).
+void mark_slot(orl_ctx* c, uint64_t i) {
+    if (c->dir_dirty) return;  // the whole table goes up anyway
+    if (c->slot_marked.size() != c->table.size()) c->slot_marked.assign(c->table.size(), 0);
+    if (c->slot_marked[i]) return;
+    c->slot_marked[i] = 1;
+    c->dirty_slots.push_back((uint32_t)i);
+    if (c->dirty_slots.size() > c->table.size() / 16 + 64) c->dir_dirty = true;  // a bulk load: one full upload
+}
+
+void clear_dirty_slots(orl_ctx* c) {
+    for (uint32_t i : c->dirty_slots) c->slot_marked[i] = 0;
+    c->dirty_slots.clear();
+}
+
+// Upload only the host-changed slots of the partition and patch the probe forms in place (k_dir_patch), instead of
+// re-uploading the whole table and rebuilding the probe tables on the host after every small registration batch.
+// A changed slot that no longer fits the 16-B form (an N0 != 0 key, a ninth type) makes the probe table rebuild
+// (upload_probe); one that does not fit the 8-B form retires that form.
+int patch_dirty_slots(orl_ctx* c) {
+    const size_t m = c->dirty_slots.size();
+    bool p16 = c->probe_valid, p8 = c->probe8_valid;
+    const bool dev_probe = c->probe_dev || c->probe_dev_stale;  // device-built probe table: rebuilt on the device
+    bool rebuild16 = false;
+    for (uint32_t i : c->dirty_slots) {
+        const DirSlot& d = c->table[i];
+        if (d.state != SLOT_FULL) continue;
+        if (p16 || dev_probe) {
+            uint32_t t = 0;
+            while (t < c->hp.n_probe_types && c->hp.probe_tcd[t] != d.tcd) ++t;
+            if (d.n0 != 0) {
+                rebuild16 = p16;
+            } else if (t == c->hp.n_probe_types) {
+                if (t < kProbeTypes) {  // a new long-key type: append it to the list
+                    c->hp.probe_tcd[t] = d.tcd;
+                    c->hp.n_probe_types = t + 1;
+                    c->params_dirty = true;
+                } else {
+                    rebuild16 = p16;
+                }
+            }
+        }
+        if (p8 && (c->hp.n_probe_types != 1 || !fits8(d))) p8 = false;
+    }
+    if (c->hp.n_probe_types != 1) p8 = false;
+    c->probe8_valid = p8;
+    if (rebuild16) p16 = false;
+    const size_t bytes = m * (sizeof(DirSlot) + sizeof(ProbeSlot) + sizeof(uint2) + 4);
+    if (bytes > c->patch_cap) {
+        if (c->d_patch_data) (void)hipFree(c->d_patch_data);
+        c->d_patch_data = nullptr;
+        c->patch_cap = 0;
+        ORL_HIP(c, hipMalloc(&c->d_patch_data, bytes));
+        c->patch_cap = bytes;
+    }
+    std::vector<uint8_t> h(bytes);
+    DirSlot* hs = reinterpret_cast<DirSlot*>(h.data());
+    ProbeSlot* h16 = reinterpret_cast<ProbeSlot*>(h.data() + m * sizeof(DirSlot));
+    uint2* h8 = reinterpret_cast<uint2*>(h.data() + m * (sizeof(DirSlot) + sizeof(ProbeSlot)));
+    uint32_t* hi = reinterpret_cast<uint32_t*>(h.data() + m * (sizeof(DirSlot) + sizeof(ProbeSlot) + sizeof(uint2)));
+    for (size_t k = 0; k < m; ++k) {
+        const DirSlot& d = c->table[c->dirty_slots[k]];
+        uint32_t t = 0;
+        if (d.state == SLOT_FULL)
+            while (t + 1 < c->hp.n_probe_types && c->hp.probe_tcd[t] != d.tcd) ++t;
+        hs[k] = d;
+        h16[k] = probe16_of(d, t);
+        h8[k] = probe8_of(d);
+        hi[k] = c->dirty_slots[k];
+    }
+    uint8_t* dd = static_cast<uint8_t*>(c->d_patch_data);
+    ORL_HIP(c, hipMemcpy(dd, h.data(), bytes, hipMemcpyHostToDevice));
+    int e = launch_dir_patch(reinterpret_cast<const uint32_t*>(dd + m * (sizeof(DirSlot) + sizeof(ProbeSlot) + sizeof(uint2))),
+                             reinterpret_cast<const DirSlot*>(dd), reinterpret_cast<const ProbeSlot*>(dd + m * sizeof(DirSlot)),
+                             reinterpret_cast<const uint2*>(dd + m * (sizeof(DirSlot) + sizeof(ProbeSlot))), (uint32_t)m,
+                             c->d_table, p16 ? c->d_probe : nullptr, p8 ? c->d_probe8 : nullptr, c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "directory patch launch");
+    ORL_HIP(c, hipStreamSynchronize(c->stream));
+    const uint64_t st[3] = {c->count, c->tombs, 0};
+    ORL_HIP(c, hipMemcpy(c->d_dirstate, st, sizeof st, hipMemcpyHostToDevice));
+    c->count_ub = c->count;
+    c->tombs_ub = c->tombs;
+    clear_dirty_slots(c);
+    ++c->n_patches;
+    if (dev_probe) {  // the device rebuild (next route launch) reads the patched table with the updated type list
+        c->probe_dev = false;
+        c->probe_dev_stale = true;
+    } else if (rebuild16) {
+        if (int r = upload_probe(c)) return r;
+    }
+    return ORL_OK;
+}
+
+bool state_dirty(const orl_ctx* c) {
+    return c->silo_hash_dirty || c->vr_dirty || c->silo_addr_dirty || c->gt_dirty || c->dir_dirty || c->params_dirty ||
+           !c->dirty_slots.empty();
+}
+
 int sync_device_state(orl_ctx* c) {
     if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (!state_dirty(c)) return ORL_OK;
+    // A batch launched earlier on any stream may still be reading the tables and params below: wait for the device
+    // before overwriting them, so membership / registration changes take effect between batches.
+    // Uploads happen only after host-side changes, never per batch.
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());
     if (c->silo_hash_dirty) {
         ORL_HIP(c, hipMemcpy(c->d_silo_hash, c->silo_hash, sizeof c->silo_hash, hipMemcpyHostToDevice));
         ORL_HIP(c, hipMemcpy(c->d_silo_known, c->silo_known, sizeof c->silo_known, hipMemcpyHostToDevice));
@@ -434,9 +546,13 @@ int sync_device_state(orl_ctx* c) {
         const uint64_t st[3] = {c->count, c->tombs, 0};
         ORL_HIP(c, hipMemcpy(c->d_dirstate, st, sizeof st, hipMemcpyHostToDevice));
         c->dir_dirty = false;
+        ++c->n_full_uploads;
+        if (!c->slot_marked.empty()) clear_dirty_slots(c);
         c->count_ub = c->count;
         c->tombs_ub = c->tombs;
         if (int r = upload_probe(c)) return r;
+    } else if (!c->dirty_slots.empty()) {
+        if (int r = patch_dirty_slots(c)) return r;
     }
     if (c->params_dirty) {  // last: upload_probe sets the probe type list
         ORL_HIP(c, hipMemcpy(c->d_params, &c->hp, sizeof(RouteParams), hipMemcpyHostToDevice));
@@ -542,7 +658,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp);
+    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -795,7 +911,7 @@ int orl_dir_insert_single(orl_ctx* c, const orl_grain_key* keys, const uint32_t*
                     d.tcd = k.type_code_data; d.n0 = k.n0; d.n1 = k.n1;
                     d.act = acts[i]; d.silo = silos[i]; d.state = SLOT_FULL; d.pad = 0;
                     ++c->count;
-                    c->dir_dirty = true;
+                    mark_slot(c, (uint64_t)fr);
                     st = ORL_INS_INSERTED;
                     a = acts[i];
                     s = silos[i];
@@ -818,7 +934,7 @@ int orl_dir_remove(orl_ctx* c, const orl_grain_key* keys, size_t n, uint8_t* rem
             c->table[at].state = SLOT_TOMB;
             --c->count;
             ++c->tombs;
-            c->dir_dirty = true;
+            mark_slot(c, (uint64_t)at);
         }
         if (removed) removed[i] = at >= 0 ? 1 : 0;
     }
@@ -1459,6 +1575,19 @@ int orl_sync(orl_ctx* c) {
     if (!c->device_mode) return ORL_OK;
     ORL_HIP(c, hipStreamSynchronize(c->stream));
     return ORL_OK;
+}
+
+int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
+    if (!c || !v) return ORL_E_INVALID;
+    if (int r = sync_device_state(c)) return r;
+    switch (what) {
+        case ORL_Q_PROBE_FORM:
+            *v = c->probe8_valid ? 8 : c->probe_valid ? 16 : (c->probe_dev || c->probe_dev_stale) ? 17 : 32;
+            return ORL_OK;
+        case ORL_Q_FULL_UPLOADS: *v = c->n_full_uploads; return ORL_OK;
+        case ORL_Q_SLOT_PATCHES: *v = c->n_patches; return ORL_OK;
+        default: return fail(c, ORL_E_INVALID, "unknown query %u", what);
+    }
 }
 
 int orl_set_timing(orl_ctx* c, int enable) {

@@ -237,6 +237,9 @@ struct Scratch {
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
+// Host-changed slots of the partition: dir[idx[k]] = slots[k]; probe / probe8 (when non-null) patched alike.
+int launch_dir_patch(const uint32_t* d_idx, const DirSlot* d_slots, const ProbeSlot* d_p16, const uint2* d_p8, uint32_t n,
+                     DirSlot* d_dir, ProbeSlot* d_probe, uint2* d_probe8, void* stream);
 // Compact probe table from the device partition (after device mutations), with the type list in d_params;
 // *d_bad = 1 when a FULL slot is not a long key of a listed type.
 int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* d_params, ProbeSlot* d_probe,

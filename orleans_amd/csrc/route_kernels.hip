@@ -326,6 +326,19 @@ __global__ __launch_bounds__(256) void k_probe_build(const DirSlot* __restrict__
     if (miss) atomicOr(bad, 1u);
 }
 
+// Host-changed slots (a small registration batch through the host mirror), patched in place.
+__global__ __launch_bounds__(256) void k_dir_patch(const uint32_t* __restrict__ idx, const DirSlot* __restrict__ slots,
+                                                   const ProbeSlot* __restrict__ p16, const uint2* __restrict__ p8, uint32_t n,
+                                                   DirSlot* __restrict__ dir, ProbeSlot* __restrict__ probe,
+                                                   uint2* __restrict__ probe8) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t i = idx[k];
+    dir[i] = slots[k];
+    if (probe) probe[i] = p16[k];
+    if (probe8) probe8[i] = p8[k];
+}
+
 // ---------------------------------------------------------------------------------------------------
 // stage 1 alone
 __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ out) {
@@ -556,8 +569,11 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 // counts), so every histogram write and every offset read is one coalesced row.  The column scan below
 // turns the count matrix in place into global output bases: M[t][d] = sum_{d'<d} total[d'] + sum_{t'<t} M[t'][d].
 // Pass 0's histogram is built by k_route itself; later passes read the previous pass's {key, index} pairs.
-__global__ __launch_bounds__(256) void k_hist_pairs(const uint2* __restrict__ pairs, uint32_t n, uint32_t shift, uint32_t bins,
-                                                    uint32_t* __restrict__ tile_hist) {
+// ACTS: the input is activation handles (clamped to the unresolved bucket n_act) instead of {key, index} pairs: the
+// first digit's histogram for stage 4 over messages routed earlier (orl_bucket_device, the host side of hop 2).
+template <bool ACTS>
+__global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
+                                                    uint32_t bins, uint32_t* __restrict__ tile_hist) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
     __syncthreads();
@@ -566,7 +582,8 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const uint2* __restrict__ pa
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
         const uint32_t e = base + j * 256 + threadIdx.x;
-        k[j] = pairs[e < n ? e : n - 1].x;
+        const uint32_t ec = e < n ? e : n - 1;
+        k[j] = ACTS ? bucket_key(static_cast<const uint32_t*>(in)[ec], n_act) : static_cast<const uint2*>(in)[ec].x;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j)
@@ -1131,9 +1148,13 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     const uint32_t rtile = kRouteThreads * items;
     const uint32_t base = blockIdx.x * rtile;
-    const uint32_t last = ((n - base) < rtile ? n : base + rtile) - 1;
+    // n is the caller's total (ORL_OPT_TOTAL_GIVEN) or the scanned one; messages past the scanned total (an overstated
+    // total) get ORL_ST_PAST_TOTAL and never index the CSR / publisher arrays
+    const uint32_t real = poff32[n_pub];
+    const uint32_t lim = n < real ? n : real;
+    const uint32_t last = ((lim - base) < rtile ? lim : base + rtile) - 1;
     // publisher of emitted message e = upper_bound(poff32[0..n_pub], e) - 1
-    if (threadIdx.x == 0 || threadIdx.x == 64) {
+    if (base < lim && (threadIdx.x == 0 || threadIdx.x == 64)) {
         const uint32_t v = threadIdx.x == 0 ? base : last;
         uint32_t lo = 0, hi = n_pub + 1;
         while (lo < hi) {
@@ -1143,10 +1164,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         sm.prange[threadIdx.x == 0 ? 0 : 1] = lo - 1;
     }
     __syncthreads();
-    const uint32_t p_lo = sm.prange[0], p_hi = sm.prange[1];
+    const uint32_t p_lo = base < lim ? sm.prange[0] : 0u, p_hi = base < lim ? sm.prange[1] : 0u;
     const uint32_t span = p_hi - p_lo + 1;  // publishers touching this tile
     const bool in_lds = span <= kFanLds;
-    if (in_lds)
+    if (in_lds && base < lim)
         for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
@@ -1154,6 +1175,12 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads + threadIdx.x;
         if (e >= n) break;
+        if (e >= lim) {  // past the emitted total: no message
+            route[e] = pack_route(0xFFu, 0xFFu, ORL_ST_PAST_TOTAL, 0u);
+            act_out[e] = ORL_NO_ACT;
+            if (HIST) atomicAdd(&sm.hist[(n_act >> shift) & (bins - 1)], 1u);
+            continue;
+        }
         uint32_t lo, hi, p, start;
         if (in_lds) {
             lo = 0; hi = span + 1;
@@ -1344,16 +1371,55 @@ constexpr uint32_t kPartItems = 8;
 constexpr uint32_t kPartTile = kRouteThreads * kPartItems;
 constexpr uint32_t kLbSpinLimit = 1u << 24;
 
-struct PartLbSmem {
-    RouteParams P;
-    uint8_t rank_of_silo[256];
+struct LbShared {
     uint32_t cnt[kWaves][8];   // per-wave running counts, then per-wave bases inside the tile
     uint32_t base[8];          // exclusive prefix of this tile per rank
     uint32_t tile;
 };
 
+struct PartLbSmem {
+    RouteParams P;
+    uint8_t rank_of_silo[256];
+    LbShared lb;
+};
+
 __device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_t value) {
     __hip_atomic_store(g, ((uint64_t)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// After every wave ranked its elements (lb.cnt = per-wave counts per rank): one lane per rank turns the wave counts
+// into wave bases inside the tile, publishes the tile's aggregate, looks back over the earlier tiles' granules until
+// an inclusive one, publishes its own inclusive count and leaves the tile's exclusive prefix in lb.base[r]; the last
+// tile writes the per-rank totals.  Call between two __syncthreads().
+__device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restrict__ state, uint32_t nranks, uint32_t ntiles,
+                                               uint64_t* __restrict__ counts) {
+    if (threadIdx.x >= nranks) return;
+    uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
+    const uint32_t r = threadIdx.x, t = lb.tile;
+    uint32_t tc = 0;
+    for (uint32_t q = 0; q < kWaves; ++q) {
+        const uint32_t c = lb.cnt[q][r];
+        lb.cnt[q][r] = tc;
+        tc += c;
+    }
+    store_granule(status + (size_t)t * 8 + r, 1u, tc);
+    uint32_t before = 0;
+    for (int64_t tt = (int64_t)t - 1; tt >= 0; --tt) {
+        uint64_t v;
+        uint32_t spins = 0;
+        while (((v = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0) {
+            if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
+                atomicOr(&state[1], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        before += (uint32_t)v;
+        if ((v >> 32) == 2u || spins > kLbSpinLimit) break;
+    }
+    store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
+    lb.base[r] = before;
+    if (t == ntiles - 1) counts[r] = before + tc;
 }
 
 // COMPACT: write orl_wire_msg records (16 B) and set *wire_status = 1 if a message has no compact form.
@@ -2168,8 +2234,8 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t row_step = (p == 0) ? row_step0 : 1u;
         const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
         if (p > 0)
-            hipLaunchKernelGGL(k_hist_pairs, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, (uint32_t)plan.shift[p], bins,
-                               s.tile_hist);
+            hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
+                               (uint32_t)plan.shift[p], bins, s.tile_hist);
         col_scan(s.tile_hist, nrows, bins, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
@@ -2187,6 +2253,14 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_hash, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_keys, (uint32_t)n, d_out);
+    return (int)hipGetLastError();
+}
+
+int launch_dir_patch(const uint32_t* d_idx, const DirSlot* d_slots, const ProbeSlot* d_p16, const uint2* d_p8, uint32_t n,
+                     DirSlot* d_dir, ProbeSlot* d_probe, uint2* d_probe8, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_dir_patch, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_idx, d_slots, d_p16, d_p8, n,
+                       d_dir, d_probe, d_probe8);
     return (int)hipGetLastError();
 }
 

@@ -472,6 +472,12 @@ class GrainDirectoryEngine:
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 
+    def query(self, what: int) -> int:
+        """orl_ctx_query: L.Q_PROBE_FORM (8 / 16 / 17 / 32), L.Q_FULL_UPLOADS, L.Q_SLOT_PATCHES."""
+        v = C.c_uint64()
+        self._ck(self._lib.orl_ctx_query(self._ctx, int(what), C.byref(v)))
+        return v.value
+
     def set_timing(self, enable: bool) -> None:
         self._ck(self._lib.orl_set_timing(self._ctx, 1 if enable else 0))
 

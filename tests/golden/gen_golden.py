@@ -301,6 +301,42 @@ def gen_chirper(graphml: str):
                         order=np.array(bucket_order, np.uint32), offsets=np.array(offsets, np.uint32))
 
 
+def gen_chirper_generated(n_accounts: int = 1000, followers: int = 10):
+    """BASELINE config 1: the ChirperNetworkGenerator graph in its deterministic mode
+    (Samples/Chirper/NetworkGenerator/ChirperNetworkGenerator.cs:306-345, node / edge / edge-node ids start at 1:
+    source = rel / k + 1, target = (rel / k + 1 + rel % k) % n + 1; source != target always, so the random
+    replacement never runs) on ONE silo (10.0.0.1:11111, generation 1).  Every account publishes once: 10k routed
+    messages.  Activation handle of account id v = v - 1."""
+    e = np.arange(n_accounts * followers, dtype=np.int64)
+    rel_src = e // followers
+    src = rel_src + 1
+    tgt = (rel_src + 1 + e % followers) % n_accounts + 1
+    assert (src != tgt).all()
+    pub, fol = tgt - 1, src  # `source follows target`: the target publishes to its followers
+    order = np.argsort(pub, kind="stable")
+    counts = np.bincount(pub, minlength=n_accounts)
+    off = np.zeros(n_accounts + 1, np.uint64)
+    off[1:] = np.cumsum(counts)
+    ftgt = fol[order].astype(np.uint32)  # follower account id (long key)
+    ring = P.Ring()
+    ring.add_server(0, P.silo_consistent_hash("10.0.0.1:11111", 1))
+    view = P.SiloView([True], [True])
+    tc = P.calc_id_hash(P.CHIRPER_ACCOUNT_CLASS)
+    part = P.Partition()
+    for v in range(1, n_accounts + 1):
+        part.add_single_activation(P.key_from_long(v, tc), v - 1, 0, view)
+    follower_tcd = P.type_code_data(P.CAT_GRAIN, tc)
+    msgs = [P.Msg(P.Key(follower_tcd, 0, int(ftgt[j])), 0) for p in range(n_accounts)
+            for j in range(int(off[p]), int(off[p + 1]))]
+    routes, acts = P.route_batch(msgs, ring, part, view)
+    offsets, bucket_order = P.bucket_stable(acts, n_accounts)
+    np.savez_compressed(os.path.join(HERE, "chirper_generated.npz"), csr_off=off, csr_tgt=ftgt,
+                        pubs=np.arange(n_accounts, dtype=np.uint32), pub_silo=np.zeros(n_accounts, np.uint8),
+                        follower_tcd=np.uint64(follower_tcd), silo_hash=np.int32(ring.entries[0][0]),
+                        route=np.array(routes, np.uint32), act=np.array(acts, np.uint32),
+                        order=np.array(bucket_order, np.uint32), offsets=np.array(offsets, np.uint32))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graphml", default=GRAPHML)
@@ -319,6 +355,7 @@ def main():
     functional[5] = 0
     gen_routing("routing_membership", 4096, 16384, 8192, running, functional, P.NULL_SILO, 1, P.POLICY_HASH_SPREAD,
                 0xBEEF)
+    gen_chirper_generated()
     if os.path.exists(args.graphml):
         gen_chirper(args.graphml)
     else:

@@ -1,0 +1,423 @@
+"""GPU parity at the BASELINE workloads (configs 1, 3, 4, 5 of SURVEY §8(d)) and the host-mutation contract.
+
+Each full-size config runs the HIP path (through the C ABI) at its BASELINE size, asserts the size-independent
+properties of the outputs (a permutation grouped by activation, arrival order inside each bucket, offsets = the
+histogram prefix, route words consistent with the directory) and checks a >= 1M-message oracle sample bit for bit
+(config 5's 590k messages per step are checked in full).  All integer work: exact equality, no tolerance.
+"""
+import numpy as np
+import pytest
+
+from oracle import cpu_ref
+from orleans_amd import _lib as L
+from orleans_amd import workloads as W
+from orleans_amd.engine import GrainDirectoryEngine, decode_route
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need an MI355X"
+    return t
+
+
+def _u32(x):
+    return x.cpu().numpy().view(np.uint32)
+
+
+def check_buckets(a, od, of, n_act):
+    """Stage-4 properties for activation handles a[n] (ORL_NO_ACT = unresolved bucket n_act)."""
+    n = len(a)
+    key = np.minimum(a.astype(np.int64), n_act)
+    cnt = np.bincount(key, minlength=n_act + 1)
+    exp_off = np.zeros(n_act + 2, np.int64)
+    exp_off[1:] = np.cumsum(cnt)
+    np.testing.assert_array_equal(of.astype(np.int64), exp_off)
+    assert (np.bincount(od, minlength=n) == 1).all()             # a permutation
+    srt = key[od]
+    assert (np.diff(srt) >= 0).all()                             # grouped by activation
+    same = np.diff(srt) == 0
+    assert (np.diff(od.astype(np.int64))[same] > 0).all()        # arrival order inside a bucket
+
+
+def _oracle_for(cl, keys, acts, silos, n_silos=None):
+    o = cpu_ref.Oracle(n_silos or cl.n_silos)
+    for s in range(n_silos or cl.n_silos):
+        o.add_server(s, int(cl.hashes[s]))
+    o.register(keys, acts, silos)
+    return o
+
+
+# ---- config 1 -----------------------------------------------------------------------------------------------
+def test_config1_chirper_generated_golden(torch, golden_dir):
+    """Config 1: ChirperNetworkGenerator's deterministic graph (ChirperNetworkGenerator.cs:306-345), 1k accounts x 10
+    followers on ONE silo, every account publishes once: 10k fan-out messages == the committed golden."""
+    import os
+    t = torch
+    d = np.load(os.path.join(golden_dir, "chirper_generated.npz"))
+    eng = GrainDirectoryEngine(n_act=1000, dir_capacity=1000, max_batch=1 << 15, device=0)
+    eng.set_silos(1)
+    eng.add_server(0, int(d["silo_hash"]))
+    keys = np.zeros(1000, L.KEY_DTYPE)
+    keys["tcd"] = int(d["follower_tcd"])
+    keys["n1"] = np.arange(1, 1001, dtype=np.uint64)
+    st, _, _ = eng.register_single_activation(keys, np.arange(1000, dtype=np.uint32), np.zeros(1000, np.uint8))
+    assert (st == L.INS_INSERTED).all()
+    dv = "cuda"
+    n = len(d["route"])
+    outs = [t.empty(n, dtype=t.int32, device=dv) for _ in range(3)]
+    off = t.empty(1002, dtype=t.int32, device=dv)
+    poff = t.empty(1001, dtype=t.int64, device=dv)
+    got = eng.fanout_device(t.from_numpy(d["csr_off"].astype(np.int64)).to(dv),
+                            t.from_numpy(d["csr_tgt"].astype(np.int32)).to(dv),
+                            t.from_numpy(d["pubs"].astype(np.int32)).to(dv), t.from_numpy(d["pub_silo"]).to(dv), 1000,
+                            int(d["follower_tcd"]), poff, *outs, off, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    assert got == n == 10_000
+    for x, k in zip(outs + [off], ("route", "act", "order", "offsets")):
+        np.testing.assert_array_equal(_u32(x), d[k], err_msg=k)
+    eng.close()
+
+
+# ---- host-side directory changes vs batches in flight ----------------------------------
+def test_host_mutation_waits_for_inflight_batch(torch):
+    """A host registration / unregistration issued while a routed batch is still running on a side stream must not
+    change that batch's decisions (the upload waits for the device); the next batch sees the change."""
+    t = torch
+    cl = W.default_cluster()
+    n_grains, n = 1_000_000, 32 << 20
+    eng = GrainDirectoryEngine(n_act=2 * n_grains, dir_capacity=2 * n_grains, max_batch=n, device=0)
+    W.setup_engine(eng, cl)
+    keys, uni, owner, reg = W.grain_population(cl, 2 * n_grains)
+    o = _oracle_for(cl, keys[:n_grains], np.arange(n_grains, dtype=np.uint32), owner[:n_grains])
+    eng.register_single_activation(keys[:n_grains], np.arange(n_grains, dtype=np.uint32), owner[:n_grains])
+    msgs = W.uniform_messages(cl, 2 * n_grains, n, seed=4)  # half the targets unregistered yet
+    d_in = t.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
+    s = t.cuda.Stream()
+    outs = [[t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)] + [t.empty(2 * n_grains + 2, dtype=t.int32,
+                                                                                      device="cuda")] for _ in range(3)]
+    samp = np.random.default_rng(1).choice(n, 1_000_000, replace=False)
+    refs = [o.route(msgs[samp])]
+    # (1) a small unregistration (slot patch) right behind batch 0; (2) a bulk registration (full upload) behind batch 1
+    eng.address_messages_device(d_in, n, *outs[0], stream=s.cuda_stream)
+    rm = keys[:100_000]
+    eng.unregister(rm)
+    o.unregister(rm)
+    refs.append(o.route(msgs[samp]))
+    eng.address_messages_device(d_in, n, *outs[1], stream=s.cuda_stream)
+    new = np.arange(n_grains, 2 * n_grains)
+    eng.register_single_activation(keys[new], new.astype(np.uint32), owner[new])
+    o.register(keys[new], new.astype(np.uint32), owner[new])
+    refs.append(o.route(msgs[samp]))
+    eng.address_messages_device(d_in, n, *outs[2], stream=s.cuda_stream)
+    s.synchronize()
+    assert eng.query(L.Q_SLOT_PATCHES) >= 1 and eng.query(L.Q_FULL_UPLOADS) >= 2
+    for b in range(3):
+        r = _u32(outs[b][0])
+        np.testing.assert_array_equal(r[samp], refs[b][0], err_msg=f"batch {b}")
+        np.testing.assert_array_equal(_u32(outs[b][1])[samp], refs[b][1], err_msg=f"batch {b}")
+    eng.close()
+
+
+# ---- incremental slot uploads and the probe-table forms -----------------------------------
+def test_incremental_slot_patches_vs_oracle(torch):
+    """Small host registration batches are uploaded as slot patches (no whole-table upload), and the compact
+    probe forms follow them: 8-B while one type with 32-bit ids fits, 16-B after an id >= 2^32 - 2 or a second
+    type, the 32-B table after a Guid key; routing == the oracle after every step."""
+    cl = W.default_cluster()
+    n_grains = 30_000
+    eng = GrainDirectoryEngine(n_act=1 << 16, dir_capacity=4 * n_grains, max_batch=1 << 18, device=0)
+    W.setup_engine(eng, cl)
+    o = cpu_ref.Oracle(cl.n_silos)
+    for s in range(cl.n_silos):
+        o.add_server(s, int(cl.hashes[s]))
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+
+    def register(k, a, s):
+        st_e, wa_e, _ = eng.register_single_activation(k, a, s)
+        st_o, wa_o, _ = o.register(k, a, s)
+        np.testing.assert_array_equal(st_e, st_o)
+        np.testing.assert_array_equal(wa_e, wa_o)
+
+    def route_check(seed, extra=None):
+        m = W.uniform_messages(cl, n_grains + 1000, 200_000, seed=seed)
+        if extra is not None:
+            m = np.concatenate([m, extra])
+        res = eng.address_messages(m)
+        r, a = o.route(m)
+        np.testing.assert_array_equal(res.route, r)
+        np.testing.assert_array_equal(res.act, a)
+        order, off = o.bucket(a, 1 << 16)
+        np.testing.assert_array_equal(res.order, order)
+        np.testing.assert_array_equal(res.offsets, off)
+
+    register(keys[:20_000], np.arange(20_000, dtype=np.uint32), owner[:20_000])
+    route_check(0)
+    assert eng.query(L.Q_PROBE_FORM) == 8
+    full0, p0 = eng.query(L.Q_FULL_UPLOADS), eng.query(L.Q_SLOT_PATCHES)
+    for b in range(5):  # small batches: patches
+        lo = 20_000 + 2000 * b
+        register(keys[lo:lo + 2000], np.arange(lo, lo + 2000, dtype=np.uint32), owner[lo:lo + 2000])
+        o.unregister(keys[b * 700:(b + 1) * 700])
+        eng.unregister(keys[b * 700:(b + 1) * 700])
+        route_check(b + 1)
+    assert eng.query(L.Q_FULL_UPLOADS) == full0 and eng.query(L.Q_SLOT_PATCHES) == p0 + 5
+    assert eng.query(L.Q_PROBE_FORM) == 8
+    # an id that does not fit the 8-B form (N1 >= 2^32 - 2) and messages sharing its low 32 bits
+    from orleans_amd.engine import grain_keys_from_longs, grain_keys_from_guid_bytes
+    kb = grain_keys_from_longs(cl.type_code, np.array([(1 << 33) + 5, 0xFFFFFFFE], np.int64))
+    ob = cl.owner_of(W.jenkins3_np(kb["tcd"], kb["n0"], kb["n1"]))
+    register(kb, np.array([60_001, 60_002], np.uint32), ob)
+    assert eng.query(L.Q_PROBE_FORM) == 16
+    ex = np.zeros(4, L.MSG_DTYPE)
+    ex["tcd"] = kb["tcd"][0]
+    ex["n1"] = [(1 << 33) + 5, 5, 0xFFFFFFFE, (1 << 32) + 0xFFFFFFFE]
+    ex["category"] = 2
+    route_check(10, ex)
+    # a second grain type: still 16-B (two types listed)
+    k2 = grain_keys_from_longs(cl.type_code ^ 0x5A5A, np.arange(100, dtype=np.int64))
+    o2 = cl.owner_of(W.jenkins3_np(k2["tcd"], k2["n0"], k2["n1"]))
+    register(k2, np.arange(61_000, 61_100, dtype=np.uint32), o2)
+    assert eng.query(L.Q_PROBE_FORM) == 16
+    ex2 = np.zeros(100, L.MSG_DTYPE)
+    ex2["tcd"], ex2["n1"], ex2["category"] = k2["tcd"], k2["n1"], 2
+    route_check(11, ex2)
+    # a Guid key (N0 != 0): the full 32-B table
+    kg = grain_keys_from_guid_bytes(cl.type_code, np.arange(32, dtype=np.uint8).reshape(2, 16))
+    og = cl.owner_of(W.jenkins3_np(kg["tcd"], kg["n0"], kg["n1"]))
+    register(kg, np.array([62_000, 62_001], np.uint32), og)
+    assert eng.query(L.Q_PROBE_FORM) == 32
+    exg = np.zeros(2, L.MSG_DTYPE)
+    exg["tcd"], exg["n0"], exg["n1"], exg["category"] = kg["tcd"], kg["n0"], kg["n1"], 2
+    route_check(12, exg)
+    eng.close()
+
+
+def test_probe8_sentinel_edges(torch):
+    """The 8-B probe form at its edges: a registered N1 = 0xFFFFFFFD with handle 2^24 - 1 keeps the 8-B form; messages
+    with N1 = 0xFFFFFFFE / 0xFFFFFFFF (the empty / tombstone keys) and N1 sharing the low 32 bits of a registered id
+    route as the oracle does."""
+    from orleans_amd.engine import grain_keys_from_longs
+    cl = W.default_cluster()
+    n_act = 1 << 24
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=4096, max_batch=1 << 16, device=0)
+    W.setup_engine(eng, cl)
+    ids = np.array(list(range(1000)) + [0xFFFFFFFD, 0xFFFFFFFC], np.int64)
+    k = grain_keys_from_longs(cl.type_code, ids)
+    own = cl.owner_of(W.jenkins3_np(k["tcd"], k["n0"], k["n1"]))
+    acts = np.arange(len(ids), dtype=np.uint32)
+    acts[-2] = n_act - 1
+    eng.register_single_activation(k, acts, own)
+    o = _oracle_for(cl, k, acts, own)
+    assert eng.query(L.Q_PROBE_FORM) == 8
+    eng.unregister(k[5:10])  # tombstones on some chains
+    o.unregister(k[5:10])
+    m = np.zeros(20_000, L.MSG_DTYPE)
+    m["tcd"] = k["tcd"][0]
+    m["category"] = 2
+    m["sending_silo"] = np.arange(20_000) % 8
+    cand = np.array([0xFFFFFFFE, 0xFFFFFFFF, 0xFFFFFFFD, 0xFFFFFFFC, (1 << 32) + 0xFFFFFFFD, (1 << 32) + 3, 3, 7, 1001,
+                     (1 << 40) | 0xFFFFFFFF], np.uint64)
+    m["n1"] = cand[np.arange(20_000) % len(cand)]
+    res = eng.address_messages(m)
+    r, a = o.route(m)
+    np.testing.assert_array_equal(res.route, r)
+    np.testing.assert_array_equal(res.act, a)
+    assert (res.act == n_act - 1).sum() == 2000  # the 2^24 - 1 handle is found
+    assert eng.query(L.Q_PROBE_FORM) == 8
+    eng.close()
+
+
+def test_fanout_overstated_total(torch):
+    """ORL_OPT_TOTAL_GIVEN with a total larger than the CSR emits: indices past the real total get ORL_ST_PAST_TOTAL
+    and the unresolved bucket (no CSR / publisher access past the end); the real messages are unchanged."""
+    t = torch
+    cl = W.default_cluster()
+    n_acc = 50_000
+    off, tgt = W.powerlaw_csr(n_acc)
+    from orleans_amd.engine import grain_keys_from_longs
+    keys = grain_keys_from_longs(cl.type_code, np.arange(n_acc, dtype=np.int64))
+    owner = cl.owner_of(W.jenkins3_np(keys["tcd"], keys["n0"], keys["n1"]))
+    pubs = (W.stream(7, 0, 3000) % np.uint64(n_acc)).astype(np.uint32)
+    real = int(np.diff(off.astype(np.int64))[pubs].sum())
+    extra = 5000
+    eng = GrainDirectoryEngine(n_act=n_acc, dir_capacity=n_acc, max_batch=real + extra + 1, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, keys, owner, np.ones(n_acc, bool))
+    dv = "cuda"
+    args = [t.from_numpy(off.view(np.int64)).to(dv), t.from_numpy(tgt.view(np.int32)).to(dv),
+            t.from_numpy(pubs.view(np.int32)).to(dv), t.from_numpy(owner[pubs]).to(dv), len(pubs),
+            (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)]
+    res = []
+    for total in (None, real + extra):
+        m = real + extra
+        poff = t.empty(len(pubs) + 1, dtype=t.int64, device=dv)
+        outs = [t.full((m,), -3, dtype=t.int32, device=dv) for _ in range(3)]
+        of = t.empty(n_acc + 2, dtype=t.int32, device=dv)
+        eng.fanout_device(*args, poff, *outs, of, stream=t.cuda.current_stream().cuda_stream, total=total)
+        t.cuda.synchronize()
+        res.append([_u32(x) for x in outs] + [_u32(of)])
+    (r0, a0, o0, f0), (r1, a1, o1, f1) = res
+    np.testing.assert_array_equal(r1[:real], r0[:real])
+    np.testing.assert_array_equal(a1[:real], a0[:real])
+    assert (decode_route(r1[real:]).status == L.ST_PAST_TOTAL).all()
+    assert (a1[real:] == L.NO_ACT).all()
+    check_buckets(a1, o1, f1, n_acc)
+    np.testing.assert_array_equal(f1[:n_acc + 1], f0[:n_acc + 1])
+    eng.close()
+
+
+# ---- config 3: Zipf(1.1) over 16M grains, 24-bit handles (LSD stage 4) ---------------------------------------
+def test_config3_full_size_zipf(torch):
+    """BASELINE config 3 on one GPU: 16M long-key grains, 64M messages, targets Zipf(1.1) through a seeded
+    permutation (hot activations), activation handles up to 2^24 (the LSD bucketing path)."""
+    t = torch
+    n_grains, n = 16_000_000, 64 << 20
+    cl = W.balanced_cluster()
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=n, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, keys, owner, reg)
+    msgs = W.zipf_messages(cl, n_grains, n)
+    d_in = t.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
+    outs = [t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)]
+    off = t.empty(n_grains + 2, dtype=t.int32, device="cuda")
+    eng.address_messages_device(d_in, n, *outs, off, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    del d_in
+    r, a, od, of = (_u32(x) for x in outs + [off])
+    tg = msgs["n1"].astype(np.int64)
+    np.testing.assert_array_equal(a, tg.astype(np.uint32))  # handle of grain i is i
+    v = decode_route(r)
+    assert (v.status == L.ST_HIT).all()
+    np.testing.assert_array_equal(v.owner, owner[tg])
+    hot = np.bincount(tg, minlength=n_grains).max()
+    assert hot > 1_000_000  # Zipf(1.1): the hottest activation gets > 1M of the 64M messages
+    check_buckets(a, od, of, n_grains)
+    samp = np.random.default_rng(3).choice(n, 1_000_000, replace=False)
+    o = _oracle_for(cl, keys, np.arange(n_grains, dtype=np.uint32), owner)
+    ro, ao = o.route(msgs[samp])
+    np.testing.assert_array_equal(r[samp], ro)
+    np.testing.assert_array_equal(a[samp], ao)
+    eng.close()
+
+
+# ---- config 4: 10M-account power-law CSR fan-out --------------------------------------------------------------
+def test_config4_full_size_fanout(torch):
+    """BASELINE config 4: 10M accounts, power-law followers (exponent 2.1, 1..1e5), 1M publishers: the fan-out +
+    stages 1-4 on the device; the first >= 1M emitted messages (whole publishers) bit-exact vs the oracle's CSR
+    expansion + routing, the rest by properties."""
+    t = torch
+    n_acc, n_pub = 10_000_000, 1_000_000
+    cl = W.default_cluster()
+    off, tgt = W.powerlaw_csr(n_acc)
+    from orleans_amd.engine import grain_keys_from_longs
+    keys = grain_keys_from_longs(cl.type_code, np.arange(n_acc, dtype=np.int64))
+    owner = cl.owner_of(W.jenkins3_np(keys["tcd"], keys["n0"], keys["n1"]))
+    pubs = (W.stream(W.SEED_C4 ^ 0xB0B, 0, n_pub) % np.uint64(n_acc)).astype(np.uint32)
+    deg = np.diff(off.astype(np.int64))
+    total = int(deg[pubs].sum())
+    eng = GrainDirectoryEngine(n_act=n_acc, dir_capacity=n_acc, max_batch=total + 1, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, keys, owner, np.ones(n_acc, bool))
+    dv = "cuda"
+    poff = t.empty(n_pub + 1, dtype=t.int64, device=dv)
+    outs = [t.empty(total, dtype=t.int32, device=dv) for _ in range(3)]
+    of = t.empty(n_acc + 2, dtype=t.int32, device=dv)
+    tcd = (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+    got = eng.fanout_device(t.from_numpy(off.view(np.int64)).to(dv), t.from_numpy(tgt.view(np.int32)).to(dv),
+                            t.from_numpy(pubs.view(np.int32)).to(dv), t.from_numpy(owner[pubs]).to(dv), n_pub, tcd, poff,
+                            *outs, of, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    assert got == total > 5_000_000
+    r, a, od, f = (_u32(x) for x in outs + [of])
+    pf = poff.cpu().numpy()
+    exp_poff = np.zeros(n_pub + 1, np.int64)
+    exp_poff[1:] = np.cumsum(deg[pubs])
+    np.testing.assert_array_equal(pf, exp_poff)
+    # every emitted follower is a registered account: handle = follower id, host = owner
+    fol = np.concatenate([tgt[int(off[p]):int(off[p + 1])] for p in pubs[:1]])  # shape check of the first publisher
+    np.testing.assert_array_equal(a[:len(fol)], fol)
+    v = decode_route(r)
+    assert (v.status == L.ST_HIT).all()
+    np.testing.assert_array_equal(v.owner, owner[a.astype(np.int64)])
+    check_buckets(a, od, f, n_acc)
+    # oracle: whole publishers until >= 1M emitted messages
+    k = int(np.searchsorted(exp_poff, 1_000_000)) + 1
+    exp, _ = cpu_ref.fanout_expand(off, tgt, pubs[:k], owner[pubs[:k]], tcd)
+    o = _oracle_for(cl, keys, np.arange(n_acc, dtype=np.uint32), owner)
+    ro, ao = o.route(exp)
+    m = len(exp)
+    assert m >= 1_000_000
+    np.testing.assert_array_equal(r[:m], ro)
+    np.testing.assert_array_equal(a[:m], ao)
+    eng.close()
+
+
+# ---- config 5: Presence heartbeats, 64k batches, eager and hipGraph --------------------------------------------
+def test_config5_full_size_presence(torch):
+    """BASELINE config 5: 100k Guid-keyed games x 8 players, one 64k-heartbeat batch = 64k game messages + 512k
+    player messages (fan-out through the player key table), checked in full vs the oracle, eagerly and replayed from a
+    captured hipGraph."""
+    t = torch
+    cl = W.default_cluster()
+    n_games, per_game, n_hb = 100_000, 8, 64 * 1024
+    pr = W.presence_population(n_games, per_game)
+    all_keys = np.concatenate([pr.game_keys, pr.player_keys])
+    n_keys = len(all_keys)
+    owner = cl.owner_of(W.jenkins3_np(all_keys["tcd"], all_keys["n0"], all_keys["n1"]))
+    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_hb * per_game, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, all_keys, owner, np.ones(n_keys, bool))
+    o = _oracle_for(cl, all_keys, np.arange(n_keys, dtype=np.uint32), owner)
+    games, gm = W.heartbeat_batch(pr, cl, n_hb, 0)
+    gsilo = owner[games.astype(np.int64)]
+    exp, poff_ref = cpu_ref.fanout_expand(pr.csr_off, pr.csr_tgt, games, gsilo, 0)
+    kk = pr.player_keys[exp["n1"].astype(np.int64)]
+    exp["tcd"], exp["n0"], exp["n1"] = kk["tcd"], kk["n0"], kk["n1"]
+    r1, a1 = o.route(gm)
+    o1, f1 = o.bucket(a1, n_keys)
+    r2, a2 = o.route(exp)
+    o2, f2 = o.bucket(a2, n_keys)
+    dv = "cuda"
+    d_gm = t.from_numpy(gm.view(np.int32).reshape(-1, 8)).to(dv)
+    d_off = t.from_numpy(pr.csr_off.view(np.int64)).to(dv)
+    d_tgt = t.from_numpy(pr.csr_tgt.view(np.int32)).to(dv)
+    d_keys = t.from_numpy(pr.player_keys.view(np.uint8).reshape(-1, 24)).to(dv)
+    d_g = t.from_numpy(games.view(np.int32)).to(dv)
+    d_s = t.from_numpy(gsilo).to(dv)
+    n_fan = n_hb * per_game
+    g1 = [t.empty(n_hb, dtype=t.int32, device=dv) for _ in range(3)] + [t.empty(n_keys + 2, dtype=t.int32, device=dv)]
+    g2 = [t.empty(n_fan, dtype=t.int32, device=dv) for _ in range(3)] + [t.empty(n_keys + 2, dtype=t.int32, device=dv)]
+    poff = t.empty(n_hb + 1, dtype=t.int64, device=dv)
+    s = t.cuda.Stream()
+
+    def step():
+        eng.address_messages_device(d_gm, n_hb, *g1, stream=s.cuda_stream)
+        eng.fanout_keys_device(d_off, d_tgt, d_keys, d_g, d_s, n_hb, poff, *g2[:3], g2[3], stream=s.cuda_stream,
+                               total=n_fan)
+
+    def check():
+        for x, e in zip(g1, (r1, a1, o1, f1)):
+            np.testing.assert_array_equal(_u32(x), e)
+        for x, e in zip(g2, (r2, a2, o2, f2)):
+            np.testing.assert_array_equal(_u32(x), e)
+        np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), poff_ref)
+
+    with t.cuda.stream(s):
+        step()
+    s.synchronize()
+    check()
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g, stream=s):
+        step()
+    for x in g1 + g2:
+        x.fill_(-1)
+    t.cuda.synchronize()
+    with t.cuda.stream(s):
+        g.replay()
+    s.synchronize()
+    check()
+    eng.close()
