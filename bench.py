@@ -1,22 +1,26 @@
 #!/usr/bin/env python3
 """bench.py — routed grain messages/sec on MI355X (BASELINE.json metric), one process per GPU.
 
-Default workload (BASELINE.json configs[1]): 8 logical silos 10.0.0.{1..8}:11111 gen 1,
-1M ChirperAccount long-key grains all registered (activation on the directory owner), 64M single-target
-messages per GPU per step, targets Uniform[0,1M) (splitmix64 seed 0x5EED0002), resident in HBM before the
-timed region.  A step = one pass of the hot path over the batch: stages 1-4 (hash, ring owner, directory
-probe + placement, stable per-activation bucketing).  With N GPUs (torchrun), each GPU hosts silos
-s*N//8 == rank, holds their directory partition, originates 64M messages from its own silos (weak
-scaling) and the step adds the owner partition + RCCL all-to-all exchange.
+Default workload at N=1 (BASELINE.json configs[1]): 8 logical silos 10.0.0.{1..8}:11111
+(balanced generations), 1M ChirperAccount long-key grains all registered (activation on the directory owner), 64M
+single-target messages per step, targets Uniform[0,1M) (splitmix64 seed 0x5EED0002), generated on the device and
+resident in HBM before the timed region.  A step = one pass of the hot path over the batch: stages 1-4 (hash, ring owner,
+directory probe + placement, stable per-activation bucketing).
 
-Other SURVEY §8(d) workloads (measurement legs, recorded under profiles/; not the driver's bench line):
-  --config 3   Zipf(1.1) over 16M grains (seeded permutation), 64M messages per GPU, stages 1-4
-  --config 4   Chirper-scale CSR: 10M accounts, power-law followers (exp 2.1, 1..1e5), 1M publishers per
-               step → fan-out + stages 1-4 (1 GPU)
-  --config 5   Presence: 100k Guid-keyed games x 8 players, 64k heartbeats per step = 64k game messages +
-               512k player messages (fan-out), per-step latency p50/p99, eager and hipGraph-replayed (1 GPU)
+Default at N>1 (torchrun; BASELINE.json configs[2], config 3): Zipf(1.1) over 16M grains, 256M messages in total split
+256M/N per GPU (strong scaling); each GPU hosts silos s*N//8 == rank and their directory partition, originates its share
+from its own silos, and a step runs the node exchange behind the C ABI (orl_node: owner partition, RCCL counts all-gather
++ grouped send/recv, routing at the owner, hop 2, stage 4 at the host).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+Other SURVEY §8(d) workloads (measurement legs recorded under profiles/; not the driver's bench line):
+  --config 1   Chirper generator graph, 1k accounts x 10 followers on one silo, every account publishes (10k messages)
+  --config 2   with N > 1: 64M messages per GPU (weak scaling) through the node exchange
+  --config 3   at N = 1: the whole 256M-message Zipf batch on one GPU
+  --config 4   Chirper-scale CSR: 10M accounts, power-law followers (exp 2.1, 1..1e5), 1M publishers per step
+  --config 5   Presence: 100k Guid-keyed games x 8 players, 64k heartbeats per step, eager and hipGraph-replayed
+  --config 6/7/8   directory mutation (f1), stream / reminder rings (f3), receive path (f2) legs
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..8]
        python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 """
 from __future__ import annotations
@@ -31,6 +35,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+L_NODE_ID_BYTES = 128
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 ROUTE_KERNEL_BYTES_PER_MSG = 72  # 32 B header + 32 B directory slot + 4 B route word + 4 B activation handle
@@ -48,14 +53,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7, 8],
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4, 5, 6, 7, 8],
                     help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches; "
                          "7 = stream / reminder ring leg (f3); 8 = receive path leg (f2): frames -> headers -> route")
     ap.add_argument("--c5-contexts", type=int, default=1, choices=[1, 2],
                     help="config 5: routing contexts/streams per step (2: game messages and fan-out concurrently)")
     ap.add_argument("--frames", type=int, default=4 * 1024 * 1024, help="frames per step (config 8)")
     ap.add_argument("--grains", type=int, default=None)
-    ap.add_argument("--msgs", type=int, default=64 * 1024 * 1024, help="messages per GPU per step (configs 2, 3)")
+    ap.add_argument("--msgs", type=int, default=None,
+                    help="messages per GPU per step (default: config 2 64M per GPU; config 3 256M in total, split over the GPUs)")
+    ap.add_argument("--chunks", type=int, default=4, help="node exchange pipeline depth (N > 1)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--router", action="store_true",
                     help="configs 2/3 at N=1: go through the pipelined multi-GPU router (partition + routing on two "
@@ -74,12 +81,16 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local_rank)
+    if args.config is None:  # the headline: config 2 on one GPU; the 8-GPU config (3, strong scaling) on several
+        args.config = 2 if world == 1 else 3
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if args.config in (4, 5, 6, 7, 8):
-            raise SystemExit("--config 4/5/6/7/8 are single-GPU measurement legs")
+        if args.config in (1, 4, 5, 6, 7, 8):
+            raise SystemExit("--config 1/4/5/6/7/8 are single-GPU measurement legs")
 
-    if args.config in (2, 3):
+    if args.config == 1:
+        res = run_chirper(args, torch)
+    elif args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
     elif args.config == 4:
         res = run_fanout(args, torch)
@@ -139,43 +150,54 @@ def read_traffic(path, msgs_per_launch, world):
 def run_single_target(args, torch, dist, rank, world, local_rank):
     from orleans_amd import workloads as W
     from orleans_amd.engine import GrainDirectoryEngine
-    from orleans_amd.node import HipExecutor, PipelinedRouter, local_silos, rank_of_silo
+    from orleans_amd.node import GrainNode, HipExecutor, PipelinedRouter, local_silos, rank_of_silo
 
     zipf = args.config == 3
     n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
-    n_msgs = args.msgs
+    # config 2: 64M messages per GPU (weak scaling); config 3: 256M messages in total, 256M / N per GPU (strong)
+    strong = zipf and not args.msgs
+    n_total = args.msgs * world if args.msgs else (256 << 20 if zipf else (64 << 20) * world)
+    n_msgs = n_total // world
     # balanced ring (silo generations, W.balanced_cluster): the reference's one-point-per-silo ring with
-    # generation-1 silos gives one of 8 GPUs 2.85x the average share (DESIGN.md §5)
+    # generation-1 silos gives one of 8 GPUs 2.85x the average share (DESIGN.md §6)
     cl = W.balanced_cluster()
     ros = rank_of_silo(cl.n_silos, world)
     mine = local_silos(cl.n_silos, world, rank)
     t_setup = time.perf_counter()
     keys, uni, owner, reg = W.grain_population(cl, n_grains)
-    gen = W.zipf_messages if zipf else W.uniform_messages
     seed = W.SEED_C3 if zipf else W.SEED_C2
-    msgs = gen(cl, n_grains, n_msgs, seed=seed, start=rank * n_msgs, sender_silos=mine if world > 1 else None)
+    ztab = W.zipf_tables(torch, n_grains, seed) if zipf else None
+    # this rank's share of the workload's message stream, generated on the device (== the numpy generators)
+    d_msgs = W.device_messages(torch, cl, n_grains, n_msgs, seed, start=rank * n_msgs,
+                               sender_silos=mine if world > 1 else None, zipf=ztab)
+    torch.cuda.synchronize()
+    node = part_eng = None
     cap = n_msgs
-    if world > 1 or args.router:  # exact receive capacity: every rank's per-destination counts, summed
-        dest = ros[owner[msgs["n1"].astype(np.int64)].astype(np.int64)]
-        per_dest = torch.from_numpy(np.bincount(dest, minlength=world).astype(np.int64)).cuda()
+    local_mask = None
+    n_act = n_grains
+    if world > 1 or args.router:
+        # receive capacity: every rank's per-destination counts, summed over ranks (Zipf: the hot owners get more)
+        d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
+        d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
+        n1 = d_msgs.view(torch.int64).view(-1, 4)[:, 2]
+        per_dest = torch.bincount(d_ros[d_owner[n1]], minlength=world).to(torch.int64)
+        del d_owner, d_ros, n1
         if world > 1:
             dist.all_reduce(per_dest)
         cap = max(n_msgs, int(per_dest.max().item()))
-    local_mask = None
-    n_act = n_grains
+        cap += cap // 64 + 4096
     if world > 1:  # this rank's silos hold only their own partition; their catalog numbers its activations densely
         local_mask = np.zeros(cl.n_silos, np.uint8)
         local_mask[mine] = 1
         n_act = max(1, int((reg & local_mask[owner].astype(bool)).sum()))
-    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=cap, device=local_rank)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, n_msgs), device=local_rank)
     W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
     n_reg = W.register_population(eng, keys, owner, reg, local_mask, dense_local=world > 1)
+    del keys, uni
     log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
         f"receive capacity {cap}")
-    d_msgs = torch.from_numpy(msgs.view(np.int32).reshape(-1, 8)).cuda()
     stream = torch.cuda.current_stream().cuda_stream
-
-    part_eng = None
+    stats = {}
     if world == 1 and not args.router:
         route = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         act = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
@@ -185,8 +207,24 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         def step():
             eng.address_messages_device(d_msgs, n_msgs, route, act, order, offsets, stream=stream)
             return n_msgs
+    elif world > 1 and not args.router:
+        # the node exchange behind the C ABI: owner partition, counts all-gather, grouped send/recv over RCCL, routing
+        # at the owner, hop 2 when activations live elsewhere, stage 4 at the host (orl_node_route_batch_device)
+        gid = torch.zeros(L_NODE_ID_BYTES, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            gid.copy_(torch.frombuffer(bytearray(GrainNode.unique_id()), dtype=torch.uint8))
+        dist.broadcast(gid, 0)
+        node = GrainNode(eng, world, rank, ros, max_batch=n_msgs, max_recv=cap, group_id=bytes(gid.cpu().numpy()),
+                         chunks=args.chunks)
+
+        def step():
+            res = node.route_batch_device(d_msgs, n_msgs, stream=stream)
+            stats["owned"] = stats.get("owned", 0) + res.n_owned
+            stats["remote"] = stats.get("remote", 0) + res.n_sent_remote
+            stats["fwd"] = stats.get("fwd", 0) + res.n_forwarded
+            return res.n_owned
     else:
-        # a ring-only context for the owner partition, so it runs beside the route context on its own stream
+        # the Python torch.distributed reference protocol (orleans_amd/node.py PipelinedRouter), two batches in flight
         part_eng = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=cap, device=local_rank)
         W.setup_engine(part_eng, cl, local_silos=mine if world > 1 else None)
         router = PipelinedRouter(HipExecutor(eng, cap, torch, part_eng=part_eng, slots=2, nranks=world,
@@ -205,28 +243,40 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     for _ in range(max(args.warmup, 1 if (world > 1 or args.router) else 0)):  # the router's first step fills its pipeline
         step()
     sync()
+    torch.cuda.synchronize()
     eng.set_timing(True)
+    stats.clear()
     args_w = argparse.Namespace(**{**vars(args), "warmup": 0})
     elapsed, recv_total = timed_steps(args_w, torch, dist, world, step, sync)
     nb, route_ms, bucket_ms, total_ms = eng.timing_summary()
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n_msgs * args.steps / elapsed
-    per_launch_msgs = recv_total / args.steps
-    achieved = ROUTE_KERNEL_BYTES_PER_MSG * per_launch_msgs / (route_ms * 1e-3) / 1e9
-    log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms, bucketing {bucket_ms:.3f} ms, "
-        f"call {total_ms:.3f} ms over {nb} batches")
+    # route kernel launches per step: 1 (one GPU), or one per received chunk (node)
+    launches = max(1, nb // args.steps)
+    per_launch_msgs = recv_total / args.steps / launches
+    wire = node is not None or args.router
+    kbytes = ROUTE_KERNEL_BYTES_PER_MSG - (16 if wire else 0)  # 16-B exchange records instead of 32-B headers
+    achieved = kbytes * per_launch_msgs / (route_ms * 1e-3) / 1e9
+    log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms x {launches}, bucketing {bucket_ms:.3f} ms, "
+        f"call {total_ms:.3f} ms over {nb} launches")
     traffic = read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cl, keys, owner, msgs, n_grains, args.cpu_wall)
+        cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf)
+    if node is not None:
+        node.close()
     eng.close()
     if part_eng is not None:
         part_eng.close()
-    name = ("config3: Zipf(1.1) over 16M long-key grains" if zipf else
-            "config2: uniform 1M long-key grains") + f", {n_msgs >> 20}M single-target messages per GPU, 8-silo ring, stages 1-4"
-    if world > 1 or args.router:
-        name += ", + owner partition + RCCL all-to-all (two batches in flight)"
-    return {
+    name = (f"config3: Zipf(1.1) over {n_grains >> 20}M long-key grains, {n_total >> 20}M messages in total "
+            f"({n_msgs >> 20}M per GPU)" if zipf else
+            f"config2: uniform {n_grains // 1_000_000}M long-key grains, {n_msgs >> 20}M single-target messages per GPU")
+    name += ", 8-silo ring, stages 1-4"
+    if world > 1:
+        name += (", + owner partition, RCCL counts all-gather + grouped send/recv, routing at the owner, hop 2, "
+                 f"stage 4 at the host (orl_node, {args.chunks} chunks)" if node is not None else
+                 ", + Python torch.distributed exchange (PipelinedRouter)")
+    out = {
         "metric": "routed grain messages/sec (node)",
         "value": value,
         "unit": "messages/s",
@@ -235,48 +285,161 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
-        "data": f"synthetic (seeded splitmix64; config {args.config} of SURVEY §8(d))",
-        "config": {"workload": name, "grains": n_grains, "messages_per_gpu": n_msgs, "silos": cl.n_silos,
-                   "ring": "balanced (silo generations %s)" % W.balanced_generations(cl.n_silos),
+        "data": f"synthetic (seeded splitmix64 on the device; config {args.config} of SURVEY §8(d))",
+        "config": {"workload": name, "grains": n_grains, "messages_total": n_total, "messages_per_gpu": n_msgs,
+                   "silos": cl.n_silos, "ring": "balanced (silo generations %s)" % W.balanced_generations(cl.n_silos),
                    "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_per_msg": ROUTE_KERNEL_BYTES_PER_MSG, "msgs_per_launch": per_launch_msgs,
-                     "avg_launch_ms": route_ms},
+                     "bytes_per_msg": kbytes, "msgs_per_launch": per_launch_msgs, "avg_launch_ms": route_ms},
         "pipeline": {"bytes_per_msg": PIPELINE_BYTES_PER_MSG, "route_kernel_ms": route_ms,
                      "bucketing_ms": bucket_ms, "call_ms": total_ms,
                      "algorithmic_GBs": PIPELINE_BYTES_PER_MSG * value / world / 1e9,
                      "frac_of_hbm_peak": PIPELINE_BYTES_PER_MSG * value / world / 1e9 / HBM_PEAK_GBS},
         "cpu_baseline": cpu,
     }
+    if stats:
+        out["exchange"] = {"rank0_owned_per_step": stats["owned"] / args.steps,
+                           "rank0_sent_remote_per_step": stats["remote"] / args.steps,
+                           "rank0_forwarded_hop2_per_step": stats["fwd"] / args.steps,
+                           "rank0_xgmi_bytes_per_step": 16 * stats["remote"] / args.steps,
+                           "receive_capacity": cap}
+    return out
 
 
-def cpu_baseline(cl, keys, owner, msgs, n_grains, target_wall):
-    """The oracle (C++ restatement of the reference per-message path) on the host cores, on a bounded
-    sample of the same workload, as the reference's CPU path stand-in (.NET cannot run here)."""
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1, len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf):
+    """The oracle (C++ restatement of the reference per-message path: linear FindLast ring scan, unordered_map partition,
+    per-activation FIFO) on the host cores, as the reference's CPU path stand-in (.NET cannot run here): every available
+    thread on the whole batch (or a bounded prefix), and 1 thread on a prefix."""
     from oracle import cpu_ref
+    from orleans_amd import _lib as L
+    from orleans_amd import workloads as W
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    model, ncpu, navail = cpu_info()
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
     o = cpu_ref.Oracle(cl.n_silos)
     for s in range(cl.n_silos):
         o.add_server(s, int(cl.hashes[s]))
     o.register(keys, np.arange(n_grains, dtype=np.uint32), owner)
-    probe = msgs[: 1 << 20]
+    n_all = d_msgs.shape[0]
+
+    def host(k):
+        return d_msgs[:k].cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+
+    probe = host(min(n_all, 1 << 21))
     t0 = time.perf_counter()
-    o.route_bucket_mt(probe, n_grains, threads)
+    o.route_bucket_mt(probe, n_grains, navail)
     t_probe = time.perf_counter() - t0
-    n = int(min(len(msgs), max(len(probe), len(probe) * target_wall / max(t_probe, 1e-6))))
-    sample = msgs[:n]
+    n_mt = int(min(n_all, max(len(probe), len(probe) * target_wall / max(t_probe, 1e-6))))
+    sample = host(n_mt)
     t0 = time.perf_counter()
-    o.route_bucket_mt(sample, n_grains, threads)
-    wall = time.perf_counter() - t0
-    log(f"cpu baseline: {n} messages in {wall:.2f}s on {threads} threads")
-    return {"value": n / wall, "unit": "messages/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of the {len(msgs)} messages of this workload (same directory, stages 1-4), "
-                      f"oracle/cpu_ref.cpp ref_route_bucket_mt, {wall:.2f}s wall"}
+    o.route_bucket_mt(sample, n_grains, navail)
+    wall_mt = time.perf_counter() - t0
+    n_1 = min(len(sample), 1 << 22)
+    t0 = time.perf_counter()
+    o.route_bucket_mt(sample[:n_1], n_grains, 1)
+    wall_1 = time.perf_counter() - t0
+    log(f"cpu baseline: {n_mt} messages in {wall_mt:.2f}s on {navail} threads; {n_1} in {wall_1:.2f}s on 1 thread ({model})")
+    return {"value": n_mt / wall_mt, "unit": "messages/s", "cores": navail, "kind": "port",
+            "threads_all": {"threads": navail, "messages": n_mt, "seconds": wall_mt, "value": n_mt / wall_mt},
+            "threads_1": {"threads": 1, "messages": n_1, "seconds": wall_1, "value": n_1 / wall_1},
+            "cpu_model": model, "os_cpu_count": ncpu, "sched_affinity": navail,
+            "box_thread_share_env": os.environ.get("OMP_NUM_THREADS"),
+            "sample": f"first {n_mt} of the {n_all} messages of this workload"
+                      f"{' (the whole batch)' if n_mt == n_all else ''} on every available thread, and the first {n_1} on "
+                      f"1 thread; same directory, stages 1-4, oracle/cpu_ref.cpp ref_route_bucket_mt"}
+
+
+# ---- config 1: Chirper generator graph, one silo --------------------------------------------------------------
+def run_chirper(args, torch):
+    """BASELINE configs[0]: the ChirperNetworkGenerator deterministic graph (1k accounts x 10 followers) on one silo,
+    every account publishes once = 10k routed messages per step (fan-out + stages 1-4); the CPU leg is the oracle's
+    expansion + routing + bucketing of the same step on 1 thread (the reference runs it in one silo process)."""
+    from oracle import cpu_ref
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine, grain_keys_from_longs, silo_consistent_hash
+
+    n_acc, k = 1000, 10
+    src, tgt = W.chirper_graph_deterministic(n_acc, k)
+    off, ftgt = W.csr_from_edges(tgt - 1, src, n_acc)  # `source follows target`: the target publishes to its followers
+    tc = W.calc_id_hash(W.CHIRPER_ACCOUNT_CLASS)
+    h0 = silo_consistent_hash(f"10.0.0.1:{W.PORT}", 1)
+    eng = GrainDirectoryEngine(n_act=n_acc, dir_capacity=n_acc, max_batch=1 << 15, device=0)
+    eng.set_silos(1)
+    eng.add_server(0, h0)
+    keys = grain_keys_from_longs(tc, np.arange(1, n_acc + 1, dtype=np.int64))
+    eng.register_single_activation(keys, np.arange(n_acc, dtype=np.uint32), np.zeros(n_acc, np.uint8))
+    tcd = (3 << 56) + (tc & 0x00FFFFFFFFFFFFFF)
+    dv = "cuda"
+    d_off = torch.from_numpy(off.view(np.int64)).to(dv)
+    d_tgt = torch.from_numpy(ftgt.view(np.int32)).to(dv)
+    pubs = np.arange(n_acc, dtype=np.uint32)
+    d_pubs = torch.from_numpy(pubs.view(np.int32)).to(dv)
+    d_ps = torch.zeros(n_acc, dtype=torch.uint8, device=dv)
+    n = n_acc * k
+    poff = torch.empty(n_acc + 1, dtype=torch.int64, device=dv)
+    outs = [torch.empty(n, dtype=torch.int32, device=dv) for _ in range(3)]
+    offs = torch.empty(n_acc + 2, dtype=torch.int32, device=dv)
+    s = torch.cuda.Stream()
+
+    def step():
+        eng.fanout_device(d_off, d_tgt, d_pubs, d_ps, n_acc, tcd, poff, *outs, offs, stream=s.cuda_stream, total=n)
+
+    with torch.cuda.stream(s):
+        for _ in range(max(args.warmup, 2)):
+            step()
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        step()
+    steps = max(args.steps, 100)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for _ in range(steps):
+            g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    eng.close()
+    # CPU: the oracle's per-message path over the same step (1 thread, the reference's single silo)
+    o = cpu_ref.Oracle(1)
+    o.add_server(0, h0)
+    o.register(keys, np.arange(n_acc, dtype=np.uint32), np.zeros(n_acc, np.uint8))
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        msgs, _ = cpu_ref.fanout_expand(off, ftgt, pubs, np.zeros(n_acc, np.uint8), tcd)
+        o.route_bucket_mt(msgs, n_acc, 1)
+        reps += 1
+        if time.perf_counter() - t0 > args.cpu_wall:
+            break
+    cpu_wall = time.perf_counter() - t0
+    log(f"config 1: {el * 1e6 / steps:.1f} us/step on the GPU (graph replay), {cpu_wall * 1e6 / reps:.1f} us/step on 1 CPU thread")
+    return {"metric": "routed grain messages/sec (node)", "value": n * steps / el, "unit": "messages/s", "n_gpus": 1,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64 integer",
+            "data": "ChirperNetworkGenerator deterministic graph (ChirperNetworkGenerator.cs:306-345)",
+            "config": {"workload": "config1: Chirper 1k accounts x 10 followers on one silo, every account publishes once "
+                                   "(10k routed messages per step), fan-out + stages 1-4, hipGraph replay"},
+            "roofline": None,
+            "cpu_baseline": {"value": n * reps / cpu_wall, "unit": "messages/s", "cores": 1, "kind": "port",
+                             "cpu_model": cpu_info()[0],
+                             "sample": f"{reps} whole steps (expand + route + bucket, oracle/cpu_ref.cpp) on 1 thread"}}
 
 
 # ---- config 4: CSR multicast fan-out ---------------------------------------------------------------------

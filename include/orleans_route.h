@@ -426,6 +426,98 @@ int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n
 int orl_route_compact_device(orl_ctx* ctx, const orl_wire_msg* d_in, size_t n, uint32_t opts, uint32_t* d_route,
                              uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
 
+/* Stage 4 alone: group already-routed messages by activation handle, FIFO inside each bucket (ActivationData.EnqueueMessage,
+ * ActivationData.cs:483-514) — the receiving silo's side when the routing ran elsewhere (node hop 2).  Same outputs as
+ * orl_route_batch_device's order / bucket_offsets for these handles (ORL_NO_ACT and handles >= n_act: bucket n_act). */
+int orl_bucket_device(orl_ctx* ctx, const uint32_t* d_act, size_t n, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
+
+/* ---- device memory for callers without a GPU runtime (the P/Invoke silo) ---------------------------------
+ * A .NET host drives the *_device entry points through these: allocate HBM on the context's device, copy host arrays
+ * in and out on a stream (a NULL stream is the context's own), wait.  orl_host_register page-locks a caller array once
+ * (a pinned GCHandle buffer) so copies from / to it run at full PCIe rate and asynchronously.  Reference call sites:
+ * the per-message managed objects these batches replace (Message header dictionary, Message.cs:90). */
+int orl_device_alloc(orl_ctx* ctx, size_t bytes, void** d_out);
+int orl_device_free(orl_ctx* ctx, void* d_ptr);
+int orl_copy_to_device(orl_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream);
+int orl_copy_to_host(orl_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
+int orl_stream_sync(orl_ctx* ctx, void* stream);
+int orl_host_register(orl_ctx* ctx, void* h_ptr, size_t bytes);
+int orl_host_unregister(orl_ctx* ctx, void* h_ptr);
+
+/* ---- follower graph held by the context + host-array fan-out (SURVEY §8(b) orl_fanout_batch) -------------
+ * orl_csr_set uploads a follower graph once (csr_off[n_nodes + 1], csr_tgt[n_edges]; follower of CSR entry j = the
+ * long-key grain (follower_tcd, 0, csr_tgt[j])); orl_fanout_batch then expands host publisher arrays against it and
+ * returns every output in host arrays (route/act/order: cap entries; pub_offsets[n_pub + 1]; bucket_offsets[n_act + 2]),
+ * *n_out = the emitted count (ORL_E_CAPACITY, nothing written, when it exceeds cap).  Reference:
+ * ChirperAccount.PublishMessage (Samples/Chirper/ChirperGrains/ChirperAccount.cs:154-157). */
+int orl_csr_set(orl_ctx* ctx, const uint64_t* csr_off, size_t n_nodes, const uint32_t* csr_tgt, size_t n_edges);
+int orl_fanout_batch(orl_ctx* ctx, const uint32_t* pubs, const uint8_t* pub_silo, size_t n_pub, uint64_t follower_tcd,
+                     uint32_t opts, uint64_t* pub_offsets, uint32_t* route, uint32_t* act, uint32_t* order,
+                     uint32_t* bucket_offsets, size_t cap, uint64_t* n_out);
+
+/* ---- node: the silos of one GPU in a multi-GPU node (SURVEY §8(b) orl_node_create, §8(e)) ------------------
+ * One process per GPU; a node binds a routing context (this GPU's directory partitions) to the other ranks.  Per batch
+ * (orl_node_route_batch_device, called by every rank with its own local batch, in lockstep):
+ *   hop 1  stages 1-2 + stable partition of the local batch by the rank of each message's directory owner (messages
+ *          that need no directory stay: complete addresses, system targets, null owners), a counts all-gather, and a
+ *          grouped send/recv of the per-rank regions — 16-B orl_wire_msg records when every message of the chunk has
+ *          that form, 32-B headers otherwise.  The batch is cut into `chunks` pieces: the exchange of one overlaps the
+ *          routing (stages 1-3) of the previous one.  Replaces OutboundMessageQueue.SendMessage's per-target-silo
+ *          sender queues (OutboundMessageQueue.cs:113-145) + the remote directory lookup (LocalGrainDirectory.cs:719-765).
+ *   owner  stages 1-3 over the received records; the owned set is the received blocks in (chunk, source rank) order.
+ *   hop 2  messages whose activation is hosted on another rank (route word host silo; Dispatcher.TransportMessage,
+ *          Dispatcher.cs:618-622) travel on with their route word and activation handle, in owner order.  Skipped (no
+ *          collective beyond one counts all-gather) when no rank has anything to forward.
+ *   host   stage 4 over the hosted messages: per-activation FIFO by (source rank, source order), so per-sender order
+ *          holds (a sender's messages originate on one rank).
+ * transport ORL_TRANSPORT_RCCL: RCCL over xGMI (group_id = the ncclUniqueId from orl_node_unique_id on rank 0, shared out
+ * of band); ORL_TRANSPORT_LOCAL: the ranks are nodes of one process (same group_id bytes), exchanging by device copies —
+ * a one-GPU rehearsal of the protocol for tests.  Every rank must use the same config apart from `rank`. */
+#define ORL_NODE_ID_BYTES 128u
+#define ORL_TRANSPORT_RCCL 0u
+#define ORL_TRANSPORT_LOCAL 1u
+#define ORL_NODE_WIDE_ONLY 0x1u    /* always exchange 32-B headers */
+#define ORL_NODE_MAX_RANKS 8u
+#define ORL_NODE_MAX_CHUNKS 16u
+typedef struct orl_node_config {
+    uint32_t abi_version;
+    uint32_t nranks;
+    uint32_t rank;
+    uint32_t transport;              /* ORL_TRANSPORT_* */
+    uint8_t group_id[ORL_NODE_ID_BYTES];
+    uint8_t rank_of_silo[256];       /* rank hosting each silo index */
+    uint64_t max_batch;              /* messages a rank originates per batch */
+    uint64_t max_recv;               /* messages a rank may own, and host, per batch */
+    uint32_t chunks;                 /* 1 .. ORL_NODE_MAX_CHUNKS */
+    uint32_t flags;                  /* ORL_NODE_* */
+} orl_node_config;
+
+typedef struct orl_node_result {
+    uint64_t n_owned;                /* messages routed here as directory owner (hop 1 receive) */
+    uint64_t n_hosted;               /* messages hosted here (bucketed here) */
+    uint64_t n_forwarded;            /* of n_owned, sent on to another rank in hop 2 */
+    uint64_t n_sent_remote;          /* of the local batch, sent to another rank in hop 1 */
+    uint32_t hop2;                   /* 1 if hop 2 moved messages between ranks in this batch */
+    uint32_t n_segments;             /* the hosted messages' records: orl_node_segment 0 .. n_segments-1, back to back */
+    const uint32_t* route;           /* device [n_hosted]; valid until the next batch */
+    const uint32_t* act;             /* device [n_hosted] */
+    const uint32_t* order;           /* device [n_hosted]: hosted-message indices grouped per activation, FIFO */
+    const uint32_t* bucket_offsets;  /* device [n_act + 2] */
+} orl_node_result;
+
+typedef struct orl_node orl_node;
+int orl_node_unique_id(uint8_t id[ORL_NODE_ID_BYTES]);
+int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out);
+int orl_node_destroy(orl_node* node);
+const char* orl_node_last_error(const orl_node* node);
+/* One batch (device headers, n <= max_batch).  The outputs are complete on `stream` when the call returns (the call
+ * waits on the host for each chunk's counts; the routing work may still run). */
+int orl_node_route_batch_device(orl_node* node, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* out,
+                                void* stream);
+/* Record segment i of the last batch's hosted messages: device pointer, message count, record width (16 = orl_wire_msg,
+ * 32 = orl_msg_hdr). */
+int orl_node_segment(const orl_node* node, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width);
+
 int orl_sync(orl_ctx* ctx);
 
 /* ---- introspection for benchmarks / profiling ------------------------------------------------ */
@@ -440,6 +532,9 @@ int orl_sync(orl_ctx* ctx);
 #define ORL_Q_PROBE_FORM 1u
 #define ORL_Q_FULL_UPLOADS 2u
 #define ORL_Q_SLOT_PATCHES 3u
+#define ORL_Q_DEVICE 4u       /* the context's HIP device ordinal */
+#define ORL_Q_N_ACT 5u        /* orl_config.n_act */
+#define ORL_Q_MAX_BATCH 6u    /* messages the scratch is sized for */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 
 #define ORL_TIMING_SLOTS 256u

@@ -58,7 +58,7 @@ STAMP_OK, STAMP_COMPLETE, STAMP_SKIPPED, STAMP_UNSUPPORTED, STAMP_MALFORMED, STA
 STAMP_MAX_GROWTH = 72
 MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
-Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES = 1, 2, 3
+Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH = 1, 2, 3, 4, 5, 6
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -72,6 +72,25 @@ assert KEY_DTYPE.itemsize == 24 and MSG_DTYPE.itemsize == 32
 class orl_config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("dir_capacity", C.c_uint64),
                 ("n_act", C.c_uint32), ("placement_policy", C.c_uint32), ("max_batch", C.c_uint64)]
+
+
+NODE_ID_BYTES = 128
+TRANSPORT_RCCL, TRANSPORT_LOCAL = 0, 1
+NODE_WIDE_ONLY = 0x1
+NODE_MAX_RANKS = 8
+NODE_MAX_CHUNKS = 16
+
+
+class orl_node_config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("nranks", C.c_uint32), ("rank", C.c_uint32), ("transport", C.c_uint32),
+                ("group_id", C.c_uint8 * NODE_ID_BYTES), ("rank_of_silo", C.c_uint8 * 256), ("max_batch", C.c_uint64),
+                ("max_recv", C.c_uint64), ("chunks", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class orl_node_result(C.Structure):
+    _fields_ = [("n_owned", C.c_uint64), ("n_hosted", C.c_uint64), ("n_forwarded", C.c_uint64),
+                ("n_sent_remote", C.c_uint64), ("hop2", C.c_uint32), ("n_segments", C.c_uint32), ("route", C.c_void_p),
+                ("act", C.c_void_p), ("order", C.c_void_p), ("bucket_offsets", C.c_void_p)]
 
 
 # Every symbol include/orleans_route.h declares, with its ctypes signature.
@@ -135,6 +154,23 @@ _SIGS = {
     "orl_cache_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_sync": (C.c_int, [_P]),
     "orl_ctx_query": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "orl_bucket_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, _P]),
+    "orl_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    "orl_device_free": (C.c_int, [_P, _P]),
+    "orl_copy_to_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
+    "orl_copy_to_host": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
+    "orl_stream_sync": (C.c_int, [_P, _P]),
+    "orl_host_register": (C.c_int, [_P, _P, C.c_size_t]),
+    "orl_host_unregister": (C.c_int, [_P, _P]),
+    "orl_csr_set": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t]),
+    "orl_fanout_batch": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint64, C.c_uint32, _P, _P, _P, _P, _P, C.c_size_t,
+                                   C.POINTER(C.c_uint64)]),
+    "orl_node_unique_id": (C.c_int, [_P]),
+    "orl_node_create": (C.c_int, [_P, C.POINTER(orl_node_config), C.POINTER(_P)]),
+    "orl_node_destroy": (C.c_int, [_P]),
+    "orl_node_last_error": (C.c_char_p, [_P]),
+    "orl_node_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.POINTER(orl_node_result), _P]),
+    "orl_node_segment": (C.c_int, [_P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),

@@ -178,6 +178,11 @@ struct orl_ctx {
     void* d_patch_data = nullptr;       // device staging of a slot patch (grows to the largest patch)
     size_t patch_cap = 0;
     uint64_t n_full_uploads = 0, n_patches = 0;
+    // follower graph of orl_csr_set (host-array fan-out)
+    uint64_t* d_csr_off = nullptr;
+    uint32_t* d_csr_tgt = nullptr;
+    size_t csr_nodes = 0;
+    std::vector<uint64_t> h_csr_off;
     bool mirror_stale = false;       // device mutations since the mirror was last downloaded
     uint64_t count_ub = 0, tombs_ub = 0;  // upper bounds while the mirror is stale (capacity checks without a sync)
     // device state
@@ -658,7 +663,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data);
+    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -1577,8 +1582,145 @@ int orl_sync(orl_ctx* c) {
     return ORL_OK;
 }
 
+int orl_bucket_device(orl_ctx* c, const uint32_t* d_act, size_t n, uint32_t* d_order, uint32_t* d_off, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (!d_off || (n && (!d_act || !d_order))) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    int e = launch_bucket_acts(d_act, n, c->cfg.n_act, d_order, d_off, c->s, stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "bucket launch");
+    return ORL_OK;
+}
+
+// ---- device memory helpers for callers without a GPU runtime ----------------------------------------
+int orl_device_alloc(orl_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return ORL_E_INVALID;
+    *out = nullptr;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    hipError_t e = hipMalloc(out, std::max<size_t>(bytes, 1));
+    if (e != hipSuccess) return fail(c, ORL_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return ORL_OK;
+}
+
+int orl_device_free(orl_ctx* c, void* p) {
+    if (!c) return ORL_E_INVALID;
+    if (!p) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipFree(p));
+    return ORL_OK;
+}
+
+int orl_copy_to_device(orl_ctx* c, void* d_dst, const void* h_src, size_t bytes, void* stream) {
+    if (!c || (bytes && (!d_dst || !h_src))) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (bytes) ORL_HIP(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, stream ? (hipStream_t)stream : c->stream));
+    return ORL_OK;
+}
+
+int orl_copy_to_host(orl_ctx* c, void* h_dst, const void* d_src, size_t bytes, void* stream) {
+    if (!c || (bytes && (!h_dst || !d_src))) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (bytes) ORL_HIP(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : c->stream));
+    return ORL_OK;
+}
+
+int orl_stream_sync(orl_ctx* c, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return ORL_OK;
+    ORL_HIP(c, hipStreamSynchronize(stream ? (hipStream_t)stream : c->stream));
+    return ORL_OK;
+}
+
+int orl_host_register(orl_ctx* c, void* p, size_t bytes) {
+    if (!c || !p || !bytes) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return ORL_OK;
+}
+
+int orl_host_unregister(orl_ctx* c, void* p) {
+    if (!c || !p) return ORL_E_INVALID;
+    ORL_HIP(c, hipHostUnregister(p));
+    return ORL_OK;
+}
+
+// ---- follower graph + host-array fan-out ------------------------------------------------------------
+int orl_csr_set(orl_ctx* c, const uint64_t* off, size_t n_nodes, const uint32_t* tgt, size_t n_edges) {
+    if (!c || !off || (n_edges && !tgt)) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (off[0] != 0 || off[n_nodes] != n_edges) return fail(c, ORL_E_INVALID, "csr_off must start at 0 and end at n_edges");
+    for (size_t i = 0; i < n_nodes; ++i)
+        if (off[i + 1] < off[i]) return fail(c, ORL_E_INVALID, "csr_off not monotone at %zu", i);
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());  // a previous fan-out may still read the old graph
+    (void)hipFree(c->d_csr_off); (void)hipFree(c->d_csr_tgt);
+    c->d_csr_off = nullptr; c->d_csr_tgt = nullptr; c->csr_nodes = 0;
+    ORL_HIP(c, hipMalloc((void**)&c->d_csr_off, (n_nodes + 1) * 8));
+    ORL_HIP(c, hipMalloc((void**)&c->d_csr_tgt, std::max<size_t>(n_edges, 1) * 4));
+    ORL_HIP(c, hipMemcpy(c->d_csr_off, off, (n_nodes + 1) * 8, hipMemcpyHostToDevice));
+    if (n_edges) ORL_HIP(c, hipMemcpy(c->d_csr_tgt, tgt, n_edges * 4, hipMemcpyHostToDevice));
+    c->csr_nodes = n_nodes;
+    c->h_csr_off.assign(off, off + n_nodes + 1);
+    return ORL_OK;
+}
+
+int orl_fanout_batch(orl_ctx* c, const uint32_t* pubs, const uint8_t* pub_silo, size_t n_pub, uint64_t follower_tcd,
+                     uint32_t opts, uint64_t* pub_offsets, uint32_t* route, uint32_t* act, uint32_t* order, uint32_t* offsets,
+                     size_t cap, uint64_t* n_out) {
+    if (!c || !n_out || !pub_offsets) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (!c->d_csr_off) return fail(c, ORL_E_STATE, "no follower graph (orl_csr_set)");
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    if (n_pub && (!pubs || !pub_silo)) return fail(c, ORL_E_INVALID, "null publisher array");
+    if (!route || !act || (buckets && (!order || !offsets))) return fail(c, ORL_E_INVALID, "null output array");
+    // the emitted total from the host copy of the offsets: no device round trip before the launch
+    uint64_t total = 0;
+    for (size_t p = 0; p < n_pub; ++p) {
+        if (pubs[p] >= c->csr_nodes) return fail(c, ORL_E_INVALID, "publisher %u >= %zu nodes", pubs[p], c->csr_nodes);
+        total += c->h_csr_off[pubs[p] + 1] - c->h_csr_off[pubs[p]];
+    }
+    *n_out = total;
+    if (total > cap) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > cap %zu", (unsigned long long)total, cap);
+    if (total > c->s.max_batch || n_pub + 1 > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "fan-out larger than max_batch");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    const size_t in_bytes = n_pub * 5 + 16, out_words = 3 * std::max<uint64_t>(total, 1) + 1 + 2 * (n_pub + 1);
+    if (int r = ensure_staging(c, in_bytes, out_words)) return r;
+    uint32_t* d_pubs = static_cast<uint32_t*>(c->st_in);
+    uint8_t* d_psilo = static_cast<uint8_t*>(c->st_in) + ((n_pub * 4 + 15) & ~size_t(15));
+    uint32_t* d_route = c->st_out;
+    uint32_t* d_act = d_route + total;
+    uint32_t* d_order = d_act + total;
+    uint64_t* d_poff = reinterpret_cast<uint64_t*>(d_order + total + (total & 1));
+    hipStream_t st = c->stream;
+    if (n_pub) {
+        ORL_HIP(c, hipMemcpyAsync(d_pubs, pubs, n_pub * 4, hipMemcpyHostToDevice, st));
+        ORL_HIP(c, hipMemcpyAsync(d_psilo, pub_silo, n_pub, hipMemcpyHostToDevice, st));
+    }
+    uint64_t n_dev = total;
+    int r = orl_fanout_route_device(c, c->d_csr_off, c->d_csr_tgt, d_pubs, d_psilo, n_pub, follower_tcd, opts | ORL_OPT_TOTAL_GIVEN,
+                                    d_poff, d_route, d_act, d_order, c->st_off, &n_dev, st);
+    if (r) return r;
+    if (total) {
+        ORL_HIP(c, hipMemcpyAsync(route, d_route, total * 4, hipMemcpyDeviceToHost, st));
+        ORL_HIP(c, hipMemcpyAsync(act, d_act, total * 4, hipMemcpyDeviceToHost, st));
+        if (buckets) ORL_HIP(c, hipMemcpyAsync(order, d_order, total * 4, hipMemcpyDeviceToHost, st));
+    }
+    ORL_HIP(c, hipMemcpyAsync(pub_offsets, d_poff, (n_pub + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (buckets) ORL_HIP(c, hipMemcpyAsync(offsets, c->st_off, ((size_t)c->cfg.n_act + 2) * 4, hipMemcpyDeviceToHost, st));
+    ORL_HIP(c, hipStreamSynchronize(st));
+    return ORL_OK;
+}
+
 int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
     if (!c || !v) return ORL_E_INVALID;
+    switch (what) {
+        case ORL_Q_DEVICE: *v = (uint64_t)(int64_t)c->cfg.device; return ORL_OK;
+        case ORL_Q_N_ACT: *v = c->cfg.n_act; return ORL_OK;
+        case ORL_Q_MAX_BATCH: *v = c->s.max_batch; return ORL_OK;
+        default: break;
+    }
     if (int r = sync_device_state(c)) return r;
     switch (what) {
         case ORL_Q_PROBE_FORM:

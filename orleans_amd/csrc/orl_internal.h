@@ -300,6 +300,19 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
                             const Scratch& s, void* stream);
+// Stage 4 alone over already-routed messages (activation handles): histogram + bucket_after_route.
+int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
+                       void* stream);
+// Node hop 2: per-rank counts of routed messages by their host silo's rank (d_counts[8] u64, zeroed here), and the
+// stable partition of {record, route, act} by host rank into padded regions (d_state: part_state_bytes(n) bytes).
+int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_ros, uint32_t my_rank, uint64_t* d_counts,
+                           void* stream);
+size_t part_state_bytes(size_t n);
+// d_base_in (optional, device u64[nranks]): positions continue after an earlier partition into the same regions
+// (its totals); d_counts receives base + this input's counts.
+int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
+                       size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
+                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

@@ -1,0 +1,528 @@
+// orl_node.cpp — the silos of one GPU in a multi-GPU node: the two-hop message exchange behind the C ABI
+// (SURVEY §8(b) "node-level orl_node_create", §8(e)).  Reference: OutboundMessageQueue.SendMessage's per-target-silo
+// sender queues (src/OrleansRuntime/Messaging/OutboundMessageQueue.cs:113-145), the remote directory lookup
+// (LocalGrainDirectory.FullLookup, LocalGrainDirectory.cs:719-765) and Dispatcher.TransportMessage (Dispatcher.cs:618-622).
+//
+// Per batch, every rank in lockstep (include/orleans_route.h documents the contract):
+//   hop 1   per chunk: one-pass owner partition (k_part_lb) on stream P → all-gather of the per-rank counts (the host
+//           needs them to size the sends) → grouped send/recv on stream X → stages 1-3 of the received chunk on stream R,
+//           overlapping the next chunk's exchange;
+//   hop 2   host-rank counts of the routed messages (k_host_rank_count) → all-gather → if any rank forwards: stable
+//           partition of {record, route, act} by host rank (k_part_routed) → grouped send/recv;
+//   host    stage 4 over the hosted messages (orl_bucket_device).
+// Transports: RCCL (one process per GPU; xGMI) and LOCAL (ranks = nodes of one process, device copies + host barriers),
+// the latter a one-GPU rehearsal of the exact protocol for the parity tests.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orl_internal.h"
+
+using namespace orl;
+
+namespace {
+
+constexpr uint32_t kHeadWords = 16;  // [0, nranks) per-rank counts, [8] wire status (1 = no compact form)
+constexpr int kBarrierSeconds = 120;
+
+// ORL_TRANSPORT_LOCAL: the ranks are node objects of one process.  All-gathers and exchanges are host barriers around
+// published host words / device pointers; the data moves with device-to-device copies.
+struct LocalGroup {
+    uint32_t nranks = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t arrived = 0;
+    uint64_t gen = 0;
+    std::vector<std::vector<uint64_t>> words;  // per rank: its all-gather contribution
+    struct Lane {
+        const uint8_t* base;  // send regions of this rank: region for destination r at base + r * stride
+        uint64_t stride;      // bytes
+    };
+    std::vector<std::vector<Lane>> lanes;      // per rank: the send regions of the current exchange
+    // false on timeout (a rank stopped calling): the caller reports an error instead of hanging
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == nranks) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        return cv.wait_for(lk, std::chrono::seconds(kBarrierSeconds), [&] { return gen != g; });
+    }
+};
+std::mutex g_groups_mu;
+std::map<std::string, std::weak_ptr<LocalGroup>> g_groups;
+
+std::shared_ptr<LocalGroup> join_group(const uint8_t* id, uint32_t nranks) {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    const std::string key(reinterpret_cast<const char*>(id), ORL_NODE_ID_BYTES);
+    std::shared_ptr<LocalGroup> g = g_groups[key].lock();
+    if (!g) {
+        g = std::make_shared<LocalGroup>();
+        g->nranks = nranks;
+        g->words.assign(nranks, std::vector<uint64_t>(kHeadWords, 0));
+        g->lanes.assign(nranks, {});
+        g_groups[key] = g;
+    }
+    return g->nranks == nranks ? g : nullptr;
+}
+
+// One array moved by an exchange: rank me sends count[r] elements of `elem` bytes from send + r * stride to rank r and
+// receives recv_count[r] elements from rank r, laid out back to back in source-rank order at recv.
+struct Lane {
+    const uint8_t* send;
+    uint64_t stride;  // bytes between destination regions
+    uint8_t* recv;
+    uint32_t elem;
+};
+
+}  // namespace
+
+struct orl_node {
+    orl_ctx* ctx = nullptr;
+    orl_node_config cfg{};
+    std::string err;
+    int device = 0;
+    uint32_t n_act = 0, nr = 1, me = 0;
+    uint64_t chunk_cap = 0;
+    ncclComm_t comm = nullptr;
+    std::shared_ptr<LocalGroup> group;
+    hipStream_t sp = nullptr, sx = nullptr, sr = nullptr;
+    hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_x = nullptr, ev_r = nullptr;
+    hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
+    uint8_t* d_ros = nullptr;
+    uint8_t* d_send[2] = {nullptr, nullptr};      // hop-1 send regions: nranks x chunk_cap x 32 B per slot
+    uint64_t* d_head = nullptr;                   // [2][kHeadWords]
+    uint64_t* d_heads = nullptr;                  // [nranks][kHeadWords] (RCCL all-gather target)
+    uint64_t* h_heads = nullptr;                  // pinned copy
+    uint8_t* d_recv = nullptr;                    // owned records, chunk after chunk (max_recv x 32 B)
+    uint32_t *d_route = nullptr, *d_act = nullptr, *d_order = nullptr, *d_off = nullptr;
+    uint64_t* d_hcount = nullptr;                 // [8] hop-2 counts by host rank
+    // hop 2 (allocated on first use)
+    uint64_t f_cap = 0;
+    uint8_t* d_fsend = nullptr;
+    uint32_t *d_fsend_route = nullptr, *d_fsend_act = nullptr;
+    uint8_t* d_frecv = nullptr;
+    uint32_t *d_frecv_route = nullptr, *d_frecv_act = nullptr, *d_forder = nullptr, *d_foff = nullptr;
+    uint32_t* d_fstate = nullptr;
+    uint64_t* d_fcounts = nullptr;                // [ORL_NODE_MAX_CHUNKS][8] chained partition totals
+    struct Seg {
+        const void* p;
+        uint64_t count;
+        uint32_t width;
+    };
+    std::vector<Seg> segs;
+};
+
+namespace {
+
+int nfail(orl_node* nd, int code, const char* fmt, ...) {
+    char b[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    nd->err = b;
+    return code;
+}
+
+#define NODE_HIP(nd, call)                                                                           \
+    do {                                                                                             \
+        hipError_t _e = (call);                                                                      \
+        if (_e != hipSuccess) return nfail((nd), ORL_E_DEVICE, "%s: %s", #call, hipGetErrorString(_e)); \
+    } while (0)
+#define NODE_NCCL(nd, call)                                                                            \
+    do {                                                                                               \
+        ncclResult_t _r = (call);                                                                      \
+        if (_r != ncclSuccess) return nfail((nd), ORL_E_DEVICE, "%s: %s", #call, ncclGetErrorString(_r)); \
+    } while (0)
+#define NODE_CTX(nd, call)                                                                              \
+    do {                                                                                                \
+        int _r = (call);                                                                                \
+        if (_r != ORL_OK) return nfail((nd), _r, "%s: %s", #call, orl_last_error((nd)->ctx));           \
+    } while (0)
+
+// All-gather of kHeadWords u64 per rank from device `d_src` (ready once `ready` has fired) into nd->h_heads.
+int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready) {
+    NODE_HIP(nd, hipStreamWaitEvent(nd->sx, ready, 0));
+    if (nd->comm) {
+        NODE_NCCL(nd, ncclAllGather(d_src, nd->d_heads, kHeadWords, ncclUint64, nd->comm, nd->sx));
+        NODE_HIP(nd, hipMemcpyAsync(nd->h_heads, nd->d_heads, (size_t)nd->nr * kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
+        NODE_HIP(nd, hipStreamSynchronize(nd->sx));
+        return ORL_OK;
+    }
+    LocalGroup& g = *nd->group;
+    NODE_HIP(nd, hipMemcpyAsync(nd->h_heads + (size_t)nd->me * kHeadWords, d_src, kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
+    NODE_HIP(nd, hipStreamSynchronize(nd->sx));
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        std::memcpy(g.words[nd->me].data(), nd->h_heads + (size_t)nd->me * kHeadWords, kHeadWords * 8);
+    }
+    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node all-gather: a rank did not arrive (barrier timeout)");
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        for (uint32_t r = 0; r < nd->nr; ++r) std::memcpy(nd->h_heads + (size_t)r * kHeadWords, g.words[r].data(), kHeadWords * 8);
+    }
+    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node all-gather: a rank did not arrive (barrier timeout)");
+    return ORL_OK;
+}
+
+// Grouped send/recv of `lanes` (enqueued on nd->sx after `ready`); send[r] / recv[r] are element counts.
+int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send, const uint64_t* recv, hipEvent_t ready) {
+    NODE_HIP(nd, hipStreamWaitEvent(nd->sx, ready, 0));
+    const uint32_t nr = nd->nr, me = nd->me;
+    std::vector<uint64_t> roff(nr + 1, 0);
+    for (uint32_t r = 0; r < nr; ++r) roff[r + 1] = roff[r] + recv[r];
+    if (nd->comm) {
+        NODE_NCCL(nd, ncclGroupStart());
+        for (const Lane& L : lanes)
+            for (uint32_t r = 0; r < nr; ++r) {
+                if (r == me) {
+                    if (send[r])
+                        NODE_HIP(nd, hipMemcpyAsync(L.recv + roff[r] * L.elem, L.send + r * L.stride, send[r] * L.elem,
+                                                    hipMemcpyDeviceToDevice, nd->sx));
+                    continue;
+                }
+                if (send[r]) NODE_NCCL(nd, ncclSend(L.send + r * L.stride, send[r] * L.elem, ncclUint8, (int)r, nd->comm, nd->sx));
+                if (recv[r]) NODE_NCCL(nd, ncclRecv(L.recv + roff[r] * L.elem, recv[r] * L.elem, ncclUint8, (int)r, nd->comm, nd->sx));
+            }
+        NODE_NCCL(nd, ncclGroupEnd());
+        return ORL_OK;
+    }
+    LocalGroup& g = *nd->group;
+    NODE_HIP(nd, hipStreamSynchronize(nd->sx));  // my send regions are complete
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.lanes[me].clear();
+        for (const Lane& L : lanes) g.lanes[me].push_back(LocalGroup::Lane{L.send, L.stride});
+    }
+    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive (barrier timeout)");
+    std::vector<std::vector<LocalGroup::Lane>> peers;
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        peers = g.lanes;
+    }
+    for (size_t k = 0; k < lanes.size(); ++k)
+        for (uint32_t r = 0; r < nr; ++r)
+            if (recv[r]) {
+                if (peers[r].size() != lanes.size()) return nfail(nd, ORL_E_STATE, "node exchange: ranks disagree on the lanes");
+                NODE_HIP(nd, hipMemcpyAsync(lanes[k].recv + roff[r] * lanes[k].elem, peers[r][k].base + me * peers[r][k].stride,
+                                            recv[r] * lanes[k].elem, hipMemcpyDeviceToDevice, nd->sx));
+            }
+    NODE_HIP(nd, hipStreamSynchronize(nd->sx));
+    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive (barrier timeout)");  // regions free
+    return ORL_OK;
+}
+
+void free_node(orl_node* nd) {
+    auto f = [](void* p) { if (p) (void)hipFree(p); };
+    f(nd->d_ros); f(nd->d_send[0]); f(nd->d_send[1]); f(nd->d_head); f(nd->d_heads); f(nd->d_recv); f(nd->d_route); f(nd->d_act);
+    f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
+    f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts);
+    if (nd->h_heads) (void)hipHostFree(nd->h_heads);
+    for (hipEvent_t e : {nd->ev_in, nd->ev_part, nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t s : {nd->sp, nd->sx, nd->sr})
+        if (s) (void)hipStreamDestroy(s);
+    if (nd->comm) (void)ncclCommDestroy(nd->comm);
+}
+
+// Hop-2 buffers for an owned set of up to `owned` messages (regions of that stride), grown on demand.
+int ensure_hop2(orl_node* nd, uint64_t owned) {
+    if (owned <= nd->f_cap && nd->d_frecv) return ORL_OK;
+    NODE_HIP(nd, hipDeviceSynchronize());
+    const uint64_t cap = std::max<uint64_t>(owned, 1) + (std::max<uint64_t>(owned, 1) >> 3);
+    auto f = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
+    f(reinterpret_cast<void*&>(nd->d_fsend)); f(reinterpret_cast<void*&>(nd->d_fsend_route));
+    f(reinterpret_cast<void*&>(nd->d_fsend_act)); f(reinterpret_cast<void*&>(nd->d_fstate));
+    nd->f_cap = 0;
+    NODE_HIP(nd, hipMalloc((void**)&nd->d_fsend, (size_t)nd->nr * cap * 32));
+    NODE_HIP(nd, hipMalloc((void**)&nd->d_fsend_route, (size_t)nd->nr * cap * 4));
+    NODE_HIP(nd, hipMalloc((void**)&nd->d_fsend_act, (size_t)nd->nr * cap * 4));
+    NODE_HIP(nd, hipMalloc((void**)&nd->d_fstate, part_state_bytes(cap)));
+    if (!nd->d_frecv) {
+        const uint64_t m = nd->cfg.max_recv;
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_frecv, m * 32));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_frecv_route, m * 4));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_frecv_act, m * 4));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_forder, m * 4));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_foff, ((size_t)nd->n_act + 2) * 4));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_fcounts, ORL_NODE_MAX_CHUNKS * 8 * 8));
+    }
+    nd->f_cap = cap;
+    return ORL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orl_node_unique_id(uint8_t id[ORL_NODE_ID_BYTES]) {
+    if (!id) return ORL_E_INVALID;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return ORL_E_DEVICE;
+    std::memcpy(id, u.internal, ORL_NODE_ID_BYTES);
+    return ORL_OK;
+}
+
+const char* orl_node_last_error(const orl_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+
+int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
+    if (!ctx || !cfg || !out) return ORL_E_INVALID;
+    *out = nullptr;
+    if (cfg->abi_version != ORL_ABI_VERSION) return ORL_E_INVALID;
+    if (cfg->nranks == 0 || cfg->nranks > ORL_NODE_MAX_RANKS || cfg->rank >= cfg->nranks) return ORL_E_INVALID;
+    if (cfg->transport > ORL_TRANSPORT_LOCAL || cfg->chunks == 0 || cfg->chunks > ORL_NODE_MAX_CHUNKS) return ORL_E_INVALID;
+    if (cfg->max_batch == 0 || cfg->max_recv == 0 || cfg->max_recv >= (1ull << 31)) return ORL_E_INVALID;
+    for (uint32_t s = 0; s < 256; ++s)
+        if (cfg->rank_of_silo[s] >= cfg->nranks) return ORL_E_INVALID;
+    uint64_t dev = 0, n_act = 0, mb = 0;
+    if (orl_ctx_query(ctx, ORL_Q_DEVICE, &dev) || orl_ctx_query(ctx, ORL_Q_N_ACT, &n_act) ||
+        orl_ctx_query(ctx, ORL_Q_MAX_BATCH, &mb))
+        return ORL_E_INVALID;
+    if ((int64_t)dev < 0) return ORL_E_STATE;
+    orl_node* nd = new (std::nothrow) orl_node();
+    if (!nd) return ORL_E_NOMEM;
+    nd->ctx = ctx;
+    nd->cfg = *cfg;
+    nd->device = (int)(int64_t)dev;
+    nd->n_act = (uint32_t)n_act;
+    nd->nr = cfg->nranks;
+    nd->me = cfg->rank;
+    nd->chunk_cap = (cfg->max_batch + cfg->chunks - 1) / cfg->chunks;
+    auto bail = [&](int code) {
+        free_node(nd);
+        delete nd;
+        return code;
+    };
+    // the routing context routes one chunk's received records and buckets the owned / hosted set
+    if (mb < std::max<uint64_t>(nd->chunk_cap, cfg->max_recv)) return bail(ORL_E_CAPACITY);
+    if (hipSetDevice(nd->device) != hipSuccess) return bail(ORL_E_DEVICE);
+    hipError_t e = hipSuccess;
+    auto ok = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; return x == hipSuccess; };
+    ok(hipStreamCreateWithFlags(&nd->sp, hipStreamNonBlocking));
+    ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
+    ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
+    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part, &nd->ev_x, &nd->ev_r, &nd->ev_slot[0], &nd->ev_slot[1]})
+        ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    const uint64_t nr = cfg->nranks, mr = cfg->max_recv;
+    ok(hipMalloc((void**)&nd->d_ros, 256));
+    ok(hipMemcpy(nd->d_ros, cfg->rank_of_silo, 256, hipMemcpyHostToDevice));
+    for (int s = 0; s < 2; ++s) ok(hipMalloc((void**)&nd->d_send[s], nr * nd->chunk_cap * 32));
+    ok(hipMalloc((void**)&nd->d_head, 2 * kHeadWords * 8));
+    ok(hipMalloc((void**)&nd->d_heads, nr * kHeadWords * 8));
+    ok(hipHostMalloc((void**)&nd->h_heads, nr * kHeadWords * 8, hipHostMallocDefault));
+    ok(hipMalloc((void**)&nd->d_recv, mr * 32));
+    ok(hipMalloc((void**)&nd->d_route, mr * 4));
+    ok(hipMalloc((void**)&nd->d_act, mr * 4));
+    ok(hipMalloc((void**)&nd->d_order, mr * 4));
+    ok(hipMalloc((void**)&nd->d_off, ((size_t)nd->n_act + 2) * 4));
+    ok(hipMalloc((void**)&nd->d_hcount, 16 * 8));
+    if (e != hipSuccess) return bail(ORL_E_NOMEM);
+    for (hipEvent_t ev : {nd->ev_slot[0], nd->ev_slot[1]}) (void)hipEventRecord(ev, nd->sx);  // both slots free
+    if (cfg->transport == ORL_TRANSPORT_RCCL) {
+        ncclUniqueId u;
+        std::memcpy(u.internal, cfg->group_id, ORL_NODE_ID_BYTES);
+        if (ncclCommInitRank(&nd->comm, (int)nr, u, (int)cfg->rank) != ncclSuccess) {
+            nd->comm = nullptr;
+            return bail(ORL_E_DEVICE);
+        }
+    } else {
+        nd->group = join_group(cfg->group_id, cfg->nranks);
+        if (!nd->group) return bail(ORL_E_INVALID);
+    }
+    *out = nd;
+    return ORL_OK;
+}
+
+int orl_node_destroy(orl_node* nd) {
+    if (!nd) return ORL_E_INVALID;
+    (void)hipSetDevice(nd->device);
+    (void)hipDeviceSynchronize();
+    free_node(nd);
+    delete nd;
+    return ORL_OK;
+}
+
+int orl_node_segment(const orl_node* nd, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width) {
+    if (!nd || i >= nd->segs.size()) return ORL_E_INVALID;
+    if (d_records) *d_records = nd->segs[i].p;
+    if (count) *count = nd->segs[i].count;
+    if (width) *width = nd->segs[i].width;
+    return ORL_OK;
+}
+
+int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* res,
+                                void* stream) {
+    if (!nd || !res) return ORL_E_INVALID;
+    if (n && !d_in) return nfail(nd, ORL_E_INVALID, "null device buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)nd->cfg.max_batch);
+    std::memset(res, 0, sizeof *res);
+    const uint32_t nr = nd->nr, me = nd->me, K = nd->cfg.chunks;
+    const uint64_t W = kHeadWords;
+    const uint32_t ropts = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) | ORL_OPT_NO_BUCKETS;
+    hipStream_t caller = (hipStream_t)stream;
+    NODE_HIP(nd, hipSetDevice(nd->device));
+    NODE_HIP(nd, hipEventRecord(nd->ev_in, caller));  // the caller's batch is ready
+    NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_in, 0));
+    nd->segs.clear();
+    const uint64_t cs = (n + K - 1) / K;
+    uint64_t owned = 0;                       // messages received so far (this rank)
+    uint64_t owned_bytes = 0;
+    std::vector<uint64_t> owned_all(nr, 0);   // every rank's running receive total (capacity checks agree)
+    uint64_t sent_remote = 0;
+    bool any_wide = false;
+    // ---- hop 1 -------------------------------------------------------------------------------------------
+    for (uint32_t c = 0; c < K; ++c) {
+        const uint32_t slot = c & 1u;
+        const uint64_t start = std::min<uint64_t>((uint64_t)c * cs, n), len = std::min<uint64_t>(cs, n - start);
+        uint64_t* head = nd->d_head + slot * kHeadWords;
+        uint8_t* send = nd->d_send[slot];
+        NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_slot[slot], 0));  // the slot's previous exchange has finished
+        NODE_HIP(nd, hipMemsetAsync(head, 0, kHeadWords * 8, nd->sp));
+        bool wide = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
+        if (wide)
+            NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
+                                                              nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
+                                                              head, nd->sp));
+        else
+            NODE_CTX(nd, orl_partition_compact_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
+                                                      nd->chunk_cap, reinterpret_cast<orl_wire_msg*>(send), nullptr, head,
+                                                      reinterpret_cast<uint32_t*>(head + 8), nd->sp));
+        NODE_HIP(nd, hipEventRecord(nd->ev_part, nd->sp));
+        if (int r = allgather_heads(nd, head, nd->ev_part)) return r;
+        const uint64_t* H = nd->h_heads;
+        if (!wide) {
+            for (uint32_t r = 0; r < nr; ++r) wide |= (H[r * W + 8] & 0xFFFFFFFFull) != 0;
+            if (wide) {  // some rank's chunk has a message without the compact form: every rank sends 32-B headers
+                NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
+                                                                  nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
+                                                                  head, nd->sp));
+                NODE_HIP(nd, hipEventRecord(nd->ev_part, nd->sp));
+            }
+        }
+        any_wide |= wide;
+        const uint32_t width = wide ? 32u : 16u;
+        std::vector<uint64_t> sendc(nr), recvc(nr);
+        uint64_t got = 0;
+        for (uint32_t r = 0; r < nr; ++r) {
+            sendc[r] = H[me * W + r];
+            recvc[r] = H[r * W + me];
+            got += recvc[r];
+            if (r != me) sent_remote += sendc[r];
+        }
+        for (uint32_t d = 0; d < nr; ++d) {  // every rank checks every rank: all return the same error, none waits
+            uint64_t in = 0;
+            for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
+            owned_all[d] += in;
+            if (owned_all[d] > nd->cfg.max_recv)
+                return nfail(nd, ORL_E_CAPACITY, "rank %u receives %llu > max_recv %llu messages", d,
+                             (unsigned long long)owned_all[d], (unsigned long long)nd->cfg.max_recv);
+        }
+        uint8_t* recv = nd->d_recv + owned_bytes;
+        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, sendc.data(), recvc.data(), nd->ev_part)) return r;
+        NODE_HIP(nd, hipEventRecord(nd->ev_slot[slot], nd->sx));
+        nd->segs.push_back(orl_node::Seg{recv, got, width});
+        if (got) {  // stages 1-3 of the received chunk, overlapping the next chunk's exchange
+            NODE_HIP(nd, hipStreamWaitEvent(nd->sr, nd->ev_slot[slot], 0));
+            if (wide)
+                NODE_CTX(nd, orl_route_batch_device(nd->ctx, reinterpret_cast<const orl_msg_hdr*>(recv), got, ropts,
+                                                    nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
+            else
+                NODE_CTX(nd, orl_route_compact_device(nd->ctx, reinterpret_cast<const orl_wire_msg*>(recv), got, ropts,
+                                                      nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
+        }
+        owned += got;
+        owned_bytes += got * width;
+    }
+    // ---- hop 2: does any rank host activations of messages another rank owns? -----------------------------------
+    {
+        int e = launch_host_rank_count(nd->d_route, owned, nd->d_ros, me, nd->d_hcount, nd->sr);
+        if (e) return nfail(nd, ORL_E_DEVICE, "host rank count launch: %s", hipGetErrorString((hipError_t)e));
+        NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
+    }
+    if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_r)) return r;
+    const uint64_t* H = nd->h_heads;
+    bool forward = false;
+    uint64_t fwd = 0;
+    for (uint32_t s = 0; s < nr; ++s)
+        for (uint32_t d = 0; d < nr; ++d)
+            if (s != d && H[s * W + d]) {
+                forward = true;
+                if (s == me) fwd += H[s * W + d];
+            }
+    res->n_owned = owned;
+    res->n_forwarded = fwd;
+    res->n_sent_remote = sent_remote;
+    if (!forward) {  // every routed message is hosted where it was routed: stage 4 over the owned set
+        NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
+        res->n_hosted = owned;
+        res->route = nd->d_route;
+        res->act = nd->d_act;
+        res->order = nd->d_order;
+        res->bucket_offsets = nd->d_off;
+    } else {
+        uint64_t hosted = 0;
+        for (uint32_t d = 0; d < nr; ++d) {
+            uint64_t in = 0;
+            for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
+            if (in > nd->cfg.max_recv)
+                return nfail(nd, ORL_E_CAPACITY, "rank %u hosts %llu > max_recv %llu messages", d, (unsigned long long)in,
+                             (unsigned long long)nd->cfg.max_recv);
+            if (d == me) hosted = in;
+        }
+        if (int r = ensure_hop2(nd, owned)) return r;
+        const uint32_t wout = any_wide ? 32u : 16u;
+        uint64_t off = 0;
+        for (size_t k = 0; k < nd->segs.size(); ++k) {  // one partition per segment, positions chained through the totals
+            const orl_node::Seg& sg = nd->segs[k];
+            int e = launch_part_routed(nd->d_ros, sg.p, (int)sg.width, (int)wout, nd->d_route + off, nd->d_act + off, sg.count, me,
+                                       nr, nd->f_cap, nd->d_fsend, nd->d_fsend_route, nd->d_fsend_act, nd->d_fstate,
+                                       k ? nd->d_fcounts + 8 * (k - 1) : nullptr, nd->d_fcounts + 8 * k, nd->sr);
+            if (e) return nfail(nd, ORL_E_DEVICE, "hop-2 partition launch: %s", hipGetErrorString((hipError_t)e));
+            off += sg.count;
+        }
+        NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
+        std::vector<uint64_t> sendc(nr), recvc(nr);
+        for (uint32_t r = 0; r < nr; ++r) {
+            sendc[r] = H[me * W + r];
+            recvc[r] = H[r * W + me];
+        }
+        const std::vector<Lane> lanes = {Lane{nd->d_fsend, nd->f_cap * wout, nd->d_frecv, wout},
+                                         Lane{reinterpret_cast<uint8_t*>(nd->d_fsend_route), nd->f_cap * 4,
+                                              reinterpret_cast<uint8_t*>(nd->d_frecv_route), 4},
+                                         Lane{reinterpret_cast<uint8_t*>(nd->d_fsend_act), nd->f_cap * 4,
+                                              reinterpret_cast<uint8_t*>(nd->d_frecv_act), 4}};
+        if (int r = exchange(nd, lanes, sendc.data(), recvc.data(), nd->ev_r)) return r;
+        NODE_HIP(nd, hipEventRecord(nd->ev_x, nd->sx));
+        NODE_HIP(nd, hipStreamWaitEvent(nd->sr, nd->ev_x, 0));
+        NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_frecv_act, hosted, nd->d_forder, nd->d_foff, nd->sr));
+        nd->segs.assign(1, orl_node::Seg{nd->d_frecv, hosted, wout});
+        res->hop2 = 1;
+        res->n_hosted = hosted;
+        res->route = nd->d_frecv_route;
+        res->act = nd->d_frecv_act;
+        res->order = nd->d_forder;
+        res->bucket_offsets = nd->d_foff;
+    }
+    res->n_segments = (uint32_t)nd->segs.size();
+    NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
+    NODE_HIP(nd, hipStreamWaitEvent(caller, nd->ev_r, 0));  // the caller's stream sees complete outputs
+    return ORL_OK;
+}
+
+}  // extern "C"

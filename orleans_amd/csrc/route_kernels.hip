@@ -1391,8 +1391,9 @@ __device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_
 // into wave bases inside the tile, publishes the tile's aggregate, looks back over the earlier tiles' granules until
 // an inclusive one, publishes its own inclusive count and leaves the tile's exclusive prefix in lb.base[r]; the last
 // tile writes the per-rank totals.  Call between two __syncthreads().
+// base_in (optional, device, per rank): added to every position and total (a partition continued over several inputs).
 __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restrict__ state, uint32_t nranks, uint32_t ntiles,
-                                               uint64_t* __restrict__ counts) {
+                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ base_in = nullptr) {
     if (threadIdx.x >= nranks) return;
     uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
     const uint32_t r = threadIdx.x, t = lb.tile;
@@ -1418,8 +1419,9 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
         if ((v >> 32) == 2u || spins > kLbSpinLimit) break;
     }
     store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
-    lb.base[r] = before;
-    if (t == ntiles - 1) counts[r] = before + tc;
+    const uint64_t b0 = base_in ? base_in[r] : 0ull;
+    lb.base[r] = (uint32_t)(b0 + before);
+    if (t == ntiles - 1) counts[r] = b0 + before + tc;
 }
 
 // COMPACT: write orl_wire_msg records (16 B) and set *wire_status = 1 if a message has no compact form.
@@ -1433,13 +1435,12 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
     __shared__ PartLbSmem sm;
     stage_params(&sm.P, gp);
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
-    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
-    if (threadIdx.x == 0) sm.tile = atomicAdd(&state[0], 1u);
+    if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sm.lb.tile = atomicAdd(&state[0], 1u);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t t = sm.tile;
+    const uint32_t t = sm.lb.tile;
     const uint32_t wbase = t * kPartTile + w * (kPartItems * 64u);
-    uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
     u32x4 h0[kPartItems], h1[kPartItems];
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {  // unconditional (clamped) loads: all in flight together
@@ -1460,44 +1461,18 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
             m.meta = h1[j].z;
             m.aux = h1[j].w;
             dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
-            rank[j] = wave_rank_wide(&sm.cnt[w][0], dig[j]);
+            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j]);
         }
     }
     __syncthreads();
-    if (threadIdx.x < nranks) {  // one lane per rank: publish, look back, publish inclusive
-        const uint32_t r = threadIdx.x;
-        uint32_t tc = 0;
-        for (uint32_t q = 0; q < kWaves; ++q) {
-            const uint32_t c = sm.cnt[q][r];
-            sm.cnt[q][r] = tc;
-            tc += c;
-        }
-        store_granule(status + (size_t)t * 8 + r, 1u, tc);
-        uint32_t before = 0;
-        for (int64_t tt = (int64_t)t - 1; tt >= 0; --tt) {
-            uint64_t v;
-            uint32_t spins = 0;
-            while (((v = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0) {
-                if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
-                    atomicOr(&state[1], 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            before += (uint32_t)v;
-            if ((v >> 32) == 2u || spins > kLbSpinLimit) break;
-        }
-        store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
-        sm.base[r] = before;
-        if (t == ntiles - 1) counts[r] = before + tc;
-    }
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
         if (e < n) {
             const uint32_t d = dig[j];
-            const uint64_t g = (uint64_t)d * stride + sm.base[d] + sm.cnt[w][d] + rank[j];
+            const uint64_t g = (uint64_t)d * stride + sm.lb.base[d] + sm.lb.cnt[w][d] + rank[j];
             if (COMPACT) {
                 u32x4 wr;
                 if (!encode_wire(h0[j], h1[j], wr)) atomicOr(wire_status, 1u);
@@ -1508,6 +1483,113 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
                 dp[1] = h1[j];
             }
             if (src_index) src_index[g] = e;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Node exchange, hop 2 (Dispatcher.TransportMessage → OutboundMessageQueue.SendMessage,
+// OutboundMessageQueue.cs:113-145): after the directory owner routed a message, it travels on to the rank hosting its
+// activation (the route word's host silo); messages without a host (host 0xFF) stay.
+__device__ __forceinline__ uint32_t host_rank(const uint8_t* ros, uint32_t route, uint32_t my_rank) {
+    const uint32_t host = ORL_ROUTE_HOST(route);
+    return host == 0xFFu ? my_rank : ros[host];
+}
+
+// Per-rank message counts by host rank of routed messages (u64 counts[8], accumulated: zero them first).
+__global__ __launch_bounds__(256) void k_host_rank_count(const uint32_t* __restrict__ route, uint32_t n,
+                                                         const uint8_t* __restrict__ ros, uint32_t my_rank,
+                                                         unsigned long long* __restrict__ counts) {
+    __shared__ uint8_t r[256];
+    __shared__ uint32_t h[8];
+    r[threadIdx.x] = ros[threadIdx.x];
+    if (threadIdx.x < 8) h[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t d = host_rank(r, route[i], my_rank);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) mine[k] += d == k ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {  // wave sums, one LDS add per wave and rank
+        uint32_t v = mine[k];
+        for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63u) == 0 && v) atomicAdd(&h[k], v);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+// Stable partition of routed messages by host rank into padded per-rank regions: record (WIN bytes: 16 = orl_wire_msg,
+// 32 = orl_msg_hdr; written as WOUT bytes, a compact record widened to the header when WOUT = 32) and {route, act}.
+// Same one-pass look-back as k_part_lb (state zeroed before the launch).
+struct PartRoutedSmem {
+    uint8_t rank_of_silo[256];
+    LbShared lb;
+};
+
+template <int WIN, int WOUT>
+__global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __restrict__ ros, const void* __restrict__ in,
+                                                               const uint32_t* __restrict__ route, const uint32_t* __restrict__ act,
+                                                               uint32_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride,
+                                                               void* __restrict__ out, uint32_t* __restrict__ route_out,
+                                                               uint32_t* __restrict__ act_out, uint32_t* __restrict__ state,
+                                                               uint32_t ntiles, const uint64_t* __restrict__ base_in,
+                                                               uint64_t* __restrict__ counts) {
+    static_assert((WIN == 16 || WIN == 32) && WOUT >= WIN, "record widths");
+    __shared__ PartRoutedSmem sm;
+    sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
+    if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sm.lb.tile = atomicAdd(&state[0], 1u);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = sm.lb.tile;
+    const uint32_t wbase = t * kPartTile + w * (kPartItems * 64u);
+    u32x4 h0[kPartItems], h1[kPartItems];
+    uint32_t rw[kPartItems], aw[kPartItems], dig[kPartItems], rank[kPartItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        const uint32_t ec = e < n ? e : n - 1;
+        const u32x4* sp = reinterpret_cast<const u32x4*>(static_cast<const uint8_t*>(in) + (size_t)ec * WIN);
+        h0[j] = __builtin_nontemporal_load(sp);
+        if (WIN == 32) h1[j] = __builtin_nontemporal_load(sp + 1);
+        rw[j] = route[ec];
+        aw[j] = act[ec];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {
+        dig[j] = 0;
+        if (wbase + j * 64u + lane < n) {
+            dig[j] = host_rank(sm.rank_of_silo, rw[j], my_rank);
+            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j]);
+        }
+    }
+    __syncthreads();
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPartItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e < n) {
+            const uint32_t d = dig[j];
+            const uint64_t g = (uint64_t)d * stride + sm.lb.base[d] + sm.lb.cnt[w][d] + rank[j];
+            u32x4* dp = reinterpret_cast<u32x4*>(static_cast<uint8_t*>(out) + g * WOUT);
+            if (WIN == 16 && WOUT == 32) {  // orl_wire_msg → orl_msg_hdr (the decoder of load_wire)
+                const uint32_t meta = h0[j].w;
+                const uint64_t tcd = ((uint64_t)((meta >> 16) & 0xFFu) << 56) |
+                                     ((uint64_t)(int64_t)(int32_t)h0[j].z & 0x00FFFFFFFFFFFFFFull);
+                const uint32_t m2 = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) |
+                                    (meta & 0xFF000000u);
+                dp[0] = u32x4{(uint32_t)tcd, (uint32_t)(tcd >> 32), 0u, 0u};
+                dp[1] = u32x4{h0[j].x, h0[j].y, m2, 0u};
+            } else {
+                dp[0] = h0[j];
+                if (WIN == 32) dp[1] = h1[j];
+            }
+            route_out[g] = rw[j];
+            act_out[g] = aw[j];
         }
     }
 }
@@ -2497,6 +2579,52 @@ int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_bucket
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_client_buckets, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_msgs, (uint32_t)n, n_buckets,
                        d_bucket);
+    return (int)hipGetLastError();
+}
+
+int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
+                       void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
+    const RouteHist rh = route_hist(n_act);
+    const uint32_t ntiles = ceil_div(n, kTile);
+    if (rh.on)
+        hipLaunchKernelGGL(k_hist_pairs<true>, dim3(ntiles), dim3(256), 0, st, d_act, (uint32_t)n, n_act, rh.shift, rh.bins,
+                           s.tile_hist);
+    int e = (int)hipGetLastError();
+    if (e) return e;
+    return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st);
+}
+
+int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_ros, uint32_t my_rank, uint64_t* d_counts,
+                           void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    int e = (int)hipMemsetAsync(d_counts, 0, 8 * sizeof(uint64_t), st);
+    if (e || n == 0) return e;
+    const uint32_t g = std::min<uint32_t>(ceil_div(n, 256 * 16), 2048);
+    hipLaunchKernelGGL(k_host_rank_count, dim3(g), dim3(256), 0, st, d_route, (uint32_t)n, d_ros, my_rank,
+                       reinterpret_cast<unsigned long long*>(d_counts));
+    return (int)hipGetLastError();
+}
+
+size_t part_state_bytes(size_t n) { return 16 + (size_t)ceil_div(n, kPartTile) * 64; }
+
+int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
+                       size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
+                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = d_base_in ? hipMemcpyAsync(d_counts, d_base_in, sizeof(uint64_t) * nranks, hipMemcpyDeviceToDevice, st)
+                             : hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
+    if (e != hipSuccess || n == 0) return (int)e;
+    const uint32_t ntiles = ceil_div(n, kPartTile);
+    if ((e = hipMemsetAsync(d_state, 0, part_state_bytes(n), st)) != hipSuccess) return (int)e;
+#define ORL_PR(WI, WO) hipLaunchKernelGGL((k_part_routed<WI, WO>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_ros, d_in, d_route,  \
+                                          d_act, (uint32_t)n, my_rank, nranks, stride, d_out, d_route_out, d_act_out, d_state,   \
+                                          ntiles, d_base_in, d_counts)
+    if (win == 16 && wout == 16) ORL_PR(16, 16);
+    else if (win == 16) ORL_PR(16, 32);
+    else ORL_PR(32, 32);
+#undef ORL_PR
     return (int)hipGetLastError();
 }
 

@@ -472,6 +472,37 @@ class GrainDirectoryEngine:
     def sync(self) -> None:
         self._ck(self._lib.orl_sync(self._ctx))
 
+    def bucket_device(self, d_act, n: int, d_order, d_offsets, stream=None) -> None:
+        """Stage 4 alone over routed activation handles (the receiving silo's side of hop 2)."""
+        self._ck(self._lib.orl_bucket_device(self._ctx, ptr(d_act), int(n), ptr(d_order), ptr(d_offsets), ptr(stream)))
+
+    def copy_to_host(self, h_dst: np.ndarray, d_src, nbytes: Optional[int] = None, stream=None) -> np.ndarray:
+        """orl_copy_to_host + orl_stream_sync (the P/Invoke caller's way to read device outputs)."""
+        nb = h_dst.nbytes if nbytes is None else int(nbytes)
+        self._ck(self._lib.orl_copy_to_host(self._ctx, ptr(h_dst), ptr(d_src), nb, ptr(stream)))
+        self._ck(self._lib.orl_stream_sync(self._ctx, ptr(stream)))
+        return h_dst
+
+    def csr_set(self, csr_off: np.ndarray, csr_tgt: np.ndarray) -> None:
+        """Upload the follower graph once (host-array fan-out, orl_fanout_batch)."""
+        off = np.ascontiguousarray(csr_off, dtype=np.uint64)
+        tgt = np.ascontiguousarray(csr_tgt, dtype=np.uint32)
+        self._ck(self._lib.orl_csr_set(self._ctx, ptr(off), len(off) - 1, ptr(tgt), len(tgt)))
+
+    def fanout_batch(self, pubs: np.ndarray, pub_silo: np.ndarray, follower_tcd: int, cap: int, opts: int = 0):
+        """ChirperAccount.PublishMessage for host publisher arrays against the context's follower graph: host outputs
+        (route, act, order, bucket offsets, publish offsets)."""
+        pubs = np.ascontiguousarray(pubs, dtype=np.uint32)
+        ps = np.ascontiguousarray(pub_silo, dtype=np.uint8)
+        route, act, order = (np.zeros(cap, np.uint32) for _ in range(3))
+        off = np.zeros(self.n_act + 2, np.uint32)
+        poff = np.zeros(len(pubs) + 1, np.uint64)
+        n_out = C.c_uint64()
+        self._ck(self._lib.orl_fanout_batch(self._ctx, ptr(pubs), ptr(ps), len(pubs), int(follower_tcd), int(opts), ptr(poff),
+                                            ptr(route), ptr(act), ptr(order), ptr(off), int(cap), C.byref(n_out)))
+        n = n_out.value
+        return route[:n], act[:n], order[:n], off, poff
+
     def query(self, what: int) -> int:
         """orl_ctx_query: L.Q_PROBE_FORM (8 / 16 / 17 / 32), L.Q_FULL_UPLOADS, L.Q_SLOT_PATCHES."""
         v = C.c_uint64()

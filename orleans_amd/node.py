@@ -236,6 +236,119 @@ class PipelinedRouter:
         return self.flush()
 
 
+def wire_records_to_headers(raw: np.ndarray) -> np.ndarray:
+    """16-B orl_wire_msg records → orl_msg_hdr (the layout include/orleans_route.h documents; aux = 0)."""
+    w = np.ascontiguousarray(raw).view(np.uint32).reshape(-1, 4)
+    meta = w[:, 3]
+    out = np.zeros(len(w), L.MSG_DTYPE)
+    low56 = np.uint64(0x00FFFFFFFFFFFFFF)
+    out["tcd"] = (((meta >> 16) & 0xFF).astype(np.uint64) << np.uint64(56)) | \
+        (w[:, 2].view(np.int32).astype(np.int64).view(np.uint64) & low56)
+    out["n1"] = w[:, 0].astype(np.uint64) | (w[:, 1].astype(np.uint64) << np.uint64(32))
+    out["sending_silo"] = (meta & 0xFF).astype(np.uint8)
+    out["category"] = ((meta >> 8) & 0x3).astype(np.uint8)
+    out["flags"] = ((meta >> 10) & 0x3F).astype(np.uint8)
+    out["target_silo"] = (meta >> 24).astype(np.uint8)
+    return out
+
+
+@dataclass
+class NodeResult:
+    n_owned: int
+    n_hosted: int
+    n_forwarded: int
+    n_sent_remote: int
+    hop2: bool
+    route: int    # device pointers, valid until the next batch of the node
+    act: int
+    order: int
+    offsets: int
+    segments: List[tuple]  # (device pointer, count, record width)
+
+
+class GrainNode:
+    """orl_node (include/orleans_route.h): this GPU's silos in a multi-GPU node — owner partition, counts all-gather,
+    grouped send/recv (RCCL over xGMI, or the in-process LOCAL rehearsal), routing at the directory owner, hop 2 to the
+    activation's host, and stage 4 at the host, all behind the C ABI (no Python collective on the path).  Reference:
+    OutboundMessageQueue.SendMessage (OutboundMessageQueue.cs:113-145), Dispatcher.TransportMessage (Dispatcher.cs:618-622)."""
+
+    def __init__(self, eng, nranks: int, rank: int, rank_of_silo: Sequence[int], max_batch: int, max_recv: int,
+                 transport: int = L.TRANSPORT_RCCL, group_id: Optional[bytes] = None, chunks: int = 4,
+                 wide_only: bool = False):
+        import ctypes as C
+        self._C = C
+        self._lib = L.load()
+        self.eng = eng
+        cfg = L.orl_node_config()
+        cfg.abi_version = L.ABI_VERSION
+        cfg.nranks, cfg.rank, cfg.transport = int(nranks), int(rank), int(transport)
+        gid = bytes(group_id or b"")[:L.NODE_ID_BYTES].ljust(L.NODE_ID_BYTES, b"\0")
+        C.memmove(cfg.group_id, gid, L.NODE_ID_BYTES)
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        C.memmove(cfg.rank_of_silo, ros.tobytes(), 256)
+        cfg.max_batch, cfg.max_recv, cfg.chunks = int(max_batch), int(max_recv), int(chunks)
+        cfg.flags = L.NODE_WIDE_ONLY if wide_only else 0
+        h = C.c_void_p()
+        rc = self._lib.orl_node_create(eng.handle, C.byref(cfg), C.byref(h))
+        if rc != L.OK:
+            raise L.OrleansRouteError(rc, "orl_node_create failed (rank %d of %d, transport %d)" % (rank, nranks, transport))
+        self._node = h
+        self.nranks, self.rank = int(nranks), int(rank)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """A fresh RCCL group id (rank 0 creates it and shares it, e.g. by a torch.distributed broadcast)."""
+        import ctypes as C
+        buf = (C.c_uint8 * L.NODE_ID_BYTES)()
+        rc = L.load().orl_node_unique_id(buf)
+        if rc != L.OK:
+            raise L.OrleansRouteError(rc, "orl_node_unique_id failed")
+        return bytes(buf)
+
+    def route_batch_device(self, d_msgs, n: int, stream=None, opts: int = 0) -> NodeResult:
+        C = self._C
+        r = L.orl_node_result()
+        rc = self._lib.orl_node_route_batch_device(self._node, L.ptr(d_msgs), int(n), int(opts), C.byref(r), L.ptr(stream))
+        if rc != L.OK:
+            raise L.OrleansRouteError(rc, (self._lib.orl_node_last_error(self._node) or b"").decode(errors="replace"))
+        segs = []
+        for i in range(r.n_segments):
+            p, cnt, w = C.c_void_p(), C.c_uint64(), C.c_uint32()
+            assert self._lib.orl_node_segment(self._node, i, C.byref(p), C.byref(cnt), C.byref(w)) == L.OK
+            segs.append((p.value or 0, cnt.value, w.value))
+        return NodeResult(r.n_owned, r.n_hosted, r.n_forwarded, r.n_sent_remote, bool(r.hop2), r.route or 0, r.act or 0,
+                          r.order or 0, r.bucket_offsets or 0, segs)
+
+    def fetch(self, res: NodeResult, stream=None):
+        """Host copies of a result: (route, act, order, offsets, hosted message headers as MSG_DTYPE)."""
+        e = self.eng
+        u32 = lambda k: np.zeros(k, np.uint32)  # noqa: E731
+        route = e.copy_to_host(u32(res.n_hosted), res.route, stream=stream) if res.n_hosted else u32(0)
+        act = e.copy_to_host(u32(res.n_hosted), res.act, stream=stream) if res.n_hosted else u32(0)
+        order = e.copy_to_host(u32(res.n_hosted), res.order, stream=stream) if res.n_hosted else u32(0)
+        off = e.copy_to_host(u32(e.n_act + 2), res.offsets, stream=stream)
+        parts = []
+        for p, cnt, w in res.segments:
+            raw = np.zeros(cnt * w, np.uint8)
+            if cnt:
+                e.copy_to_host(raw, p, stream=stream)
+            parts.append(raw.view(L.MSG_DTYPE) if w == 32 else wire_records_to_headers(raw))
+        hdrs = np.concatenate(parts) if parts else np.zeros(0, L.MSG_DTYPE)
+        return route, act, order, off, hdrs
+
+    def close(self) -> None:
+        if getattr(self, "_node", None):
+            self._lib.orl_node_destroy(self._node)
+            self._node = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def rank_of_silo(n_silos: int, world: int) -> np.ndarray:
     """Silo s lives on GPU s * world // n_silos (contiguous blocks of logical silos per GPU)."""
     return np.array([s * world // n_silos for s in range(n_silos)], np.uint8)

@@ -186,6 +186,69 @@ def zipf_messages(cl: Cluster, n_grains: int, n_msgs: int, s_exp: float = 1.1, s
     return m
 
 
+# ---- the same generators as torch int64 arithmetic (on the device: 256M-message batches in milliseconds) ----------
+def _s64(c: int) -> int:
+    c &= 0xFFFFFFFFFFFFFFFF
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _lsr(t, z, k: int):
+    """Logical right shift of int64 tensors holding uint64 bits."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def _t_stream(t, seed: int, start: int, n: int, device):
+    idx = t.arange(start, start + n, dtype=t.int64, device=device)
+    z = idx * _s64(0x2545F4914F6CDD1D) + _s64(seed)
+    z = z + _s64(0x9E3779B97F4A7C15)
+    z = (z ^ _lsr(t, z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _lsr(t, z, 27)) * _s64(0x94D049BB133111EB)
+    return z ^ _lsr(t, z, 31)
+
+
+def _t_umod(t, z, m: int):
+    """uint64 z mod m for int64 tensors holding uint64 bits (m < 2^62)."""
+    return ((_lsr(t, z, 1) % m) * 2 + (z & 1)) % m
+
+
+def zipf_cdf(n_grains: int, s_exp: float = 1.1) -> np.ndarray:
+    ranks = np.arange(1, n_grains + 1, dtype=np.float64)
+    cdf = np.cumsum(ranks ** -s_exp)
+    cdf /= cdf[-1]
+    return cdf
+
+
+def device_messages(t, cl: Cluster, n_grains: int, n_msgs: int, seed: int, start: int = 0, sender_silos=None,
+                    zipf: Optional[tuple] = None, device="cuda", chunk: int = 1 << 25):
+    """uniform_messages / zipf_messages generated on `device` as an int32 [n, 8] tensor (orl_msg_hdr rows), bit-identical
+    to the numpy generators.  zipf = (cdf tensor (float64, zipf_cdf), permutation tensor (int64)) for config 3."""
+    out = t.zeros((n_msgs, 4), dtype=t.int64, device=device)
+    silos = np.arange(cl.n_silos) if sender_silos is None else np.asarray(sender_silos)
+    silos_t = t.as_tensor(silos.astype(np.int64), device=device)
+    out[:, 0] = _s64(((L.CAT_GRAIN << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF)
+    for lo in range(0, n_msgs, chunk):
+        k = min(chunk, n_msgs - lo)
+        r = _t_stream(t, seed, start + lo, k, device)
+        if zipf is None:
+            tgt = _t_umod(t, r, n_grains)
+        else:
+            cdf, perm = zipf
+            u = _lsr(t, r, 11).to(t.float64) * (1.0 / (1 << 53))
+            rk = t.clamp(t.searchsorted(cdf, u, right=True), max=n_grains - 1)
+            tgt = perm[rk]
+        s = _t_stream(t, seed ^ 0x5E4D, start + lo, k, device)
+        out[lo:lo + k, 2] = tgt
+        out[lo:lo + k, 3] = silos_t[_t_umod(t, s, len(silos))] | (2 << 8)  # sending silo | Application category
+    return out.view(t.int32)
+
+
+def zipf_tables(t, n_grains: int, seed: int = SEED_C3, device="cuda"):
+    """(cdf, permutation) device tensors of zipf_messages."""
+    cdf = t.as_tensor(zipf_cdf(n_grains), device=device)
+    perm = t.as_tensor(np.random.default_rng(seed).permutation(n_grains).astype(np.int64), device=device)
+    return cdf, perm
+
+
 def chirper_graph_deterministic(n_accounts: int = 1000, followers: int = 10, first_id: int = 1):
     """ChirperNetworkGenerator deterministic edges (NetworkGenerator/ChirperNetworkGenerator.cs:336-342):
     edge e: source = e // k, target = (source + 1 + e % k) % n (relative ids); `source follows target`,
