@@ -535,7 +535,12 @@ int orl_sync(orl_ctx* ctx);
 #define ORL_Q_DEVICE 4u       /* the context's HIP device ordinal */
 #define ORL_Q_N_ACT 5u        /* orl_config.n_act */
 #define ORL_Q_MAX_BATCH 6u    /* messages the scratch is sized for */
+#define ORL_Q_RANK_MODE 7u    /* stage-4 stable ranking on this device: bit 0 = ballot match (else LDS atomics), bit 1 = the
+                                 lane-order self-check failed (ballot forced) */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
+/* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
+ * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */
+int orl_ctx_set_rank_mode(orl_ctx* ctx, uint32_t mode);
 
 #define ORL_TIMING_SLOTS 256u
 int orl_set_timing(orl_ctx* ctx, int enable);

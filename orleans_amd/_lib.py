@@ -58,7 +58,7 @@ STAMP_OK, STAMP_COMPLETE, STAMP_SKIPPED, STAMP_UNSUPPORTED, STAMP_MALFORMED, STA
 STAMP_MAX_GROWTH = 72
 MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
-Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH = 1, 2, 3, 4, 5, 6
+Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_RANK_MODE = 1, 2, 3, 4, 5, 6, 7
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -155,6 +155,7 @@ _SIGS = {
     "orl_sync": (C.c_int, [_P]),
     "orl_ctx_query": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint64)]),
     "orl_bucket_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, _P]),
+    "orl_ctx_set_rank_mode": (C.c_int, [_P, C.c_uint32]),
     "orl_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
     "orl_device_free": (C.c_int, [_P, _P]),
     "orl_copy_to_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),

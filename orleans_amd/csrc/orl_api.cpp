@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -149,6 +150,27 @@ uint32_t jenkins_bytes(const uint8_t* d, size_t len) {
     }
     ORL_MIX(a, b, c);
     return c;
+}
+
+// Stage-4 rank mode per device (launch_rank_selfcheck): -1 = not checked yet; else ballot | self-check error << 1.
+std::mutex g_rank_mu;
+int g_rank_state[64];
+bool g_rank_init = false;
+
+int ensure_rank_mode(int device) {
+    std::lock_guard<std::mutex> lk(g_rank_mu);
+    if (!g_rank_init) {
+        for (int& x : g_rank_state) x = -1;
+        g_rank_init = true;
+    }
+    if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
+    if (g_rank_state[device] >= 0) return 0;
+    const char* m = getenv("ORL_RANK_MODE");
+    uint32_t st = 0;
+    int e = launch_rank_selfcheck(m && std::strcmp(m, "ballot") == 0 ? 1 : 0, &st);
+    if (e) return e;
+    g_rank_state[device] = (int)st;
+    return 0;
 }
 
 uint64_t next_pow2(uint64_t v) {
@@ -712,6 +734,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         hipError_t e;
         if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
         if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
+        if ((e = (hipError_t)ensure_rank_mode(cfg->device)) != hipSuccess) return bail(e, "stage-4 rank self-check");
         if ((e = hipMalloc((void**)&c->d_table, slots * sizeof(DirSlot))) != hipSuccess) return bail(e, "hipMalloc(directory)");
         if ((e = hipMalloc((void**)&c->d_probe, slots * sizeof(ProbeSlot))) != hipSuccess) return bail(e, "hipMalloc(probe table)");
         if ((e = hipMalloc((void**)&c->d_probe_bad, 4)) != hipSuccess) return bail(e, "hipMalloc(probe flag)");
@@ -1719,6 +1742,12 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
         case ORL_Q_DEVICE: *v = (uint64_t)(int64_t)c->cfg.device; return ORL_OK;
         case ORL_Q_N_ACT: *v = c->cfg.n_act; return ORL_OK;
         case ORL_Q_MAX_BATCH: *v = c->s.max_batch; return ORL_OK;
+        case ORL_Q_RANK_MODE: {
+            if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+            std::lock_guard<std::mutex> lk(g_rank_mu);
+            *v = (uint64_t)(int64_t)g_rank_state[c->cfg.device];
+            return ORL_OK;
+        }
         default: break;
     }
     if (int r = sync_device_state(c)) return r;
@@ -1730,6 +1759,19 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
         case ORL_Q_SLOT_PATCHES: *v = c->n_patches; return ORL_OK;
         default: return fail(c, ORL_E_INVALID, "unknown query %u", what);
     }
+}
+
+int orl_ctx_set_rank_mode(orl_ctx* c, uint32_t mode) {
+    if (!c || mode > 1) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+    std::lock_guard<std::mutex> lk(g_rank_mu);
+    const int st = g_rank_state[c->cfg.device];
+    if (mode == 0 && (st & 2)) return fail(c, ORL_E_STATE, "the LDS lane-order self-check failed on this device: ballot ranking only");
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());  // kernels in flight keep the mode they started with
+    ORL_HIP(c, (hipError_t)set_rank_mode(mode));
+    g_rank_state[c->cfg.device] = (int)(mode | (st & 2));
+    return ORL_OK;
 }
 
 int orl_set_timing(orl_ctx* c, int enable) {

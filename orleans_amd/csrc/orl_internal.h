@@ -237,6 +237,10 @@ struct Scratch {
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
+// Stage-4 ranking self-check on the current device (k_rank_selfcheck): selects the LDS-atomic rank (0) or the ballot
+// fallback (1) for every kernel of this process on the device; mode 1 forces the fallback.  *ballot_out = mode | err << 1.
+int launch_rank_selfcheck(int mode, uint32_t* ballot_out);
+int set_rank_mode(uint32_t ballot);
 // Host-changed slots of the partition: dir[idx[k]] = slots[k]; probe / probe8 (when non-null) patched alike.
 int launch_dir_patch(const uint32_t* d_idx, const DirSlot* d_slots, const ProbeSlot* d_p16, const uint2* d_p8, uint32_t n,
                      DirSlot* d_dir, ProbeSlot* d_probe, uint2* d_probe8, void* stream);

@@ -278,17 +278,91 @@ __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { r
 // in lane order, so lane order == arrival order inside each 64-element step, and consecutive steps of the
 // wave are ordered by the wave's instruction order.  Measured on MI355X (scripts/rank_lab.hip,
 // profiles/r01_rank_lab.txt): identical ranks to the BITS-ballot match over 4 x 64M elements (uniform,
-// 50 % on 8 hot digits, all-equal, 4 distinct) at 1.8x its speed; every GPU parity test re-checks it
-// bit-exactly against the oracle.  Exec-masked (inactive) lanes do not count.
-// The counters are packed two per LDS word (digit d: word d >> 1, bits 16 * (d & 1)); a wave ranks at most 1024
-// elements per round, so a half never carries into its neighbour, and 12-bit digits fit the LDS.
-__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) {
-    const uint32_t sh = (d & 1u) << 4;
-    return (atomicAdd(&wave_cnt[d >> 1], 1u << sh) >> sh) & 0xFFFFu;
+// 50 % on 8 hot digits, all-equal, 4 distinct) at 1.8x its speed.  That lane order is a measured property, not a
+// documented one, so every process checks it once per device before the first routing context is used
+// (k_rank_selfcheck, launch_rank_selfcheck) and falls back to the ballot match (g_rank_ballot = 1) if it ever
+// disagrees; ORL_RANK_MODE=ballot forces the fallback.  Exec-masked (inactive) lanes do not count.
+// A wave step whose active lanes all carry ONE digit (a hot activation: Zipf) is ranked by lane prefix with a single
+// counter update instead of 64 same-address atomics.
+// PACKED: counters two per LDS word (digit d: word d >> 1, bits 16 * (d & 1)); a wave ranks at most 1024 elements
+// per round, so a half never carries into its neighbour, and 12-bit digits fit the LDS.  Otherwise one per word.
+__device__ uint32_t g_rank_ballot = 0;
+
+__device__ __forceinline__ uint64_t lanes_below() {
+    const uint32_t lane = __lane_id();
+    return lane ? (~0ull >> (64u - lane)) : 0ull;
 }
 
-// Unpacked form (one counter per word) for the few-digit exchange partition.
-__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d) { return atomicAdd(&wave_cnt[d], 1u); }
+template <bool PACKED>
+__device__ __forceinline__ uint32_t counter_add(uint32_t* cnt, uint32_t d, uint32_t v) {
+    if (!PACKED) return atomicAdd(&cnt[d], v);
+    const uint32_t sh = (d & 1u) << 4;
+    return (atomicAdd(&cnt[d >> 1], v << sh) >> sh) & 0xFFFFu;
+}
+
+template <int BITS, bool PACKED>
+__device__ __forceinline__ uint32_t wave_rank_ballot(uint32_t* cnt, uint32_t d, uint64_t active, uint64_t lt) {
+    uint64_t m = active;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    const uint32_t base = PACKED ? (cnt[d >> 1] >> ((d & 1u) << 4)) & 0xFFFFu : cnt[d];  // read by every lane first
+    if ((m & lt) == 0) counter_add<PACKED>(cnt, d, (uint32_t)__popcll(m));              // one update per digit group
+    return base + (uint32_t)__popcll(m & lt);
+}
+
+template <int BITS, bool PACKED>
+__device__ __forceinline__ uint32_t wave_rank_t(uint32_t* cnt, uint32_t d) {
+    const uint64_t active = __ballot(1);
+    const uint64_t lt = lanes_below();
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    if (__ballot(d == d0) == active) {  // one digit in the whole step
+        uint32_t base = 0;
+        if ((active & lt) == 0) base = counter_add<PACKED>(cnt, d0, (uint32_t)__popcll(active));
+        return (uint32_t)__builtin_amdgcn_readfirstlane(base) + (uint32_t)__popcll(active & lt);
+    }
+    if (g_rank_ballot) return wave_rank_ballot<BITS, PACKED>(cnt, d, active, lt);
+    return counter_add<PACKED>(cnt, d, 1u);
+}
+
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) { return wave_rank_t<BITS, true>(wave_cnt, d); }
+
+// Unpacked form (one counter per word) for the few-digit exchange partitions (ranks < 8).
+__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d) { return wave_rank_t<3, false>(wave_cnt, d); }
+
+// The lane-order self-check: every wave ranks pseudo-random digit streams (uniform 10-bit, 8 hot of 1024, 4 distinct,
+// 3-bit) with the LDS atomic and with the ballot match; *err = 1 on any difference.  One launch per device.
+__global__ __launch_bounds__(256) void k_rank_selfcheck(uint32_t seed, uint32_t* __restrict__ err) {
+    __shared__ uint32_t ca[kWaves][512], cb[kWaves][512];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    bool bad = false;
+    for (uint32_t pat = 0; pat < 4; ++pat) {
+        for (uint32_t i = lane; i < 512; i += 64) ca[w][i] = cb[w][i] = 0;
+        __syncthreads();
+        for (uint32_t step = 0; step < 16; ++step) {
+            uint32_t x = fmix32(seed ^ (blockIdx.x * 0x9E3779B1u) ^ (threadIdx.x << 8) ^ (step << 20) ^ (pat << 28));
+            uint32_t d = pat == 0 ? x & 1023u : pat == 1 ? ((x >> 12) & 1u ? (x & 7u) * 97u : x & 1023u)
+                                  : pat == 2 ? x & 3u : x & 7u;
+            if (lane % 13 == 5 && step % 3 == 1) continue;  // some exec-masked lanes
+            const uint64_t active = __ballot(1), lt = lanes_below();
+            uint32_t ra, rb;
+            if (pat < 3) {
+                ra = counter_add<true>(&ca[w][0], d, 1u);
+                rb = wave_rank_ballot<10, true>(&cb[w][0], d, active, lt);
+            } else {
+                ra = counter_add<false>(&ca[w][0], d, 1u);
+                rb = wave_rank_ballot<3, false>(&cb[w][0], d, active, lt);
+            }
+            bad |= ra != rb;
+        }
+        __syncthreads();
+    }
+    if (bad) atomicOr(err, 1u);
+}
 
 __device__ __forceinline__ uint32_t packed_get(const uint32_t* row, uint32_t d) { return (row[d >> 1] >> ((d & 1u) << 4)) & 0xFFFFu; }
 
@@ -682,10 +756,12 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //   3. per-bin tile-local starts (block scan) and delta[d] = global base of (tile, d) - local start;
 //   4. scatter into an LDS image sorted by digit, then write it out in image order, so the global stores
 //      are runs of consecutive positions per bin.  OUT_PAIR writes 8-B {key, index} pairs (one store
-//      request per run instead of two); OUT_FINAL writes the index to `order` and the key to `keys`.
+//      request per run instead of two); OUT_FINAL writes the index to `order` and the key to `keys`;
+//      OUT_SOA8 / OUT_SOA16 (the MSD pass of the two-level path) write the index to `order` (an index array) and only
+//      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
-enum : int { IN_ACT = 0, IN_PAIR = 1 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1 };
+enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3 };
 
 // Digits per thread in the per-round column phase: digit pairs (one packed word) are never split between threads.
 template <int BITS>
@@ -776,7 +852,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j)
-        if (wbase + j * 64u + lane < n) rank[j] = wave_rank(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u));
+        if (wbase + j * 64u + lane < n) rank[j] = wave_rank<BITS>(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u));
     __syncthreads();
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
     // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
@@ -809,6 +885,12 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = kv;
+            } else if (OUT == OUT_SOA8) {
+                order_out[g] = kv.y;
+                reinterpret_cast<uint8_t*>(key_out)[g] = (uint8_t)(k & ((1u << shift) - 1u));
+            } else if (OUT == OUT_SOA16) {
+                order_out[g] = kv.y;
+                reinterpret_cast<uint16_t*>(key_out)[g] = (uint16_t)(k & ((1u << shift) - 1u));
             } else {
                 key_out[g] = k;
                 order_out[g] = kv.y;
@@ -948,11 +1030,18 @@ __device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart
     return true;
 }
 
+// IN_SOA8 / IN_SOA16: `in` = the MSD pass's index array [n_total], followed by its low-digit array (u8 / u16).
 template <int IN>
-__device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t e, uint32_t n_act, uint32_t& key, uint32_t& idx) {
+__device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n_total, uint32_t e, uint32_t n_act, uint32_t& key,
+                                         uint32_t& idx) {
     if (IN == IN_ACT) {
         key = bucket_key(static_cast<const uint32_t*>(in)[e], n_act);
         idx = e;
+    } else if (IN == IN_SOA8 || IN == IN_SOA16) {
+        const uint32_t* ix = static_cast<const uint32_t*>(in);
+        key = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[e]
+                            : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[e];
+        idx = ix[e];
     } else {
         const uint2 v = static_cast<const uint2*>(in)[e];
         key = v.x;
@@ -961,9 +1050,9 @@ __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t e
 }
 
 template <int LB, int IN>
-__global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_act, uint32_t nbk, uint32_t seg,
-                                                   const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                                   uint32_t* __restrict__ seg_hist) {
+__global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
+                                                   uint32_t seg, const uint32_t* __restrict__ bstart,
+                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist) {
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
     SegRange r;
@@ -975,8 +1064,15 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {  // clamped loads: all 16 in flight at once
             const uint32_t e = c0 + j * 256u + threadIdx.x;
-            uint32_t idx;
-            seg_load<IN>(in, e < r.hi ? e : r.hi - 1, n_act, key[j], idx);
+            const uint32_t ec = e < r.hi ? e : r.hi - 1;
+            if (IN == IN_SOA8 || IN == IN_SOA16) {  // the digit array only
+                const uint32_t* ix = static_cast<const uint32_t*>(in);
+                key[j] = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[ec]
+                                       : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[ec];
+            } else {
+                uint32_t idx;
+                seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
+            }
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
@@ -1034,7 +1130,8 @@ struct SegSmem {
 };
 
 template <int LB, int IN>
-__global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in, uint32_t n_act, uint32_t nbk, uint32_t seg,
+__global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
+                                                     uint32_t seg,
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, uint32_t* __restrict__ order) {
@@ -1058,7 +1155,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t e = wbase + j * 64u + lane;
-            seg_load<IN>(in, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
+            seg_load<IN>(in, n_total, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
         }
         for (uint32_t k = threadIdx.x; k < BL / 2u; k += 256) {
 #pragma unroll
@@ -1067,7 +1164,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
-            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank(&sm.cnt[w][0], key[j] & (BL - 1u));
+            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank<LB>(&sm.cnt[w][0], key[j] & (BL - 1u));
         __syncthreads();
         uint32_t tot[PER], start[PER];
         round_starts<LB>(sm.cnt, sm.wsum, tot, start);
@@ -2211,14 +2308,21 @@ template <int BITS>
 void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     const dim3 g(ntiles), b(256);
-    if (in == IN_ACT && out == OUT_PAIR)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
-    else if (in == IN_ACT)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_ACT, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
-    else if (out == OUT_PAIR)
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_PAIR>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
-    else
-        hipLaunchKernelGGL((k_radix_pass<BITS, IN_PAIR, OUT_FINAL>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys);
+#define ORL_RP(I, O) hipLaunchKernelGGL((k_radix_pass<BITS, I, O>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, \
+                                        order, keys)
+    if (in == IN_ACT) {
+        switch (out) {
+            case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR); break;
+            case OUT_FINAL: ORL_RP(IN_ACT, OUT_FINAL); break;
+            case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8); break;
+            default: ORL_RP(IN_ACT, OUT_SOA16); break;
+        }
+    } else if (out == OUT_PAIR) {
+        ORL_RP(IN_PAIR, OUT_PAIR);
+    } else {
+        ORL_RP(IN_PAIR, OUT_FINAL);
+    }
+#undef ORL_RP
 }
 
 void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
@@ -2258,18 +2362,16 @@ template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
                      uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
     const uint32_t nb = n_act + 2;
-    if (in == IN_ACT)
-        hipLaunchKernelGGL((k_seg_count<LB, IN_ACT>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart, s.seg_hist);
-    else
-        hipLaunchKernelGGL((k_seg_count<LB, IN_PAIR>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart, s.seg_hist);
+#define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
+                                     s.seg_hist)
+#define ORL_SS(I) hipLaunchKernelGGL((k_seg_scatter<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,      \
+                                     s.sstart, s.seg_hist, d_offsets, nb, n, d_order)
+    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
     scan_inplace(d_offsets, nb, s.scan_sums, st);  // per-key counts → bucket offsets
-    if (in == IN_ACT)
-        hipLaunchKernelGGL((k_seg_scatter<LB, IN_ACT>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart,
-                           s.seg_hist, d_offsets, nb, n, d_order);
-    else
-        hipLaunchKernelGGL((k_seg_scatter<LB, IN_PAIR>), dim3(grid), dim3(256), 0, st, kin, n_act, nbk, seg, s.bstart, s.sstart,
-                           s.seg_hist, d_offsets, nb, n, d_order);
+    if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_SOA8) ORL_SS(IN_SOA8); else ORL_SS(IN_SOA16);
+#undef ORL_SC
+#undef ORL_SS
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
@@ -2301,12 +2403,15 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const void* kin = d_act;
         if (bp.hb > 0) {
             col_scan(s.tile_hist, nrows0, nbk, s, st);
-            launch_pass(bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
-                        nullptr, nullptr, st);
+            // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
+            uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
+            launch_pass(bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0,
+                        ntiles, nullptr, idx, idx + n, st);
             kin = s.pairs_a;
         }
         hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
-        launch_seg(bp.lb, bp.hb > 0 ? IN_PAIR : IN_ACT, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st);
+        launch_seg(bp.lb, bp.hb > 0 ? (bp.lb <= 8 ? IN_SOA8 : IN_SOA16) : IN_ACT, kin, n, n_act, nbk, seg, grid, d_order, d_offsets,
+                   s, st);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
@@ -2331,6 +2436,28 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
 }
 
 }  // namespace
+
+int launch_rank_selfcheck(int mode, uint32_t* ballot_out) {
+    uint32_t* d_err = nullptr;
+    uint32_t err = 0;
+    hipError_t e = hipMalloc((void**)&d_err, 4);
+    if (e == hipSuccess) e = hipMemset(d_err, 0, 4);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_rank_selfcheck, dim3(1024), dim3(256), 0, nullptr, 0x5EEDu, d_err);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(&err, d_err, 4, hipMemcpyDeviceToHost);
+    if (d_err) (void)hipFree(d_err);
+    if (e != hipSuccess) return (int)e;
+    const uint32_t ballot = (mode == 1 || err) ? 1u : 0u;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_ballot), &ballot, 4);
+    *ballot_out = ballot | (err << 1);
+    return (int)e;
+}
+
+int set_rank_mode(uint32_t ballot) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rank_ballot), &ballot, 4);
+}
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return 0;

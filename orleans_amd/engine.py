@@ -503,6 +503,10 @@ class GrainDirectoryEngine:
         n = n_out.value
         return route[:n], act[:n], order[:n], off, poff
 
+    def set_rank_mode(self, mode: int) -> None:
+        """Stage-4 ranking: 0 = LDS atomics (self-checked), 1 = ballot match (process-wide on this device)."""
+        self._ck(self._lib.orl_ctx_set_rank_mode(self._ctx, int(mode)))
+
     def query(self, what: int) -> int:
         """orl_ctx_query: L.Q_PROBE_FORM (8 / 16 / 17 / 32), L.Q_FULL_UPLOADS, L.Q_SLOT_PATCHES."""
         v = C.c_uint64()

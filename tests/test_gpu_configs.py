@@ -421,3 +421,38 @@ def test_config5_full_size_presence(torch):
     s.synchronize()
     check()
     eng.close()
+
+
+# ---- stage-4 ranking: the LDS lane-order self-check and the ballot fallback ---------------
+@pytest.mark.parametrize("n_act", [5000, 1_000_000, 12_000_000])
+def test_stage4_rank_modes_vs_oracle(torch, n_act):
+    """The self-check passed on this device (LDS-atomic ranking in use); with the ballot fallback forced, and back,
+    stage 4 is bit-exact vs the oracle on uniform, Zipf-hot and single-activation batches (both stage-4 plans)."""
+    cl = W.default_cluster()
+    n_grains = 50_000
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    acts = (np.arange(n_grains, dtype=np.uint64) * np.uint64(2654435761) % np.uint64(n_act)).astype(np.uint32)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 21, device=0)
+    W.setup_engine(eng, cl)
+    eng.register_single_activation(keys, acts, owner)
+    o = _oracle_for(cl, keys, acts, owner)
+    assert eng.query(L.Q_RANK_MODE) == 0, "the LDS lane-order self-check failed on this device"
+    batches = [W.uniform_messages(cl, n_grains + 500, 1_500_000, seed=1),
+               W.zipf_messages(cl, n_grains, 1_500_000, seed=2)]
+    one = W.uniform_messages(cl, n_grains, 600_000, seed=3)
+    one["n1"] = 7  # every message to one activation: whole waves of one digit
+    batches.append(one)
+    try:
+        for mode in (1, 0):
+            eng.set_rank_mode(mode)
+            assert eng.query(L.Q_RANK_MODE) == mode
+            for m in batches:
+                res = eng.address_messages(m)
+                r, a = o.route(m)
+                np.testing.assert_array_equal(res.act, a)
+                order, off = o.bucket(a, n_act)
+                np.testing.assert_array_equal(res.offsets, off)
+                np.testing.assert_array_equal(res.order, order)
+    finally:
+        eng.set_rank_mode(0)
+    eng.close()
