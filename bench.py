@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--msgs", type=int, default=None,
                     help="messages per GPU per step (default: config 2 64M per GPU; config 3 256M in total, split over the GPUs)")
     ap.add_argument("--chunks", type=int, default=4, help="node exchange pipeline depth (N > 1)")
+    ap.add_argument("--host-io", choices=["pinned", "pageable"], default=None,
+                    help="config 2 at N=1: time the host-array P/Invoke call (orl_route_batch: PCIe in and out) instead")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--router", action="store_true",
                     help="configs 2/3 at N=1: go through the pipelined multi-GPU router (partition + routing on two "
@@ -198,6 +200,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         f"receive capacity {cap}")
     stream = torch.cuda.current_stream().cuda_stream
     stats = {}
+    if args.host_io:
+        return run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains)
     if world == 1 and not args.router:
         route = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         act = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
@@ -308,6 +312,37 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
                            "rank0_xgmi_bytes_per_step": 16 * stats["remote"] / args.steps,
                            "receive_capacity": cap}
     return out
+
+
+def run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains):
+    """The host-array call a .NET silo makes (orl_route_batch): headers in host memory, outputs to host memory, PCIe
+    both ways, chunked H2D / route / D2H overlap.  Not the bench headline (inputs are not HBM-resident)."""
+    from orleans_amd import _lib as L
+    msgs = d_msgs.cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+    outs = [np.empty(n_msgs, np.uint32) for _ in range(3)] + [np.empty(n_act + 2, np.uint32)]
+    pinned = args.host_io == "pinned"
+    if pinned:
+        for a in [msgs] + outs:
+            eng.host_register(a)
+    for _ in range(max(1, args.warmup)):
+        eng.route_batch_host(msgs, *outs)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.route_batch_host(msgs, *outs)
+    el = time.perf_counter() - t0
+    if pinned:
+        for a in [msgs] + outs:
+            eng.host_unregister(a)
+    eng.close()
+    pcie = n_msgs * (32 + 12) + 4 * (n_act + 2)
+    log(f"host io ({args.host_io}): {el * 1e3 / args.steps:.2f} ms per {n_msgs} messages, {pcie / (el / args.steps) / 1e9:.1f} GB/s PCIe")
+    return {"metric": "routed grain messages/sec (node), host arrays over PCIe", "value": n_msgs * args.steps / el,
+            "unit": "messages/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32/u64 integer", "data": "synthetic (config 2)",
+            "config": {"workload": f"config2 through orl_route_batch with {args.host_io} host arrays: 32 B in, 12 B + offsets "
+                                   "out per message over PCIe, chunked upload / route / download overlap"},
+            "pcie_bytes_per_step": pcie, "pcie_GBs": pcie / (el / args.steps) / 1e9, "roofline": None, "cpu_baseline": None}
 
 
 def cpu_info():

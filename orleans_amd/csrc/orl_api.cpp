@@ -173,6 +173,10 @@ int ensure_rank_mode(int device) {
     return 0;
 }
 
+// orl_route_batch: chunks per host-array batch (and the smallest chunk)
+constexpr size_t kHostChunks = 8;
+constexpr size_t kHostChunk = 1u << 20;
+
 uint64_t next_pow2(uint64_t v) {
     uint64_t p = 16;
     while (p < v) p <<= 1;
@@ -235,8 +239,10 @@ struct orl_ctx {
     bool ros_valid = false;
     Scratch s{};
     hipStream_t stream = nullptr;
-    // host-buffer staging (orl_route_batch / orl_hash_batch)
-    void* st_in = nullptr; size_t st_in_cap = 0;
+    // host-buffer staging (orl_route_batch / orl_hash_batch) and its copy streams / per-chunk events
+    uint8_t* st_in = nullptr; size_t st_in_cap = 0;
+    hipStream_t hstream[2] = {nullptr, nullptr};
+    hipEvent_t hev[2 * (kHostChunks + 1)] = {};
     uint32_t* st_out = nullptr; size_t st_out_cap = 0;
     uint32_t* st_off = nullptr;
     // silo consistent hashes (SiloAddress.GetConsistentHashCode) for outbound sender queues
@@ -671,7 +677,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
     if (in_bytes > c->st_in_cap) {
         if (c->st_in) (void)hipFree(c->st_in);
         c->st_in = nullptr; c->st_in_cap = 0;
-        ORL_HIP(c, hipMalloc(&c->st_in, in_bytes));
+        ORL_HIP(c, hipMalloc((void**)&c->st_in, in_bytes));
         c->st_in_cap = in_bytes;
     }
     if (out_words > c->st_out_cap) {
@@ -689,6 +695,8 @@ void free_device(orl_ctx* c) {
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->hev) if (e) (void)hipEventDestroy(e);
+    for (auto& st : c->hstream) if (st) (void)hipStreamDestroy(st);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -1040,6 +1048,11 @@ int orl_route_compact_device(orl_ctx* c, const orl_wire_msg* d_in, size_t n, uin
     return route_impl(c, d_in, true, n, opts, d_route, d_act, d_order, d_off, stream);
 }
 
+// Host-array form (the P/Invoke call): the batch is cut into chunks; chunk k's upload (copy stream), its stages 1-3
+// (the context's stream) and the download of its route words / handles (second copy stream) overlap with the
+// neighbouring chunks', and stage 4 runs once over the whole batch at the end.  Caller arrays registered with
+// orl_host_register (pinned) are copied asynchronously at full PCIe rate; pageable ones go through the runtime's
+// staging (correct, slower).
 int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
                     uint32_t* order, uint32_t* offsets) {
     if (!c) return ORL_E_INVALID;
@@ -1047,22 +1060,43 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     if (n && (!in || !route || !act)) return fail(c, ORL_E_INVALID, "null host buffer");
     if (buckets && (!offsets || (n && !order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     int r = ensure_staging(c, std::max<size_t>(n, 1) * sizeof(orl_msg_hdr), std::max<size_t>(n, 1) * 3);
     if (r) return r;
+    if (!c->hstream[0]) {
+        for (auto& st : c->hstream) ORL_HIP(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        for (auto& ev : c->hev) ORL_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
     uint32_t* d_route = c->st_out;
     uint32_t* d_act = d_route + n;
     uint32_t* d_order = d_act + n;
-    if (n) ORL_HIP(c, hipMemcpyAsync(c->st_in, in, n * sizeof(orl_msg_hdr), hipMemcpyHostToDevice, c->stream));
-    r = orl_route_batch_device(c, (const orl_msg_hdr*)c->st_in, n, opts, d_route, d_act, d_order, c->st_off, c->stream);
-    if (r) return r;
-    if (n) {
-        ORL_HIP(c, hipMemcpyAsync(route, d_route, n * 4, hipMemcpyDeviceToHost, c->stream));
-        ORL_HIP(c, hipMemcpyAsync(act, d_act, n * 4, hipMemcpyDeviceToHost, c->stream));
-        if (buckets) ORL_HIP(c, hipMemcpyAsync(order, d_order, n * 4, hipMemcpyDeviceToHost, c->stream));
+    const orl_msg_hdr* d_in = reinterpret_cast<const orl_msg_hdr*>(c->st_in);
+    const size_t chunk = std::max<size_t>(kHostChunk, (n + kHostChunks - 1) / kHostChunks);
+    hipStream_t up = c->hstream[0], down = c->hstream[1];
+    size_t k = 0;
+    for (size_t lo = 0; lo < n; lo += chunk, ++k) {
+        const size_t len = std::min(chunk, n - lo);
+        hipEvent_t ev_up = c->hev[2 * (k % (kHostChunks + 1))], ev_rt = c->hev[2 * (k % (kHostChunks + 1)) + 1];
+        ORL_HIP(c, hipMemcpyAsync(c->st_in + lo * sizeof(orl_msg_hdr), in + lo, len * sizeof(orl_msg_hdr), hipMemcpyHostToDevice, up));
+        ORL_HIP(c, hipEventRecord(ev_up, up));
+        ORL_HIP(c, hipStreamWaitEvent(c->stream, ev_up, 0));
+        if ((r = route_impl(c, d_in + lo, false, len, opts | ORL_OPT_NO_BUCKETS, d_route + lo, d_act + lo, nullptr, nullptr, c->stream)))
+            return r;
+        ORL_HIP(c, hipEventRecord(ev_rt, c->stream));
+        ORL_HIP(c, hipStreamWaitEvent(down, ev_rt, 0));
+        ORL_HIP(c, hipMemcpyAsync(route + lo, d_route + lo, len * 4, hipMemcpyDeviceToHost, down));
+        ORL_HIP(c, hipMemcpyAsync(act + lo, d_act + lo, len * 4, hipMemcpyDeviceToHost, down));
     }
-    if (buckets) ORL_HIP(c, hipMemcpyAsync(offsets, c->st_off, ((size_t)c->cfg.n_act + 2) * 4, hipMemcpyDeviceToHost, c->stream));
+    if (buckets) {
+        int e = launch_bucket_acts(d_act, n, c->cfg.n_act, d_order, c->st_off, c->s, c->stream);
+        if (e) return hipfail(c, (hipError_t)e, "bucket launch");
+        if (n) ORL_HIP(c, hipMemcpyAsync(order, d_order, n * 4, hipMemcpyDeviceToHost, c->stream));
+        ORL_HIP(c, hipMemcpyAsync(offsets, c->st_off, ((size_t)c->cfg.n_act + 2) * 4, hipMemcpyDeviceToHost, c->stream));
+    }
     ORL_HIP(c, hipStreamSynchronize(c->stream));
+    ORL_HIP(c, hipStreamSynchronize(down));
+    ORL_HIP(c, hipStreamSynchronize(up));
     return ORL_OK;
 }
 
@@ -1710,8 +1744,8 @@ int orl_fanout_batch(orl_ctx* c, const uint32_t* pubs, const uint8_t* pub_silo, 
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     const size_t in_bytes = n_pub * 5 + 16, out_words = 3 * std::max<uint64_t>(total, 1) + 1 + 2 * (n_pub + 1);
     if (int r = ensure_staging(c, in_bytes, out_words)) return r;
-    uint32_t* d_pubs = static_cast<uint32_t*>(c->st_in);
-    uint8_t* d_psilo = static_cast<uint8_t*>(c->st_in) + ((n_pub * 4 + 15) & ~size_t(15));
+    uint32_t* d_pubs = reinterpret_cast<uint32_t*>(c->st_in);
+    uint8_t* d_psilo = c->st_in + ((n_pub * 4 + 15) & ~size_t(15));
     uint32_t* d_route = c->st_out;
     uint32_t* d_act = d_route + total;
     uint32_t* d_order = d_act + total;

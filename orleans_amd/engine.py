@@ -258,6 +258,19 @@ class GrainDirectoryEngine:
                                            ptr(offsets)))
         return RouteResult(route, act, order, offsets)
 
+    def route_batch_host(self, msgs: np.ndarray, route: np.ndarray, act: np.ndarray, order: np.ndarray,
+                         offsets: np.ndarray, opts: int = 0) -> None:
+        """orl_route_batch into caller-owned host arrays (the P/Invoke call shape; pin them with host_register)."""
+        self._ck(self._lib.orl_route_batch(self._ctx, ptr(msgs), len(msgs), int(opts), ptr(route), ptr(act), ptr(order),
+                                           ptr(offsets)))
+
+    def host_register(self, a: np.ndarray) -> None:
+        """Page-lock a host array for asynchronous full-rate copies (a pinned GCHandle buffer on the C# side)."""
+        self._ck(self._lib.orl_host_register(self._ctx, ptr(a), a.nbytes))
+
+    def host_unregister(self, a: np.ndarray) -> None:
+        self._ck(self._lib.orl_host_unregister(self._ctx, ptr(a)))
+
     def calculate_target_silo(self, keys: np.ndarray, me: int, exclude_if_stopping: bool = True) -> np.ndarray:
         """Owner silo per key as silo `me` computes it (0xFF = null)."""
         keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
