@@ -16,6 +16,8 @@
 // so a 64M batch is 16384 workgroups (>> 256 CUs).  All LDS lives in one __shared__ block per kernel.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "orl_internal.h"
 
 namespace orl {
@@ -286,7 +288,12 @@ __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { r
 // counter update instead of 64 same-address atomics.
 // PACKED: counters two per LDS word (digit d: word d >> 1, bits 16 * (d & 1)); a wave ranks at most 1024 elements
 // per round, so a half never carries into its neighbour, and 12-bit digits fit the LDS.  Otherwise one per word.
-__device__ uint32_t g_rank_ballot = 0;
+// bit 0: ballot match (the fallback); bit 1: the one-digit-step fast path (ORL_RANK_UNIFORM=0 clears it: A/B runs).
+// Kernels read it ONCE (rank_flags()) and pass it down: a load per call cannot be hoisted past the LDS atomics.
+constexpr uint32_t kRankBallot = 1u, kRankUniform = 2u;
+__device__ uint32_t g_rank_flags = kRankUniform;
+
+__device__ __forceinline__ uint32_t rank_flags() { return __builtin_amdgcn_readfirstlane(g_rank_flags); }
 
 __device__ __forceinline__ uint64_t lanes_below() {
     const uint32_t lane = __lane_id();
@@ -315,24 +322,30 @@ __device__ __forceinline__ uint32_t wave_rank_ballot(uint32_t* cnt, uint32_t d, 
 }
 
 template <int BITS, bool PACKED>
-__device__ __forceinline__ uint32_t wave_rank_t(uint32_t* cnt, uint32_t d) {
-    const uint64_t active = __ballot(1);
-    const uint64_t lt = lanes_below();
-    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-    if (__ballot(d == d0) == active) {  // one digit in the whole step
-        uint32_t base = 0;
-        if ((active & lt) == 0) base = counter_add<PACKED>(cnt, d0, (uint32_t)__popcll(active));
-        return (uint32_t)__builtin_amdgcn_readfirstlane(base) + (uint32_t)__popcll(active & lt);
+__device__ __forceinline__ uint32_t wave_rank_t(uint32_t* cnt, uint32_t d, uint32_t flags) {
+    if (flags & kRankUniform) {
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        const uint64_t active = __builtin_amdgcn_read_exec();
+        if (__ballot(d == d0) == active) {  // one digit in the whole step
+            const uint64_t lt = lanes_below();
+            uint32_t base = 0;
+            if ((active & lt) == 0) base = counter_add<PACKED>(cnt, d0, (uint32_t)__popcll(active));
+            return (uint32_t)__builtin_amdgcn_readfirstlane(base) + (uint32_t)__popcll(active & lt);
+        }
     }
-    if (g_rank_ballot) return wave_rank_ballot<BITS, PACKED>(cnt, d, active, lt);
+    if (flags & kRankBallot) return wave_rank_ballot<BITS, PACKED>(cnt, d, __builtin_amdgcn_read_exec(), lanes_below());
     return counter_add<PACKED>(cnt, d, 1u);
 }
 
 template <int BITS>
-__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d) { return wave_rank_t<BITS, true>(wave_cnt, d); }
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d, uint32_t flags) {
+    return wave_rank_t<BITS, true>(wave_cnt, d, flags);
+}
 
 // Unpacked form (one counter per word) for the few-digit exchange partitions (ranks < 8).
-__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d) { return wave_rank_t<3, false>(wave_cnt, d); }
+__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d, uint32_t flags) {
+    return wave_rank_t<3, false>(wave_cnt, d, flags);
+}
 
 // The lane-order self-check: every wave ranks pseudo-random digit streams (uniform 10-bit, 8 hot of 1024, 4 distinct,
 // 3-bit) with the LDS atomic and with the ballot match; *err = 1 on any difference.  One launch per device.
@@ -827,6 +840,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     __shared__ PassSmem<BITS> sm;
+    const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
     for (uint32_t b = threadIdx.x; b < B / 2u; b += 256) {
@@ -852,7 +866,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j)
-        if (wbase + j * 64u + lane < n) rank[j] = wave_rank<BITS>(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u));
+        if (wbase + j * 64u + lane < n) rank[j] = wave_rank<BITS>(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u), rflags);
     __syncthreads();
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
     // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
@@ -1140,6 +1154,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
     __shared__ SegSmem<LB> sm;
     SegRange r;
     if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
+    const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t run[PER];  // global position of the next message with digit threadIdx.x * PER + q
     const uint32_t* hrow = seg_hist + (size_t)r.index * BL;
@@ -1164,7 +1179,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
-            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank<LB>(&sm.cnt[w][0], key[j] & (BL - 1u));
+            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank<LB>(&sm.cnt[w][0], key[j] & (BL - 1u), rflags);
         __syncthreads();
         uint32_t tot[PER], start[PER];
         round_starts<LB>(sm.cnt, sm.wsum, tot, start);
@@ -1530,6 +1545,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
                                                            uint32_t* __restrict__ state, uint32_t ntiles,
                                                            uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status) {
     __shared__ PartLbSmem sm;
+    const uint32_t rflags = rank_flags();
     stage_params(&sm.P, gp);
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
     if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
@@ -1558,7 +1574,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
             m.meta = h1[j].z;
             m.aux = h1[j].w;
             dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
-            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j]);
+            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j], rflags);
         }
     }
     __syncthreads();
@@ -1636,6 +1652,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
                                                                uint64_t* __restrict__ counts) {
     static_assert((WIN == 16 || WIN == 32) && WOUT >= WIN, "record widths");
     __shared__ PartRoutedSmem sm;
+    const uint32_t rflags = rank_flags();
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
     if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
     if (threadIdx.x == 0) sm.lb.tile = atomicAdd(&state[0], 1u);
@@ -1660,7 +1677,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
         dig[j] = 0;
         if (wbase + j * 64u + lane < n) {
             dig[j] = host_rank(sm.rank_of_silo, rw[j], my_rank);
-            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j]);
+            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j], rflags);
         }
     }
     __syncthreads();
@@ -2366,10 +2383,12 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
                                      s.seg_hist)
 #define ORL_SS(I) hipLaunchKernelGGL((k_seg_scatter<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,      \
                                      s.sstart, s.seg_hist, d_offsets, nb, n, d_order)
-    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
+    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
+    else ORL_SC(IN_SOA16);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
     scan_inplace(d_offsets, nb, s.scan_sums, st);  // per-key counts → bucket offsets
-    if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_SOA8) ORL_SS(IN_SOA8); else ORL_SS(IN_SOA16);
+    if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
+    else ORL_SS(IN_SOA16);
 #undef ORL_SC
 #undef ORL_SS
 }
@@ -2383,6 +2402,17 @@ void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uin
 #undef ORL_CASE
         default: break;
     }
+}
+
+// Level-2 input layout of the two-level path: {key, index} pairs, or (ORL_STAGE4_SOA=1) SoA — indices + the low digit
+// only.  SoA cuts level 2's bytes (k_seg_count 130 -> 38 us at config 2) but the MSD pass's narrow scattered digit stores
+// double its write requests (221 -> 330 us): a wash, measured in profiles/r02_stage4_ab.txt, so pairs stay the default.
+bool stage4_soa() {
+    static const bool soa = [] {
+        const char* e = getenv("ORL_STAGE4_SOA");
+        return e && e[0] == '1';
+    }();
+    return soa;
 }
 
 // Stage 4 after a route kernel that already wrote route_hist()'s tile histogram into s.tile_hist.
@@ -2403,15 +2433,19 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const void* kin = d_act;
         if (bp.hb > 0) {
             col_scan(s.tile_hist, nrows0, nbk, s, st);
-            // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
-            uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
-            launch_pass(bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0,
-                        ntiles, nullptr, idx, idx + n, st);
+            if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
+                uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
+                launch_pass(bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
+                            row_step0, ntiles, nullptr, idx, idx + n, st);
+            } else {
+                launch_pass(bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
+                            nullptr, nullptr, st);
+            }
             kin = s.pairs_a;
         }
         hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
-        launch_seg(bp.lb, bp.hb > 0 ? (bp.lb <= 8 ? IN_SOA8 : IN_SOA16) : IN_ACT, kin, n, n_act, nbk, seg, grid, d_order, d_offsets,
-                   s, st);
+        const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
+        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
@@ -2450,13 +2484,15 @@ int launch_rank_selfcheck(int mode, uint32_t* ballot_out) {
     if (d_err) (void)hipFree(d_err);
     if (e != hipSuccess) return (int)e;
     const uint32_t ballot = (mode == 1 || err) ? 1u : 0u;
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_ballot), &ballot, 4);
+    e = (hipError_t)set_rank_mode(ballot);
     *ballot_out = ballot | (err << 1);
     return (int)e;
 }
 
 int set_rank_mode(uint32_t ballot) {
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rank_ballot), &ballot, 4);
+    const char* u = getenv("ORL_RANK_UNIFORM");
+    const uint32_t flags = (ballot ? kRankBallot : 0u) | ((u && u[0] == '0') ? 0u : kRankUniform);
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rank_flags), &flags, 4);
 }
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream) {
