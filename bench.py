@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--msgs", type=int, default=None,
                     help="messages per GPU per step (default: config 2 64M per GPU; config 3 256M in total, split over the GPUs)")
     ap.add_argument("--chunks", type=int, default=4, help="node exchange pipeline depth (N > 1)")
+    ap.add_argument("--local-ranks", type=int, default=0,
+                    help="rehearse the N-rank node exchange on ONE GPU: N ranks as threads over the in-process transport "
+                         "(orl_node LOCAL); measures the protocol, not xGMI scaling")
     ap.add_argument("--host-io", choices=["pinned", "pageable"], default=None,
                     help="config 2 at N=1: time the host-array P/Invoke call (orl_route_batch: PCIe in and out) instead")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -90,7 +93,9 @@ def main():
         if args.config in (1, 4, 5, 6, 7, 8):
             raise SystemExit("--config 1/4/5/6/7/8 are single-GPU measurement legs")
 
-    if args.config == 1:
+    if args.local_ranks:
+        res = run_rehearsal(args, torch)
+    elif args.config == 1:
         res = run_chirper(args, torch)
     elif args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
@@ -312,6 +317,89 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
                            "rank0_xgmi_bytes_per_step": 16 * stats["remote"] / args.steps,
                            "receive_capacity": cap}
     return out
+
+
+def run_rehearsal(args, torch):
+    """--local-ranks R: the multi-GPU step of configs 2 / 3 (owner partition, counts all-gather, grouped send/recv, routing
+    at the owner, hop 2, stage 4 at the host) with R ranks as threads of this process on one GPU, exchanging through the
+    in-process transport (device copies).  Same workload split as `torchrun --nproc-per-node R`; every rank's work shares
+    the one GPU, so the time is the sum of the ranks' work, not a scaling measurement."""
+    from concurrent.futures import ThreadPoolExecutor
+    from orleans_amd import _lib as L
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+    from orleans_amd.node import GrainNode, local_silos, rank_of_silo
+
+    R = args.local_ranks
+    zipf = args.config == 3
+    n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
+    n_total = args.msgs * R if args.msgs else (256 << 20 if zipf else (64 << 20) * R)
+    n_msgs = n_total // R
+    cl = W.balanced_cluster()
+    ros = rank_of_silo(cl.n_silos, R)
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    seed = W.SEED_C3 if zipf else W.SEED_C2
+    ztab = W.zipf_tables(torch, n_grains, seed) if zipf else None
+    d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
+    d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
+    msgs, per_dest = [], torch.zeros(R, dtype=torch.int64, device="cuda")
+    for r in range(R):
+        m = W.device_messages(torch, cl, n_grains, n_msgs, seed, start=r * n_msgs, sender_silos=local_silos(cl.n_silos, R, r),
+                              zipf=ztab)
+        per_dest += torch.bincount(d_ros[d_owner[m.view(torch.int64).view(-1, 4)[:, 2]]], minlength=R)
+        msgs.append(m)
+    cap = max(n_msgs, int(per_dest.max().item()))
+    cap += cap // 64 + 4096
+    del d_owner, d_ros
+    engs, nodes, streams = [], [], []
+    gid = b"bench-rehearsal"
+    for r in range(R):
+        mine = local_silos(cl.n_silos, R, r)
+        mask = np.zeros(cl.n_silos, np.uint8)
+        mask[mine] = 1
+        n_act = max(1, int((reg & mask[owner].astype(bool)).sum()))
+        e = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, n_msgs), device=0)
+        W.setup_engine(e, cl, local_silos=mine)
+        W.register_population(e, keys, owner, reg, mask, dense_local=True)
+        engs.append(e)
+        nodes.append(GrainNode(e, R, r, ros, max_batch=n_msgs, max_recv=cap, transport=L.TRANSPORT_LOCAL, group_id=gid,
+                               chunks=args.chunks))
+        streams.append(torch.cuda.Stream())
+    torch.cuda.synchronize()
+    stats = [dict(owned=0, remote=0) for _ in range(R)]
+
+    def one(r):
+        res = nodes[r].route_batch_device(msgs[r], n_msgs, stream=streams[r].cuda_stream)
+        stats[r]["owned"] += res.n_owned
+        stats[r]["remote"] += res.n_sent_remote
+        streams[r].synchronize()
+        return res.n_owned
+
+    with ThreadPoolExecutor(R) as ex:
+        for _ in range(max(1, args.warmup)):
+            list(ex.map(one, range(R)))
+        torch.cuda.synchronize()
+        for st in stats:
+            st.update(owned=0, remote=0)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            list(ex.map(one, range(R)))
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    for nd in nodes:
+        nd.close()
+    for e in engs:
+        e.close()
+    owned = [st["owned"] / args.steps for st in stats]
+    log(f"rehearsal {R} ranks on one GPU: {el * 1e3 / args.steps:.2f} ms/step; owned per rank {[int(x) for x in owned]}")
+    return {"metric": "routed grain messages/sec, node protocol rehearsal on ONE GPU (not a scaling number)",
+            "value": n_total * args.steps / el, "unit": "messages/s", "n_gpus": 1, "local_ranks": R, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "u32/u64 integer", "data": f"synthetic (config {args.config})",
+            "config": {"workload": f"config{args.config} split over {R} ranks ({n_msgs} messages each), orl_node LOCAL "
+                                   f"transport, {args.chunks} chunks", "receive_capacity": cap},
+            "owned_per_rank": owned, "max_over_mean_owned": max(owned) / (sum(owned) / R),
+            "sent_remote_per_rank": [st["remote"] / args.steps for st in stats], "roofline": None, "cpu_baseline": None}
 
 
 def run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains):

@@ -291,9 +291,18 @@ __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { r
 // bit 0: ballot match (the fallback); bit 1: the one-digit-step fast path (ORL_RANK_UNIFORM=0 clears it: A/B runs).
 // Kernels read it ONCE (rank_flags()) and pass it down: a load per call cannot be hoisted past the LDS atomics.
 constexpr uint32_t kRankBallot = 1u, kRankUniform = 2u;
+// RM (compile time, chosen by the host per launch from the device's rank flags): kRmPlain = atomics only (the
+// straight-line loop), kRmHot = with the once-per-wave one-digit check, kRmBallot = the fallback.  RM < 0: decide from
+// `flags` at run time (the exchange partitions).
+constexpr int kRmPlain = 0, kRmHot = 1, kRmBallot = 2, kRmRuntime = -1;
 __device__ uint32_t g_rank_flags = kRankUniform;
 
 __device__ __forceinline__ uint32_t rank_flags() { return __builtin_amdgcn_readfirstlane(g_rank_flags); }
+
+// Host mirror of g_rank_flags (last set on any device: the modes are set process-wide in practice), which picks the
+// ranking-kernel variant of each launch.
+uint32_t g_host_rank_flags = kRankUniform;
+int host_rm() { return (g_host_rank_flags & kRankBallot) ? kRmBallot : (g_host_rank_flags & kRankUniform) ? kRmHot : kRmPlain; }
 
 __device__ __forceinline__ uint64_t lanes_below() {
     const uint32_t lane = __lane_id();
@@ -321,30 +330,52 @@ __device__ __forceinline__ uint32_t wave_rank_ballot(uint32_t* cnt, uint32_t d, 
     return base + (uint32_t)__popcll(m & lt);
 }
 
-template <int BITS, bool PACKED>
-__device__ __forceinline__ uint32_t wave_rank_t(uint32_t* cnt, uint32_t d, uint32_t flags) {
-    if (flags & kRankUniform) {
-        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-        const uint64_t active = __builtin_amdgcn_read_exec();
-        if (__ballot(d == d0) == active) {  // one digit in the whole step
-            const uint64_t lt = lanes_below();
-            uint32_t base = 0;
-            if ((active & lt) == 0) base = counter_add<PACKED>(cnt, d0, (uint32_t)__popcll(active));
-            return (uint32_t)__builtin_amdgcn_readfirstlane(base) + (uint32_t)__popcll(active & lt);
-        }
+// One step with the one-digit check: a step whose active lanes all carry one digit costs one counter update.
+template <bool PACKED>
+__device__ __forceinline__ uint32_t rank_step_uniform(uint32_t* cnt, uint32_t d) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t active = __builtin_amdgcn_read_exec();
+    if (__ballot(d == d0) == active) {
+        const uint64_t lt = lanes_below();
+        uint32_t base = 0;
+        if ((active & lt) == 0) base = counter_add<PACKED>(cnt, d0, (uint32_t)__popcll(active));
+        return (uint32_t)__builtin_amdgcn_readfirstlane(base) + (uint32_t)__popcll(active & lt);
     }
-    if (flags & kRankBallot) return wave_rank_ballot<BITS, PACKED>(cnt, d, __builtin_amdgcn_read_exec(), lanes_below());
     return counter_add<PACKED>(cnt, d, 1u);
 }
 
-template <int BITS>
-__device__ __forceinline__ uint32_t wave_rank(uint32_t* wave_cnt, uint32_t d, uint32_t flags) {
-    return wave_rank_t<BITS, true>(wave_cnt, d, flags);
-}
+// Rank a wave's N steps of 64 digits d[j] (element j * 64 + lane valid while < lim) on its counter row.  The mode is
+// chosen once per wave, so the common loop is straight-line atomics: the ballot fallback when the self-check failed;
+// the one-digit check per step when the wave's FIRST step is one digit (clustered hot activations: Zipf buckets, sorted
+// input); else one returning LDS atomic per element.
 
-// Unpacked form (one counter per word) for the few-digit exchange partitions (ranks < 8).
-__device__ __forceinline__ uint32_t wave_rank_wide(uint32_t* wave_cnt, uint32_t d, uint32_t flags) {
-    return wave_rank_t<3, false>(wave_cnt, d, flags);
+template <int BITS, bool PACKED, int N, int RM = kRmRuntime>
+__device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
+                                           uint32_t flags) {
+    const uint32_t lane = __lane_id();
+    if (RM == kRmPlain) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j * 64u + lane < lim) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
+        return;
+    }
+    if (RM == kRmBallot || (RM == kRmRuntime && (flags & kRankBallot))) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j * 64u + lane < lim) rank[j] = wave_rank_ballot<BITS, PACKED>(cnt, d[j], __builtin_amdgcn_read_exec(), lanes_below());
+        return;
+    }
+    bool hot = false;
+    if ((RM == kRmHot || (flags & kRankUniform)) && lim >= 64u) hot = __ballot(d[0] == (uint32_t)__builtin_amdgcn_readfirstlane(d[0])) == ~0ull;
+    if (hot) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j * 64u + lane < lim) rank[j] = rank_step_uniform<PACKED>(cnt, d[j]);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        if (j * 64u + lane < lim) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
 }
 
 // The lane-order self-check: every wave ranks pseudo-random digit streams (uniform 10-bit, 8 hot of 1024, 4 distinct,
@@ -774,7 +805,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
 enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4 };  // LSD_PAIR: an LSD pass's pairs
 
 // Digits per thread in the per-round column phase: digit pairs (one packed word) are never split between threads.
 template <int BITS>
@@ -824,22 +855,25 @@ __device__ __forceinline__ void round_starts(uint32_t (*cnt)[(1u << BITS) / 2u],
     }
 }
 
-template <int BITS>
+template <int BITS, int ITEMS>
 struct PassSmem {
     uint32_t cnt[kWaves][(1u << BITS) / 2u];  // packed per-wave running counts, then per-(wave, bin) tile-local starts
     uint32_t delta[1u << BITS];               // global base - tile-local start, per bin
-    uint2 stage[kTile];  // {key, index}: one 8-B LDS write per element (half the conflicted scatter instructions)
+    uint2 stage[256 * ITEMS];  // {key, index}: one 8-B LDS write per element (half the conflicted scatter instructions)
     uint32_t wsum[kWaves];
 };
 
-template <int BITS, int IN, int OUT>
+// ITEMS: elements per thread; the tile is 256 * ITEMS (the MSD pass of the two-level path takes kMsdItems: half the
+// digit-histogram rows of 4096-element tiles and twice the run length per digit in its scattered writes).
+template <int BITS, int IN, int OUT, int ITEMS, int RM>
 __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
-    __shared__ PassSmem<BITS> sm;
+    constexpr uint32_t TILE = 256u * ITEMS;
+    __shared__ PassSmem<BITS, ITEMS> sm;
     const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
@@ -847,11 +881,11 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
 #pragma unroll
         for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
     }
-    const uint32_t tbase = tile * kTile;
-    const uint32_t wbase = tbase + w * (kItems * 64u);
-    uint32_t key[kItems], idx[kItems], rank[kItems];
+    const uint32_t tbase = tile * TILE;
+    const uint32_t wbase = tbase + w * (ITEMS * 64u);
+    uint32_t key[ITEMS], idx[ITEMS], rank[ITEMS];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
         const uint32_t ec = e < n ? e : n - 1;
         if (IN == IN_ACT) {
@@ -864,9 +898,12 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         }
     }
     __syncthreads();
+    {
+        uint32_t dg[ITEMS];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j)
-        if (wbase + j * 64u + lane < n) rank[j] = wave_rank<BITS>(&sm.cnt[w][0], (key[j] >> shift) & (B - 1u), rflags);
+        for (uint32_t j = 0; j < ITEMS; ++j) dg[j] = (key[j] >> shift) & (B - 1u);
+        rank_steps<BITS, true, ITEMS, RM>(&sm.cnt[w][0], dg, n > wbase ? n - wbase : 0u, rank, rflags);
+    }
     __syncthreads();
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
     // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
@@ -880,7 +917,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < ITEMS; ++j) {
         if (wbase + j * 64u + lane < n) {
             const uint32_t d = (key[j] >> shift) & (B - 1u);
             const uint32_t lpos = packed_get(sm.cnt[w], d) + rank[j];
@@ -888,9 +925,9 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         }
     }
     __syncthreads();
-    const uint32_t cnt = (n - tbase) < kTile ? (n - tbase) : kTile;
+    const uint32_t cnt = (n - tbase) < TILE ? (n - tbase) : TILE;
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
+    for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t i = j * 256u + threadIdx.x;
         if (i < cnt) {
             const uint2 kv = sm.stage[i];
@@ -1143,7 +1180,7 @@ struct SegSmem {
     uint32_t wsum[kWaves];
 };
 
-template <int LB, int IN>
+template <int LB, int IN, int RM>
 __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
                                                      uint32_t seg,
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
@@ -1177,9 +1214,12 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][k] = 0;
         }
         __syncthreads();
+        {
+            uint32_t dg[kItems];
 #pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j)
-            if (wbase + j * 64u + lane < r.hi) rank[j] = wave_rank<LB>(&sm.cnt[w][0], key[j] & (BL - 1u), rflags);
+            for (uint32_t j = 0; j < kItems; ++j) dg[j] = key[j] & (BL - 1u);
+            rank_steps<LB, true, kItems, RM>(&sm.cnt[w][0], dg, r.hi > wbase ? r.hi - wbase : 0u, rank, rflags);
+        }
         __syncthreads();
         uint32_t tot[PER], start[PER];
         round_starts<LB>(sm.cnt, sm.wsum, tot, start);
@@ -1574,9 +1614,9 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
             m.meta = h1[j].z;
             m.aux = h1[j].w;
             dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
-            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j], rflags);
         }
     }
+    rank_steps<3, false, kPartItems>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts);
     __syncthreads();
@@ -1675,11 +1715,9 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
         dig[j] = 0;
-        if (wbase + j * 64u + lane < n) {
-            dig[j] = host_rank(sm.rank_of_silo, rw[j], my_rank);
-            rank[j] = wave_rank_wide(&sm.lb.cnt[w][0], dig[j], rflags);
-        }
+        if (wbase + j * 64u + lane < n) dig[j] = host_rank(sm.rank_of_silo, rw[j], my_rank);
     }
+    rank_steps<3, false, kPartItems>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in);
     __syncthreads();
@@ -2315,8 +2353,19 @@ int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
 // Messages per thread in the route / fan-out kernels: 16 (one 4096-message radix tile per workgroup) for
 // large batches; fewer for small batches so the grid still has >= 2048 workgroups to hide the probe latency
 // (a 64k-message batch at 16 per thread is 16 workgroups on a 256-CU chip).
-uint32_t route_items(uint64_t n) {
-    uint32_t items = kItems;
+// Elements per thread of the two-level path's MSD pass (tile 8192) and of the route kernels feeding it.
+// (32 = 8192-element tiles measured slower: route 1297 -> 1321 us, MSD pass 221 -> 256 us; profiles/r02_stage4_ab.txt)
+constexpr uint32_t kMsdItems = 16;
+
+// Messages per thread of a route launch feeding stage 4 for n_act activations: the MSD tile of the two-level path,
+// else the LSD tile.
+uint32_t max_route_items(uint32_t n_act) {
+    const BucketPlan bp = make_bucket_plan(n_act);
+    return bp.two_level && bp.hb > 0 ? kMsdItems : kItems;
+}
+
+uint32_t route_items(uint64_t n, uint32_t max_items) {
+    uint32_t items = max_items;
     while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < 2048) items >>= 1;
     return items;
 }
@@ -2325,21 +2374,25 @@ template <int BITS>
 void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     const dim3 g(ntiles), b(256);
-#define ORL_RP(I, O) hipLaunchKernelGGL((k_radix_pass<BITS, I, O>), g, b, 0, st, kin, n, n_act, shift, toff, row_step, ntiles, pout, \
-                                        order, keys)
-    if (in == IN_ACT) {
+#define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
+                                                row_step, ntiles, pout, order, keys)
+#define ORL_RP(I, O, IT) do { const int rm_ = host_rm(); if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
+                              else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
+    if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
         switch (out) {
-            case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR); break;
-            case OUT_FINAL: ORL_RP(IN_ACT, OUT_FINAL); break;
-            case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8); break;
-            default: ORL_RP(IN_ACT, OUT_SOA16); break;
+            case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kMsdItems); break;
+            case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8, kMsdItems); break;
+            case OUT_SOA16: ORL_RP(IN_ACT, OUT_SOA16, kMsdItems); break;
+            case OUT_LSD_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kItems); break;
+            default: ORL_RP(IN_ACT, OUT_FINAL, kItems); break;
         }
-    } else if (out == OUT_PAIR) {
-        ORL_RP(IN_PAIR, OUT_PAIR);
+    } else if (out == OUT_PAIR || out == OUT_LSD_PAIR) {
+        ORL_RP(IN_PAIR, OUT_PAIR, kItems);
     } else {
-        ORL_RP(IN_PAIR, OUT_FINAL);
+        ORL_RP(IN_PAIR, OUT_FINAL, kItems);
     }
 #undef ORL_RP
+#undef ORL_RP3
 }
 
 void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
@@ -2381,8 +2434,10 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     const uint32_t nb = n_act + 2;
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
-#define ORL_SS(I) hipLaunchKernelGGL((k_seg_scatter<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,      \
-                                     s.sstart, s.seg_hist, d_offsets, nb, n, d_order)
+#define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, d_order)
+#define ORL_SS(I) do { const int rm_ = host_rm(); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
+                           ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
     if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
     else ORL_SC(IN_SOA16);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
@@ -2391,6 +2446,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     else ORL_SS(IN_SOA16);
 #undef ORL_SC
 #undef ORL_SS
+#undef ORL_SS3
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
@@ -2424,9 +2480,10 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
     // pass 0's histogram rows were written by the route kernel, one per route tile of 256 * route_items
-    const uint32_t row_step0 = kItems / route_items;
     const uint32_t nrows0 = ceil_div(n, kRouteThreads * route_items);
     if (bp.two_level) {
+        const uint32_t row_step0 = kMsdItems / route_items;
+        const uint32_t ntiles = ceil_div(n, kRouteThreads * kMsdItems);
         const uint32_t nbk = 1u << bp.hb;
         const uint32_t seg = seg_elems(n);
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
@@ -2449,6 +2506,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
+    const uint32_t row_step0 = kItems / route_items;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
@@ -2460,7 +2518,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         col_scan(s.tile_hist, nrows, bins, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
-        launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
+        launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
                     s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
     hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
@@ -2492,6 +2550,7 @@ int launch_rank_selfcheck(int mode, uint32_t* ballot_out) {
 int set_rank_mode(uint32_t ballot) {
     const char* u = getenv("ORL_RANK_UNIFORM");
     const uint32_t flags = (ballot ? kRankBallot : 0u) | ((u && u[0] == '0') ? 0u : kRankUniform);
+    g_host_rank_flags = flags;
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rank_flags), &flags, 4);
 }
 
@@ -2529,7 +2588,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t items = route_items(n);
+    const uint32_t items = route_items(n, max_route_items(n_act));
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
@@ -2595,7 +2654,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t items = route_items(total);
+    const uint32_t items = route_items(total, max_route_items(n_act));
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
