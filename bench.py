@@ -57,7 +57,10 @@ def main():
                     help="6 = directory mutation leg (SURVEY §8(f) f1): device registration / unregistration batches; "
                          "7 = stream / reminder ring leg (f3); 8 = receive path leg (f2): frames -> headers -> route")
     ap.add_argument("--c5-contexts", type=int, default=1, choices=[1, 2],
-                    help="config 5: routing contexts/streams per step (2: game messages and fan-out concurrently)")
+                    help="config 5 split mode: routing contexts/streams per step (2: game messages and fan-out concurrently)")
+    ap.add_argument("--c5-mode", default="mixed", choices=["mixed", "split"],
+                    help="config 5: one orl_fanout_route_mixed_device call per step (game messages + player fan-out as "
+                         "one batch), or two calls (route the game messages, then the fan-out)")
     ap.add_argument("--frames", type=int, default=4 * 1024 * 1024, help="frames per step (config 8)")
     ap.add_argument("--grains", type=int, default=None)
     ap.add_argument("--msgs", type=int, default=None,
@@ -894,14 +897,15 @@ def run_presence(args, torch):
     all_keys = np.concatenate([pr.game_keys, pr.player_keys])
     owner = cl.owner_of(W.jenkins3_np(all_keys["tcd"], all_keys["n0"], all_keys["n1"]))
     n_fan = n_hb * per_game
-    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan, device=0)
+    mixed = args.c5_mode == "mixed"
+    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan + (n_hb if mixed else 0), device=0)
     W.setup_engine(eng, cl)
     W.register_population(eng, all_keys, owner, np.ones(n_keys, bool))
     # --c5-contexts 2: the game messages and the player fan-out of a step are independent, so they run concurrently on
     # two routing contexts (each with its own scratch and a copy of the partition) and two streams, forked and
     # joined inside the step; a 64k-message batch alone fills only a few dozen workgroups.
     eng2 = eng
-    if args.c5_contexts > 1:
+    if args.c5_contexts > 1 and not mixed:
         eng2 = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=n_fan, device=0)
         W.setup_engine(eng2, cl)
         W.register_population(eng2, all_keys, owner, np.ones(n_keys, bool))
@@ -915,7 +919,7 @@ def run_presence(args, torch):
     d_tgt = torch.from_numpy(pr.csr_tgt.view(np.int32)).to(dev)
     d_pkeys = torch.from_numpy(pr.player_keys.view(np.uint8).reshape(-1, 24)).to(dev)
     o1 = [torch.empty(n_hb, dtype=torch.int32, device=dev) for _ in range(3)]
-    o2 = [torch.empty(n_fan, dtype=torch.int32, device=dev) for _ in range(3)]
+    o2 = [torch.empty(n_fan + (n_hb if mixed else 0), dtype=torch.int32, device=dev) for _ in range(3)]
     off1 = torch.empty(n_keys + 2, dtype=torch.int32, device=dev)
     off2 = torch.empty(n_keys + 2, dtype=torch.int32, device=dev)
     poff = torch.empty(n_hb + 1, dtype=torch.int64, device=dev)
@@ -924,7 +928,16 @@ def run_presence(args, torch):
     s2 = torch.cuda.Stream() if eng2 is not eng else s
     sp2 = s2.cuda_stream
 
+    def one_mixed(i):
+        # the step's outbound batch in one call: the 64k game messages (PresenceGrain.Heartbeat →
+        # GameGrain.UpdateGameStatus) then their 8-way player fan-out (GameGrain.UpdateGameStatus →
+        # PlayerGrain.JoinGame/LeaveGame), one route launch and one stage-4 pass
+        eng.fanout_mixed_device(d_msgs[i], n_hb, d_off, d_tgt, d_pkeys, 0, d_games[i], d_gsilo[i], n_hb, poff,
+                                o2[0], o2[1], o2[2], off2, stream=sp, total=n_hb + n_fan)
+
     def one(i):
+        if mixed:
+            return one_mixed(i)
         if s2 is not s:
             s2.wait_stream(s)  # fork
         # 1 game message per heartbeat (PresenceGrain.Heartbeat → GameGrain.UpdateGameStatus) ...
@@ -975,7 +988,7 @@ def run_presence(args, torch):
         graphs.append(g)
     s.synchronize()
     # the replayed graphs must produce the eager call's words (guards against an empty or stale capture)
-    outs = o1 + o2 + [off1, off2]
+    outs = o2 + [off2] if mixed else o1 + o2 + [off1, off2]
     for i in range(n_sets):
         for x in outs:
             x.fill_(-1)
@@ -992,25 +1005,36 @@ def run_presence(args, torch):
     log("config 5: graphs verified")
     lat_graph = lat_run(lambda i: graphs[i % n_sets].replay(), steps)
     thr_graph = thr_run(lambda i: graphs[i % n_sets].replay(), steps)
+    # all n_sets steps in one graph (one launch per n_sets ticks: the per-launch gap amortised)
+    g_all = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_all, stream=s):
+        for i in range(n_sets):
+            one(i)
+    s.synchronize()
+    reps = max(1, steps // n_sets)
+    thr_graph_all = thr_run(lambda i: g_all.replay(), reps)
     eng.close()
     if eng2 is not eng:
         eng2.close()
     value = per_step * steps / thr_graph
     log(f"config 5: eager {thr_eager * 1e3 / steps:.3f} ms/step (p50 {np.percentile(lat_eager, 50):.3f}, "
         f"p99 {np.percentile(lat_eager, 99):.3f} ms); graph {thr_graph * 1e3 / steps:.3f} ms/step "
-        f"(p50 {np.percentile(lat_graph, 50):.3f}, p99 {np.percentile(lat_graph, 99):.3f} ms)")
+        f"(p50 {np.percentile(lat_graph, 50):.3f}, p99 {np.percentile(lat_graph, 99):.3f} ms); "
+        f"{n_sets} steps per graph {thr_graph_all * 1e3 / (reps * n_sets):.3f} ms/step")
     return {"metric": "routed grain messages/sec (node)", "value": value, "unit": "messages/s", "n_gpus": 1,
             "steps": steps, "warmup": args.warmup, "ms_per_step": thr_graph * 1e3 / steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64 integer",
             "data": "synthetic (seeded Guids; config 5 of SURVEY §8(d))",
             "config": {"workload": f"config5: {n_games} Guid-keyed games x {per_game} players, {n_hb} heartbeats per "
                                    f"step = {n_hb} game + {n_fan} player messages, stages 1-5, hipGraph replay",
-                       "messages_per_step": per_step, "routing_contexts": args.c5_contexts},
+                       "messages_per_step": per_step, "mode": args.c5_mode,
+                       "routing_contexts": 1 if mixed else args.c5_contexts},
             "latency_ms": {"eager_p50": float(np.percentile(lat_eager, 50)),
                            "eager_p99": float(np.percentile(lat_eager, 99)),
                            "graph_p50": float(np.percentile(lat_graph, 50)),
                            "graph_p99": float(np.percentile(lat_graph, 99))},
-            "throughput_msgs_per_s": {"eager": per_step * steps / thr_eager, "graph": value},
+            "throughput_msgs_per_s": {"eager": per_step * steps / thr_eager, "graph": value,
+                                      f"graph_{n_sets}_steps_per_launch": per_step * reps * n_sets / thr_graph_all},
             "roofline": None, "cpu_baseline": None}
 
 

@@ -270,6 +270,18 @@ int orl_fanout_route_keys_device(orl_ctx* ctx, const uint64_t* d_csr_off, const 
                                  const orl_grain_key* d_follower_keys, const uint32_t* d_pubs, const uint8_t* d_pub_silo,
                                  size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                  uint32_t* d_order, uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
+/* One batch of direct messages + a CSR fan-out, routed and bucketed together (one route launch, one stage-4 pass):
+ * output message j < n_direct is d_direct[j] (as orl_route_batch_device); message n_direct + k is fan-out message k
+ * (as orl_fanout_route_device: followers d_follower_keys[csr_tgt[...]], or GrainId(follower_tcd, csr_tgt[...]) when
+ * d_follower_keys is NULL).  d_pub_offsets[n_pub+1] are absolute output positions (they start at n_direct); *n_out
+ * = n_direct + emitted (with ORL_OPT_TOTAL_GIVEN it holds that total on entry, at least n_direct).  A silo tick's
+ * outbound messages in one call, e.g. Samples/Presence: PresenceGrain.Heartbeat's game messages
+ * (PresenceGrain.cs:42-47) + GameGrain.UpdateGameStatus's player fan-out (GameGrain.cs:62-113). */
+int orl_fanout_route_mixed_device(orl_ctx* ctx, const orl_msg_hdr* d_direct, size_t n_direct, const uint64_t* d_csr_off,
+                                  const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys, uint64_t follower_tcd,
+                                  const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts,
+                                  uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                                  uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
 
 /* ---- stream / reminder rings -------------------------------------------------
  * Two ring providers route stream queues and reminders; both look CLOCKWISE (first ring point >= key):

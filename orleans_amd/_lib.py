@@ -120,6 +120,8 @@ _SIGS = {
                                           C.POINTER(C.c_uint64), _P]),
     "orl_fanout_route_keys_device": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P,
                                                C.POINTER(C.c_uint64), _P]),
+    "orl_fanout_route_mixed_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32,
+                                                _P, _P, _P, _P, _P, C.POINTER(C.c_uint64), _P]),
     "orl_partition_by_owner_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P, _P, _P,
                                                 _P]),
     "orl_partition_by_owner_padded_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32,

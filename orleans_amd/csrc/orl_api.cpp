@@ -1101,17 +1101,21 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
 }
 
 namespace {
-int fanout_impl(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_keys,
-                const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
-                uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order, uint32_t* d_off,
-                uint64_t* n_out, void* stream) {
+int fanout_impl(orl_ctx* c, const orl_msg_hdr* d_direct, size_t n_direct, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                const orl_grain_key* d_keys, const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub,
+                uint64_t follower_tcd, uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
+                uint32_t* d_order, uint32_t* d_off, uint64_t* n_out, void* stream) {
     if (!c || !n_out) return ORL_E_INVALID;
     if (!d_csr_off || !d_csr_tgt || !d_pub_offsets || !d_route || !d_act) return fail(c, ORL_E_INVALID, "null device buffer");
     if (n_pub && (!d_pubs || !d_pub_silo)) return fail(c, ORL_E_INVALID, "null publisher buffer");
+    if (n_direct && !d_direct) return fail(c, ORL_E_INVALID, "null direct message buffer");
     if (!(opts & ORL_OPT_NO_BUCKETS) && (!d_order || !d_off)) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
     if (n_pub + 1 > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "too many publishers");
+    if (n_direct > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "%zu direct messages > max_batch", n_direct);
     if ((opts & ORL_OPT_TOTAL_GIVEN) && *n_out > c->s.max_batch)
         return fail(c, ORL_E_CAPACITY, "given fan-out total %llu > max_batch", (unsigned long long)*n_out);
+    if ((opts & ORL_OPT_TOTAL_GIVEN) && *n_out < n_direct)
+        return fail(c, ORL_E_INVALID, "given total %llu < %zu direct messages", (unsigned long long)*n_out, n_direct);
     if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
     int r = sync_device_state(c);
     if (r) return r;
@@ -1120,7 +1124,8 @@ int fanout_impl(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt
     if (c->timing && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
     if ((r = prepare_probe(c, st))) return r;
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
-    int e = launch_fanout_route_bucket(c->d_params, dir_view(c), d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub,
+    int e = launch_fanout_route_bucket(c->d_params, dir_view(c), d_direct, n_direct, d_csr_off, d_csr_tgt, d_keys, d_pubs,
+                                       d_pub_silo, n_pub,
                                        follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
                                        c->s.max_batch, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > max_batch", (unsigned long long)*n_out);
@@ -1140,8 +1145,8 @@ int orl_fanout_route_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_
                             const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
                             uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                             uint32_t* d_off, uint64_t* n_out, void* stream) {
-    return fanout_impl(c, d_csr_off, d_csr_tgt, nullptr, d_pubs, d_pub_silo, n_pub, follower_tcd, opts, d_pub_offsets, d_route,
-                       d_act, d_order, d_off, n_out, stream);
+    return fanout_impl(c, nullptr, 0, d_csr_off, d_csr_tgt, nullptr, d_pubs, d_pub_silo, n_pub, follower_tcd, opts, d_pub_offsets,
+                       d_route, d_act, d_order, d_off, n_out, stream);
 }
 
 int orl_fanout_route_keys_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
@@ -1149,8 +1154,17 @@ int orl_fanout_route_keys_device(orl_ctx* c, const uint64_t* d_csr_off, const ui
                                  uint32_t opts, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                                  uint32_t* d_off, uint64_t* n_out, void* stream) {
     if (c && !d_keys) return fail(c, ORL_E_INVALID, "null follower key table");
-    return fanout_impl(c, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub, 0, opts, d_pub_offsets, d_route, d_act,
-                       d_order, d_off, n_out, stream);
+    return fanout_impl(c, nullptr, 0, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub, 0, opts, d_pub_offsets, d_route,
+                       d_act, d_order, d_off, n_out, stream);
+}
+
+int orl_fanout_route_mixed_device(orl_ctx* c, const orl_msg_hdr* d_direct, size_t n_direct, const uint64_t* d_csr_off,
+                                  const uint32_t* d_csr_tgt, const orl_grain_key* d_keys, uint64_t follower_tcd,
+                                  const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts,
+                                  uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                                  uint32_t* d_off, uint64_t* n_out, void* stream) {
+    return fanout_impl(c, d_direct, n_direct, d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub, d_keys ? 0 : follower_tcd,
+                       opts, d_pub_offsets, d_route, d_act, d_order, d_off, n_out, stream);
 }
 
 namespace {

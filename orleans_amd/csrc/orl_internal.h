@@ -252,7 +252,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv,
                         const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
                         void* ev_route_begin, void* ev_route_end);
-int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv,
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
                                const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
                                const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
                                uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,

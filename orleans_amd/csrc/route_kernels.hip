@@ -636,13 +636,50 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     return pre + incl - v;
 }
 
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums) {
+// SRC 0: sums of a[0..m).  SRC 1: the fan-out publish offsets' input: element p < m-1 is the out-degree of publisher
+// pubs[p] (csr_off[pubs[p]+1] - csr_off[pubs[p]]), element m-1 is 0; written to a, with pstart[p] = csr_off[pubs[p]]
+// (the publisher's first CSR entry, so the route kernel skips two dependent loads).
+template <int SRC>
+__global__ __launch_bounds__(256) void k_scan_reduce(uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums,
+                                                     const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
+                                                     uint64_t* __restrict__ pstart) {
     __shared__ uint32_t wsum[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
+    constexpr uint32_t J = kScanChunk / 256;
     uint32_t s = 0;
-    for (uint32_t i = threadIdx.x; i < kScanChunk; i += 256) {
-        const uint64_t e = base + i;
-        if (e < m) s += a[e];
+    if (SRC == 0) {
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint64_t e = base + j * 256 + threadIdx.x;
+            if (e < m) s += a[e];
+        }
+    } else {  // staged so every level of loads is in flight at once: publishers, then both CSR offsets
+        uint32_t p[J];
+        uint64_t c0[J], c1[J];
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint64_t e = base + j * 256 + threadIdx.x;
+            p[j] = e + 1 < m ? pubs[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint64_t e = base + j * 256 + threadIdx.x;
+            c0[j] = c1[j] = 0;
+            if (e + 1 < m) {
+                c0[j] = csr_off[p[j]];
+                c1[j] = csr_off[p[j] + 1];
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint64_t e = base + j * 256 + threadIdx.x;
+            if (e < m) {
+                const uint32_t v = (uint32_t)(c1[j] - c0[j]);
+                a[e] = v;
+                if (e + 1 < m) pstart[e] = c0[j];
+                s += v;
+            }
+        }
     }
     uint32_t total;
     block_excl_scan(s, wsum, total);
@@ -662,8 +699,12 @@ __global__ __launch_bounds__(256) void k_scan_sums(uint32_t* __restrict__ sums, 
     }
 }
 
-// Each thread owns 16 consecutive elements of the block's 4096-chunk.
-__global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums) {
+// Each thread owns 16 consecutive elements of the block's 4096-chunk.  DIRECT: the block adds up the earlier chunks'
+// sums itself (a few hundred at most: no k_scan_sums launch); else sums[] holds the scanned chunk prefixes.  WIDEN:
+// also out64[e] = add64 + a[e] (the fan-out's u64 publish offsets).
+template <bool DIRECT, bool WIDEN>
+__global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums,
+                                                   uint64_t* __restrict__ out64, uint64_t add64) {
     __shared__ uint32_t wsum[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16u;
     uint32_t v[16];
@@ -673,11 +714,22 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
         v[i] = (base + i < m) ? a[base + i] : 0u;
         s += v[i];
     }
+    uint32_t pre;
+    if (DIRECT) {
+        uint32_t q = 0;
+        for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) q += sums[i];
+        block_excl_scan(q, wsum, pre);
+    } else {
+        pre = sums[blockIdx.x];
+    }
     uint32_t total;
-    uint32_t run = block_excl_scan(s, wsum, total) + sums[blockIdx.x];
+    uint32_t run = block_excl_scan(s, wsum, total) + pre;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (base + i < m) a[base + i] = run;
+        if (base + i < m) {
+            a[base + i] = run;
+            if (WIDEN) out64[base + i] = add64 + run;
+        }
         run += v[i];
     }
 }
@@ -729,7 +781,9 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M,
     S[(size_t)blockIdx.x * bins + d] = acc;
 }
 
-// 16 columns per block; 16 threads per column each own a contiguous run of chunks.
+// 16 columns per block; 16 threads per column each own a contiguous run of chunks.  (Running k_seg_plan in the last
+// block to finish, to save its launch, measured slower: 5.1 + 4.9 -> 12.0 us at config 5 — the fences and the
+// serialised plan cost more than the launch.)
 __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
                                                   uint32_t* __restrict__ T) {
     __shared__ uint32_t part[16][17];
@@ -758,8 +812,11 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
     }
 }
 
+// row_step: the pass reading the result reads only rows t % row_step == 0 (route tiles smaller than its tile), so
+// only those are written.
 __global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
-                                                   const uint32_t* __restrict__ S, const uint32_t* __restrict__ T) {
+                                                   const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
+                                                   uint32_t row_step) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
     const uint32_t d0 = blockIdx.y * 256;
@@ -776,10 +833,17 @@ __global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uin
     uint32_t run = red + ex + S[(size_t)blockIdx.x * bins + d];
     const uint32_t t0 = blockIdx.x * kScanRows;
     const uint32_t t1 = min(t0 + kScanRows, ntiles);
-    for (uint32_t t = t0; t < t1; ++t) {
-        const uint32_t v = M[(size_t)t * bins + d];
-        M[(size_t)t * bins + d] = run;
-        run += v;
+    // 8 rows per step: all 8 loads in flight before the stores (a load-store-load chain per row measured 10.7 us over
+    // config 5's 2304 rows)
+    for (uint32_t t = t0; t < t1; t += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v[k] = t + k < t1 ? M[(size_t)(t + k) * bins + d] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            if (t + k < t1 && (t + k) % row_step == 0) M[(size_t)(t + k) * bins + d] = run;
+            run += v[k];
+        }
     }
 }
 
@@ -1013,10 +1077,11 @@ __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict
 //
 // k_seg_plan: one workgroup; bstart = exclusive scan of the MSD column totals (or {0, n}), sstart = exclusive
 // scan of ceil(count / seg).  nbk <= 4096 buckets (2048 with 11-bit digits), four per thread.
-__global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
-                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
-    constexpr uint32_t Q = 4;
-    __shared__ uint32_t wsum[2][16];
+template <uint32_t NT>
+__device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
+                                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart,
+                                              uint32_t (*wsum)[16]) {
+    constexpr uint32_t Q = 4096 / NT, NW = NT / 64;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t c[Q], p[Q], cs = 0, ps = 0;
 #pragma unroll
@@ -1034,7 +1099,7 @@ __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ 
     }
     __syncthreads();
     uint32_t cb = ci - cs, pb = pi - ps, ct = 0, pt = 0;
-    for (uint32_t i = 0; i < 16; ++i) {
+    for (uint32_t i = 0; i < NW; ++i) {
         if (i < w) {
             cb += wsum[0][i];
             pb += wsum[1][i];
@@ -1056,6 +1121,12 @@ __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ 
         bstart[nbk] = ct;
         sstart[nbk] = pt;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
+                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
+    __shared__ uint32_t wsum[2][16];
+    seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum);
 }
 
 // Segment j of the launch: blocks [0, nseg) map XCD-contiguously onto segments (consecutive segments of one
@@ -1259,20 +1330,25 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
-__global__ __launch_bounds__(256) void k_fanout_deg(const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
-                                                    uint32_t n_pub, uint32_t* __restrict__ deg) {
-    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-    if (p < n_pub) {
-        const uint32_t s = pubs[p];
-        deg[p] = (uint32_t)(csr_off[s + 1] - csr_off[s]);
-    } else if (p == n_pub) {
-        deg[p] = 0;
+// Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
+// zero-degree publishers share an offset with the next one and are skipped).  Whole wave, same v in every lane: each
+// round samples 64 evenly spaced candidates and keeps the interval between the last one <= v and the next one.
+__device__ __forceinline__ uint32_t wave_find_pub(const uint32_t* __restrict__ poff, uint32_t n_pub, uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t lo = 0, hi = n_pub - 1;  // invariant: poff[lo] <= v, and hi = n_pub - 1 or poff[hi + 1] > v
+    while (lo < hi) {
+        const uint32_t step = (hi - lo + 64u) / 64u;  // ceil((span + 1) / 64): samples reach past hi
+        const uint32_t sl = min(lo + lane * step, hi);
+        const uint64_t le = __ballot(poff[sl] <= v);  // a prefix of lanes (lane 0 always)
+        const uint32_t L = 63u - (uint32_t)__builtin_clzll(le);
+        const uint32_t nlo = min(lo + L * step, hi);
+        if (L < 63u) {
+            const uint32_t nx = min(lo + (L + 1u) * step, hi);
+            if (nx > nlo) hi = nx - 1u;  // poff[nx] > v
+        }
+        lo = nlo;
     }
-}
-
-__global__ __launch_bounds__(256) void k_widen64(const uint32_t* __restrict__ a, uint32_t m, uint64_t* __restrict__ out) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < m) out[i] = a[i];
+    return lo;
 }
 
 constexpr uint32_t kFanLds = 2048;  // publishers staged per tile; beyond that fall back to global search
@@ -1289,9 +1365,10 @@ template <int HB, int PW>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
     uint64_t cmask, const ProbeSlot* __restrict__ probe, const uint32_t* __restrict__ probe_bad,
-    const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ csr_tgt, const uint32_t* __restrict__ pubs,
+    const uint64_t* __restrict__ pstart, const uint32_t* __restrict__ csr_tgt,
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
-    const orl_grain_key* __restrict__ follower_keys, uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
+    const orl_grain_key* __restrict__ follower_keys, const orl_msg_hdr* __restrict__ direct, uint32_t nd, uint32_t n,
+    uint32_t excl, uint32_t* __restrict__ route,
     uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist, uint32_t bins, uint32_t shift, uint32_t items) {
     __shared__ FanSmem<HB> sm;
     constexpr bool HIST = HB > 0;
@@ -1300,26 +1377,25 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
     const uint32_t rtile = kRouteThreads * items;
     const uint32_t base = blockIdx.x * rtile;
-    // n is the caller's total (ORL_OPT_TOTAL_GIVEN) or the scanned one; messages past the scanned total (an overstated
-    // total) get ORL_ST_PAST_TOTAL and never index the CSR / publisher arrays
-    const uint32_t real = poff32[n_pub];
+    // Output [0, nd) = the direct messages, [nd, nd + emitted) = the fan-out.  n is the caller's total
+    // (ORL_OPT_TOTAL_GIVEN) or the scanned one; messages past the scanned total (an overstated total) get
+    // ORL_ST_PAST_TOTAL and never index the CSR / publisher arrays
+    const uint32_t real = nd + poff32[n_pub];
     const uint32_t lim = n < real ? n : real;
     const uint32_t last = ((lim - base) < rtile ? lim : base + rtile) - 1;
-    // publisher of emitted message e = upper_bound(poff32[0..n_pub], e) - 1
-    if (base < lim && (threadIdx.x == 0 || threadIdx.x == 64)) {
-        const uint32_t v = threadIdx.x == 0 ? base : last;
-        uint32_t lo = 0, hi = n_pub + 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (poff32[mid] <= v) lo = mid + 1; else hi = mid;
-        }
-        sm.prange[threadIdx.x == 0 ? 0 : 1] = lo - 1;
+    const uint32_t fbase = base > nd ? base : nd;  // first fan-out message of the tile
+    const bool fan = base < lim && last >= nd;
+    // publisher of fan-out message f = upper_bound(poff32[0..n_pub], f) - 1
+    // (waves 0 and 1, a 64-way search each: 3 dependent loads for 64k publishers instead of 17)
+    if (fan && threadIdx.x < 128) {
+        const uint32_t p = wave_find_pub(poff32, n_pub, (threadIdx.x < 64 ? fbase : last) - nd);
+        if ((threadIdx.x & 63u) == 0) sm.prange[threadIdx.x >> 6] = p;
     }
     __syncthreads();
-    const uint32_t p_lo = base < lim ? sm.prange[0] : 0u, p_hi = base < lim ? sm.prange[1] : 0u;
+    const uint32_t p_lo = fan ? sm.prange[0] : 0u, p_hi = fan ? sm.prange[1] : 0u;
     const uint32_t span = p_hi - p_lo + 1;  // publishers touching this tile
     const bool in_lds = span <= kFanLds;
-    if (in_lds && base < lim)
+    if (in_lds && fan)
         for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
@@ -1333,39 +1409,43 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
             if (HIST) atomicAdd(&sm.hist[(n_act >> shift) & (bins - 1)], 1u);
             continue;
         }
-        uint32_t lo, hi, p, start;
-        if (in_lds) {
-            lo = 0; hi = span + 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (sm.poff[mid] <= e) lo = mid + 1; else hi = mid;
-            }
-            p = p_lo + lo - 1;
-            start = sm.poff[lo - 1];
-        } else {
-            lo = p_lo; hi = p_hi + 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (poff32[mid] <= e) lo = mid + 1; else hi = mid;
-            }
-            p = lo - 1;
-            start = poff32[p];
-        }
-        const uint32_t src = pubs[p];
-        const uint32_t tgt = csr_tgt[csr_off[src] + (e - start)];
         Msg m;
-        if (follower_keys) {  // followers named by a key table (e.g. Guid-keyed players)
-            const orl_grain_key k = follower_keys[tgt];
-            m.tcd = k.type_code_data;
-            m.n0 = k.n0;
-            m.n1 = k.n1;
-        } else {  // GrainId(follower_tcd, long id)
-            m.tcd = follower_tcd;
-            m.n0 = 0;
-            m.n1 = (uint64_t)tgt;
+        if (e < nd) {  // a direct message of the same batch
+            m = load_hdr(direct, e);
+        } else {
+            const uint32_t f = e - nd;
+            uint32_t lo, hi, p, start;
+            if (in_lds) {
+                lo = 0; hi = span + 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sm.poff[mid] <= f) lo = mid + 1; else hi = mid;
+                }
+                p = p_lo + lo - 1;
+                start = sm.poff[lo - 1];
+            } else {
+                lo = p_lo; hi = p_hi + 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (poff32[mid] <= f) lo = mid + 1; else hi = mid;
+                }
+                p = lo - 1;
+                start = poff32[p];
+            }
+            const uint32_t tgt = csr_tgt[pstart[p] + (f - start)];
+            if (follower_keys) {  // followers named by a key table (e.g. Guid-keyed players)
+                const orl_grain_key k = follower_keys[tgt];
+                m.tcd = k.type_code_data;
+                m.n0 = k.n0;
+                m.n1 = k.n1;
+            } else {  // GrainId(follower_tcd, long id)
+                m.tcd = follower_tcd;
+                m.n0 = 0;
+                m.n1 = (uint64_t)tgt;
+            }
+            m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
+            m.aux = 0;
         }
-        m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
-        m.aux = 0;
         uint32_t act;
         route[e] = use16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
                        : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
@@ -2342,11 +2422,22 @@ __global__ __launch_bounds__(256) void k_client_buckets(const orl_msg_hdr* __res
 // ---------------------------------------------------------------------------------------------------
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-int scan_inplace(uint32_t* a, uint64_t m, uint32_t* sums, hipStream_t st) {
+// Exclusive scan in place: 2 launches up to 1024 chunks (4M elements; the down-sweep adds the chunk sums itself), else
+// 3.  (A single-launch decoupled look-back scan measured slower at these sizes: 13-20 us per scan at config 5 against
+// ~9 us for the 2 launches — each chunk's ticket, granule and look-back atomics are device-coherent round trips — and
+// no faster at config 2's 16M offsets.)
+constexpr uint32_t kScanDirectChunks = 1024;
+
+int scan_inplace(uint32_t* a, uint64_t m, const Scratch& s, hipStream_t st) {
     const uint32_t nb = ceil_div(m, kScanChunk);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(256), 0, st, a, m, sums);
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, sums, nb);
-    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(256), 0, st, a, m, sums);
+    if (nb == 0) return 0;
+    hipLaunchKernelGGL(k_scan_reduce<0>, dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, nullptr, nullptr);
+    if (nb <= kScanDirectChunks) {
+        hipLaunchKernelGGL((k_scan_down<true, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull);
+    } else {
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nb);
+        hipLaunchKernelGGL((k_scan_down<false, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull);
+    }
     return (int)hipGetLastError();
 }
 
@@ -2364,9 +2455,19 @@ uint32_t max_route_items(uint32_t n_act) {
     return bp.two_level && bp.hb > 0 ? kMsdItems : kItems;
 }
 
+uint32_t route_min_wgs() {  // ORL_ROUTE_MIN_WG: A/B knob for the small-batch grid (default 2048)
+    static const uint32_t v = [] {
+        const char* e = getenv("ORL_ROUTE_MIN_WG");
+        const long x = e ? atol(e) : 0;
+        return x > 0 ? (uint32_t)x : 2048u;
+    }();
+    return v;
+}
+
 uint32_t route_items(uint64_t n, uint32_t max_items) {
     uint32_t items = max_items;
-    while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < 2048) items >>= 1;
+    const uint32_t min_wg = route_min_wgs();
+    while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < min_wg) items >>= 1;
     return items;
 }
 
@@ -2407,12 +2508,13 @@ void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_
 }
 
 // Column scan of a tile-major [ntiles][bins] histogram into per-(tile, bin) output bases, in place.
-void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, const Scratch& s, hipStream_t st) {
+// row_step: the reading pass uses rows t % row_step == 0 only.
+void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st) {
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
     hipLaunchKernelGGL(k_col_sum, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums);
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot);
-    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot);
+    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot, row_step);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -2441,7 +2543,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
     else ORL_SC(IN_SOA16);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
-    scan_inplace(d_offsets, nb, s.scan_sums, st);  // per-key counts → bucket offsets
+    scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
 #undef ORL_SC
@@ -2489,7 +2591,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk, s, st);
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st);
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
@@ -2515,7 +2617,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
                                (uint32_t)plan.shift[p], bins, s.tile_hist);
-        col_scan(s.tile_hist, nrows, bins, s, st);
+        col_scan(s.tile_hist, nrows, bins, row_step, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
         launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
@@ -2624,21 +2726,31 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st);
 }
 
-int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const uint64_t* d_csr_off,
-                               const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys, const uint32_t* d_pubs,
-                               const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts, uint32_t n_act,
+int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
+                               const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
+                               const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
+                               uint32_t opts, uint32_t n_act,
                                uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                                uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out, const Scratch& s, void* stream,
                                void* ev_route_begin, void* ev_route_end) {
     hipStream_t st = (hipStream_t)stream;
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
-    // degrees → exclusive scan (u32, in s.idx_a) → u64 publish offsets
+    // degrees (+ publisher CSR starts) → exclusive scan (u32 in s.idx_a, relative to the fan-out) → u64 publish offsets
+    // (absolute: + n_direct), in 2 launches (3 beyond 4M publishers)
     uint32_t* poff32 = s.idx_a;
+    uint64_t* pstart = reinterpret_cast<uint64_t*>(s.pairs_b);  // free until a later LSD pass (after the route kernel)
     const uint32_t m = (uint32_t)n_pub + 1;
-    hipLaunchKernelGGL(k_fanout_deg, dim3(ceil_div(m, 256)), dim3(256), 0, st, d_csr_off, d_pubs, (uint32_t)n_pub, poff32);
-    scan_inplace(poff32, m, s.scan_sums, st);
-    hipLaunchKernelGGL(k_widen64, dim3(ceil_div(m, 256)), dim3(256), 0, st, poff32, m, d_pub_offsets);
+    const uint32_t nbs = ceil_div(m, kScanChunk);
+    hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+    if (nbs <= kScanDirectChunks) {
+        hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
+                           d_pub_offsets, (uint64_t)n_direct);
+    } else {
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
+        hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
+                           d_pub_offsets, (uint64_t)n_direct);
+    }
     uint64_t total = *n_out;
     if (!(opts & ORL_OPT_TOTAL_GIVEN)) {  // read the emitted count back (one stream sync)
         uint32_t t32 = 0;
@@ -2646,7 +2758,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
         if (e) return e;
         e = (int)hipStreamSynchronize(st);
         if (e) return e;
-        total = t32;
+        total = n_direct + t32;
         *n_out = total;
     }
     if (total > max_out) return -1;
@@ -2663,8 +2775,9 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
 // the fan-out kernel takes the 16-B form: the 8-B form measured slower here (config 4: 0.266 vs 0.247 ms)
 #define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe) ORL_FAN_(H, 16, TH, BINS, SHIFT); else ORL_FAN_(H, 0, TH, BINS, SHIFT); } while (0)
 #define ORL_FAN_(H, Q, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
-                                                       dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_csr_off, d_csr_tgt, d_pubs, d_pub_silo, poff32, (uint32_t)n_pub,     \
-                                                       follower_tcd, d_follower_keys, (uint32_t)total, excl, d_route, d_act, TH, BINS, \
+                                                       dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
+                                                       follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
+                                                       excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);
     else ORL_FAN(0, nullptr, 1u, 0u);
@@ -2685,7 +2798,7 @@ int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_
     const uint32_t ntiles = ceil_div(n, kTile);
     hipLaunchKernelGGL(k_part_digits, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
                        excl, my_rank, s.digits, s.tile_hist, ntiles, nranks);
-    scan_inplace(s.tile_hist, (uint64_t)nranks * ntiles, s.scan_sums, st);
+    scan_inplace(s.tile_hist, (uint64_t)nranks * ntiles, s, st);
     hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(256), 0, st, d_in, s.digits, (uint32_t)n, s.tile_hist, ntiles, nranks,
                        d_out, d_src_index);
     hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, s.tile_hist, ntiles, nranks, (uint32_t)n, d_counts);
@@ -2752,7 +2865,7 @@ int launch_dir_split(const RouteParams* d_params, DirSlot* d_dir, uint64_t slots
     hipStream_t st = (hipStream_t)stream;
     const uint32_t ntiles = ceil_div(slots, kTile);
     hipLaunchKernelGGL(k_split_count, dim3(ntiles), dim3(256), 0, st, d_params, d_dir, slots, me, s.tile_hist);
-    scan_inplace(s.tile_hist, ntiles, s.scan_sums, st);
+    scan_inplace(s.tile_hist, ntiles, s, st);
     hipLaunchKernelGGL(k_split_emit, dim3(ntiles), dim3(256), 0, st, d_params, d_dir, slots, me, remove ? 1u : 0u, s.tile_hist,
                        d_keys, d_acts, d_silos, cap, d_n_out, d_cnt);
     return (int)hipGetLastError();

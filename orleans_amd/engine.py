@@ -314,6 +314,22 @@ class GrainDirectoryEngine:
                                                         ptr(d_offsets), C.byref(n_out), ptr(stream)))
         return n_out.value
 
+    def fanout_mixed_device(self, d_direct, n_direct: int, d_csr_off, d_csr_tgt, d_follower_keys, follower_tcd: int,
+                            d_pubs, d_pub_silo, n_pub: int, d_pub_offsets, d_route, d_act, d_order=None, d_offsets=None,
+                            stream=None, opts: int = 0, total: Optional[int] = None) -> int:
+        """n_direct direct messages + a CSR fan-out routed and bucketed as ONE batch (output [0, n_direct) = the direct
+        messages, then the fan-out; pub_offsets absolute).  d_follower_keys None = GrainId(follower_tcd, long id).
+        `total` = n_direct + emitted makes the call sync-free.  Returns that total."""
+        if total is not None:
+            opts |= L.OPT_TOTAL_GIVEN
+        n_out = C.c_uint64(int(total or 0))
+        self._ck(self._lib.orl_fanout_route_mixed_device(self._ctx, ptr(d_direct), int(n_direct), ptr(d_csr_off),
+                                                         ptr(d_csr_tgt), ptr(d_follower_keys), int(follower_tcd),
+                                                         ptr(d_pubs), ptr(d_pub_silo), int(n_pub), int(opts),
+                                                         ptr(d_pub_offsets), ptr(d_route), ptr(d_act), ptr(d_order),
+                                                         ptr(d_offsets), C.byref(n_out), ptr(stream)))
+        return n_out.value
+
     def partition_by_owner_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
                                   d_out, d_src_index, d_counts, stream=None, opts: int = 0) -> None:
         ros = np.zeros(256, np.uint8)

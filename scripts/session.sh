@@ -1,5 +1,5 @@
 #!/bin/bash
-# A GPU-box session: optional GPU tests ($TESTS, -k $K), then bench legs ($LEGS: "name:args;name:args").  Every GPU step has
+# A GPU-box session: optional GPU tests ($TESTS, -k $K), then bench legs ($LEGS: "name:[VAR=v ...] args;name:args").  Every GPU step has
 # its own time limit; a crash-like exit (abort, segfault, timeout, kill) ends the session (no further GPU step).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -20,7 +20,11 @@ IFS=';' read -ra LG <<< "$LEGS"
 for leg in "${LG[@]}"; do
   [ -z "$leg" ] && continue
   name=${leg%%:*}; a=${leg#*:}
-  step "bench_$name" ${BLIM:-400} python bench.py $a
+  envs=(); args=()
+  for tok in $a; do  # leading VAR=value tokens set the leg's environment (e.g. ORL_SCAN3=1)
+    if [ ${#args[@]} -eq 0 ] && [[ $tok == [A-Z]*=* ]]; then envs+=("$tok"); else args+=("$tok"); fi
+  done
+  step "bench_$name" ${BLIM:-400} env "${envs[@]}" python bench.py "${args[@]}"
   grep '^{' "gpurun_out/bench_$name.log" > "gpurun_out/bench_$name.json" || true
 done
 echo "=== done"

@@ -423,6 +423,78 @@ def test_config5_full_size_presence(torch):
     eng.close()
 
 
+@pytest.mark.parametrize("over", [None, 0, 777])
+def test_config5_mixed_batch(torch, over):
+    """Config 5 as ONE batch (orl_fanout_route_mixed_device): the 64k game messages then their 512k-message player
+    fan-out, routed and bucketed together == the oracle's route + bucket of the concatenated batch; publish offsets
+    absolute.  over None: emitted count read back; 0: exact total given (eager + hipGraph replay); 777: total
+    overstated, the tail is ORL_ST_PAST_TOTAL in the unresolved bucket."""
+    t = torch
+    cl = W.default_cluster()
+    n_games, per_game, n_hb = 100_000, 8, 64 * 1024
+    pr = W.presence_population(n_games, per_game)
+    all_keys = np.concatenate([pr.game_keys, pr.player_keys])
+    n_keys = len(all_keys)
+    owner = cl.owner_of(W.jenkins3_np(all_keys["tcd"], all_keys["n0"], all_keys["n1"]))
+    n_fan = n_hb * per_game
+    n_tot = n_hb + n_fan
+    cap = n_tot + 1024
+    eng = GrainDirectoryEngine(n_act=n_keys, dir_capacity=n_keys, max_batch=cap, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, all_keys, owner, np.ones(n_keys, bool))
+    o = _oracle_for(cl, all_keys, np.arange(n_keys, dtype=np.uint32), owner)
+    games, gm = W.heartbeat_batch(pr, cl, n_hb, 1)
+    gsilo = owner[games.astype(np.int64)]
+    exp, poff_ref = cpu_ref.fanout_expand(pr.csr_off, pr.csr_tgt, games, gsilo, 0)
+    kk = pr.player_keys[exp["n1"].astype(np.int64)]
+    exp["tcd"], exp["n0"], exp["n1"] = kk["tcd"], kk["n0"], kk["n1"]
+    batch = np.concatenate([gm, exp])
+    re, ae = o.route(batch)
+    n_out = n_tot + (over or 0)
+    if over:  # the overstated tail: no message, unresolved bucket
+        re = np.concatenate([re, np.full(over, (L.ST_PAST_TOTAL << 16) | 0xFFFF, np.uint32)])
+        ae = np.concatenate([ae, np.full(over, L.NO_ACT, np.uint32)])
+    oe, fe = o.bucket(ae, n_keys)
+    dv = "cuda"
+    d_gm = t.from_numpy(gm.view(np.int32).reshape(-1, 8)).to(dv)
+    d_off = t.from_numpy(pr.csr_off.view(np.int64)).to(dv)
+    d_tgt = t.from_numpy(pr.csr_tgt.view(np.int32)).to(dv)
+    d_keys = t.from_numpy(pr.player_keys.view(np.uint8).reshape(-1, 24)).to(dv)
+    d_g = t.from_numpy(games.view(np.int32)).to(dv)
+    d_s = t.from_numpy(gsilo).to(dv)
+    outs = [t.empty(cap, dtype=t.int32, device=dv) for _ in range(3)] + [t.empty(n_keys + 2, dtype=t.int32, device=dv)]
+    poff = t.empty(n_hb + 1, dtype=t.int64, device=dv)
+    s = t.cuda.Stream()
+    total = None if over is None else n_out
+
+    def step():
+        return eng.fanout_mixed_device(d_gm, n_hb, d_off, d_tgt, d_keys, 0, d_g, d_s, n_hb, poff, *outs[:3], outs[3],
+                                       stream=s.cuda_stream, total=total)
+
+    def check():
+        for x, e, m in zip(outs, (re, ae, oe, fe), (n_out, n_out, n_out, n_keys + 2)):
+            np.testing.assert_array_equal(_u32(x)[:m], e)
+        np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), poff_ref + np.uint64(n_hb))
+
+    with t.cuda.stream(s):
+        got = step()
+    s.synchronize()
+    assert got == n_out
+    check()
+    if over == 0:
+        g = t.cuda.CUDAGraph()
+        with t.cuda.graph(g, stream=s):
+            step()
+        for x in outs:
+            x.fill_(-1)
+        t.cuda.synchronize()
+        with t.cuda.stream(s):
+            g.replay()
+        s.synchronize()
+        check()
+    eng.close()
+
+
 # ---- stage-4 ranking: the LDS lane-order self-check and the ballot fallback (VERDICT r1 item 7) ---------------
 @pytest.mark.parametrize("n_act", [5000, 1_000_000, 12_000_000])
 def test_stage4_rank_modes_vs_oracle(torch, n_act):
