@@ -29,6 +29,7 @@
 // Jenkins == u64-path Jenkins) and its shipped Chirper graph: ring ownership, directory lookup,
 // placement, bucketing and fan-out have no reference golden vector.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <thread>
@@ -299,11 +300,19 @@ int ref_bucket(const uint32_t* act, size_t n, uint32_t n_act, uint32_t* order, u
 // concatenated in thread order, so the per-activation FIFO order is identical to ref_bucket's.
 int ref_route_bucket_mt(const ref_cluster* cl, void* dir, const ref_msg* in, size_t n, uint32_t opts, uint32_t n_act,
                         uint32_t* route, uint32_t* act, uint32_t* order, uint32_t* offsets, int nthreads) {
+    // Same outputs as ref_route_bucket (a stable counting sort by key = min(act, n_act)), computed in parallel as a
+    // stable MSD split by the key's high bits followed by a counting sort of each high bucket by the low bits (one
+    // thread per bucket), so the working set per thread is 2^HB + 2^(bits-HB) counters, not n_act.
     if (nthreads < 1) nthreads = 1;
     const Partition& p = *static_cast<Partition*>(dir);
-    const size_t nb = (size_t)n_act + 1;
-    std::vector<std::vector<uint32_t>> hist(nthreads, std::vector<uint32_t>(nb, 0));
+    const size_t nb = (size_t)n_act + 1;  // keys 0 .. n_act
+    uint32_t bits = 1;
+    while (((size_t)1 << bits) < nb) ++bits;
+    const uint32_t hb = bits < 12 ? bits : 12, sh = bits - hb;
+    const size_t nhi = (size_t)1 << hb;
+    std::vector<std::vector<uint32_t>> hist(nthreads, std::vector<uint32_t>(nhi, 0));
     auto range = [&](int t, size_t& lo, size_t& hi) { lo = n * t / nthreads; hi = n * (t + 1) / nthreads; };
+    auto key_of = [&](size_t i) { return act[i] < n_act ? act[i] : n_act; };
     std::vector<std::thread> th;
     for (int t = 0; t < nthreads; ++t)
         th.emplace_back([&, t] {
@@ -312,30 +321,61 @@ int ref_route_bucket_mt(const ref_cluster* cl, void* dir, const ref_msg* in, siz
             auto& h = hist[t];
             for (size_t i = lo; i < hi; ++i) {
                 route[i] = route_one(cl, p, in[i], (opts & 1) != 0, &act[i]);
-                ++h[act[i] < n_act ? act[i] : n_act];
+                ++h[key_of(i) >> sh];
             }
         });
     for (auto& x : th) x.join();
     th.clear();
-    // bucket-major, thread-minor exclusive scan
-    uint32_t run = 0;
-    for (size_t b = 0; b < nb; ++b) {
-        offsets[b] = run;
+    // high-bucket-major, thread-minor exclusive scan: stable split
+    std::vector<size_t> bstart(nhi + 1);
+    size_t run = 0;
+    for (size_t b = 0; b < nhi; ++b) {
+        bstart[b] = run;
         for (int t = 0; t < nthreads; ++t) {
             const uint32_t c = hist[t][b];
-            hist[t][b] = run;
+            hist[t][b] = (uint32_t)run;
             run += c;
         }
     }
-    offsets[nb] = run;
+    bstart[nhi] = run;
+    std::vector<uint32_t> tkey(n), tidx(n);
     for (int t = 0; t < nthreads; ++t)
         th.emplace_back([&, t] {
             size_t lo, hi;
             range(t, lo, hi);
             auto& h = hist[t];
-            for (size_t i = lo; i < hi; ++i) order[h[act[i] < n_act ? act[i] : n_act]++] = (uint32_t)i;
+            for (size_t i = lo; i < hi; ++i) {
+                const uint32_t k = key_of(i);
+                const uint32_t pos = h[k >> sh]++;
+                tkey[pos] = k;
+                tidx[pos] = (uint32_t)i;
+            }
         });
     for (auto& x : th) x.join();
+    th.clear();
+    // each high bucket: stable counting sort by the low bits; writes its keys' offsets and its part of `order`
+    std::atomic<size_t> next{0};
+    for (int t = 0; t < nthreads; ++t)
+        th.emplace_back([&] {
+            std::vector<uint32_t> cnt((size_t)1 << sh);
+            for (size_t b; (b = next.fetch_add(1)) < nhi;) {
+                const size_t k0 = b << sh;
+                if (k0 >= nb) continue;
+                const size_t k1 = std::min(nb, (b + 1) << sh);
+                std::fill(cnt.begin(), cnt.end(), 0u);
+                for (size_t j = bstart[b]; j < bstart[b + 1]; ++j) ++cnt[tkey[j] - k0];
+                uint32_t r = (uint32_t)bstart[b];
+                for (size_t k = k0; k < k1; ++k) {
+                    const uint32_t c = cnt[k - k0];
+                    offsets[k] = r;
+                    cnt[k - k0] = r;
+                    r += c;
+                }
+                for (size_t j = bstart[b]; j < bstart[b + 1]; ++j) order[cnt[tkey[j] - k0]++] = tidx[j];
+            }
+        });
+    for (auto& x : th) x.join();
+    offsets[nb] = (uint32_t)n;
     return 0;
 }
 
