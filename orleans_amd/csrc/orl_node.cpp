@@ -102,7 +102,8 @@ struct orl_node {
     ncclComm_t comm = nullptr;
     std::shared_ptr<LocalGroup> group;
     hipStream_t sp = nullptr, sx = nullptr, sr = nullptr;
-    hipEvent_t ev_in = nullptr, ev_part = nullptr, ev_x = nullptr, ev_r = nullptr;
+    hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
+    hipEvent_t ev_part[2] = {nullptr, nullptr};  // the slot's partition (and heads) are complete
     hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
     uint8_t* d_ros = nullptr;
     uint8_t* d_send[2] = {nullptr, nullptr};      // hop-1 send regions: nranks x chunk_cap x 32 B per slot
@@ -234,7 +235,7 @@ void free_node(orl_node* nd) {
     f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
     f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
-    for (hipEvent_t e : {nd->ev_in, nd->ev_part, nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
+    for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr})
         if (s) (void)hipStreamDestroy(s);
@@ -317,7 +318,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipStreamCreateWithFlags(&nd->sp, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part, &nd->ev_x, &nd->ev_r, &nd->ev_slot[0], &nd->ev_slot[1]})
+    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_slot[0], &nd->ev_slot[1]})
         ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     const uint64_t nr = cfg->nranks, mr = cfg->max_recv;
     ok(hipMalloc((void**)&nd->d_ros, 256));
@@ -387,14 +388,16 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     uint64_t sent_remote = 0;
     bool any_wide = false;
     // ---- hop 1 -------------------------------------------------------------------------------------------
-    for (uint32_t c = 0; c < K; ++c) {
+    // Partition of chunk c into send slot c & 1 (after the slot's previous exchange): per-rank counts + wire status
+    // in the slot's head words.  Chunk c + 1 is partitioned before the host waits for chunk c's counts, so the
+    // partition stream does not idle through the all-gather round trip.
+    auto partition = [&](uint32_t c, bool wide) -> int {
         const uint32_t slot = c & 1u;
         const uint64_t start = std::min<uint64_t>((uint64_t)c * cs, n), len = std::min<uint64_t>(cs, n - start);
         uint64_t* head = nd->d_head + slot * kHeadWords;
         uint8_t* send = nd->d_send[slot];
         NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_slot[slot], 0));  // the slot's previous exchange has finished
         NODE_HIP(nd, hipMemsetAsync(head, 0, kHeadWords * 8, nd->sp));
-        bool wide = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
         if (wide)
             NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
                                                               nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
@@ -403,17 +406,25 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             NODE_CTX(nd, orl_partition_compact_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
                                                       nd->chunk_cap, reinterpret_cast<orl_wire_msg*>(send), nullptr, head,
                                                       reinterpret_cast<uint32_t*>(head + 8), nd->sp));
-        NODE_HIP(nd, hipEventRecord(nd->ev_part, nd->sp));
-        if (int r = allgather_heads(nd, head, nd->ev_part)) return r;
+        NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+        return ORL_OK;
+    };
+    const bool wide_only = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
+    if (K > 0)
+        if (int r = partition(0, wide_only)) return r;
+    for (uint32_t c = 0; c < K; ++c) {
+        const uint32_t slot = c & 1u;
+        uint64_t* head = nd->d_head + slot * kHeadWords;
+        uint8_t* send = nd->d_send[slot];
+        if (c + 1 < K)
+            if (int r = partition(c + 1, wide_only)) return r;
+        if (int r = allgather_heads(nd, head, nd->ev_part[slot])) return r;
         const uint64_t* H = nd->h_heads;
+        bool wide = wide_only;
         if (!wide) {
             for (uint32_t r = 0; r < nr; ++r) wide |= (H[r * W + 8] & 0xFFFFFFFFull) != 0;
-            if (wide) {  // some rank's chunk has a message without the compact form: every rank sends 32-B headers
-                NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
-                                                                  nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
-                                                                  head, nd->sp));
-                NODE_HIP(nd, hipEventRecord(nd->ev_part, nd->sp));
-            }
+            if (wide)  // some rank's chunk has a message without the compact form: every rank sends 32-B headers
+                if (int r = partition(c, true)) return r;
         }
         any_wide |= wide;
         const uint32_t width = wide ? 32u : 16u;
@@ -434,7 +445,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
                              (unsigned long long)owned_all[d], (unsigned long long)nd->cfg.max_recv);
         }
         uint8_t* recv = nd->d_recv + owned_bytes;
-        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, sendc.data(), recvc.data(), nd->ev_part)) return r;
+        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, sendc.data(), recvc.data(), nd->ev_part[slot]))
+            return r;
         NODE_HIP(nd, hipEventRecord(nd->ev_slot[slot], nd->sx));
         nd->segs.push_back(orl_node::Seg{recv, got, width});
         if (got) {  // stages 1-3 of the received chunk, overlapping the next chunk's exchange
