@@ -692,7 +692,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->hev) if (e) (void)hipEventDestroy(e);
@@ -791,8 +791,11 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         const uint64_t seg_rows = std::max<uint64_t>(max_segments(mb, bp.hb), max_segments(std::min<uint64_t>(mb, (16u << 20) - 1), bp.hb));
         const uint64_t seg_words = bp.two_level ? seg_rows << bp.lb : 1;
         if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
+        const uint64_t carry_words = bp.two_level ? ((seg_rows + 63) / 64) << bp.lb : 1;
+        if ((e = hipMalloc((void**)&c->s.seg_carry, carry_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_carry)");
+        if ((e = hipMalloc((void**)&c->s.seg_meta, ((seg_rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_meta)");
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
-        if ((e = hipMalloc((void**)&c->s.sstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
+        if ((e = hipMalloc((void**)&c->s.sstart, 4098 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
         if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");

@@ -229,8 +229,10 @@ struct Scratch {
     uint32_t* col_tot;      // [2048] column totals
     uint8_t* digits;        // [max_batch] (partition by owner)
     uint32_t* seg_hist;     // [max segments][2^lb] two-level path: per-segment low-digit counts → bases
+    uint32_t* seg_carry;    // [ceil(max segments / 64)][2^lb] chunked segment scan: chunk sums, then carry-ins
+    uint32_t* seg_meta;     // [ceil(max segments / 64)] chunked segment scan: each chunk's first bucket + shape bits
     uint32_t* bstart;       // [4097] bucket starts (two-level path; k_seg_plan handles up to 4096)
-    uint32_t* sstart;       // [4097] first segment of each bucket
+    uint32_t* sstart;       // [4098] first segment of each bucket; [4097] = a bucket has > 64 segments (skew flag)
     uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile
     uint64_t max_batch;
     uint64_t max_tiles;

@@ -1077,13 +1077,17 @@ __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict
 //
 // k_seg_plan: one workgroup; bstart = exclusive scan of the MSD column totals (or {0, n}), sstart = exclusive
 // scan of ceil(count / seg).  nbk <= 4096 buckets (2048 with 11-bit digits), four per thread.
+// sstart[kSkewSlot] = 1 when some bucket has more than kScanRows segments (a hot activation): the segment scan then
+// takes the chunked kernels, else the one-pass k_seg_scan (cheaper when every bucket is short).
+constexpr uint32_t kSkewSlot = 4097;
+
 template <uint32_t NT>
 __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart,
                                               uint32_t (*wsum)[16]) {
     constexpr uint32_t Q = 4096 / NT, NW = NT / 64;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t c[Q], p[Q], cs = 0, ps = 0;
+    uint32_t c[Q], p[Q], cs = 0, ps = 0, pmax = 0;
 #pragma unroll
     for (uint32_t q = 0; q < Q; ++q) {
         const uint32_t b = threadIdx.x * Q + q;
@@ -1091,13 +1095,22 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
         p[q] = (c[q] + seg - 1) / seg;
         cs += c[q];
         ps += p[q];
+        pmax = max(pmax, p[q]);
     }
     const uint32_t ci = wave_incl_scan(cs), pi = wave_incl_scan(ps);
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) pmax = max(pmax, (uint32_t)__shfl_xor(pmax, d, 64));
     if (lane == 63) {
         wsum[0][w] = ci;
         wsum[1][w] = pi;
+        wsum[2][w] = pmax;
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < NW; ++i) m = max(m, wsum[2][i]);
+        sstart[kSkewSlot] = m > kScanRows ? 1u : 0u;
+    }
     uint32_t cb = ci - cs, pb = pi - ps, ct = 0, pt = 0;
     for (uint32_t i = 0; i < NW; ++i) {
         if (i < w) {
@@ -1125,7 +1138,7 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
 
 __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
-    __shared__ uint32_t wsum[2][16];
+    __shared__ uint32_t wsum[3][16];
     seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum);
 }
 
@@ -1205,16 +1218,15 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
     for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
 }
 
-// grid (nbk, ceil(BL/256)): per bucket and low digit, the segment rows become exclusive prefixes inside the
-// bucket and the column total (messages with key = b << lb | l) goes to counts[key] (keys < nb only).
+// Per bucket b and low digit l (every bucket has <= kScanRows segments): the segment rows become exclusive prefixes
+// inside the bucket and the column total (messages with key = b << lb | l) goes to counts[key] (keys < nb only).
 template <int LB>
-__global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
-                                                  uint32_t nb, uint32_t* __restrict__ counts) {
+__device__ __forceinline__ void seg_scan_bucket(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
+                                                uint32_t nbk, uint32_t nb, uint32_t* __restrict__ counts, uint32_t b,
+                                                uint32_t l) {
     constexpr uint32_t BL = 1u << LB;
-    const uint32_t l = blockIdx.y * 256u + threadIdx.x;
-    const uint32_t b = blockIdx.x;
     if (b == 0 && l == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
-        for (uint32_t k = gridDim.x << LB; k < nb; ++k) counts[k] = 0;
+        for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
     if (l >= BL) return;
     const uint32_t j0 = sstart[b], j1 = sstart[b + 1];
     uint32_t run = 0, j = j0;
@@ -1237,6 +1249,155 @@ __global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_his
     if (key < nb) counts[key] = run;
 }
 
+// The same scan, parallel over segments: a bucket of a hot activation (Zipf) has thousands of segments, which
+// k_seg_scan walks with one thread per column (278 us per call at config 3 on 8 ranks, ~1 ms on the hottest rank).
+// The segment rows are cut into chunks of kScanRows rows regardless of buckets:
+//   seg_csum_chunk: per chunk and digit, exclusive prefixes inside the chunk restarting at every bucket start; the
+//                 sum of the bucket still open at the chunk's end -> carry[c][l]; buckets ending inside the chunk
+//                 write their (possibly partial) total to counts[key]; buckets without segments get 0;
+//   k_seg_carry:  per digit, a segmented scan over the chunks (each chunk maps the incoming open-bucket sum
+//                 acc -> A*acc + B, A in {0, 1}): carry[c][l] becomes the chunk's carry-in, added to the total of the
+//                 chunk's first bucket when that bucket ends inside the chunk;
+//   k_seg_scatter adds the carry-in to the row base of every segment of a chunk's first bucket.
+// k_seg_plan flags the skew on the device, so both forms are launched and the one not taken returns at once: the
+// short-bucket form shares k_seg_scan's launch, and k_seg_carry exits.
+// Each thread loads 16 rows at a time (all in flight) before it rewrites them.
+__device__ __forceinline__ uint32_t bucket_of_segment(const uint32_t* __restrict__ sstart, uint32_t nbk, uint32_t j) {
+    uint32_t lo = 0, hi = nbk + 1;  // upper_bound(sstart, j) - 1 (skips empty buckets)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sstart[mid] <= j) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1;
+}
+
+constexpr uint32_t kMetaBucket = (1u << 29) - 1, kMetaEnds = 1u << 29, kMetaCont = 1u << 30, kMetaInside = 1u << 31;
+
+template <int LB>
+__device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
+                                               uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
+                                               uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t c,
+                                               uint32_t l) {
+    constexpr uint32_t BL = 1u << LB, G = 16;
+    const uint32_t nseg = sstart[nbk];
+    const uint32_t j0 = c * kScanRows;
+    if (l >= BL || j0 >= nseg) return;
+    const uint32_t j1 = min(j0 + kScanRows, nseg);
+    uint32_t b = bucket_of_segment(sstart, nbk, j0);
+    if (l == 0)  // the chunk's shape: first bucket, it ends inside, it continues an earlier one, a bucket starts inside
+        meta[c] = b | (sstart[b + 1] <= j1 ? kMetaEnds : 0u) | (sstart[b] < j0 ? kMetaCont : 0u) |
+                  (sstart[b + 1] < j1 ? kMetaInside : 0u);
+    auto put = [&](uint32_t k, uint32_t v) {
+        const uint32_t key = (k << LB) | l;
+        if (key < nb) counts[key] = v;
+    };
+    if (sstart[b] == j0)  // b starts this chunk: the empty buckets just before it (no other chunk meets them)
+        for (uint32_t k = b; k > 0 && sstart[k - 1] == j0;) put(--k, 0u);
+    uint32_t next = sstart[b + 1];
+    uint32_t run = 0;
+    for (uint32_t g = j0; g < j1; g += G) {
+        uint32_t v[G];
+#pragma unroll
+        for (uint32_t q = 0; q < G; ++q) v[q] = g + q < j1 ? seg_hist[(size_t)(g + q) * BL + l] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < G; ++q) {
+            const uint32_t j = g + q;
+            const bool live = j < j1;
+            if (live && j == next) {  // bucket b ends before row j: its (partial, if it began before j0) total
+                put(b, run);
+                run = 0;
+                while ((next = sstart[++b + 1]) <= j) put(b, 0u);  // skipped buckets are empty
+            }
+            if (live) {
+                seg_hist[(size_t)j * BL + l] = run;
+                run += v[q];
+            }
+        }
+    }
+    if (next == j1) {  // the open bucket ends exactly at the chunk's end
+        put(b, run);
+        if (j1 == nseg)
+            for (uint32_t k = b + 1; k < nbk; ++k) put(k, 0u);  // empty buckets after the last segment
+    }
+    if (l == 0 && j1 == nseg)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+        for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
+    carry[(size_t)c * BL + l] = run;
+}
+
+// One launch for both forms: grid (max(nbk, chunks), ceil(BL / 256)); k_seg_plan's skew flag picks the role.
+template <int LB>
+__global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
+                                                  uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts) {
+    const uint32_t l = blockIdx.y * 256u + threadIdx.x;
+    if (!sstart[kSkewSlot]) {
+        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l);
+    } else {
+        seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l);
+    }
+}
+
+// 16 digits per block, 16 threads per digit, each owning a contiguous run of chunks: the run's composed map, a scan of
+// the maps across the 16 threads in LDS, then the run's carry-ins.  Chunk c maps the open-bucket sum entering it,
+// acc -> A * acc + B: A = 1 when it continues an earlier bucket and no bucket starts inside it, B = its carry.
+template <int LB>
+__global__ __launch_bounds__(256) void k_seg_carry(const uint32_t* __restrict__ sstart, uint32_t nbk, uint32_t n_keys,
+                                                   const uint32_t* __restrict__ meta, uint32_t* __restrict__ carry,
+                                                   uint32_t* __restrict__ counts) {
+    constexpr uint32_t BL = 1u << LB, U = 8;
+    if (!sstart[kSkewSlot]) return;
+    __shared__ uint32_t mapA[16][17], mapB[16][17];
+    const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
+    const uint32_t l = blockIdx.x * 16u + col;
+    const uint32_t nseg = sstart[nbk];
+    const uint32_t nch = (nseg + kScanRows - 1) / kScanRows;
+    const uint32_t per = (nch + 15) / 16;
+    const uint32_t c0 = min(grp * per, nch), c1 = min(c0 + per, nch);
+    const bool on = l < BL;
+    const uint32_t nb = n_keys;
+    uint32_t A = 1, B = 0;  // identity
+    for (uint32_t c = c0; c < c1; c += U) {
+        uint32_t m[U], v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            m[u] = c + u < c1 ? meta[c + u] : 0u;
+            v[u] = (c + u < c1 && on) ? carry[(size_t)(c + u) * BL + l] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (c + u >= c1) continue;
+            const uint32_t a = (m[u] & kMetaCont) && !(m[u] & kMetaInside) ? 1u : 0u;
+            B = a * B + v[u];  // (a, v) o (A, B)
+            A = a * A;
+        }
+    }
+    mapA[grp][col] = A;
+    mapB[grp][col] = B;
+    __syncthreads();
+    uint32_t acc = 0;  // the open-bucket sum entering this thread's run
+    for (uint32_t g = 0; g < grp; ++g) acc = mapA[g][col] * acc + mapB[g][col];
+    if (!on) return;
+    for (uint32_t c = c0; c < c1; c += U) {
+        uint32_t m[U], v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            m[u] = c + u < c1 ? meta[c + u] : 0u;
+            v[u] = c + u < c1 ? carry[(size_t)(c + u) * BL + l] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (c + u >= c1) continue;
+            const bool cont = (m[u] & kMetaCont) != 0;
+            const uint32_t a = cont && !(m[u] & kMetaInside) ? 1u : 0u;
+            const uint32_t cin = cont ? acc : 0u;
+            carry[(size_t)(c + u) * BL + l] = cin;  // k_seg_scatter adds it to the rows of the chunk's first bucket
+            const uint32_t key = ((m[u] & kMetaBucket) << LB) | l;
+            if (cin && (m[u] & kMetaEnds) && key < nb) counts[key] += cin;  // that bucket's total, when it ends here
+            acc = a * acc + v[u];
+        }
+    }
+}
+
 // One segment: LDS rounds of kSegChunk messages.  Each round ranks its messages with wave_rank (wave w owns
 // [w*1024, w*1024+1024) of the round, 16 steps of 64 lanes, so (round, wave, step, lane) order is arrival
 // order), turns the per-wave counts into round-local sorted starts, stages the indices in LDS in sorted
@@ -1256,7 +1417,8 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      uint32_t seg,
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
-                                                     uint32_t nb, uint32_t n, uint32_t* __restrict__ order) {
+                                                     uint32_t nb, uint32_t n, const uint32_t* __restrict__ seg_carry,
+                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order) {
     constexpr uint32_t BL = 1u << LB;
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
@@ -1266,11 +1428,15 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t run[PER];  // global position of the next message with digit threadIdx.x * PER + q
     const uint32_t* hrow = seg_hist + (size_t)r.index * BL;
+    // a hot bucket's segments (chunked segment scan): the carry-in of the chunk whose first bucket this segment is in
+    const uint32_t ch = r.index / kScanRows;
+    const uint32_t cin_on = (sstart[kSkewSlot] && (seg_meta[ch] & kMetaBucket) == r.bucket) ? 1u : 0u;
+    const uint32_t* cin_row = seg_carry + (cin_on ? (size_t)ch * BL : 0);
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t l = threadIdx.x * PER + q;
         const uint32_t key = (r.bucket << LB) | l;
-        run[q] = (l < BL && key < nb) ? offsets[key] + hrow[l] : 0u;
+        run[q] = (l < BL && key < nb) ? offsets[key] + hrow[l] + cin_row[l] * cin_on : 0u;
     }
     for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
         const uint32_t wbase = c0 + w * (kItems * 64u);
@@ -2537,12 +2703,19 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
-                                         s.sstart, s.seg_hist, d_offsets, nb, n, d_order)
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
 #define ORL_SS(I) do { const int rm_ = host_rm(); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
     if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
     else ORL_SC(IN_SOA16);
-    hipLaunchKernelGGL((k_seg_scan<LB>), dim3(nbk, ceil_div(1u << LB, 256)), dim3(256), 0, st, s.seg_hist, s.sstart, nb, d_offsets);
+    // the segment scan: k_seg_scan when every bucket has <= kScanRows segments, else the chunked kernels (k_seg_plan
+    // sets the flag on the device; the path not taken returns at once)
+    const uint32_t cb = ceil_div(1u << LB, 256);
+    const uint32_t nch = ceil_div(grid, kScanRows);
+    hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb, s.seg_carry,
+                       s.seg_meta, d_offsets);
+    hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
+                       d_offsets);
     scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
