@@ -699,6 +699,34 @@ __global__ __launch_bounds__(256) void k_scan_sums(uint32_t* __restrict__ sums, 
     }
 }
 
+// 16 consecutive u32 of a thread (4 x 16-B loads when they are all in range and the caller's array is 16-B aligned;
+// `fill` past m).
+__device__ __forceinline__ void load16(const uint32_t* __restrict__ a, uint64_t base, uint64_t m, uint32_t fill, uint32_t (&v)[16]) {
+    if (base + 16 <= m && (reinterpret_cast<uintptr_t>(a) & 15u) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(a + base);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 x = p[q];
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = base + i < m ? a[base + i] : fill;
+    }
+}
+
+__device__ __forceinline__ void store16(uint32_t* __restrict__ a, uint64_t base, uint64_t m, const uint32_t (&v)[16]) {
+    if (base + 16 <= m && (reinterpret_cast<uintptr_t>(a) & 15u) == 0) {
+        uint4* p = reinterpret_cast<uint4*>(a + base);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (base + i < m) a[base + i] = v[i];
+    }
+}
+
 // Each thread owns 16 consecutive elements of the block's 4096-chunk.  DIRECT: the block adds up the earlier chunks'
 // sums itself (a few hundred at most: no k_scan_sums launch); else sums[] holds the scanned chunk prefixes.  WIDEN:
 // also out64[e] = add64 + a[e] (the fan-out's u64 publish offsets).
@@ -708,12 +736,10 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
     __shared__ uint32_t wsum[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16u;
     uint32_t v[16];
+    load16(a, base, m, 0u, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        v[i] = (base + i < m) ? a[base + i] : 0u;
-        s += v[i];
-    }
+    for (int i = 0; i < 16; ++i) s += v[i];
     uint32_t pre;
     if (DIRECT) {
         uint32_t q = 0;
@@ -724,14 +750,14 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
     }
     uint32_t total;
     uint32_t run = block_excl_scan(s, wsum, total) + pre;
+    uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (base + i < m) {
-            a[base + i] = run;
-            if (WIDEN) out64[base + i] = add64 + run;
-        }
+        o[i] = run;
+        if (WIDEN && base + i < m) out64[base + i] = add64 + run;
         run += v[i];
     }
+    store16(a, base, m, o);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -749,15 +775,39 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
     __syncthreads();
     const uint32_t base = blockIdx.x * kTile;
     uint32_t k[kItems];
+    if (ACTS) {  // arrival order: element j * 256 + x (coalesced)
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
-        const uint32_t e = base + j * 256 + threadIdx.x;
-        const uint32_t ec = e < n ? e : n - 1;
-        k[j] = ACTS ? bucket_key(static_cast<const uint32_t*>(in)[ec], n_act) : static_cast<const uint2*>(in)[ec].x;
+        for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
+            const uint32_t e = base + j * 256 + threadIdx.x;
+            k[j] = bucket_key(static_cast<const uint32_t*>(in)[e < n ? e : n - 1], n_act);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+            if (base + j * 256 + threadIdx.x < n) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
+    } else {
+        // pairs of an LSD pass: sorted by the previous digit, so a hot key's pairs sit in consecutive lanes.  Loads stay
+        // coalesced (element j * 256 + x); each run of equal digits inside a 64-lane step adds its length with one
+        // atomic from its first lane, so a hot key no longer serialises 64 lanes on one LDS address.
+        const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
+            const uint32_t e = base + j * 256 + threadIdx.x;
+            k[j] = static_cast<const uint2*>(in)[e < n ? e : n - 1].x;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+            const uint32_t e = base + j * 256 + threadIdx.x;
+            const uint32_t d = e < n ? (k[j] >> shift) & (bins - 1) : 0xFFFFFFFFu;  // past the end: a run never counted
+            const uint32_t prev = __shfl_up(d, 1, 64);
+            const bool head = lane == 0 || d != prev;
+            const uint64_t heads = __ballot(head);
+            if (head && d != 0xFFFFFFFFu) {
+                const uint64_t after = lane == 63 ? 0ull : heads >> (lane + 1);
+                const uint32_t len = after ? (uint32_t)__builtin_ctzll(after) + 1u : 64u - lane;
+                atomicAdd(&hist[d], len);
+            }
+        }
     }
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j)
-        if (base + j * 256 + threadIdx.x < n) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
     __syncthreads();
     uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
@@ -1058,6 +1108,88 @@ __global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict
         if (i0 + q < n && k[q] != prev && k[q] < nb) offsets[k[q]] = (uint32_t)(i0 + q);
         prev = k[q];
     }
+}
+
+// Empty buckets by a suffix-min scan instead of one binary search per key (k_offsets_fill: 306 us at config 3, whose
+// 16M handles are mostly absent from a Zipf batch): present keys hold their first position and positions grow with
+// the key, so offsets[b] = min(offsets[b .. nb), n) is lower_bound(sorted, b) for every b.  In 4096-element chunks:
+// chunk minima; their exclusive suffix minima (one block); each chunk rescanned from its end.
+__device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_down(v, d, 64);
+        if (lane + d < 64) v = min(v, t);
+    }
+    return v;
+}
+
+// Minimum over the threads after this one (256 threads; `after_all` = the value past the last thread).
+__device__ __forceinline__ uint32_t block_excl_suffix_min(uint32_t v, uint32_t* wmin, uint32_t after_all) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_suffix_min(v);
+    if (lane == 0) wmin[w] = incl;
+    __syncthreads();
+    uint32_t later = after_all;  // waves after w
+    for (uint32_t i = w + 1; i < kWaves; ++i) later = min(later, wmin[i]);
+    const uint32_t next = __shfl_down(incl, 1, 64);
+    __syncthreads();
+    return lane == 63 ? later : min(next, later);
+}
+
+__global__ __launch_bounds__(256) void k_sufmin_reduce(const uint32_t* __restrict__ a, uint32_t m, uint32_t* __restrict__ mins) {
+    __shared__ uint32_t wmin[kWaves];
+    const uint32_t base = blockIdx.x * kScanChunk;
+    uint32_t v = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanChunk / 256; ++i) {
+        const uint32_t e = base + i * 256 + threadIdx.x;
+        if (e < m) v = min(v, a[e]);
+    }
+    const uint32_t inc = wave_incl_suffix_min(v);
+    if ((threadIdx.x & 63u) == 0) wmin[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = wmin[0];
+        for (uint32_t i = 1; i < kWaves; ++i) r = min(r, wmin[i]);
+        mins[blockIdx.x] = r;
+    }
+}
+
+// One block: mins[c] becomes min(mins[c + 1 ..], tail), walking the chunks from the end 256 at a time.
+__global__ __launch_bounds__(256) void k_sufmin_chunks(uint32_t* __restrict__ mins, uint32_t nch, uint32_t tail) {
+    __shared__ uint32_t wmin[kWaves];
+    uint32_t carry = tail;
+    for (int64_t hi = (int64_t)nch; hi > 0; hi -= 256) {
+        const int64_t i = hi - 256 + threadIdx.x;  // this round covers [hi - 256, hi)
+        const uint32_t v = i >= 0 ? mins[i] : 0xFFFFFFFFu;
+        const uint32_t ex = block_excl_suffix_min(v, wmin, carry);
+        const uint32_t all = min(v, ex);  // thread 0's inclusive value = the round's minimum with the carry
+        if (i >= 0) mins[i] = ex;
+        __shared__ uint32_t s_all;
+        if (threadIdx.x == 0) s_all = all;
+        __syncthreads();
+        carry = s_all;
+        __syncthreads();
+    }
+}
+
+// Each thread owns 16 consecutive elements of the chunk.
+__global__ __launch_bounds__(256) void k_sufmin_down(uint32_t* __restrict__ a, uint32_t m, const uint32_t* __restrict__ mins) {
+    __shared__ uint32_t wmin[kWaves];
+    const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * 16u;
+    uint32_t v[16];
+    load16(a, base, m, 0xFFFFFFFFu, v);
+    uint32_t tmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tmin = min(tmin, v[i]);
+    uint32_t run = block_excl_suffix_min(tmin, wmin, mins[blockIdx.x]);
+#pragma unroll
+    for (int i = 15; i >= 0; --i) {
+        run = min(run, v[i]);
+        v[i] = run;
+    }
+    store16(a, base, m, v);
 }
 
 __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
@@ -2798,7 +2930,12 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     }
     hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
     hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
-    hipLaunchKernelGGL(k_offsets_fill, dim3(ceil_div(nb, 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
+    {  // empty buckets: suffix minima (the next present key's start, n after the last)
+        const uint32_t nch = ceil_div(nb, kScanChunk);
+        hipLaunchKernelGGL(k_sufmin_reduce, dim3(nch), dim3(256), 0, st, d_offsets, nb, s.scan_sums);
+        hipLaunchKernelGGL(k_sufmin_chunks, dim3(1), dim3(256), 0, st, s.scan_sums, nch, n);
+        hipLaunchKernelGGL(k_sufmin_down, dim3(nch), dim3(256), 0, st, d_offsets, nb, s.scan_sums);
+    }
     return (int)hipGetLastError();
 }
 
