@@ -480,8 +480,8 @@ def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf):
     n_mt = int(min(n_all, max(len(probe), len(probe) * target_wall / max(t_probe, 1e-6))))
     sample = host(n_mt)
     runs = {"share": {"threads": share, "messages": n_mt, "seconds": timed(sample, share)}}
-    # every listed CPU: per-thread stage-4 histograms are n_act + 1 counters each, so bound the thread count by memory
-    n_cpu_threads = int(min(ncpu, max(1, (8 << 30) // (4 * (n_grains + 1)))))
+    # every listed CPU (the parallel stage 4 keeps 2^12 + 2^(bits-12) counters per thread: no memory bound)
+    n_cpu_threads = ncpu
     if n_cpu_threads > share:
         runs["all_cpus"] = {"threads": n_cpu_threads, "messages": n_mt, "seconds": timed(sample, n_cpu_threads)}
     n_1 = min(len(sample), 1 << 22)
