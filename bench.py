@@ -93,17 +93,19 @@ def main():
         args.config = 2 if world == 1 else 3
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if args.config in (1, 4, 5, 6, 7, 8):
-            raise SystemExit("--config 1/4/5/6/7/8 are single-GPU measurement legs")
+        if args.config in (1, 5, 6, 7, 8):
+            raise SystemExit("--config 1/5/6/7/8 are single-GPU measurement legs")
 
-    if args.local_ranks:
+    if args.local_ranks and args.config == 4:
+        res = run_fanout_node(args, torch, None, 0, args.local_ranks, 0, rehearsal=True)
+    elif args.local_ranks:
         res = run_rehearsal(args, torch)
     elif args.config == 1:
         res = run_chirper(args, torch)
     elif args.config in (2, 3):
         res = run_single_target(args, torch, dist, rank, world, local_rank)
     elif args.config == 4:
-        res = run_fanout(args, torch)
+        res = run_fanout(args, torch) if world == 1 else run_fanout_node(args, torch, dist, rank, world, local_rank)
     elif args.config == 6:
         res = run_directory(args, torch)
     elif args.config == 7:
@@ -647,6 +649,124 @@ def run_fanout(args, torch):
                          "avg_launch_ms": route_ms},
             "pipeline": {"route_kernel_ms": route_ms, "bucketing_ms": bucket_ms, "call_ms": total_ms},
             "cpu_baseline": None}
+
+
+def run_fanout_node(args, torch, dist, rank, world, local_rank, rehearsal=False):
+    """Config 4 sharded across GPUs: the CSR is replicated, each rank publishes for the accounts its
+    silos own (1M uniformly random publishers per step in total), expands its publishes and routes the emitted messages
+    across the node (orl_node_fanout_batch_device: owner partition, RCCL exchange, routing at the follower's owner,
+    stage 4).  rehearsal: `world` ranks as threads of this process on one GPU (LOCAL transport), not a scaling number."""
+    from concurrent.futures import ThreadPoolExecutor
+    from orleans_amd import _lib as L
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine, grain_keys_from_longs
+    from orleans_amd.node import GrainNode, local_silos, rank_of_silo
+
+    n_acc = args.grains or 10_000_000
+    n_pub = 1_000_000
+    cl = W.balanced_cluster()
+    ros = rank_of_silo(cl.n_silos, world)
+    t_setup = time.perf_counter()
+    csr_off, csr_tgt = W.powerlaw_csr(n_acc)
+    keys = grain_keys_from_longs(cl.type_code, np.arange(n_acc, dtype=np.int64))
+    owner = cl.owner_of(W.jenkins3_np(keys["tcd"], keys["n0"], keys["n1"]))
+    n_sets = max(1, min(4, args.steps + args.warmup))
+    pub_sets = [(W.stream(W.SEED_C4 ^ 0xB0B, i * n_pub, n_pub) % np.uint64(n_acc)).astype(np.uint32) for i in range(n_sets)]
+    deg = np.diff(csr_off.astype(np.int64))
+    pub_rank = [ros[owner[p.astype(np.int64)]] for p in pub_sets]
+    totals = [int(deg[p].sum()) for p in pub_sets]
+    ranks = list(range(world)) if rehearsal else [rank]
+    # per (rank, set): publishers, their silos, emitted count; receive capacity from the followers' owner ranks
+    per = {}
+    recv = np.zeros(world, np.int64)
+    for r in range(world):
+        for i, p in enumerate(pub_sets):
+            mine_p = p[pub_rank[i] == r]
+            emitted = int(deg[mine_p].sum())
+            per[(r, i)] = (mine_p, owner[mine_p.astype(np.int64)].astype(np.uint8), emitted)
+    for i, p in enumerate(pub_sets):  # every emitted message lands at its follower's owner rank
+        starts = csr_off[p.astype(np.int64)].astype(np.int64)
+        lens = csr_off[p.astype(np.int64) + 1].astype(np.int64) - starts
+        idx = np.repeat(starts - np.cumsum(lens) + lens, lens) + np.arange(int(lens.sum()))  # every emitted CSR entry
+        recv = np.maximum(recv, np.bincount(ros[owner[csr_tgt[idx].astype(np.int64)]], minlength=world))
+    max_batch = max(e for (_, _, e) in per.values()) + 1
+    cap = int(recv.max())
+    cap += cap // 64 + 4096
+    dev = f"cuda:{local_rank}"
+    d_off = torch.from_numpy(csr_off.view(np.int64)).to(dev)
+    d_tgt = torch.from_numpy(csr_tgt.view(np.int32)).to(dev)
+    tcd = (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+    gid = b"bench-fanout-rehearsal"
+    if not rehearsal:
+        g = torch.zeros(L.NODE_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            g.copy_(torch.frombuffer(bytearray(GrainNode.unique_id()), dtype=torch.uint8))
+        dist.broadcast(g, 0)
+        gid = bytes(g.cpu().numpy())
+    state = {}
+    for r in ranks:
+        mine = local_silos(cl.n_silos, world, r)
+        mask = np.zeros(cl.n_silos, np.uint8)
+        mask[mine] = 1
+        n_act = max(1, int(mask[owner].astype(bool).sum()))
+        eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, max_batch), device=local_rank)
+        W.setup_engine(eng, cl, local_silos=mine)
+        W.register_population(eng, keys, owner, np.ones(n_acc, bool), mask, dense_local=True)
+        node = GrainNode(eng, world, r, ros, max_batch=max_batch, max_recv=cap,
+                         transport=L.TRANSPORT_LOCAL if rehearsal else L.TRANSPORT_RCCL, group_id=gid, chunks=args.chunks)
+        sets = [(torch.from_numpy(per[(r, i)][0].view(np.int32)).to(dev), torch.from_numpy(per[(r, i)][1]).to(dev),
+                 len(per[(r, i)][0]), per[(r, i)][2]) for i in range(n_sets)]
+        state[r] = dict(eng=eng, node=node, sets=sets, poff=torch.empty(n_pub + 1, dtype=torch.int64, device=dev),
+                        stream=torch.cuda.Stream(device=dev))
+    del keys
+    log(f"config 4 node: {world} ranks{' (one-GPU rehearsal)' if rehearsal else ''}, {n_acc} accounts, {len(csr_tgt)} edges, "
+        f"{n_pub} publishers/step, emitted {totals}, receive capacity {cap}; setup {time.perf_counter() - t_setup:.1f}s")
+    k = [0]
+
+    def one(r, i):
+        st = state[r]
+        d_pubs, d_psilo, npub, emitted = st["sets"][i]
+        res = st["node"].fanout_batch_device(d_off, d_tgt, None, tcd, d_pubs, d_psilo, npub, st["poff"], total=emitted,
+                                             stream=st["stream"].cuda_stream)
+        st["stream"].synchronize()
+        return res.n_owned
+
+    if rehearsal:
+        ex = ThreadPoolExecutor(world)
+
+        def step():
+            i = k[0] % n_sets
+            k[0] += 1
+            list(ex.map(lambda r: one(r, i), ranks))
+            return totals[i]
+    else:
+        def step():
+            i = k[0] % n_sets
+            k[0] += 1
+            one(rank, i)
+            return totals[i]
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    args_w = argparse.Namespace(**{**vars(args), "warmup": 0})
+    elapsed, emitted = timed_steps(args_w, torch, None if rehearsal else dist, 1 if rehearsal else world, step,
+                                   torch.cuda.synchronize)
+    for st in state.values():
+        st["node"].close()
+        st["eng"].close()
+    ms = elapsed * 1e3 / args.steps
+    log(f"config 4 node: {ms:.3f} ms/step, {emitted / args.steps:.0f} emitted messages per step over {world} ranks")
+    return {"metric": "routed grain messages/sec (node)" + (", node protocol rehearsal on ONE GPU (not a scaling number)"
+                                                           if rehearsal else ""),
+            "value": emitted / elapsed, "unit": "messages/s", "n_gpus": 1 if rehearsal else world,
+            "local_ranks": world if rehearsal else None, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "none" if rehearsal else "strong", "vs_baseline": None,
+            "dtype": "u32/u64 integer", "data": "synthetic (seeded power-law CSR; config 4 of SURVEY §8(d))",
+            "config": {"workload": f"config4 sharded by publisher over {world} ranks: {n_acc} accounts, power-law followers, "
+                                   f"{n_pub} publishers per step in total, each rank expands its own and routes the emitted "
+                                   f"messages across the node (orl_node_fanout_batch_device, {args.chunks} chunks)",
+                       "edges": int(len(csr_tgt)), "emitted_per_step": emitted / args.steps, "receive_capacity": cap},
+            "roofline": None, "cpu_baseline": None}
 
 
 # ---- leg 6: directory mutation (f1) ------------------------------------------------------------------------

@@ -283,6 +283,18 @@ int orl_fanout_route_mixed_device(orl_ctx* ctx, const orl_msg_hdr* d_direct, siz
                                   uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                                   uint32_t* d_bucket_offsets, uint64_t* n_out, void* stream);
 
+/* Stage 5 alone: the messages a batch of publishes sends, as orl_msg_hdr records in d_out (cap records), publisher-
+ * major in CSR order (followers as in orl_fanout_route_mixed_device; sending silo = the publisher's, category
+ * Application).  For a node whose followers' directory partitions live on other GPUs: the records go through
+ * orl_node_route_batch_device (orl_node_fanout_batch_device does both).  *n_out = the emitted count (one stream sync),
+ * unless ORL_OPT_TOTAL_GIVEN (then records past the real count are null, address-complete headers with target silo
+ * 0xFF).  ORL_E_CAPACITY when the count exceeds cap.  Reference: ChirperAccount.PublishMessage's per-follower sends
+ * (Samples/Chirper/ChirperGrains/ChirperAccount.cs:154-157), each a GrainReference call from the publisher's silo. */
+int orl_fanout_expand_device(orl_ctx* ctx, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                             const orl_grain_key* d_follower_keys, uint64_t follower_tcd, const uint32_t* d_pubs,
+                             const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets,
+                             orl_msg_hdr* d_out, uint64_t cap, uint64_t* n_out, void* stream);
+
 /* ---- stream / reminder rings -------------------------------------------------
  * Two ring providers route stream queues and reminders; both look CLOCKWISE (first ring point >= key):
  *   ORL_RING_CONSISTENT  ConsistentRingProvider (src/OrleansRuntime/ConsistentRing/ConsistentRingProvider.cs:
@@ -526,6 +538,13 @@ const char* orl_node_last_error(const orl_node* node);
  * waits on the host for each chunk's counts; the routing work may still run). */
 int orl_node_route_batch_device(orl_node* node, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* out,
                                 void* stream);
+/* A multicast batch across the node (config 4 sharded by publisher): every rank expands its own publishes
+ * (orl_fanout_expand_device into a node buffer of max_batch records) and routes the emitted messages as
+ * orl_node_route_batch_device does.  *total: in = the exact emitted count with ORL_OPT_TOTAL_GIVEN, out = the count. */
+int orl_node_fanout_batch_device(orl_node* node, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                                 const orl_grain_key* d_follower_keys, uint64_t follower_tcd, const uint32_t* d_pubs,
+                                 const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets,
+                                 uint64_t* total, orl_node_result* out, void* stream);
 /* Record segment i of the last batch's hosted messages: device pointer, message count, record width (16 = orl_wire_msg,
  * 32 = orl_msg_hdr). */
 int orl_node_segment(const orl_node* node, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width);

@@ -174,6 +174,10 @@ _SIGS = {
     "orl_node_last_error": (C.c_char_p, [_P]),
     "orl_node_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.POINTER(orl_node_result), _P]),
     "orl_node_segment": (C.c_int, [_P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "orl_node_fanout_batch_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P,
+                                               C.POINTER(C.c_uint64), C.POINTER(orl_node_result), _P]),
+    "orl_fanout_expand_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64,
+                                           C.POINTER(C.c_uint64), _P]),
     "orl_set_timing": (C.c_int, [_P, C.c_int]),
     "orl_timing_summary": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),

@@ -1170,6 +1170,25 @@ int orl_fanout_route_mixed_device(orl_ctx* c, const orl_msg_hdr* d_direct, size_
                        opts, d_pub_offsets, d_route, d_act, d_order, d_off, n_out, stream);
 }
 
+int orl_fanout_expand_device(orl_ctx* c, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_keys,
+                             uint64_t follower_tcd, const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts,
+                             uint64_t* d_pub_offsets, orl_msg_hdr* d_out, uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!c || !n_out) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (!d_csr_off || !d_csr_tgt || !d_pub_offsets || (cap && !d_out)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n_pub && (!d_pubs || !d_pub_silo)) return fail(c, ORL_E_INVALID, "null publisher buffer");
+    if (n_pub + 1 > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "too many publishers");
+    if ((opts & ORL_OPT_TOTAL_GIVEN) && *n_out > cap)
+        return fail(c, ORL_E_CAPACITY, "given fan-out total %llu > cap %llu", (unsigned long long)*n_out, (unsigned long long)cap);
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const int e = launch_fanout_expand(d_csr_off, d_csr_tgt, d_keys, d_pubs, d_pub_silo, n_pub, d_keys ? 0 : follower_tcd, opts,
+                                       d_pub_offsets, d_out, n_out, cap, c->s, st);
+    if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > cap %llu", (unsigned long long)*n_out, (unsigned long long)cap);
+    if (e) return hipfail(c, (hipError_t)e, "fan-out expand launch");
+    return ORL_OK;
+}
+
 namespace {
 // Shared checks of the two partition entry points + the rank_of_silo upload (only when it changes).
 int partition_prologue(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, const uint8_t* rank_of_silo, uint32_t nranks,

@@ -260,6 +260,11 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
                                uint32_t opts, uint32_t n_act, uint64_t* d_pub_offsets, uint32_t* d_route, uint32_t* d_act,
                                uint32_t* d_order, uint32_t* d_offsets, uint64_t* n_out, uint64_t max_out,
                                const Scratch& s, void* stream, void* ev_route_begin, void* ev_route_end);
+// Stage 5 alone: emitted messages as headers into d_out (cap records); -1 when the emitted count exceeds cap.
+int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
+                         const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                         uint64_t* d_pub_offsets, orl_msg_hdr* d_out, uint64_t* n_out, uint64_t cap, const Scratch& s,
+                         void* stream);
 // Directory mutation on the device (dir kernels in route_kernels.hip).  d_claim: one u32 per table slot, all
 // 0xFFFFFFFF between calls; d_cnt: {entries, tombstones} device counters; d_slot: one u32 per batch message.
 int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt,

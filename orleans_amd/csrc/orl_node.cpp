@@ -127,6 +127,7 @@ struct orl_node {
         uint32_t width;
     };
     std::vector<Seg> segs;
+    orl_msg_hdr* d_fan = nullptr;                 // expanded multicast records (orl_node_fanout_batch_device), max_batch
 };
 
 namespace {
@@ -233,7 +234,7 @@ void free_node(orl_node* nd) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(nd->d_ros); f(nd->d_send[0]); f(nd->d_send[1]); f(nd->d_head); f(nd->d_heads); f(nd->d_recv); f(nd->d_route); f(nd->d_act);
     f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
-    f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts);
+    f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts); f(nd->d_fan);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
@@ -357,6 +358,18 @@ int orl_node_destroy(orl_node* nd) {
     free_node(nd);
     delete nd;
     return ORL_OK;
+}
+
+int orl_node_fanout_batch_device(orl_node* nd, const uint64_t* d_csr_off, const uint32_t* d_csr_tgt,
+                                 const orl_grain_key* d_follower_keys, uint64_t follower_tcd, const uint32_t* d_pubs,
+                                 const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets,
+                                 uint64_t* total, orl_node_result* res, void* stream) {
+    if (!nd || !res || !total) return ORL_E_INVALID;
+    NODE_HIP(nd, hipSetDevice(nd->device));
+    if (!nd->d_fan) NODE_HIP(nd, hipMalloc((void**)&nd->d_fan, nd->cfg.max_batch * sizeof(orl_msg_hdr)));
+    NODE_CTX(nd, orl_fanout_expand_device(nd->ctx, d_csr_off, d_csr_tgt, d_follower_keys, follower_tcd, d_pubs, d_pub_silo, n_pub,
+                                          opts & ORL_OPT_TOTAL_GIVEN, d_pub_offsets, nd->d_fan, nd->cfg.max_batch, total, stream));
+    return orl_node_route_batch_device(nd, nd->d_fan, *total, opts & ~ORL_OPT_TOTAL_GIVEN, res, stream);
 }
 
 int orl_node_segment(const orl_node* nd, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width) {

@@ -1757,6 +1757,82 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     }
 }
 
+// Stage 5 alone: the emitted messages as orl_msg_hdr records (publisher-major, CSR order), for a node whose followers'
+// directory partitions live on other GPUs (orl_node_fanout_batch_device).  Same tile-local publisher search as
+// k_fanout_route.  Indices past the scanned total (an overstated ORL_OPT_TOTAL_GIVEN) get a null header: category
+// None, ORL_HDR_ADDRESS_COMPLETE, target silo 0xFF (routed as a pass-through, bucketed as unresolved).
+struct ExpandSmem {
+    uint32_t poff[kFanLds + 1];
+    uint32_t prange[2];
+};
+
+__global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t* __restrict__ pstart, const uint32_t* __restrict__ csr_tgt,
+                                                                 const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32,
+                                                                 uint32_t n_pub, uint64_t follower_tcd,
+                                                                 const orl_grain_key* __restrict__ follower_keys, uint32_t n,
+                                                                 uint32_t items, orl_msg_hdr* __restrict__ out) {
+    __shared__ ExpandSmem sm;
+    const uint32_t rtile = kRouteThreads * items;
+    const uint32_t base = blockIdx.x * rtile;
+    const uint32_t real = poff32[n_pub];
+    const uint32_t lim = n < real ? n : real;
+    const bool fan = base < lim;
+    const uint32_t last = fan ? ((lim - base) < rtile ? lim : base + rtile) - 1 : 0u;
+    if (fan && threadIdx.x < 128) {
+        const uint32_t p = wave_find_pub(poff32, n_pub, threadIdx.x < 64 ? base : last);
+        if ((threadIdx.x & 63u) == 0) sm.prange[threadIdx.x >> 6] = p;
+    }
+    __syncthreads();
+    const uint32_t p_lo = fan ? sm.prange[0] : 0u, p_hi = fan ? sm.prange[1] : 0u;
+    const uint32_t span = p_hi - p_lo + 1;
+    const bool in_lds = span <= kFanLds;
+    if (in_lds && fan)
+        for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
+    __syncthreads();
+    for (uint32_t j = 0; j < items; ++j) {
+        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
+        if (e >= n) break;
+        u32x4 h0, h1;
+        if (e >= lim) {  // past the emitted total: a null, address-complete header
+            h0 = u32x4{0u, 0u, 0u, 0u};
+            h1 = u32x4{0u, 0u, 0xFFu | ((uint32_t)ORL_HDR_ADDRESS_COMPLETE << 16) | (0xFFu << 24), 0u};
+        } else {
+            uint32_t lo, hi, p, start;
+            if (in_lds) {
+                lo = 0; hi = span + 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sm.poff[mid] <= e) lo = mid + 1; else hi = mid;
+                }
+                p = p_lo + lo - 1;
+                start = sm.poff[lo - 1];
+            } else {
+                lo = p_lo; hi = p_hi + 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (poff32[mid] <= e) lo = mid + 1; else hi = mid;
+                }
+                p = lo - 1;
+                start = poff32[p];
+            }
+            const uint32_t tgt = csr_tgt[pstart[p] + (e - start)];
+            uint64_t tcd = follower_tcd, n0 = 0, n1 = (uint64_t)tgt;
+            if (follower_keys) {
+                const orl_grain_key k = follower_keys[tgt];
+                tcd = k.type_code_data;
+                n0 = k.n0;
+                n1 = k.n1;
+            }
+            h0 = u32x4{(uint32_t)tcd, (uint32_t)(tcd >> 32), (uint32_t)n0, (uint32_t)(n0 >> 32)};
+            // sending_silo = the publisher's silo, category Application (2), no flags, no target silo
+            h1 = u32x4{(uint32_t)n1, (uint32_t)(n1 >> 32), (uint32_t)pub_silo[p] | (2u << 8), 0u};
+        }
+        u32x4* o = reinterpret_cast<u32x4*>(out + e);
+        o[0] = h0;
+        o[1] = h1;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Exchange partition: destination rank per message (stages 1-2 only) + per-tile rank histogram, then a
 // stable scatter of the 32-B headers.  Messages that are not directory-routed (complete, system target,
@@ -3097,6 +3173,42 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     int e = (int)hipGetLastError();
     if (e || !buckets) return e;
     return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st);
+}
+
+int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
+                         const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd, uint32_t opts,
+                         uint64_t* d_pub_offsets, orl_msg_hdr* d_out, uint64_t* n_out, uint64_t cap, const Scratch& s,
+                         void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t* poff32 = s.idx_a;
+    uint64_t* pstart = reinterpret_cast<uint64_t*>(s.pairs_b);
+    const uint32_t m = (uint32_t)n_pub + 1;
+    const uint32_t nbs = ceil_div(m, kScanChunk);
+    hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+    if (nbs <= kScanDirectChunks) {
+        hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
+                           0ull);
+    } else {
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
+        hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
+                           0ull);
+    }
+    uint64_t total = *n_out;
+    if (!(opts & ORL_OPT_TOTAL_GIVEN)) {
+        uint32_t t32 = 0;
+        int e = (int)hipMemcpyAsync(&t32, poff32 + n_pub, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        if (e) return e;
+        e = (int)hipStreamSynchronize(st);
+        if (e) return e;
+        total = t32;
+        *n_out = total;
+    }
+    if (total > cap) return -1;
+    if (total == 0) return 0;
+    const uint32_t items = route_items(total, 4);
+    hipLaunchKernelGGL(k_fanout_expand, dim3(ceil_div(total, kRouteThreads * items)), dim3(kRouteThreads), 0, st, pstart, d_csr_tgt,
+                       d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total, items, d_out);
+    return (int)hipGetLastError();
 }
 
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,

@@ -330,6 +330,17 @@ class GrainDirectoryEngine:
                                                          ptr(d_offsets), C.byref(n_out), ptr(stream)))
         return n_out.value
 
+    def fanout_expand_device(self, d_csr_off, d_csr_tgt, d_follower_keys, follower_tcd: int, d_pubs, d_pub_silo, n_pub: int,
+                             d_pub_offsets, d_out, cap: int, stream=None, opts: int = 0, total: Optional[int] = None) -> int:
+        """Stage 5 alone: the emitted messages as orl_msg_hdr records (ChirperAccount.cs:154-157). Returns the count."""
+        if total is not None:
+            opts |= L.OPT_TOTAL_GIVEN
+        n_out = C.c_uint64(int(total or 0))
+        self._ck(self._lib.orl_fanout_expand_device(self._ctx, ptr(d_csr_off), ptr(d_csr_tgt), ptr(d_follower_keys),
+                                                    int(follower_tcd), ptr(d_pubs), ptr(d_pub_silo), int(n_pub), int(opts),
+                                                    ptr(d_pub_offsets), ptr(d_out), int(cap), C.byref(n_out), ptr(stream)))
+        return n_out.value
+
     def partition_by_owner_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
                                   d_out, d_src_index, d_counts, stream=None, opts: int = 0) -> None:
         ros = np.zeros(256, np.uint8)

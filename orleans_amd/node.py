@@ -264,6 +264,7 @@ class NodeResult:
     order: int
     offsets: int
     segments: List[tuple]  # (device pointer, count, record width)
+    emitted: int = 0       # fanout_batch_device: messages this rank's publishes emitted
 
 
 class GrainNode:
@@ -310,6 +311,26 @@ class GrainNode:
         C = self._C
         r = L.orl_node_result()
         rc = self._lib.orl_node_route_batch_device(self._node, L.ptr(d_msgs), int(n), int(opts), C.byref(r), L.ptr(stream))
+        return self._result(rc, r)
+
+    def fanout_batch_device(self, d_csr_off, d_csr_tgt, d_follower_keys, follower_tcd: int, d_pubs, d_pub_silo, n_pub: int,
+                            d_pub_offsets, total=None, stream=None, opts: int = 0) -> NodeResult:
+        """This rank's publishes expanded (orl_fanout_expand_device) and routed across the node
+        (orl_node_fanout_batch_device): ChirperAccount.PublishMessage sharded by publisher (config 4)."""
+        C = self._C
+        if total is not None:
+            opts |= L.OPT_TOTAL_GIVEN
+        t = C.c_uint64(int(total or 0))
+        r = L.orl_node_result()
+        rc = self._lib.orl_node_fanout_batch_device(self._node, L.ptr(d_csr_off), L.ptr(d_csr_tgt), L.ptr(d_follower_keys),
+                                                    int(follower_tcd), L.ptr(d_pubs), L.ptr(d_pub_silo), int(n_pub), int(opts),
+                                                    L.ptr(d_pub_offsets), C.byref(t), C.byref(r), L.ptr(stream))
+        res = self._result(rc, r)
+        res.emitted = t.value
+        return res
+
+    def _result(self, rc, r) -> NodeResult:
+        C = self._C
         if rc != L.OK:
             raise L.OrleansRouteError(rc, (self._lib.orl_node_last_error(self._node) or b"").decode(errors="replace"))
         segs = []

@@ -495,6 +495,54 @@ def test_config5_mixed_batch(torch, over):
     eng.close()
 
 
+@pytest.mark.parametrize("keyed,over", [(False, None), (False, 1000), (True, None)])
+def test_fanout_expand_vs_oracle(torch, keyed, over):
+    """orl_fanout_expand_device: the emitted headers (publisher-major, CSR order, the publisher's silo, category
+    Application) == cpu_ref.fanout_expand, for long-key followers and for a follower key table (Guid players);
+    with an overstated total the tail is null, address-complete headers (target silo 0xFF)."""
+    t = torch
+    cl = W.default_cluster()
+    n_acc = 200_000
+    off, tgt = W.powerlaw_csr(n_acc, dmax=5000)
+    pubs = (W.stream(11, 0, 20_000) % np.uint64(n_acc)).astype(np.uint32)
+    psilo = (pubs % 8).astype(np.uint8)
+    tcd = (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+    exp, poff_ref = cpu_ref.fanout_expand(off, tgt, pubs, psilo, tcd)
+    fkeys = None
+    if keyed:  # Guid-keyed followers: the key table replaces (tcd, 0, id)
+        fk = np.zeros(n_acc, L.KEY_DTYPE)
+        fk["tcd"] = np.uint64(tcd ^ (1 << 40))
+        fk["n0"] = W.stream(12, 0, n_acc)
+        fk["n1"] = W.stream(13, 0, n_acc)
+        kk = fk[exp["n1"].astype(np.int64)]
+        exp["tcd"], exp["n0"], exp["n1"] = kk["tcd"], kk["n0"], kk["n1"]
+        fkeys = t.from_numpy(fk.view(np.uint8).reshape(-1, 24)).cuda()
+    n = len(exp) + (over or 0)
+    eng = GrainDirectoryEngine(n_act=16, dir_capacity=64, max_batch=1 << 20, device=0)
+    W.setup_engine(eng, cl)
+    dv = "cuda"
+    d_out = t.full((n + 64, 8), -1, dtype=t.int32, device=dv)
+    poff = t.empty(len(pubs) + 1, dtype=t.int64, device=dv)
+    got = eng.fanout_expand_device(t.from_numpy(off.view(np.int64)).to(dv), t.from_numpy(tgt.view(np.int32)).to(dv), fkeys,
+                                   tcd, t.from_numpy(pubs.view(np.int32)).to(dv), t.from_numpy(psilo).to(dv), len(pubs), poff,
+                                   d_out, n + 64, total=None if over is None else n)
+    t.cuda.synchronize()
+    assert got == n
+    out = d_out.cpu().numpy().view(L.MSG_DTYPE).reshape(-1)
+    np.testing.assert_array_equal(out[:len(exp)], exp)
+    np.testing.assert_array_equal(poff.cpu().numpy().view(np.uint64), poff_ref)
+    if over:
+        tail = out[len(exp):n]
+        assert (tail["tcd"] == 0).all() and (tail["flags"] == L.HDR_ADDRESS_COMPLETE).all()
+        assert (tail["target_silo"] == 0xFF).all() and (tail["sending_silo"] == 0xFF).all()
+    assert (out[n:]["tcd"] == np.uint64(0xFFFFFFFFFFFFFFFF)).all()  # nothing written past the total
+    with pytest.raises(L.OrleansRouteError):  # more emitted than cap
+        eng.fanout_expand_device(t.from_numpy(off.view(np.int64)).to(dv), t.from_numpy(tgt.view(np.int32)).to(dv), fkeys, tcd,
+                                 t.from_numpy(pubs.view(np.int32)).to(dv), t.from_numpy(psilo).to(dv), len(pubs), poff, d_out,
+                                 len(exp) - 1)
+    eng.close()
+
+
 # ---- stage-4 ranking: the LDS lane-order self-check and the ballot fallback (VERDICT r1 item 7) ---------------
 @pytest.mark.parametrize("n_act", [5000, 1_000_000, 12_000_000])
 def test_stage4_rank_modes_vs_oracle(torch, n_act):

@@ -163,6 +163,56 @@ def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix):
     world.close()
 
 
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_node_fanout_batch_vs_oracle(torch, nranks):
+    """Config 4 sharded by publisher: every rank expands its own publishes (orl_node_fanout_batch_device) and the
+    emitted messages are routed across the node; each rank's hosted output == the oracle's replay of the protocol over
+    the expanded batches (cpu_ref.fanout_expand per rank)."""
+    t = torch
+    world = World(nranks, n_grains=40_000, host_mix=0.2, ros=None if nranks != 3 else [s % 3 for s in range(8)])
+    cl = world.cl
+    off, tgt = W.powerlaw_csr(world.n_grains + 3000, dmax=2000)  # some followers are never registered
+    tcd = (3 << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+    keys, uni, owner, reg = W.grain_population(cl, world.n_grains + 3000, 0.9, 3)
+    pubs_all = (W.stream(21, 0, 6000) % np.uint64(world.n_grains)).astype(np.uint32)
+    nodes = [GrainNode(world.engs[r], nranks, r, world.ros, max_batch=200_000, max_recv=400_000,
+                       transport=L.TRANSPORT_LOCAL, group_id=b"node-fan-%d" % nranks, chunks=2) for r in range(nranks)]
+    d_off = t.from_numpy(off.view(np.int64)).cuda()
+    d_tgt = t.from_numpy(tgt.view(np.int32)).cuda()
+    batches, args = [], []
+    for r in range(nranks):  # a rank publishes for the accounts its silos own (sharded by publisher owner)
+        pubs = pubs_all[world.ros[owner[pubs_all.astype(np.int64)]] == r]
+        psilo = owner[pubs.astype(np.int64)].astype(np.uint8)
+        exp, _ = cpu_ref.fanout_expand(off, tgt, pubs, psilo, tcd)
+        batches.append(exp)
+        args.append((t.from_numpy(pubs.view(np.int32)).cuda(), t.from_numpy(psilo).cuda(), len(pubs),
+                     t.empty(len(pubs) + 1, dtype=t.int64, device="cuda")))
+    streams = [t.cuda.Stream() for _ in range(nranks)]
+    t.cuda.synchronize()
+
+    def one(r):
+        d_pubs, d_psilo, n_pub, poff = args[r]
+        res = nodes[r].fanout_batch_device(d_off, d_tgt, None, tcd, d_pubs, d_psilo, n_pub, poff, stream=streams[r].cuda_stream)
+        streams[r].synchronize()
+        return res, nodes[r].fetch(res, stream=streams[r].cuda_stream)
+
+    with ThreadPoolExecutor(nranks) as ex:
+        got = list(ex.map(one, range(nranks)))
+    exp, forward = world.expected(batches, 2)
+    for r in range(nranks):
+        res, (route, act, order, off_, hdrs) = got[r]
+        assert res.emitted == len(batches[r])
+        er, ea, eo, ef, eh = exp[r]
+        np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} headers")
+        np.testing.assert_array_equal(route, er, err_msg=f"rank {r} route")
+        np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} act")
+        np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} order")
+        np.testing.assert_array_equal(off_, ef, err_msg=f"rank {r} offsets")
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
 def test_node_capacity_error_is_consistent(torch):
     """A batch that would overflow one rank's max_recv fails on EVERY rank with ORL_E_CAPACITY (no rank waits)."""
     t = torch
