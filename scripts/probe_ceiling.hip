@@ -52,6 +52,30 @@ __global__ __launch_bounds__(256) void k_route8(const u32x4* __restrict__ hdr, c
     }
 }
 
+// k_route's pattern against a bucketized 8-B table (8 slots per 64-B line, `nbk` buckets, not a power of two): the
+// whole line read as 4 x 16-B loads, and a second line (the key's other bucket) for `second_pct` % of the messages
+__global__ __launch_bounds__(256) void k_route8_bucket(const u32x4* __restrict__ hdr, const u32x4* __restrict__ tab, uint32_t nbk,
+                                                       uint32_t second_pct, uint32_t n, uint32_t* __restrict__ o1,
+                                                       uint32_t* __restrict__ o2) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const u32x4 a = __builtin_nontemporal_load(hdr + 2 * (size_t)i);
+        const u32x4 b = __builtin_nontemporal_load(hdr + 2 * (size_t)i + 1);
+        const uint32_t h = mix32(a.x ^ b.x ^ a.z);
+        uint32_t bk = (uint32_t)(((uint64_t)h * nbk) >> 32);
+        const u32x4* line = tab + (size_t)bk * 4;
+        u32x4 v0 = line[0], v1 = line[1], v2 = line[2], v3 = line[3];
+        uint32_t x = v0.x ^ v1.y ^ v2.z ^ v3.w;
+        if ((h & 127u) * 100u < second_pct * 128u) {  // the other bucket
+            bk = (uint32_t)(((uint64_t)mix32(h + 0x9E3779B9u) * nbk) >> 32);
+            line = tab + (size_t)bk * 4;
+            v0 = line[0]; v1 = line[1]; v2 = line[2]; v3 = line[3];
+            x ^= v0.y ^ v1.z ^ v2.w ^ v3.x;
+        }
+        o1[i] = x ^ a.y;
+        o2[i] = x ^ b.w;
+    }
+}
+
 // the grouping pass a sliced table needs first, at its cheapest: stream the headers, write a 12-B record per message
 // (slot start, key, index) — here to a contiguous position, i.e. without the partition's ranking and scatter
 __global__ __launch_bounds__(256) void k_group_floor(const u32x4* __restrict__ hdr, uint32_t n, uint32_t* __restrict__ rec) {
@@ -118,5 +142,12 @@ int main() {
     timeit("route8 pattern, own-XCD 2 MiB slices", n, [&] { hipLaunchKernelGGL(k_route8<1>, g, b, 0, 0, hdr, t8, s16, n, out, out + n); });
     timeit("route8 pattern, slices b/8 (control)", n, [&] { hipLaunchKernelGGL(k_route8<2>, g, b, 0, 0, hdr, t8, s16, n, out, out + n); });
     timeit("grouping floor: 32-B hdr in, 12-B rec out", n, [&] { hipLaunchKernelGGL(k_group_floor, g, b, 0, 0, hdr, n, out); });
+    // bucketized 8-B table for 1M entries: load 0.8 / 0.9 -> 9.8 / 8.7 MB; 0 / 13 / 25 % second-bucket reads
+    for (uint32_t nbk : {163840u, 145636u, 262144u}) {
+        for (uint32_t pct : {0u, 13u, 25u}) {
+            snprintf(nm, sizeof nm, "route8 bucket table %.1f MB, %u%% 2nd", nbk * 64.0 / 1048576.0, pct);
+            timeit(nm, n, [&] { hipLaunchKernelGGL(k_route8_bucket, g, b, 0, 0, hdr, tab, nbk, pct, n, out, out + n); });
+        }
+    }
     return 0;
 }
