@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--host-io", choices=["pinned", "pageable"], default=None,
                     help="config 2 at N=1: time the host-array P/Invoke call (orl_route_batch: PCIe in and out) instead")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--wire16", action="store_true",
+                    help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
     ap.add_argument("--router", action="store_true",
                     help="configs 2/3 at N=1: go through the pipelined multi-GPU router (partition + routing on two "
                          "streams; exercises the N>1 code path on one GPU)")
@@ -204,6 +206,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         n_act = max(1, int((reg & local_mask[owner].astype(bool)).sum()))
     eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, n_msgs), device=local_rank)
     W.setup_engine(eng, cl, local_silos=mine if world > 1 else None)
+    if world > 1 and not args.wire16:  # the node's grain classes: 8-B exchange records
+        eng.set_wire_types([W.grain_tcd(cl)])
     n_reg = W.register_population(eng, keys, owner, reg, local_mask, dense_local=world > 1)
     del keys, uni
     log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
@@ -236,6 +240,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
             stats["owned"] = stats.get("owned", 0) + res.n_owned
             stats["remote"] = stats.get("remote", 0) + res.n_sent_remote
             stats["fwd"] = stats.get("fwd", 0) + res.n_forwarded
+            stats.setdefault("widths", set()).update(w for _, c, w in res.segments if c)
             return res.n_owned
     else:
         # the Python torch.distributed reference protocol (orleans_amd/node.py PipelinedRouter), two batches in flight
@@ -269,7 +274,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     launches = max(1, nb // args.steps)
     per_launch_msgs = recv_total / args.steps / launches
     wire = node is not None or args.router
-    kbytes = ROUTE_KERNEL_BYTES_PER_MSG - (16 if wire else 0)  # 16-B exchange records instead of 32-B headers
+    rec_w = max(stats.get("widths") or {16 if wire else 32})  # the exchange record the owner's route kernel reads
+    kbytes = ROUTE_KERNEL_BYTES_PER_MSG - (32 - rec_w)  # 8-B / 16-B exchange records instead of 32-B headers
     achieved = kbytes * per_launch_msgs / (route_ms * 1e-3) / 1e9
     log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms x {launches}, bucketing {bucket_ms:.3f} ms, "
         f"call {total_ms:.3f} ms over {nb} launches")
@@ -319,7 +325,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         out["exchange"] = {"rank0_owned_per_step": stats["owned"] / args.steps,
                            "rank0_sent_remote_per_step": stats["remote"] / args.steps,
                            "rank0_forwarded_hop2_per_step": stats["fwd"] / args.steps,
-                           "rank0_xgmi_bytes_per_step": 16 * stats["remote"] / args.steps,
+                           "record_bytes": rec_w,
+                           "rank0_xgmi_bytes_per_step": rec_w * stats["remote"] / args.steps,
                            "receive_capacity": cap}
     return out
 
@@ -365,6 +372,8 @@ def run_rehearsal(args, torch):
         n_act = max(1, int((reg & mask[owner].astype(bool)).sum()))
         e = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, n_msgs), device=0)
         W.setup_engine(e, cl, local_silos=mine)
+        if not args.wire16:
+            e.set_wire_types([W.grain_tcd(cl)])
         W.register_population(e, keys, owner, reg, mask, dense_local=True)
         engs.append(e)
         nodes.append(GrainNode(e, R, r, ros, max_batch=n_msgs, max_recv=cap, transport=L.TRANSPORT_LOCAL, group_id=gid,
@@ -711,6 +720,8 @@ def run_fanout_node(args, torch, dist, rank, world, local_rank, rehearsal=False)
         n_act = max(1, int(mask[owner].astype(bool).sum()))
         eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, max_batch), device=local_rank)
         W.setup_engine(eng, cl, local_silos=mine)
+        if not args.wire16:
+            eng.set_wire_types([tcd])
         W.register_population(eng, keys, owner, np.ones(n_acc, bool), mask, dense_local=True)
         node = GrainNode(eng, world, r, ros, max_batch=max_batch, max_recv=cap,
                          transport=L.TRANSPORT_LOCAL if rehearsal else L.TRANSPORT_RCCL, group_id=gid, chunks=args.chunks)

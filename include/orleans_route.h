@@ -96,6 +96,17 @@ typedef struct orl_wire_msg {
     uint32_t meta;
 } orl_wire_msg;
 
+/* Narrow 8-byte exchange record: the 16-byte form's content when N1 < 2^32 and the TypeCodeData is one of the
+ * context's wire types (orl_wire_types_set: the node's grain classes, the same table on every rank — Orleans builds
+ * one type map per cluster at silo start-up, GrainTypeManager).  meta packs sending_silo (bits 0-7), message category
+ * (8-9), header flags (10-15; ORL_HDR_HASH_VALID not allowed), the wire type index (16-19; bits 20-23 zero) and
+ * target_silo (24-31).  Lossless: decoding with the same table gives back the 32-byte orl_msg_hdr (N0 = 0, aux = 0). */
+#define ORL_MAX_WIRE_TYPES 16u
+typedef struct orl_wire8 {
+    uint32_t n1;
+    uint32_t meta;
+} orl_wire8;
+
 /* ---- Per-message route word ---------------------------------------------------------------
  * bits 0-7 directory owner silo, 8-15 target (host) silo, 16-23 ORL_ST_*, 24-31 ORL_RF_*      */
 #define ORL_ST_HIT 0u                  /* single activation found on a functional silo */
@@ -449,6 +460,20 @@ int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n
 /* orl_route_batch_device over received compact records (the owner side of the exchange). */
 int orl_route_compact_device(orl_ctx* ctx, const orl_wire_msg* d_in, size_t n, uint32_t opts, uint32_t* d_route,
                              uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
+/* The wire types of the 8-byte form (n <= ORL_MAX_WIRE_TYPES TypeCodeData values; n = 0 turns the form off).  Every
+ * rank of a node must set the same list in the same order; the node compares a digest of it before each chunk uses
+ * the 8-byte form and falls back to the 16-byte one when ranks differ. */
+int orl_wire_types_set(orl_ctx* ctx, uint32_t n, const uint64_t* type_code_data);
+/* As orl_partition_compact_device, writing 8-byte orl_wire8 records (a quarter of the header bytes).  *d_status (device
+ * u32): bit 0 = some message has no 16-byte form, bit 1 = some message has no 8-byte form (records invalid when bit 1
+ * is set: re-partition in the 16-byte form, or the 32-byte one when bit 0 is set too). */
+int orl_partition_narrow_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
+                                const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
+                                orl_wire8* d_out, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_status,
+                                void* stream);
+/* orl_route_batch_device over received 8-byte records, decoded with this context's wire types. */
+int orl_route_narrow_device(orl_ctx* ctx, const orl_wire8* d_in, size_t n, uint32_t opts, uint32_t* d_route,
+                            uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
 
 /* Stage 4 alone: group already-routed messages by activation handle, FIFO inside each bucket (ActivationData.EnqueueMessage,
  * ActivationData.cs:483-514) — the receiving silo's side when the routing ran elsewhere (node hop 2).  Same outputs as
@@ -484,8 +509,9 @@ int orl_fanout_batch(orl_ctx* ctx, const uint32_t* pubs, const uint8_t* pub_silo
  * (orl_node_route_batch_device, called by every rank with its own local batch, in lockstep):
  *   hop 1  stages 1-2 + stable partition of the local batch by the rank of each message's directory owner (messages
  *          that need no directory stay: complete addresses, system targets, null owners), a counts all-gather, and a
- *          grouped send/recv of the per-rank regions — 16-B orl_wire_msg records when every message of the chunk has
- *          that form, 32-B headers otherwise.  The batch is cut into `chunks` pieces: the exchange of one overlaps the
+ *          grouped send/recv of the per-rank regions — 8-B orl_wire8 records when every rank set the same wire types
+ *          and every message of the chunk has that form, else 16-B orl_wire_msg records when they all have that form,
+ *          32-B headers otherwise.  The batch is cut into `chunks` pieces: the exchange of one overlaps the
  *          routing (stages 1-3) of the previous one.  Replaces OutboundMessageQueue.SendMessage's per-target-silo
  *          sender queues (OutboundMessageQueue.cs:113-145) + the remote directory lookup (LocalGrainDirectory.cs:719-765).
  *   owner  stages 1-3 over the received records; the owned set is the received blocks in (chunk, source rank) order.
@@ -545,8 +571,8 @@ int orl_node_fanout_batch_device(orl_node* node, const uint64_t* d_csr_off, cons
                                  const orl_grain_key* d_follower_keys, uint64_t follower_tcd, const uint32_t* d_pubs,
                                  const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets,
                                  uint64_t* total, orl_node_result* out, void* stream);
-/* Record segment i of the last batch's hosted messages: device pointer, message count, record width (16 = orl_wire_msg,
- * 32 = orl_msg_hdr). */
+/* Record segment i of the last batch's hosted messages: device pointer, message count, record width (8 = orl_wire8 in
+ * the context's wire types, 16 = orl_wire_msg, 32 = orl_msg_hdr). */
 int orl_node_segment(const orl_node* node, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width);
 
 int orl_sync(orl_ctx* ctx);
@@ -568,6 +594,7 @@ int orl_sync(orl_ctx* ctx);
 #define ORL_Q_MAX_BATCH 6u    /* messages the scratch is sized for */
 #define ORL_Q_RANK_MODE 7u    /* stage-4 stable ranking on this device: bit 0 = ballot match (else LDS atomics), bit 1 = the
                                  lane-order self-check failed (ballot forced) */
+#define ORL_Q_WIRE_DIGEST 8u  /* FNV-1a digest of the wire types (orl_wire_types_set), 0 when the 8-B form is off */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 /* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
  * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */

@@ -206,6 +206,29 @@ def wire_encode(msgs: np.ndarray):
     return r, ok
 
 
+# ---- narrow exchange record (orl_wire8, include/orleans_route.h) ------------------------------------------
+# 8-byte form: N1 < 2^32, N0 == 0, TypeCodeData one of the node's wire types (its index is carried), message
+# category < 4, flags < 64 without HASH_VALID.  Same restatement role as wire_encode.
+WIRE8_DTYPE = np.dtype([("n1", "<u4"), ("meta", "<u4")])
+
+
+def narrow_encode(msgs: np.ndarray, wire_types):
+    """-> (records, narrow-able mask) for the wire-type list `wire_types` (<= 16 TypeCodeData values)."""
+    tcd = msgs["tcd"].astype(np.uint64)
+    types = np.asarray(list(wire_types), np.uint64)
+    idx = np.full(len(msgs), 16, np.uint32)
+    for i, t in enumerate(types):
+        idx[tcd == t] = i
+    ok = (msgs["n0"] == 0) & (msgs["n1"] < np.uint64(1 << 32)) & (idx < 16) & (msgs["category"] < 4) & \
+         (msgs["flags"] < 64) & ((msgs["flags"] & 0x02) == 0)
+    r = np.zeros(len(msgs), WIRE8_DTYPE)
+    r["n1"] = (msgs["n1"] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    r["meta"] = (msgs["sending_silo"].astype(np.uint32) | ((msgs["category"].astype(np.uint32) & 0xFF) << 8) |
+                 ((msgs["flags"].astype(np.uint32) & 0xFF) << 10) | ((idx & 0xF) << 16) |
+                 (msgs["target_silo"].astype(np.uint32) << 24))
+    return r, ok
+
+
 def wire_decode(recs: np.ndarray) -> np.ndarray:
     m = np.zeros(len(recs), MSG_DTYPE)
     meta = recs["meta"].astype(np.uint32)

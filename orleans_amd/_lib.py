@@ -59,6 +59,8 @@ STAMP_MAX_GROWTH = 72
 MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
 Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_RANK_MODE = 1, 2, 3, 4, 5, 6, 7
+Q_WIRE_DIGEST = 8
+MAX_WIRE_TYPES = 16
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -129,6 +131,10 @@ _SIGS = {
     "orl_partition_compact_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_size_t,
                                                _P, _P, _P, _P, _P]),
     "orl_route_compact_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
+    "orl_wire_types_set": (C.c_int, [_P, C.c_uint32, _P]),
+    "orl_partition_narrow_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_size_t,
+                                              _P, _P, _P, _P, _P]),
+    "orl_route_narrow_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
     "orl_dir_insert_single_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "orl_dir_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_dir_compact": (C.c_int, [_P]),

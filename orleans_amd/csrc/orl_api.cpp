@@ -281,6 +281,11 @@ struct orl_ctx {
     uint32_t tcount = 0;
 };
 
+const uint64_t* orl::ctx_wire_tcd(const orl_ctx* c) {
+    if (!c || !c->d_params) return nullptr;
+    return reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(c->d_params) + offsetof(RouteParams, wire_tcd));
+}
+
 namespace {
 
 int fail(orl_ctx* c, int code, const char* fmt, ...) {
@@ -332,14 +337,19 @@ uint32_t host_owner(const orl_ctx* c, const orl_grain_key& k, uint32_t me, bool 
 void rebuild_params(orl_ctx* c) {
     RouteParams& P = c->hp;
     const uint64_t mt = P.mem_tcd, m0 = P.mem_n0, m1 = P.mem_n1;
-    const uint32_t cache_on = P.cache_on, npt = P.n_probe_types;
-    uint64_t ptcd[kProbeTypes];
+    const uint32_t cache_on = P.cache_on, npt = P.n_probe_types, nwt = P.n_wire_types;
+    const uint64_t wdig = P.wire_digest;
+    uint64_t ptcd[kProbeTypes], wtcd[ORL_MAX_WIRE_TYPES];
     std::memcpy(ptcd, P.probe_tcd, sizeof ptcd);
+    std::memcpy(wtcd, P.wire_tcd, sizeof wtcd);
     std::memset(&P, 0, sizeof P);
     P.mem_tcd = mt; P.mem_n0 = m0; P.mem_n1 = m1;
     P.cache_on = cache_on;
     P.n_probe_types = npt;
     std::memcpy(P.probe_tcd, ptcd, sizeof ptcd);
+    P.n_wire_types = nwt;
+    P.wire_digest = wdig;
+    std::memcpy(P.wire_tcd, wtcd, sizeof wtcd);
     P.ring_n = (uint32_t)c->ring.size();
     for (size_t i = 0; i < c->ring.size(); ++i) {
         P.ring_hash[i] = c->ring[i].first;
@@ -1018,7 +1028,7 @@ int orl_hash_batch(orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* ou
 }
 
 namespace {
-int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+int route_impl(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                uint32_t* d_order, uint32_t* d_off, void* stream) {
     if (!c) return ORL_E_INVALID;
     if (n && (!d_in || !d_route || !d_act)) return fail(c, ORL_E_INVALID, "null device buffer");
@@ -1033,7 +1043,8 @@ int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts,
     if (c->timing && n > 0 && c->tcount < ORL_TIMING_SLOTS) ev = &c->tev[4 * (size_t)c->tcount++];
     if ((r = prepare_probe(c, st))) return r;
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
-    int e = launch_route_bucket(c->d_params, dir_view(c), d_in, wire, n, opts, c->cfg.n_act, d_route, d_act, d_order,
+    if (fmt == 8 && c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
+    int e = launch_route_bucket(c->d_params, dir_view(c), d_in, fmt, n, opts, c->cfg.n_act, d_route, d_act, d_order,
                                 d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e) return hipfail(c, (hipError_t)e, "route launch");
     if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
@@ -1043,12 +1054,17 @@ int route_impl(orl_ctx* c, const void* d_in, bool wire, size_t n, uint32_t opts,
 
 int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                            uint32_t* d_order, uint32_t* d_off, void* stream) {
-    return route_impl(c, d_in, false, n, opts, d_route, d_act, d_order, d_off, stream);
+    return route_impl(c, d_in, 32, n, opts, d_route, d_act, d_order, d_off, stream);
 }
 
 int orl_route_compact_device(orl_ctx* c, const orl_wire_msg* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                              uint32_t* d_order, uint32_t* d_off, void* stream) {
-    return route_impl(c, d_in, true, n, opts, d_route, d_act, d_order, d_off, stream);
+    return route_impl(c, d_in, 16, n, opts, d_route, d_act, d_order, d_off, stream);
+}
+
+int orl_route_narrow_device(orl_ctx* c, const orl_wire8* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                            uint32_t* d_order, uint32_t* d_off, void* stream) {
+    return route_impl(c, d_in, 8, n, opts, d_route, d_act, d_order, d_off, stream);
 }
 
 // Host-array form (the P/Invoke call): the batch is cut into chunks; chunk k's upload (copy stream), its stages 1-3
@@ -1237,7 +1253,7 @@ int orl_partition_by_owner_padded_device(orl_ctx* c, const orl_msg_hdr* d_in, si
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
     if (r) return r;
-    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, false, d_src,
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, 32, d_src,
                                     d_counts, nullptr, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "padded partition launch");
     return ORL_OK;
@@ -1252,9 +1268,46 @@ int orl_partition_compact_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, 
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
     if (r) return r;
-    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, true, d_src,
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, 16, d_src,
                                     d_counts, d_status, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "compact partition launch");
+    return ORL_OK;
+}
+
+int orl_partition_narrow_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                uint32_t nranks, uint32_t my_rank, size_t stride, orl_wire8* d_out, uint32_t* d_src,
+                                uint64_t* d_counts, uint32_t* d_status, void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
+    if (!d_status) return fail(c, ORL_E_INVALID, "null status word");
+    if (c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
+    if (r) return r;
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, 8, d_src,
+                                    d_counts, d_status, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "narrow partition launch");
+    return ORL_OK;
+}
+
+int orl_wire_types_set(orl_ctx* c, uint32_t n, const uint64_t* tcd) {
+    if (!c) return ORL_E_INVALID;
+    if (n > ORL_MAX_WIRE_TYPES || (n && !tcd)) return fail(c, ORL_E_INVALID, "wire types: n = %u (at most %u)", n, ORL_MAX_WIRE_TYPES);
+    for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t j = 0; j < i; ++j)
+            if (tcd[i] == tcd[j]) return fail(c, ORL_E_INVALID, "wire types: entry %u repeats entry %u", i, j);
+    RouteParams& P = c->hp;
+    std::memset(P.wire_tcd, 0, sizeof P.wire_tcd);
+    if (n) std::memcpy(P.wire_tcd, tcd, n * sizeof(uint64_t));
+    P.n_wire_types = n;
+    uint64_t h = 0xCBF29CE484222325ull;  // FNV-1a over the count and the values, little-endian bytes
+    auto mix = [&](uint64_t v) {
+        for (int b = 0; b < 8; ++b) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
+    };
+    mix(n);
+    for (uint32_t i = 0; i < n; ++i) mix(tcd[i]);
+    P.wire_digest = n ? h : 0;
+    c->params_dirty = true;
     return ORL_OK;
 }
 
@@ -1826,6 +1879,7 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             *v = c->probe8_valid ? 8 : c->probe_valid ? 16 : (c->probe_dev || c->probe_dev_stale) ? 17 : 32;
             return ORL_OK;
         case ORL_Q_FULL_UPLOADS: *v = c->n_full_uploads; return ORL_OK;
+        case ORL_Q_WIRE_DIGEST: *v = c->hp.wire_digest; return ORL_OK;
         case ORL_Q_SLOT_PATCHES: *v = c->n_patches; return ORL_OK;
         default: return fail(c, ORL_E_INVALID, "unknown query %u", what);
     }

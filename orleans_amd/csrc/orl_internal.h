@@ -132,10 +132,11 @@ struct alignas(16) RouteParams {
     uint32_t n_act;
     uint32_t cache_on;                 // directory cache populated: probe it for remote owners
     uint32_t n_probe_types;            // entries of probe_tcd (compact probe table)
-    uint32_t pad0;
+    uint32_t n_wire_types;             // entries of wire_tcd (8-B exchange records; 0 = no 8-B form)
     uint64_t mem_tcd, mem_n0, mem_n1;  // Constants.SystemMembershipTableId
-    uint64_t pad1;
+    uint64_t wire_digest;              // FNV-1a of wire_tcd[0, n_wire_types): ranks compare it before using the 8-B form
     uint64_t probe_tcd[kProbeTypes];   // TypeCodeData of type index i in ProbeSlot.w
+    uint64_t wire_tcd[ORL_MAX_WIRE_TYPES];  // TypeCodeData of wire type index i in orl_wire8.meta bits 16-19
 };
 static_assert(sizeof(RouteParams) % 16 == 0, "params must be 16-B granular");
 
@@ -251,7 +252,7 @@ int launch_dir_patch(const uint32_t* d_idx, const DirSlot* d_slots, const ProbeS
 int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* d_params, ProbeSlot* d_probe,
                        uint32_t* d_bad, void* stream);
 int launch_route_bucket(const RouteParams* d_params, const DirView& dv,
-                        const void* d_in, bool wire, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
+                        const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
                         void* ev_route_begin, void* ev_route_end);
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
@@ -309,7 +310,7 @@ int launch_stamp_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t*
 size_t stamp_scan_temp_bytes(size_t n);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
-                            void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
+                            void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
                             const Scratch& s, void* stream);
 // Stage 4 alone over already-routed messages (activation handles): histogram + bucket_after_route.
 int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
@@ -323,7 +324,10 @@ size_t part_state_bytes(size_t n);
 // (its totals); d_counts receives base + this input's counts.
 int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
                        size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
-                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts, void* stream);
+                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts,
+                       const uint64_t* d_wire_tcd, void* stream);
+// Device address of a context's wire types (RouteParams::wire_tcd), current once a route or partition call synced state.
+const uint64_t* ctx_wire_tcd(const orl_ctx* c);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

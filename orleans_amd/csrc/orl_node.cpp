@@ -34,7 +34,9 @@ using namespace orl;
 
 namespace {
 
-constexpr uint32_t kHeadWords = 16;  // [0, nranks) per-rank counts, [8] wire status (1 = no compact form)
+constexpr uint32_t kHeadWords = 16;  // [0, nranks) per-rank counts, [8] wire status (bit 0 = no 16-B form, bit 1 = no 8-B
+                                     // form), [9] record form of the partition (bits 56-63) | wire-type digest (bits 0-55)
+constexpr uint64_t kDigestMask = (1ull << 56) - 1;
 constexpr int kBarrierSeconds = 120;
 
 // ORL_TRANSPORT_LOCAL: the ranks are node objects of one process.  All-gathers and exchanges are host barriers around
@@ -110,6 +112,7 @@ struct orl_node {
     uint64_t* d_head = nullptr;                   // [2][kHeadWords]
     uint64_t* d_heads = nullptr;                  // [nranks][kHeadWords] (RCCL all-gather target)
     uint64_t* h_heads = nullptr;                  // pinned copy
+    uint64_t* h_form = nullptr;                   // pinned [2]: head word 9 of each send slot (form | digest)
     uint8_t* d_recv = nullptr;                    // owned records, chunk after chunk (max_recv x 32 B)
     uint32_t *d_route = nullptr, *d_act = nullptr, *d_order = nullptr, *d_off = nullptr;
     uint64_t* d_hcount = nullptr;                 // [8] hop-2 counts by host rank
@@ -236,6 +239,7 @@ void free_node(orl_node* nd) {
     f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
     f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts); f(nd->d_fan);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
+    if (nd->h_form) (void)hipHostFree(nd->h_form);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr})
@@ -328,6 +332,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipMalloc((void**)&nd->d_head, 2 * kHeadWords * 8));
     ok(hipMalloc((void**)&nd->d_heads, nr * kHeadWords * 8));
     ok(hipHostMalloc((void**)&nd->h_heads, nr * kHeadWords * 8, hipHostMallocDefault));
+    ok(hipHostMalloc((void**)&nd->h_form, 2 * 8, hipHostMallocDefault));
     ok(hipMalloc((void**)&nd->d_recv, mr * 32));
     ok(hipMalloc((void**)&nd->d_route, mr * 4));
     ok(hipMalloc((void**)&nd->d_act, mr * 4));
@@ -399,48 +404,69 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     uint64_t owned_bytes = 0;
     std::vector<uint64_t> owned_all(nr, 0);   // every rank's running receive total (capacity checks agree)
     uint64_t sent_remote = 0;
-    bool any_wide = false;
+    bool seen[3] = {false, false, false};     // record widths 8 / 16 / 32 among the owned segments
     // ---- hop 1 -------------------------------------------------------------------------------------------
+    // Record form per chunk: every rank first writes the narrowest form it can (8-B when its context has wire types,
+    // else 16-B; 32-B with ORL_NODE_WIDE_ONLY) and reports it with its wire-type digest in head word 9.  After the counts
+    // all-gather every rank derives the same final form: 8-B when all ranks wrote it with one digest and no message
+    // lacked it, 16-B when no message lacked that, else 32-B; a rank whose records differ re-partitions the chunk (the
+    // counts do not depend on the form).
+    uint64_t digest = 0;
+    NODE_CTX(nd, orl_ctx_query(nd->ctx, ORL_Q_WIRE_DIGEST, &digest));
+    const bool wide_only = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
+    const uint32_t first_form = wide_only ? 32u : (digest ? 8u : 16u);
     // Partition of chunk c into send slot c & 1 (after the slot's previous exchange): per-rank counts + wire status
     // in the slot's head words.  Chunk c + 1 is partitioned before the host waits for chunk c's counts, so the
     // partition stream does not idle through the all-gather round trip.
-    auto partition = [&](uint32_t c, bool wide) -> int {
+    auto partition = [&](uint32_t c, uint32_t form) -> int {
         const uint32_t slot = c & 1u;
         const uint64_t start = std::min<uint64_t>((uint64_t)c * cs, n), len = std::min<uint64_t>(cs, n - start);
         uint64_t* head = nd->d_head + slot * kHeadWords;
         uint8_t* send = nd->d_send[slot];
+        uint32_t* status = reinterpret_cast<uint32_t*>(head + 8);
         NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_slot[slot], 0));  // the slot's previous exchange has finished
         NODE_HIP(nd, hipMemsetAsync(head, 0, kHeadWords * 8, nd->sp));
-        if (wide)
+        // the slot's previous head copy was consumed before its all-gather returned, so the pinned word is free
+        nd->h_form[slot] = ((uint64_t)form << 56) | (digest & kDigestMask);
+        NODE_HIP(nd, hipMemcpyAsync(head + 9, nd->h_form + slot, 8, hipMemcpyHostToDevice, nd->sp));
+        if (form == 32)
             NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
                                                               nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
                                                               head, nd->sp));
-        else
+        else if (form == 16)
             NODE_CTX(nd, orl_partition_compact_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
                                                       nd->chunk_cap, reinterpret_cast<orl_wire_msg*>(send), nullptr, head,
-                                                      reinterpret_cast<uint32_t*>(head + 8), nd->sp));
+                                                      status, nd->sp));
+        else
+            NODE_CTX(nd, orl_partition_narrow_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
+                                                     nd->chunk_cap, reinterpret_cast<orl_wire8*>(send), nullptr, head,
+                                                     status, nd->sp));
         NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
         return ORL_OK;
     };
-    const bool wide_only = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
     if (K > 0)
-        if (int r = partition(0, wide_only)) return r;
+        if (int r = partition(0, first_form)) return r;
     for (uint32_t c = 0; c < K; ++c) {
         const uint32_t slot = c & 1u;
         uint64_t* head = nd->d_head + slot * kHeadWords;
         uint8_t* send = nd->d_send[slot];
         if (c + 1 < K)
-            if (int r = partition(c + 1, wide_only)) return r;
+            if (int r = partition(c + 1, first_form)) return r;
         if (int r = allgather_heads(nd, head, nd->ev_part[slot])) return r;
         const uint64_t* H = nd->h_heads;
-        bool wide = wide_only;
-        if (!wide) {
-            for (uint32_t r = 0; r < nr; ++r) wide |= (H[r * W + 8] & 0xFFFFFFFFull) != 0;
-            if (wide)  // some rank's chunk has a message without the compact form: every rank sends 32-B headers
-                if (int r = partition(c, true)) return r;
+        bool all8 = true, no16 = false, no8 = false, wide = false;
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t st = (uint32_t)H[r * W + 8];
+            const uint32_t f = (uint32_t)(H[r * W + 9] >> 56);
+            no16 |= (st & 1u) != 0;
+            no8 |= (st & 2u) != 0;
+            wide |= f == 32u;
+            all8 &= f == 8u && (H[r * W + 9] & kDigestMask) == (H[0 * W + 9] & kDigestMask);
         }
-        any_wide |= wide;
-        const uint32_t width = wide ? 32u : 16u;
+        const uint32_t width = (wide || no16) ? 32u : (all8 && !no8) ? 8u : 16u;
+        if (width != first_form)  // some rank's records do not fit the form: every rank rewrites the chunk in `width`
+            if (int r = partition(c, width)) return r;
+        seen[width == 8 ? 0 : width == 16 ? 1 : 2] = true;
         std::vector<uint64_t> sendc(nr), recvc(nr);
         uint64_t got = 0;
         for (uint32_t r = 0; r < nr; ++r) {
@@ -464,12 +490,15 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         nd->segs.push_back(orl_node::Seg{recv, got, width});
         if (got) {  // stages 1-3 of the received chunk, overlapping the next chunk's exchange
             NODE_HIP(nd, hipStreamWaitEvent(nd->sr, nd->ev_slot[slot], 0));
-            if (wide)
+            if (width == 32)
                 NODE_CTX(nd, orl_route_batch_device(nd->ctx, reinterpret_cast<const orl_msg_hdr*>(recv), got, ropts,
                                                     nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
-            else
+            else if (width == 16)
                 NODE_CTX(nd, orl_route_compact_device(nd->ctx, reinterpret_cast<const orl_wire_msg*>(recv), got, ropts,
                                                       nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
+            else
+                NODE_CTX(nd, orl_route_narrow_device(nd->ctx, reinterpret_cast<const orl_wire8*>(recv), got, ropts,
+                                                     nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
         }
         owned += got;
         owned_bytes += got * width;
@@ -511,13 +540,15 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             if (d == me) hosted = in;
         }
         if (int r = ensure_hop2(nd, owned)) return r;
-        const uint32_t wout = any_wide ? 32u : 16u;
+        // one record width for the forwarded set: the common width of the owned segments, or headers for a mix
+        const uint32_t wout = (seen[2] || (seen[0] && seen[1])) ? 32u : seen[1] ? 16u : 8u;
         uint64_t off = 0;
         for (size_t k = 0; k < nd->segs.size(); ++k) {  // one partition per segment, positions chained through the totals
             const orl_node::Seg& sg = nd->segs[k];
             int e = launch_part_routed(nd->d_ros, sg.p, (int)sg.width, (int)wout, nd->d_route + off, nd->d_act + off, sg.count, me,
                                        nr, nd->f_cap, nd->d_fsend, nd->d_fsend_route, nd->d_fsend_act, nd->d_fstate,
-                                       k ? nd->d_fcounts + 8 * (k - 1) : nullptr, nd->d_fcounts + 8 * k, nd->sr);
+                                       k ? nd->d_fcounts + 8 * (k - 1) : nullptr, nd->d_fcounts + 8 * k,
+                                       ctx_wire_tcd(nd->ctx), nd->sr);
             if (e) return nfail(nd, ORL_E_DEVICE, "hop-2 partition launch: %s", hipGetErrorString((hipError_t)e));
             off += sg.count;
         }

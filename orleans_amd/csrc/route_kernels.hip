@@ -112,6 +112,36 @@ __device__ __forceinline__ bool encode_wire(const u32x4& h0, const u32x4& h1, u3
     return ok;
 }
 
+// Narrow 8-B exchange record (orl_wire8): {n1 low 32 bits, meta with the wire type index in bits 16-19}.  The table
+// is the context's wire types (RouteParams::wire_tcd, staged in LDS with the params).
+__device__ __forceinline__ Msg load_narrow(const RouteParams& P, const orl_wire8* __restrict__ in, uint32_t e) {
+    const uint64_t a = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(in + e));
+    const uint32_t meta = (uint32_t)(a >> 32);
+    Msg m;
+    m.tcd = P.wire_tcd[(meta >> 16) & 0xFu];
+    m.n0 = 0;
+    m.n1 = (uint32_t)a;
+    m.meta = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) | (meta & 0xFF000000u);
+    m.aux = 0;
+    return m;
+}
+
+// Encode a header as an 8-B record; false when it has none (N0 != 0, N1 >= 2^32, a type not in the wire table, a
+// precomputed hash, flag/category bits out of range).
+__device__ __forceinline__ bool encode_narrow(const RouteParams& P, const u32x4& h0, const u32x4& h1, uint2& w) {
+    const uint64_t tcd = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    const uint32_t meta = h1.z;
+    const uint32_t cat = (meta >> 8) & 0xFFu, fl = (meta >> 16) & 0xFFu;
+    uint32_t ti = ORL_MAX_WIRE_TYPES;
+    for (uint32_t i = 0; i < P.n_wire_types; ++i)
+        if (P.wire_tcd[i] == tcd) ti = i;
+    const bool ok = h0.z == 0 && h0.w == 0 && h1.y == 0 && ti < ORL_MAX_WIRE_TYPES && cat < 4 && fl < 64 &&
+                    !(fl & ORL_HDR_HASH_VALID);
+    w.x = h1.x;
+    w.y = (meta & 0xFFu) | (cat << 8) | (fl << 10) | ((ti & 0xFu) << 16) | (meta & 0xFF000000u);
+    return ok;
+}
+
 // Stages 1-3 for one message, split so a thread can keep several messages' directory probes in flight:
 //   route_head  stages 1-2 + every decision that needs no directory (returns the final route word, or
 //               kNeedProbe when the owner's partition is local and must be probed, or kNeedProbeCache when the
@@ -479,10 +509,18 @@ struct RouteSmem {
     uint32_t hist[HB ? (1u << HB) : 1u];
 };
 
-// WIRE: the input is orl_msg_hdr (false) or compact orl_wire_msg records from the exchange (true).
+// FMT: the input is orl_msg_hdr (32), or exchange records: orl_wire_msg (16) or orl_wire8 (8, decoded with the
+// context's wire types).
 // PW: local-owner probes read the compact probe table `probe` (PW = 16: ProbeSlot, 8: u32 key/value pairs; same
 // indices) instead of `dir` (PW = 0).
-template <int HB, bool WIRE, int PW>
+template <int FMT>
+__device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __restrict__ in, uint32_t e) {
+    if (FMT == 16) return load_wire(static_cast<const orl_wire_msg*>(in), e);
+    if (FMT == 8) return load_narrow(P, static_cast<const orl_wire8*>(in), e);
+    return load_hdr(static_cast<const orl_msg_hdr*>(in), e);
+}
+
+template <int HB, int FMT, int PW>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
@@ -503,7 +541,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
         Msg m;
-        if (e < n) m = WIRE ? load_wire(static_cast<const orl_wire_msg*>(in), e) : load_hdr(static_cast<const orl_msg_hdr*>(in), e);
+        if (e < n) m = load_msg<FMT>(sm.P, in, e);
         uint32_t h = 0, own = 0, rf = 0, r = 0;
         uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
@@ -2030,8 +2068,9 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
     if (t == ntiles - 1) counts[r] = b0 + before + tc;
 }
 
-// COMPACT: write orl_wire_msg records (16 B) and set *wire_status = 1 if a message has no compact form.
-template <bool COMPACT>
+// FMT: the record written — 32 = orl_msg_hdr, 16 = orl_wire_msg (*wire_status |= 1 if a message has no 16-B form),
+// 8 = orl_wire8 (|= 1 as for 16, |= 2 if a message has no 8-B form).
+template <int FMT>
 __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
@@ -2080,10 +2119,16 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
         if (e < n) {
             const uint32_t d = dig[j];
             const uint64_t g = (uint64_t)d * stride + sm.lb.base[d] + sm.lb.cnt[w][d] + rank[j];
-            if (COMPACT) {
+            if (FMT == 16) {
                 u32x4 wr;
                 if (!encode_wire(h0[j], h1[j], wr)) atomicOr(wire_status, 1u);
                 reinterpret_cast<u32x4*>(out)[g] = wr;
+            } else if (FMT == 8) {
+                u32x4 wr;
+                uint2 nw;
+                const uint32_t bad = (encode_wire(h0[j], h1[j], wr) ? 0u : 1u) | (encode_narrow(sm.P, h0[j], h1[j], nw) ? 0u : 2u);
+                if (bad) atomicOr(wire_status, bad);
+                reinterpret_cast<uint2*>(out)[g] = nw;
             } else {
                 u32x4* dp = reinterpret_cast<u32x4*>(static_cast<orl_msg_hdr*>(out) + g);
                 dp[0] = h0[j];
@@ -2134,6 +2179,7 @@ __global__ __launch_bounds__(256) void k_host_rank_count(const uint32_t* __restr
 struct PartRoutedSmem {
     uint8_t rank_of_silo[256];
     LbShared lb;
+    uint64_t wire_tcd[ORL_MAX_WIRE_TYPES];  // WIN = 8, WOUT = 32: the wire types
 };
 
 template <int WIN, int WOUT>
@@ -2143,9 +2189,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
                                                                void* __restrict__ out, uint32_t* __restrict__ route_out,
                                                                uint32_t* __restrict__ act_out, uint32_t* __restrict__ state,
                                                                uint32_t ntiles, const uint64_t* __restrict__ base_in,
-                                                               uint64_t* __restrict__ counts) {
-    static_assert((WIN == 16 || WIN == 32) && WOUT >= WIN, "record widths");
+                                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ wire_tcd) {
+    static_assert((WIN == 8 || WIN == 16 || WIN == 32) && WOUT >= WIN && (WIN != 8 || WOUT != 16), "record widths");
     __shared__ PartRoutedSmem sm;
+    if (WIN == 8 && WOUT == 32 && threadIdx.x < ORL_MAX_WIRE_TYPES) sm.wire_tcd[threadIdx.x] = wire_tcd[threadIdx.x];
     const uint32_t rflags = rank_flags();
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
     if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
@@ -2160,9 +2207,14 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
     for (uint32_t j = 0; j < kPartItems; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
         const uint32_t ec = e < n ? e : n - 1;
-        const u32x4* sp = reinterpret_cast<const u32x4*>(static_cast<const uint8_t*>(in) + (size_t)ec * WIN);
-        h0[j] = __builtin_nontemporal_load(sp);
-        if (WIN == 32) h1[j] = __builtin_nontemporal_load(sp + 1);
+        if (WIN == 8) {
+            const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(in) + ec);
+            h0[j] = u32x4{(uint32_t)v, (uint32_t)(v >> 32), 0u, 0u};
+        } else {
+            const u32x4* sp = reinterpret_cast<const u32x4*>(static_cast<const uint8_t*>(in) + (size_t)ec * WIN);
+            h0[j] = __builtin_nontemporal_load(sp);
+            if (WIN == 32) h1[j] = __builtin_nontemporal_load(sp + 1);
+        }
         rw[j] = route[ec];
         aw[j] = act[ec];
     }
@@ -2182,7 +2234,16 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
             const uint32_t d = dig[j];
             const uint64_t g = (uint64_t)d * stride + sm.lb.base[d] + sm.lb.cnt[w][d] + rank[j];
             u32x4* dp = reinterpret_cast<u32x4*>(static_cast<uint8_t*>(out) + g * WOUT);
-            if (WIN == 16 && WOUT == 32) {  // orl_wire_msg → orl_msg_hdr (the decoder of load_wire)
+            if (WIN == 8 && WOUT == 8) {
+                reinterpret_cast<uint2*>(out)[g] = make_uint2(h0[j].x, h0[j].y);
+            } else if (WIN == 8) {  // orl_wire8 → orl_msg_hdr (the decoder of load_narrow)
+                const uint32_t meta = h0[j].y;
+                const uint64_t tcd = sm.wire_tcd[(meta >> 16) & 0xFu];
+                const uint32_t m2 = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) |
+                                    (meta & 0xFF000000u);
+                dp[0] = u32x4{(uint32_t)tcd, (uint32_t)(tcd >> 32), 0u, 0u};
+                dp[1] = u32x4{h0[j].x, 0u, m2, 0u};
+            } else if (WIN == 16 && WOUT == 32) {  // orl_wire_msg → orl_msg_hdr (the decoder of load_wire)
                 const uint32_t meta = h0[j].w;
                 const uint64_t tcd = ((uint64_t)((meta >> 16) & 0xFFu) << 56) |
                                      ((uint64_t)(int64_t)(int32_t)h0[j].z & 0x00FFFFFFFFFFFFFFull);
@@ -3066,7 +3127,7 @@ int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* 
     return (int)hipGetLastError();
 }
 
-int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const void* d_in, bool wire,
+int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const void* d_in, int fmt,
                         size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
                         uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
     hipStream_t st = (hipStream_t)stream;
@@ -3086,16 +3147,16 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
-#define ORL_ROUTE_W(H, Q) do { if (wire) ORL_ROUTE(H, true, Q); else ORL_ROUTE(H, false, Q); } while (0)
+#define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
                                             shift, items)
         if (hist) {
-            if (wire) ORL_ROUTE8(kMaxDigitBits, true); else ORL_ROUTE8(kMaxDigitBits, false);
+            if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
         } else {
-            if (wire) ORL_ROUTE8(0, true); else ORL_ROUTE8(0, false);
+            if (fmt == 16) ORL_ROUTE8(0, 16); else if (fmt == 8) ORL_ROUTE8(0, 8); else ORL_ROUTE8(0, 32);
         }
 #undef ORL_ROUTE8
     } else if (dv.probe) {
@@ -3368,7 +3429,8 @@ size_t part_state_bytes(size_t n) { return 16 + (size_t)ceil_div(n, kPartTile) *
 
 int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
                        size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
-                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts, void* stream) {
+                       uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts,
+                       const uint64_t* d_wire_tcd, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = d_base_in ? hipMemcpyAsync(d_counts, d_base_in, sizeof(uint64_t) * nranks, hipMemcpyDeviceToDevice, st)
                              : hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
@@ -3377,8 +3439,10 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
     if ((e = hipMemsetAsync(d_state, 0, part_state_bytes(n), st)) != hipSuccess) return (int)e;
 #define ORL_PR(WI, WO) hipLaunchKernelGGL((k_part_routed<WI, WO>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_ros, d_in, d_route,  \
                                           d_act, (uint32_t)n, my_rank, nranks, stride, d_out, d_route_out, d_act_out, d_state,   \
-                                          ntiles, d_base_in, d_counts)
-    if (win == 16 && wout == 16) ORL_PR(16, 16);
+                                          ntiles, d_base_in, d_counts, d_wire_tcd)
+    if (win == 8 && wout == 8) ORL_PR(8, 8);
+    else if (win == 8) ORL_PR(8, 32);
+    else if (win == 16 && wout == 16) ORL_PR(16, 16);
     else if (win == 16) ORL_PR(16, 32);
     else ORL_PR(32, 32);
 #undef ORL_PR
@@ -3387,23 +3451,24 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
 
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
-                            void* d_out, bool compact, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
+                            void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
                             const Scratch& s, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
-    if (e == hipSuccess && compact) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess && fmt != 32) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
     if (e != hipSuccess || n == 0) return (int)e;
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
     const uint32_t ntiles = ceil_div(n, kPartTile);
     // ticket + error word + one 64-B granule row per tile, zeroed before every launch (16-B multiple)
     e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ntiles * 64, st);
     if (e != hipSuccess) return (int)e;
-    if (compact)
-        hipLaunchKernelGGL(k_part_lb<true>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
-                           excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, d_wire_status);
-    else
-        hipLaunchKernelGGL(k_part_lb<false>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, (uint32_t)n,
-                           excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, d_wire_status);
+#define ORL_PLB(F) hipLaunchKernelGGL(k_part_lb<F>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in,     \
+                                      (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, \
+                                      d_wire_status)
+    if (fmt == 16) ORL_PLB(16);
+    else if (fmt == 8) ORL_PLB(8);
+    else ORL_PLB(32);
+#undef ORL_PLB
     return (int)hipGetLastError();
 }
 

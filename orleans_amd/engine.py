@@ -371,6 +371,29 @@ class GrainDirectoryEngine:
                                                         int(my_rank), int(stride), ptr(d_out), ptr(d_src_index),
                                                         ptr(d_counts), ptr(d_status), ptr(stream)))
 
+    def set_wire_types(self, type_code_data: Sequence[int]) -> None:
+        """The TypeCodeData values of the 8-B exchange form (orl_wire_types_set; the same list on every rank)."""
+        arr = np.asarray([int(t) & 0xFFFFFFFFFFFFFFFF for t in type_code_data], dtype=np.uint64)
+        self._ck(self._lib.orl_wire_types_set(self._ctx, len(arr), arr.ctypes.data if len(arr) else None))
+        self.wire_types = arr
+
+    def partition_narrow_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
+                                stride: int, d_out, d_counts, d_status, d_src_index=None, stream=None,
+                                opts: int = 0) -> None:
+        """partition_by_owner_padded_device writing 8-B orl_wire8 records; d_status[0] bit 0 = a message has no 16-B
+        form, bit 1 = a message has no 8-B form (the records are then invalid)."""
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        self._ck(self._lib.orl_partition_narrow_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(ros), int(nranks),
+                                                       int(my_rank), int(stride), ptr(d_out), ptr(d_src_index),
+                                                       ptr(d_counts), ptr(d_status), ptr(stream)))
+
+    def address_narrow_device(self, d_recs, n: int, d_route, d_act, d_order=None, d_offsets=None, stream=None,
+                              opts: int = 0) -> None:
+        """address_messages_device over 8-B exchange records (orl_wire8, this context's wire types)."""
+        self._ck(self._lib.orl_route_narrow_device(self._ctx, ptr(d_recs), int(n), int(opts), ptr(d_route), ptr(d_act),
+                                                   ptr(d_order), ptr(d_offsets), ptr(stream)))
+
     def address_compact_device(self, d_recs, n: int, d_route, d_act, d_order=None, d_offsets=None, stream=None,
                                opts: int = 0) -> None:
         """address_messages_device over compact exchange records (orl_wire_msg)."""

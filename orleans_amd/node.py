@@ -236,6 +236,22 @@ class PipelinedRouter:
         return self.flush()
 
 
+def narrow_records_to_headers(raw: np.ndarray, wire_types) -> np.ndarray:
+    """8-B orl_wire8 records → orl_msg_hdr with the wire types they were written with (include/orleans_route.h)."""
+    w = np.ascontiguousarray(raw).view(np.uint32).reshape(-1, 2)
+    meta = w[:, 1]
+    types = np.zeros(L.MAX_WIRE_TYPES, np.uint64)
+    types[:len(wire_types)] = np.asarray(wire_types, np.uint64)
+    out = np.zeros(len(w), L.MSG_DTYPE)
+    out["tcd"] = types[(meta >> 16) & 0xF]
+    out["n1"] = w[:, 0].astype(np.uint64)
+    out["sending_silo"] = (meta & 0xFF).astype(np.uint8)
+    out["category"] = ((meta >> 8) & 0x3).astype(np.uint8)
+    out["flags"] = ((meta >> 10) & 0x3F).astype(np.uint8)
+    out["target_silo"] = (meta >> 24).astype(np.uint8)
+    return out
+
+
 def wire_records_to_headers(raw: np.ndarray) -> np.ndarray:
     """16-B orl_wire_msg records → orl_msg_hdr (the layout include/orleans_route.h documents; aux = 0)."""
     w = np.ascontiguousarray(raw).view(np.uint32).reshape(-1, 4)
@@ -354,7 +370,8 @@ class GrainNode:
             raw = np.zeros(cnt * w, np.uint8)
             if cnt:
                 e.copy_to_host(raw, p, stream=stream)
-            parts.append(raw.view(L.MSG_DTYPE) if w == 32 else wire_records_to_headers(raw))
+            parts.append(raw.view(L.MSG_DTYPE) if w == 32 else wire_records_to_headers(raw) if w == 16 else
+                         narrow_records_to_headers(raw, getattr(e, "wire_types", ())))
         hdrs = np.concatenate(parts) if parts else np.zeros(0, L.MSG_DTYPE)
         return route, act, order, off, hdrs
 

@@ -120,6 +120,11 @@ def default_cluster(n_silos: int = N_SILOS, generations=None) -> Cluster:
                    calc_id_hash(CHIRPER_ACCOUNT_CLASS), tuple(gens))
 
 
+def grain_tcd(cl: Cluster, category: int = L.CAT_GRAIN) -> int:
+    """TypeCodeData of the workload's long-key grain class: (category << 56) + sign-extended type code."""
+    return ((category << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF
+
+
 def setup_engine(eng, cl: Cluster, local_silos: Optional[np.ndarray] = None, seed: int = 0) -> None:
     local = None
     if local_silos is not None:

@@ -2,7 +2,7 @@
 
 The one-GPU rehearsal (bench.py --local-ranks) runs every rank's kernels concurrently on one device, so its per-kernel
 times are not what one rank sees on its own GPU.  This lab replays one rank's share in isolation:
-  1. hop 1: the rank's own 256M/R messages, owner-partitioned in `chunks` calls (k_part_lb, 16-B records);
+  1. hop 1: the rank's own 256M/R messages, owner-partitioned in `chunks` calls (k_part_lb, 8-B or 16-B records: argv[3]);
   2. routing at the owner + stage 4 at the host over everything the rank receives (every source rank's region for it,
      built here by partitioning each source's messages);
 and prints milliseconds per step for the hottest rank and the rank with the median load.  Lab script, not a test.
@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, ".")
+from orleans_amd import _lib as L  # noqa: E402
 from orleans_amd import workloads as W  # noqa: E402
 from orleans_amd.engine import GrainDirectoryEngine  # noqa: E402
 from orleans_amd.node import local_silos, rank_of_silo  # noqa: E402
@@ -33,7 +34,7 @@ def timed(fn, reps=5):
     return float(np.median(ts))
 
 
-def main(R=8, chunks=4):
+def main(R=8, chunks=4, width=8):
     n_grains, n_total = 16_000_000, 256 << 20
     n_msgs = n_total // R
     cl = W.balanced_cluster()
@@ -42,8 +43,12 @@ def main(R=8, chunks=4):
     ztab = W.zipf_tables(torch, n_grains, W.SEED_C3)
     part = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=n_msgs, device=0)
     W.setup_engine(part, cl)
+    st = torch.cuda.current_stream().cuda_stream  # every call on torch's stream, so its events time them
+    if width == 8:
+        part.set_wire_types([W.grain_tcd(cl)])
+    partition = part.partition_narrow_device if width == 8 else part.partition_compact_device
     cap = n_msgs + n_msgs // 2
-    d_out = torch.empty(R * cap * 16, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(R * cap * width, dtype=torch.uint8, device="cuda")
     d_counts = torch.zeros(R, dtype=torch.int64, device="cuda")
     d_status = torch.zeros(1, dtype=torch.int32, device="cuda")
     recv = [[] for _ in range(R)]
@@ -55,14 +60,15 @@ def main(R=8, chunks=4):
 
         def hop1():
             for c in range(chunks):
-                part.partition_compact_device(m[c * step:], step, ros, R, s, cap, d_out, d_counts, d_status)
+                partition(m[c * step:], step, ros, R, s, cap, d_out, d_counts, d_status, stream=st)
         part_ms.append(timed(hop1))
-        part.partition_compact_device(m, n_msgs, ros, R, s, cap, d_out, d_counts, d_status)
+        partition(m, n_msgs, ros, R, s, cap, d_out, d_counts, d_status, stream=st)
         cnt = d_counts.cpu().numpy()
+        assert int(d_status.item()) == 0
         for r in range(R):
-            recv[r].append(d_out[r * cap * 16:(r * cap + int(cnt[r])) * 16].clone())
+            recv[r].append(d_out[r * cap * width:(r * cap + int(cnt[r])) * width].clone())
         del m
-    owned = np.array([sum(x.numel() // 16 for x in recv[r]) for r in range(R)])
+    owned = np.array([sum(x.numel() // width for x in recv[r]) for r in range(R)])
     print(f"hop 1 partition of {n_msgs >> 20}M messages in {chunks} calls: {np.median(part_ms):.3f} ms "
           f"(min {min(part_ms):.3f}, max {max(part_ms):.3f})", flush=True)
     print(f"owned per rank (M): {[round(x / 2**20, 1) for x in owned]}, max/mean {owned.max() / owned.mean():.2f}",
@@ -70,21 +76,24 @@ def main(R=8, chunks=4):
     order = np.argsort(owned)
     for label, r in (("hottest", int(order[-1])), ("median", int(order[R // 2]))):
         recs = torch.cat(recv[r])
-        n = recs.numel() // 16
+        n = recs.numel() // width
         mine = local_silos(cl.n_silos, R, r)
         mask = np.zeros(cl.n_silos, np.uint8)
         mask[mine] = 1
         n_act = max(1, int((reg & mask[owner].astype(bool)).sum()))
         eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=n, device=0)
         W.setup_engine(eng, cl, local_silos=mine)
+        if width == 8:
+            eng.set_wire_types([W.grain_tcd(cl)])
         W.register_population(eng, keys, owner, reg, mask, dense_local=True)
         route = torch.empty(n, dtype=torch.int32, device="cuda")
         act = torch.empty(n, dtype=torch.int32, device="cuda")
         order_o = torch.empty(n, dtype=torch.int32, device="cuda")
         offs = torch.empty(n_act + 2, dtype=torch.int32, device="cuda")
-        t_route = timed(lambda: eng.address_compact_device(recs, n, route, act))
-        t_all = timed(lambda: eng.address_compact_device(recs, n, route, act, order_o, offs))
-        xgmi_mb = n * (R - 1) / R * 16 / 1e6
+        addr = eng.address_narrow_device if width == 8 else eng.address_compact_device
+        t_route = timed(lambda: addr(recs, n, route, act, stream=st, opts=L.OPT_NO_BUCKETS))
+        t_all = timed(lambda: addr(recs, n, route, act, order_o, offs, stream=st))
+        xgmi_mb = n * (R - 1) / R * width / 1e6
         print(f"{label} rank {r}: {n / 2**20:.1f}M messages received; route {t_route:.3f} ms, route + stage 4 "
               f"{t_all:.3f} ms; n_act {n_act}; receives ~{xgmi_mb:.0f} MB over xGMI", flush=True)
         eng.close()

@@ -65,6 +65,19 @@ class World:
             self.engs.append(e)
             self.oracles.append(o)
 
+    def set_wire_types(self, mode):
+        """8-B exchange form: None (off), "both" (grain + system-target types on every rank), "grain_only" (system-target
+        messages lack the form), "mismatch" (the last rank's list differs: the digests disagree)."""
+        if mode is None:
+            return
+        grain_t = (L.CAT_GRAIN << 56) + (self.cl.type_code & 0x00FFFFFFFFFFFFFF)
+        sys_t = (L.CAT_SYSTEM_TARGET << 56) | 12
+        for r, e in enumerate(self.engs):
+            types = [grain_t] if mode == "grain_only" else [grain_t, sys_t]
+            if mode == "mismatch" and r == self.nr - 1:
+                types = [sys_t, grain_t]
+            e.set_wire_types(types)
+
     def messages(self, rank, n, seed, wide_at=None):
         silos = np.nonzero(self.ros == rank)[0].astype(np.uint8)
         m = W.uniform_messages(self.cl, self.n_grains + 3000, n, seed=seed, sender_silos=silos)
@@ -131,13 +144,20 @@ def _run(t, world, nodes, batches, streams):
         return list(ex.map(one, range(len(nodes))))
 
 
-@pytest.mark.parametrize("nranks,chunks,host_mix", [(1, 1, 0.0), (2, 3, 0.0), (2, 2, 0.3), (3, 4, 0.3), (4, 1, 0.3),
-                                                    (4, 4, 0.0)])
-def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix):
+@pytest.mark.parametrize("nranks,chunks,host_mix,wire", [(1, 1, 0.0, None), (2, 3, 0.0, None), (2, 2, 0.3, None),
+                                                         (3, 4, 0.3, None), (4, 1, 0.3, None), (4, 4, 0.0, None),
+                                                         (1, 2, 0.0, "both"), (2, 2, 0.3, "both"), (3, 4, 0.3, "both"),
+                                                         (4, 4, 0.0, "both"), (2, 3, 0.3, "grain_only"),
+                                                         (3, 2, 0.0, "mismatch")])
+def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix, wire):
+    """Every rank's hosted output == the oracle's replay of the protocol, with each record form: 16-B (no wire types),
+    8-B (wire types set; a Guid-keyed chunk in batch 1 drops that chunk to 32-B headers, so hop 2 forwards a mix), and the
+    16-B fallbacks when a message lacks the 8-B form or the ranks' wire types differ."""
     t = torch
     ros = None if nranks != 3 else [s % 3 for s in range(8)]
     world = World(nranks, host_mix=host_mix, ros=ros)
-    gid = b"node-test-%d-%d-%d" % (nranks, chunks, int(host_mix * 10))
+    world.set_wire_types(wire)
+    gid = b"node-test-%d-%d-%d-%s" % (nranks, chunks, int(host_mix * 10), str(wire).encode())
     nodes = [GrainNode(world.engs[r], nranks, r, world.ros, max_batch=200_000, max_recv=400_000,
                        transport=L.TRANSPORT_LOCAL, group_id=gid, chunks=chunks) for r in range(nranks)]
     streams = [t.cuda.Stream() for _ in range(nranks)]
@@ -149,6 +169,11 @@ def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix):
         for r in range(nranks):
             res, (route, act, order, off, hdrs) = got[r]
             er, ea, eo, ef, eh = exp[r]
+            widths = {w for _, c, w in res.segments if c}
+            if wire == "both" and b == 0:  # every chunk in the 8-B form (a forwarded set keeps it)
+                assert widths <= {8}, widths
+            elif wire in ("grain_only", "mismatch") or (wire is None and b == 0):
+                assert 8 not in widths, widths
             assert res.hop2 == forward
             assert res.n_hosted == len(er)
             np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} batch {b} headers")

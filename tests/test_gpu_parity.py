@@ -324,6 +324,79 @@ def test_compact_wire_partition_and_route(torch):
     eng.close()
 
 
+def test_narrow_wire_partition_and_route(torch):
+    """8-B exchange records (orl_wire8): the one-pass partition's regions == the oracle's partition encoded by the
+    oracle's narrow codec; the status word's bits say which forms a batch lacks; routing the 8-B records == routing
+    the 32-B headers (route, act, order, offsets)."""
+    cl, eng, o = _random_setup(10_000, 10_000)
+    t = torch
+    st = t.cuda.current_stream().cuda_stream
+    grain_t = (L.CAT_GRAIN << 56) + (cl.type_code & 0x00FFFFFFFFFFFFFF)
+    sys_t = (L.CAT_SYSTEM_TARGET << 56) | 12
+    types = [sys_t, grain_t]  # the grain type at index 1: the index is carried, not assumed
+    with pytest.raises(L.OrleansRouteError):  # no wire types yet: the 8-B form is off
+        eng.partition_narrow_device(t.zeros(32, dtype=t.uint8, device="cuda"), 1, cl.rank_of_silo(1), 1, 0, 1,
+                                    t.empty(16, dtype=t.uint8, device="cuda"), t.empty(1, dtype=t.int64, device="cuda"),
+                                    t.empty(1, dtype=t.int32, device="cuda"), stream=st)
+    eng.set_wire_types(types)
+    assert eng.query(L.Q_WIRE_DIGEST) != 0
+    for n, nranks in ((0, 2), (1, 1), (4097, 3), (100_003, 8)):
+        ros = cl.rank_of_silo(nranks) if nranks != 3 else np.array([s % 3 for s in range(8)], np.uint8)
+        msgs = W.uniform_messages(cl, 11_000, n, seed=n)
+        msgs["flags"][::89] = L.HDR_ADDRESS_COMPLETE
+        msgs["target_silo"][::89] = 3
+        msgs["category"][::7] = 1
+        msgs["tcd"][5::97] = sys_t
+        d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+        stride = n + 3
+        d_out = t.empty((nranks * stride, 8), dtype=t.uint8, device="cuda")
+        d_cnt = t.empty(nranks, dtype=t.int64, device="cuda")
+        d_st = t.full((1,), 7, dtype=t.int32, device="cuda")
+        eng.partition_narrow_device(d_in, n, ros, nranks, 0, stride, d_out, d_cnt, d_st, stream=st)
+        t.cuda.synchronize()
+        assert int(d_st.item()) == 0
+        src, cnt = o.partition(msgs, ros, nranks, 0)
+        np.testing.assert_array_equal(d_cnt.cpu().numpy(), cnt.astype(np.int64))
+        exp, ok = cpu_ref.narrow_encode(msgs[src], types)
+        assert ok.all()
+        out = d_out.cpu().numpy().reshape(-1).view(cpu_ref.WIRE8_DTYPE)
+        o0 = 0
+        for r in range(nranks):
+            c = int(cnt[r])
+            np.testing.assert_array_equal(out[r * stride:r * stride + c], exp[o0:o0 + c])
+            o0 += c
+        if n == 0:
+            continue
+        recs, _ = cpu_ref.narrow_encode(msgs, types)
+        d_recs = t.from_numpy(recs.view(np.uint8).reshape(-1, 8)).cuda()
+        outs = [t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)] + [t.empty(10_002, dtype=t.int32, device="cuda")]
+        eng.address_narrow_device(d_recs, n, *outs, stream=st)
+        t.cuda.synchronize()
+        got = [x.cpu().numpy().view(np.uint32) for x in outs]
+        r_ref, a_ref = o.route(msgs)
+        np.testing.assert_array_equal(got[0], r_ref)
+        np.testing.assert_array_equal(got[1], a_ref)
+        o_ref, f_ref = o.bucket(a_ref, 10_000)
+        np.testing.assert_array_equal(got[2], o_ref)
+        np.testing.assert_array_equal(got[3], f_ref)
+    # status bits: bit 1 = a message without the 8-B form, bit 0 = also without the 16-B form
+    for field, val, want in (("n1", 1 << 32, 2), ("tcd", grain_t + 1, 2), ("n0", 1, 3), ("flags", L.HDR_HASH_VALID, 3),
+                             ("tcd", (3 << 56) | 0x0000123412345678, 3)):
+        msgs = W.uniform_messages(cl, 11_000, 5000, seed=3)
+        msgs[field][4321] = val
+        d_in = t.from_numpy(msgs.view(np.uint8).reshape(-1, 32)).cuda()
+        d_out = t.empty((2 * 5000, 8), dtype=t.uint8, device="cuda")
+        d_cnt = t.empty(2, dtype=t.int64, device="cuda")
+        d_st = t.zeros((1,), dtype=t.int32, device="cuda")
+        eng.partition_narrow_device(d_in, 5000, cl.rank_of_silo(2), 2, 1, 5000, d_out, d_cnt, d_st, stream=st)
+        t.cuda.synchronize()
+        assert int(d_st.item()) == want, (field, val)
+        assert not cpu_ref.narrow_encode(msgs, types)[1].all()
+    eng.set_wire_types([])
+    assert eng.query(L.Q_WIRE_DIGEST) == 0
+    eng.close()
+
+
 def test_config2_full_size_properties(torch):
     """BASELINE config 2 at full size (1M grains, 64M messages) on the device-resident path."""
     t = torch
