@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -186,7 +187,8 @@ inline BucketPlan make_bucket_plan(uint32_t max_key) {
     if (total == 0) total = 1;
     BucketPlan p{};
     p.two_level = total <= 2 * (int)kMaxDigitBits;
-    p.lb = total <= (int)kMaxDigitBits ? total : (total + 1) / 2;  // 20 bits: 10 + 10
+    static const bool lb_floor = [] { const char* e = getenv("ORL_LB_FLOOR"); return e && e[0] == '1'; }();
+    p.lb = total <= (int)kMaxDigitBits ? total : lb_floor ? total / 2 : (total + 1) / 2;  // 20 bits: 10 + 10
     // (23-24-bit keys as 12 + 12 measured 2.82 ms vs 1.57 ms for 3 LSD passes at config 3: Zipf-hot digits
     // serialise the rank atomics and 4096 bins per 4096-message segment make the column work dominate)
     p.hb = total - p.lb;

@@ -43,7 +43,10 @@ def main(R=8, chunks=4, width=8):
     ztab = W.zipf_tables(torch, n_grains, W.SEED_C3)
     part = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=n_msgs, device=0)
     W.setup_engine(part, cl)
-    st = torch.cuda.current_stream().cuda_stream  # every call on torch's stream, so its events time them
+    # every call on one torch stream (not the legacy default stream, whose handle 0 means "the context's own stream" to
+    # the library), so torch's events time them and torch's copies see their results
+    torch.cuda.set_stream(torch.cuda.Stream())
+    st = torch.cuda.current_stream().cuda_stream
     if width == 8:
         part.set_wire_types([W.grain_tcd(cl)])
     partition = part.partition_narrow_device if width == 8 else part.partition_compact_device
