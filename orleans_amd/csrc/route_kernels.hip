@@ -374,10 +374,34 @@ __device__ __forceinline__ uint32_t rank_step_uniform(uint32_t* cnt, uint32_t d)
     return counter_add<PACKED>(cnt, d, 1u);
 }
 
+// One step that takes the lanes carrying the hot digit dh out of the atomics: they are ranked by lane prefix on ONE
+// counter update by their first lane (the same-address lanes of an LDS atomic are serviced one after another); the
+// other lanes keep one returning atomic each.  Different digits never share an order, so this keeps every rank.
+template <bool PACKED>
+__device__ __forceinline__ uint32_t rank_step_peel(uint32_t* cnt, uint32_t d, uint32_t dh) {
+    const uint64_t m = __ballot(d == dh);
+    if (d != dh) return counter_add<PACKED>(cnt, d, 1u);
+    const uint64_t lt = lanes_below();
+    uint32_t base = 0;
+    if ((m & lt) == 0) base = counter_add<PACKED>(cnt, dh, (uint32_t)__popcll(m));
+    return (uint32_t)__builtin_amdgcn_readlane(base, (uint32_t)__builtin_ctzll(m)) + (uint32_t)__popcll(m & lt);
+}
+
+// A wave's skewed digit: the digit of lane 0 or lane 63 of its first full step when it covers >= kSkewLanes lanes
+// (a Zipf-hot activation: 11-50 % of a batch's messages), else kNoHot.  Uniform digits never reach it.
+constexpr uint32_t kSkewLanes = 8, kNoHot = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t wave_hot_digit(uint32_t d) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    const uint32_t d63 = __builtin_amdgcn_readlane(d, 63);
+    const uint32_t c0 = (uint32_t)__popcll(__ballot(d == d0)), c63 = (uint32_t)__popcll(__ballot(d == d63));
+    return max(c0, c63) >= kSkewLanes ? (c0 >= c63 ? d0 : d63) : kNoHot;
+}
+
 // Rank a wave's N steps of 64 digits d[j] (element j * 64 + lane valid while < lim) on its counter row.  The mode is
 // chosen once per wave, so the common loop is straight-line atomics: the ballot fallback when the self-check failed;
 // the one-digit check per step when the wave's FIRST step is one digit (clustered hot activations: Zipf buckets, sorted
-// input); else one returning LDS atomic per element.
+// input); the hot-digit peel when one digit covers many lanes of the first step (an unsorted Zipf stream); else one
+// returning LDS atomic per element.
 
 template <int BITS, bool PACKED, int N, int RM = kRmRuntime>
 __device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
@@ -401,6 +425,13 @@ __device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N]
 #pragma unroll
         for (int j = 0; j < N; ++j)
             if (j * 64u + lane < lim) rank[j] = rank_step_uniform<PACKED>(cnt, d[j]);
+        return;
+    }
+    const uint32_t dh = ((RM == kRmHot || (flags & kRankUniform)) && lim >= 64u) ? wave_hot_digit(d[0]) : kNoHot;
+    if (dh != kNoHot) {
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j * 64u + lane < lim) rank[j] = rank_step_peel<PACKED>(cnt, d[j], dh);
         return;
     }
 #pragma unroll
@@ -1379,9 +1410,24 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
                 seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
             }
         }
+        // a Zipf-hot key (most of a hot bucket's segments): its lanes add with one atomic per step (the same-address
+        // lanes of an LDS atomic are serviced one by one); decided per wave from its first full step
+        const uint32_t dh = c0 + 256u * kItems <= r.hi ? wave_hot_digit(key[0] & (BL - 1u)) : kNoHot;
+        if (dh != kNoHot) {
 #pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j)
-            if (c0 + j * 256u + threadIdx.x < r.hi) atomicAdd(&hist[key[j] & (BL - 1u)], 1u);
+            for (uint32_t j = 0; j < kItems; ++j) {
+                if (c0 + j * 256u + threadIdx.x < r.hi) {
+                    const uint32_t d = key[j] & (BL - 1u);
+                    const uint64_t m = __ballot(d == dh);
+                    if (d != dh) atomicAdd(&hist[d], 1u);
+                    else if ((m & lanes_below()) == 0) atomicAdd(&hist[dh], (uint32_t)__popcll(m));
+                }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kItems; ++j)
+                if (c0 + j * 256u + threadIdx.x < r.hi) atomicAdd(&hist[key[j] & (BL - 1u)], 1u);
+        }
     }
     __syncthreads();
     uint32_t* row = seg_hist + (size_t)r.index * BL;
@@ -2012,6 +2058,9 @@ __global__ void k_part_counts(const uint32_t* __restrict__ scanned, uint32_t nti
 // and publishes its aggregate without waiting on anything: the spin always ends (bounded anyway:
 // on timeout the error word is set and the tile stops waiting).
 constexpr uint32_t kPartItems = 8;
+// Destination ranks are 3-bit digits: ~8 lanes share each one, so the per-lane LDS atomic serialises; the ballot match
+// (3 ballots, one update per digit group) ranks them without relying on the atomics' lane order.
+constexpr int kPartRm = kRmBallot;
 constexpr uint32_t kPartTile = kRouteThreads * kPartItems;
 constexpr uint32_t kLbSpinLimit = 1u << 24;
 
@@ -2109,7 +2158,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
             dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
         }
     }
-    rank_steps<3, false, kPartItems>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
+    rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts);
     __syncthreads();
@@ -2223,7 +2272,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
         dig[j] = 0;
         if (wbase + j * 64u + lane < n) dig[j] = host_rank(sm.rank_of_silo, rw[j], my_rank);
     }
-    rank_steps<3, false, kPartItems>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
+    rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in);
     __syncthreads();
