@@ -2085,36 +2085,85 @@ __device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_
 // an inclusive one, publishes its own inclusive count and leaves the tile's exclusive prefix in lb.base[r]; the last
 // tile writes the per-rank totals.  Call between two __syncthreads().
 // base_in (optional, device, per rank): added to every position and total (a partition continued over several inputs).
+// The look-back runs on wave 0 as 8 lanes per rank (lane = rank + 8 k), each lane loading kLbPerLane granules, so one
+// device round trip examines the kLbWindow tiles before the window's start for every rank at once instead of one tile
+// per round trip (the serial walk: 470 us per 32M-message partition, the 8-tile window 402 us, a 64-tile window 505 us
+// -- its 8 sc1 loads per lane and round cost more than the rounds they save; no look-back at all 300 us,
+// scripts/part_lab.py).  Per rank, the granules up to the nearest inclusive one are summed (it ends the look-back);
+// when an earlier tile has not published its aggregate yet, the published ones before it are consumed and the window
+// polls again from that tile.  Tiles before tile 0 read as inclusive 0.  Window offset of lane k's granule i: i * 8 + k.
+constexpr uint32_t kLbPerLane = 1, kLbWindow = 8 * kLbPerLane;
+
+__device__ __forceinline__ uint32_t rank_group_bits(uint64_t m, uint32_t r) {  // bit k = bit r + 8 k of m
+    uint32_t g = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) g |= (uint32_t)((m >> (r + 8u * k)) & 1ull) << k;
+    return g;
+}
+
 __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restrict__ state, uint32_t nranks, uint32_t ntiles,
                                                uint64_t* __restrict__ counts, const uint64_t* __restrict__ base_in = nullptr) {
-    if (threadIdx.x >= nranks) return;
+    if (threadIdx.x >= 64) return;
     uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
-    const uint32_t r = threadIdx.x, t = lb.tile;
+    const uint32_t lane = threadIdx.x, r = lane & 7u, k = lane >> 3, t = lb.tile;
+    const bool on = r < nranks;
     uint32_t tc = 0;
-    for (uint32_t q = 0; q < kWaves; ++q) {
-        const uint32_t c = lb.cnt[q][r];
-        lb.cnt[q][r] = tc;
-        tc += c;
-    }
-    store_granule(status + (size_t)t * 8 + r, 1u, tc);
-    uint32_t before = 0;
-    for (int64_t tt = (int64_t)t - 1; tt >= 0; --tt) {
-        uint64_t v;
-        uint32_t spins = 0;
-        while (((v = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) == 0) {
-            if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
-                atomicOr(&state[1], 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+    if (k == 0 && on) {  // one lane per rank: wave bases inside the tile, then the tile's aggregate
+        for (uint32_t q = 0; q < kWaves; ++q) {
+            const uint32_t c = lb.cnt[q][r];
+            lb.cnt[q][r] = tc;
+            tc += c;
         }
-        before += (uint32_t)v;
-        if ((v >> 32) == 2u || spins > kLbSpinLimit) break;
+        store_granule(status + (size_t)t * 8 + r, 1u, tc);
     }
-    store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
-    const uint64_t b0 = base_in ? base_in[r] : 0ull;
-    lb.base[r] = (uint32_t)(b0 + before);
-    if (t == ntiles - 1) counts[r] = b0 + before + tc;
+    tc = (uint32_t)__shfl((int)tc, (int)r, 64);
+    uint32_t before = 0, spins = 0;
+    int64_t hi = (int64_t)t - 1;  // the tile at window offset 0
+    bool done = !on;
+    while (__ballot(!done)) {  // wave-uniform: every lane takes part in the ballots and shuffles
+        uint64_t v[kLbPerLane];
+#pragma unroll
+        for (uint32_t i = 0; i < kLbPerLane; ++i) {
+            const int64_t tt = hi - (int64_t)(i * 8u + k);
+            v[i] = 2ull << 32;  // before tile 0: inclusive 0
+            if (!done && tt >= 0) v[i] = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint64_t gi = 0, g0 = 0;  // bit o = window offset o holds an inclusive / an unpublished granule
+#pragma unroll
+        for (uint32_t i = 0; i < kLbPerLane; ++i) {
+            const uint32_t tag = (uint32_t)(v[i] >> 32);
+            gi |= (uint64_t)rank_group_bits(__ballot(tag == 2u), r) << (8u * i);
+            g0 |= (uint64_t)rank_group_bits(__ballot(tag == 0u), r) << (8u * i);
+        }
+        const uint32_t fi = gi ? (uint32_t)__builtin_ctzll(gi) : kLbWindow, f0 = g0 ? (uint32_t)__builtin_ctzll(g0) : kLbWindow;
+        // consume offsets < f0 when a tile before the nearest inclusive is missing, else offsets <= fi (or the window)
+        const uint32_t lim = f0 <= fi ? f0 : min(fi + 1u, kLbWindow);
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kLbPerLane; ++i) s += (!done && i * 8u + k < lim) ? (uint32_t)v[i] : 0u;
+        s += (uint32_t)__shfl_xor((int)s, 8, 64);
+        s += (uint32_t)__shfl_xor((int)s, 16, 64);
+        s += (uint32_t)__shfl_xor((int)s, 32, 64);
+        if (!done) {
+            before += s;
+            hi -= (int64_t)lim;
+            if (fi < f0) {
+                done = true;
+            } else if (f0 == 0u) {
+                if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
+                    if (k == 0) atomicOr(&state[1], 1u);
+                    done = true;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    if (k == 0 && on) {
+        store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
+        const uint64_t b0 = base_in ? base_in[r] : 0ull;
+        lb.base[r] = (uint32_t)(b0 + before);
+        if (t == ntiles - 1) counts[r] = b0 + before + tc;
+    }
 }
 
 // FMT: the record written — 32 = orl_msg_hdr, 16 = orl_wire_msg (*wire_status |= 1 if a message has no 16-B form),
