@@ -809,6 +809,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
         if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
+        // zeroed once: later launches tag their granules with an epoch and number tiles from a host-mirrored ticket
+        if ((e = hipMemset(c->s.lb_state, 0, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMemset(lb_state)");
+        c->s.lb_ticket = 0;
+        c->s.lb_epoch = 0;
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
         if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
             return bail(e, "hipMalloc(col_sums)");

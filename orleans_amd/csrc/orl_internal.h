@@ -236,7 +236,9 @@ struct Scratch {
     uint32_t* seg_meta;     // [ceil(max segments / 64)] chunked segment scan: each chunk's first bucket + shape bits
     uint32_t* bstart;       // [4097] bucket starts (two-level path; k_seg_plan handles up to 4096)
     uint32_t* sstart;       // [4098] first segment of each bucket; [4097] = a bucket has > 64 segments (skew flag)
-    uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile
+    uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile (zeroed once)
+    uint32_t lb_ticket = 0; // host mirror of lb_state's ticket counter after the launches so far (tile = ticket - base)
+    uint32_t lb_epoch = 0;  // launches so far: the granules of launch k carry epoch k (earlier ones read as unpublished)
     uint64_t max_batch;
     uint64_t max_tiles;
 };
@@ -313,7 +315,7 @@ size_t stamp_scan_temp_bytes(size_t n);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
-                            const Scratch& s, void* stream);
+                            Scratch& s, void* stream);
 // Stage 4 alone over already-routed messages (activation handles): histogram + bucket_after_route.
 int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
                        void* stream);

@@ -107,6 +107,7 @@ struct orl_node {
     hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
     hipEvent_t ev_part[2] = {nullptr, nullptr};  // the slot's partition (and heads) are complete
     hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
+    bool last_forward = false;  // the previous batch forwarded messages (hop 2): stage 4 then waits for the counts
     uint8_t* d_ros = nullptr;
     uint8_t* d_send[2] = {nullptr, nullptr};      // hop-1 send regions: nranks x chunk_cap x 32 B per slot
     uint64_t* d_head = nullptr;                   // [2][kHeadWords]
@@ -509,6 +510,12 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         if (e) return nfail(nd, ORL_E_DEVICE, "host rank count launch: %s", hipGetErrorString((hipError_t)e));
         NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
     }
+    // Stage 4 over the owned set is what every batch without forwarding ends with: when the previous batch forwarded
+    // nothing, launch it now, so it runs while the hop-2 counts travel (the all-gather waits on ev_r, recorded before
+    // it).  If some rank does forward after all, the owned-set result is unused (the hop-2 path writes its own
+    // buffers) and costs one stage 4.
+    const bool spec = !nd->last_forward;
+    if (spec) NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
     if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_r)) return r;
     const uint64_t* H = nd->h_heads;
     bool forward = false;
@@ -522,8 +529,9 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     res->n_owned = owned;
     res->n_forwarded = fwd;
     res->n_sent_remote = sent_remote;
+    nd->last_forward = forward;
     if (!forward) {  // every routed message is hosted where it was routed: stage 4 over the owned set
-        NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
+        if (!spec) NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
         res->n_hosted = owned;
         res->route = nd->d_route;
         res->act = nd->d_act;

@@ -2101,8 +2101,12 @@ __device__ __forceinline__ uint32_t rank_group_bits(uint64_t m, uint32_t r) {  /
     return g;
 }
 
+// Granule tag word: epoch << 2 | kind (1 aggregate, 2 inclusive).  A granule of another epoch reads as unpublished, so a
+// state buffer reused launch after launch needs no zeroing when each launch has its own epoch (k_part_lb); epoch 0 with a
+// zeroed buffer is the plain form (k_part_routed).
 __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restrict__ state, uint32_t nranks, uint32_t ntiles,
-                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ base_in = nullptr) {
+                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ base_in,
+                                               uint32_t epoch) {
     if (threadIdx.x >= 64) return;
     uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
     const uint32_t lane = threadIdx.x, r = lane & 7u, k = lane >> 3, t = lb.tile;
@@ -2114,7 +2118,7 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
             lb.cnt[q][r] = tc;
             tc += c;
         }
-        store_granule(status + (size_t)t * 8 + r, 1u, tc);
+        store_granule(status + (size_t)t * 8 + r, (epoch << 2) | 1u, tc);
     }
     tc = (uint32_t)__shfl((int)tc, (int)r, 64);
     uint32_t before = 0, spins = 0;
@@ -2125,13 +2129,13 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
 #pragma unroll
         for (uint32_t i = 0; i < kLbPerLane; ++i) {
             const int64_t tt = hi - (int64_t)(i * 8u + k);
-            v[i] = 2ull << 32;  // before tile 0: inclusive 0
+            v[i] = (uint64_t)((epoch << 2) | 2u) << 32;  // before tile 0: inclusive 0
             if (!done && tt >= 0) v[i] = __hip_atomic_load(status + (size_t)tt * 8 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         uint64_t gi = 0, g0 = 0;  // bit o = window offset o holds an inclusive / an unpublished granule
 #pragma unroll
         for (uint32_t i = 0; i < kLbPerLane; ++i) {
-            const uint32_t tag = (uint32_t)(v[i] >> 32);
+            const uint32_t tw = (uint32_t)(v[i] >> 32), tag = (tw >> 2) == epoch ? (tw & 3u) : 0u;
             gi |= (uint64_t)rank_group_bits(__ballot(tag == 2u), r) << (8u * i);
             g0 |= (uint64_t)rank_group_bits(__ballot(tag == 0u), r) << (8u * i);
         }
@@ -2159,7 +2163,7 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
         }
     }
     if (k == 0 && on) {
-        store_granule(status + (size_t)t * 8 + r, 2u, before + tc);
+        store_granule(status + (size_t)t * 8 + r, (epoch << 2) | 2u, before + tc);
         const uint64_t b0 = base_in ? base_in[r] : 0ull;
         lb.base[r] = (uint32_t)(b0 + before);
         if (t == ntiles - 1) counts[r] = b0 + before + tc;
@@ -2174,13 +2178,14 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
                                                            void* __restrict__ out, uint32_t* __restrict__ src_index,
                                                            uint32_t* __restrict__ state, uint32_t ntiles,
-                                                           uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status) {
+                                                           uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status,
+                                                           uint32_t tbase, uint32_t epoch) {
     __shared__ PartLbSmem sm;
     const uint32_t rflags = rank_flags();
     stage_params(&sm.P, gp);
     sm.rank_of_silo[threadIdx.x] = ros[threadIdx.x];
     if (threadIdx.x < kWaves * 8) (&sm.lb.cnt[0][0])[threadIdx.x] = 0;
-    if (threadIdx.x == 0) sm.lb.tile = atomicAdd(&state[0], 1u);
+    if (threadIdx.x == 0) sm.lb.tile = atomicAdd(&state[0], 1u) - tbase;  // the ticket counter runs on across launches
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t t = sm.lb.tile;
@@ -2209,7 +2214,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
     }
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
-    lookback_ranks(sm.lb, state, nranks, ntiles, counts);
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts, nullptr, epoch);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
@@ -2323,7 +2328,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
     }
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
-    lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in);
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in, 0u);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
@@ -3550,24 +3555,38 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
-                            const Scratch& s, void* stream) {
+                            Scratch& s, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
-    if (e == hipSuccess && fmt != 32) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
+    hipError_t e = hipSuccess;
+    if (fmt != 32) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess && n == 0) e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);  // else the last tile writes them
     if (e != hipSuccess || n == 0) return (int)e;
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
     const uint32_t ntiles = ceil_div(n, kPartTile);
-    // ticket + error word + one 64-B granule row per tile, zeroed before every launch (16-B multiple)
-    e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ntiles * 64, st);
-    if (e != hipSuccess) return (int)e;
+    // look-back state: the ticket counter and the granules are not reset per launch (ticket base + epoch tag instead);
+    // it is zeroed again only when the 30-bit epoch wraps
+    if (++s.lb_epoch >= (1u << 30)) {
+        if ((e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ceil_div(s.max_batch, kPartTile) * 64, st)) != hipSuccess) return (int)e;
+        s.lb_ticket = 0;
+        s.lb_epoch = 1;
+    }
+    const uint32_t tbase = s.lb_ticket, epoch = s.lb_epoch;
 #define ORL_PLB(F) hipLaunchKernelGGL(k_part_lb<F>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in,     \
                                       (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, \
-                                      d_wire_status)
+                                      d_wire_status, tbase, epoch)
     if (fmt == 16) ORL_PLB(16);
     else if (fmt == 8) ORL_PLB(8);
     else ORL_PLB(32);
 #undef ORL_PLB
-    return (int)hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        s.lb_ticket += ntiles;
+    } else {  // the launch did not happen: the device counter did not move either; start over from a zeroed state
+        (void)hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ceil_div(s.max_batch, kPartTile) * 64, st);
+        s.lb_ticket = 0;
+        s.lb_epoch = 0;
+    }
+    return (int)e;
 }
 
 }  // namespace orl
