@@ -534,6 +534,13 @@ __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ 
 // slower: profiles/r01_route_variants.txt.)  The probe chain is continued by a flag loop in the same
 // basic block as the first probe (an early-return helper loop for the chain cost 13 %: 1.76 vs 1.56 ms).
 // HB: capacity of the fused digit histogram in bits (0: none; 11 or 12 so the LDS is sized for the digit).
+// k_route's outputs: write-through stores that drop the line from the XCD's L2 (sc1; MI355X_MICROARCH.md, the stores
+// row), so the 512 MB of route/act words a config-2 batch writes do not displace probe-table lines; the stores are
+// whole 256-B wave runs.  Route kernel 1.294 -> 1.283 ms at config 2 (two A/B repeats, same box).
+__device__ __forceinline__ void store_drop(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int HB>
 struct RouteSmem {
     RouteParams P;
@@ -601,8 +608,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 uint32_t act = ORL_NO_ACT, rr = r;
                 if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
-                route[e] = rr;
-                act_out[e] = act;
+                store_drop(route + e, rr);
+                store_drop(act_out + e, act);
                 if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
             }
             continue;
@@ -631,8 +638,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 uint32_t act = ORL_NO_ACT, rr = r;
                 if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
-                route[e] = rr;
-                act_out[e] = act;
+                store_drop(route + e, rr);
+                store_drop(act_out + e, act);
                 if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
             }
             continue;
@@ -661,8 +668,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         if (e < n) {
             uint32_t act = ORL_NO_ACT, rr = r;
             if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
-            route[e] = rr;
-            act_out[e] = act;
+            store_drop(route + e, rr);
+            store_drop(act_out + e, act);
             if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
         }
     }
