@@ -187,8 +187,11 @@ inline BucketPlan make_bucket_plan(uint32_t max_key) {
     if (total == 0) total = 1;
     BucketPlan p{};
     p.two_level = total <= 2 * (int)kMaxDigitBits;
-    static const bool lb_floor = [] { const char* e = getenv("ORL_LB_FLOOR"); return e && e[0] == '1'; }();
-    p.lb = total <= (int)kMaxDigitBits ? total : lb_floor ? total / 2 : (total + 1) / 2;  // 20 bits: 10 + 10
+    // an odd width gives the extra bit to the MSD digit (21 bits: 11 + 10): the hot rank of config 3 at 8 ranks buckets in
+    // 0.84 vs 0.89 ms and the median rank in 0.51 vs 0.55 ms (scripts/rank_cost_lab.py, two repeats); 20 bits stays 10 + 10
+    // (9 + 11: 0.89 ms, 11 + 9: 0.78 ms vs 0.69 ms at config 2).  ORL_LB_CEIL=1: the extra bit to level 2 (A/B).
+    static const bool lb_ceil = [] { const char* e = getenv("ORL_LB_CEIL"); return e && e[0] == '1'; }();
+    p.lb = total <= (int)kMaxDigitBits ? total : lb_ceil ? (total + 1) / 2 : total / 2;  // 20 bits: 10 + 10
     // (23-24-bit keys as 12 + 12 measured 2.82 ms vs 1.57 ms for 3 LSD passes at config 3: Zipf-hot digits
     // serialise the rank atomics and 4096 bins per 4096-message segment make the column work dominate)
     p.hb = total - p.lb;
