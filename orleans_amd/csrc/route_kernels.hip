@@ -1045,12 +1045,25 @@ __device__ __forceinline__ void round_starts(uint32_t (*cnt)[(1u << BITS) / 2u],
     }
 }
 
+// Workgroups per CU of the LDS-staged scatter kernels: 3 measured best.  At 11 bits the aliased deltas (below) bring the
+// LDS from 56 to 48 KB, 2 -> 3 workgroups per CU (hot rank of config 3 at 8 ranks: stage 4 0.84 -> 0.75 ms); at 10 bits
+// the same saving would allow 4 per CU, which made config 2's stage 4 slower (0.69 -> 0.78 ms: more scattered partial
+// lines in flight per L2), so 10-bit digits keep their LDS above a quarter of the CU's 160 KB (narrower LSD digits keep
+// the occupancy they had).
+constexpr uint32_t kScatterLdsFloor = 160u * 1024u / 4u + 16u;
+
 template <int BITS, int ITEMS>
-struct PassSmem {
-    uint32_t cnt[kWaves][(1u << BITS) / 2u];  // packed per-wave running counts, then per-(wave, bin) tile-local starts
-    uint32_t delta[1u << BITS];               // global base - tile-local start, per bin
+struct PassSmemCore {
+    // packed per-wave running counts, then per-(wave, bin) tile-local starts, then (after the LDS scatter) the per-bin
+    // delta = global base - tile-local start: 2^BITS words of the 2 * 2^BITS, so no array of its own
+    uint32_t cnt[kWaves][(1u << BITS) / 2u];
     uint2 stage[256 * ITEMS];  // {key, index}: one 8-B LDS write per element (half the conflicted scatter instructions)
-    uint32_t wsum[kWaves];
+};
+
+template <int BITS, int ITEMS>
+struct PassSmem : PassSmemCore<BITS, ITEMS> {
+    static constexpr uint32_t kCore = sizeof(PassSmemCore<BITS, ITEMS>);
+    uint8_t pad[BITS == 10 && kCore < kScatterLdsFloor ? kScatterLdsFloor - kCore : 4];  // 10 bits: <= 3 per CU
 };
 
 // ITEMS: elements per thread; the tile is 256 * ITEMS (the MSD pass of the two-level path takes kMsdItems: half the
@@ -1098,12 +1111,12 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
     // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
     const uint32_t* orow = tile_off + (size_t)tile * row_step * B;
-    uint32_t tot[PER], start[PER];
-    round_starts<BITS>(sm.cnt, sm.wsum, tot, start);
+    uint32_t tot[PER], start[PER], dl[PER];
+    round_starts<BITS>(sm.cnt, reinterpret_cast<uint32_t*>(&sm.stage[0]), tot, start);  // the scan's wave sums: stage is free here
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t b = threadIdx.x * PER + q;
-        if (b < B) sm.delta[b] = orow[b] - start[q];
+        dl[q] = b < B ? orow[b] - start[q] : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -1115,6 +1128,11 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         }
     }
     __syncthreads();
+    uint32_t* delta = &sm.cnt[0][0];  // the starts are consumed: the bins' deltas take their place
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q)
+        if (threadIdx.x * PER + q < B) delta[threadIdx.x * PER + q] = dl[q];
+    __syncthreads();
     const uint32_t cnt = (n - tbase) < TILE ? (n - tbase) : TILE;
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
@@ -1122,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         if (i < cnt) {
             const uint2 kv = sm.stage[i];
             const uint32_t k = kv.x;
-            const uint32_t g = sm.delta[(k >> shift) & (B - 1u)] + i;
+            const uint32_t g = delta[(k >> shift) & (B - 1u)] + i;
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = kv;
@@ -1628,11 +1646,15 @@ __global__ __launch_bounds__(256) void k_seg_carry(const uint32_t* __restrict__ 
 // digit l = offsets[b << lb | l] + (segment base inside the bucket) + (earlier rounds) + i - (round-local
 // start of l).  The running part lives in registers of the thread owning digit l.
 template <int LB>
-struct SegSmem {
-    uint32_t cnt[kWaves][(1u << LB) / 2u];  // packed (wave_rank)
-    uint32_t delta[1u << LB];
+struct SegSmemCore {
+    uint32_t cnt[kWaves][(1u << LB) / 2u];  // packed (wave_rank), then the per-digit deltas of the write-out (as PassSmem)
     uint2 stage[kSegChunk];  // {digit, index}
-    uint32_t wsum[kWaves];
+};
+
+template <int LB>
+struct SegSmem : SegSmemCore<LB> {
+    static constexpr uint32_t kCore = sizeof(SegSmemCore<LB>);
+    uint8_t pad[LB == 10 && kCore < kScatterLdsFloor ? kScatterLdsFloor - kCore : 4];  // 10 bits: <= 3 per CU
 };
 
 template <int LB, int IN, int RM>
@@ -1681,15 +1703,13 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             rank_steps<LB, true, kItems, RM>(&sm.cnt[w][0], dg, r.hi > wbase ? r.hi - wbase : 0u, rank, rflags);
         }
         __syncthreads();
-        uint32_t tot[PER], start[PER];
-        round_starts<LB>(sm.cnt, sm.wsum, tot, start);
+        uint32_t tot[PER], start[PER], dl[PER];
+        round_starts<LB>(sm.cnt, reinterpret_cast<uint32_t*>(&sm.stage[0]), tot, start);  // wave sums in the free stage (40 KB total)
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t l = threadIdx.x * PER + q;
-            if (l < BL) {
-                sm.delta[l] = run[q] - start[q];
-                run[q] += tot[q];
-            }
+            dl[q] = run[q] - start[q];
+            if (l < BL) run[q] += tot[q];
         }
         __syncthreads();
 #pragma unroll
@@ -1701,13 +1721,18 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             }
         }
         __syncthreads();
+        uint32_t* delta = &sm.cnt[0][0];  // the starts are consumed: the digits' deltas take their place
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q)
+            if (threadIdx.x * PER + q < BL) delta[threadIdx.x * PER + q] = dl[q];
+        __syncthreads();
         const uint32_t cnt = min(r.hi - c0, kSegChunk);
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t i = j * 256u + threadIdx.x;
             if (i < cnt) {
                 const uint2 dv = sm.stage[i];
-                const uint32_t g = sm.delta[dv.x] + i;
+                const uint32_t g = delta[dv.x] + i;
                 if (g < n) order[g] = dv.y;  // always true with consistent counts; bounds a corrupt input
             }
         }

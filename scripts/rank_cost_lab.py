@@ -35,6 +35,9 @@ def timed(fn, reps=5):
 
 
 def main(R=8, chunks=4, width=8):
+    import os
+    if os.environ.get("LAB_LIB"):  # A/B: an experimental build of the library
+        L.LIB_PATH = os.path.abspath(os.environ["LAB_LIB"])
     n_grains, n_total = 16_000_000, 256 << 20
     n_msgs = n_total // R
     cl = W.balanced_cluster()
@@ -77,7 +80,11 @@ def main(R=8, chunks=4, width=8):
     print(f"owned per rank (M): {[round(x / 2**20, 1) for x in owned]}, max/mean {owned.max() / owned.mean():.2f}",
           flush=True)
     order = np.argsort(owned)
-    for label, r in (("hottest", int(order[-1])), ("median", int(order[R // 2]))):
+    import os
+    which = (("hottest", int(order[-1])), ("median", int(order[R // 2])))
+    if os.environ.get("LAB_ONLY"):  # e.g. LAB_ONLY=hottest under rocprofv3: one rank's kernels only
+        which = tuple(w for w in which if w[0] == os.environ["LAB_ONLY"])
+    for label, r in which:
         recs = torch.cat(recv[r])
         n = recs.numel() // width
         mine = local_silos(cl.n_silos, R, r)
