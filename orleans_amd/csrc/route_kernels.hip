@@ -2283,7 +2283,10 @@ __device__ __forceinline__ uint32_t host_rank(const uint8_t* ros, uint32_t route
     return host == 0xFFu ? my_rank : ros[host];
 }
 
-// Per-rank message counts by host rank of routed messages (u64 counts[8], accumulated: zero them first).
+// Per-rank message counts by host rank of routed messages (u64 counts[8], accumulated: zero them first).  Each thread
+// takes 16 consecutive route words per step as four 16-B loads, all in flight together (one 4-B load per step left the
+// grid-stride loop latency-bound: ~66 us per 32M words, scripts/rank_cost_lab.py's node profile).  Per-thread counts are
+// packed as 8-bit fields (<= 16 per step) and unpacked every step.
 __global__ __launch_bounds__(256) void k_host_rank_count(const uint32_t* __restrict__ route, uint32_t n,
                                                          const uint8_t* __restrict__ ros, uint32_t my_rank,
                                                          unsigned long long* __restrict__ counts) {
@@ -2293,7 +2296,24 @@ __global__ __launch_bounds__(256) void k_host_rank_count(const uint32_t* __restr
     if (threadIdx.x < 8) h[threadIdx.x] = 0;
     __syncthreads();
     uint32_t mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t n16 = n / 16u;  // whole 16-word groups; the tail below
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < n16; g += gridDim.x * 256u) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(route) + (size_t)g * 4u;
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) v[q] = __builtin_nontemporal_load(p + q);
+        uint64_t pk = 0;  // 8-bit count per host rank
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            pk += 1ull << (8u * host_rank(r, v[q].x, my_rank));
+            pk += 1ull << (8u * host_rank(r, v[q].y, my_rank));
+            pk += 1ull << (8u * host_rank(r, v[q].z, my_rank));
+            pk += 1ull << (8u * host_rank(r, v[q].w, my_rank));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) mine[k] += (uint32_t)(pk >> (8u * k)) & 0xFFu;
+    }
+    for (uint32_t i = n16 * 16u + blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint32_t d = host_rank(r, route[i], my_rank);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) mine[k] += d == k ? 1u : 0u;
