@@ -235,9 +235,6 @@ struct orl_ctx {
     RouteParams* d_params = nullptr;
     bool params_dirty = true;
     uint8_t* d_rank_of_silo = nullptr;
-    const uint8_t* hc_ros = nullptr;       // host-rank count sink of route launches (set by orl_node for hop 2)
-    uint32_t hc_me = 0;
-    unsigned long long* hc_slots = nullptr;
     uint8_t h_rank_of_silo[256] = {};  // last uploaded rank_of_silo (uploads only on change: no per-batch sync)
     bool ros_valid = false;
     Scratch s{};
@@ -283,12 +280,6 @@ struct orl_ctx {
     std::vector<hipEvent_t> tev;
     uint32_t tcount = 0;
 };
-
-void orl::ctx_set_host_count_sink(orl_ctx* c, const uint8_t* d_ros, uint32_t me, uint64_t* d_slots) {
-    c->hc_ros = d_ros;
-    c->hc_me = me;
-    c->hc_slots = reinterpret_cast<unsigned long long*>(d_slots);
-}
 
 const uint64_t* orl::ctx_wire_tcd(const orl_ctx* c) {
     if (!c || !c->d_params) return nullptr;
@@ -616,7 +607,7 @@ int sync_device_state(orl_ctx* c) {
 DirView dir_view(const orl_ctx* c) {
     return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
                    (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr,
-                   c->probe8_valid ? c->d_probe8 : nullptr, c->hc_ros, c->hc_me, c->hc_slots};
+                   c->probe8_valid ? c->d_probe8 : nullptr};
 }
 
 // After a device mutation of the partition: the probe table no longer mirrors it.  When it held a type list,

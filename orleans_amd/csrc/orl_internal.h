@@ -220,11 +220,6 @@ struct DirView {
     const ProbeSlot* probe = nullptr;
     const uint32_t* probe_bad = nullptr;  // device-built probe table: nonzero = a key did not fit, probe `dir`
     const void* probe8 = nullptr;         // 8-B form of `probe` ({u32 key, u32 value} pairs) when the keys fit it
-    // node hop 2 (orl_node): while set, route launches also count their messages by host rank (rank_of_silo[host silo],
-    // `hc_me` for messages without one) into hc_slots[64][8] (slot = workgroup % 64)
-    const uint8_t* hc_ros = nullptr;
-    uint32_t hc_me = 0;
-    unsigned long long* hc_slots = nullptr;
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
@@ -340,11 +335,6 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
                        const uint64_t* d_wire_tcd, void* stream);
 // Device address of a context's wire types (RouteParams::wire_tcd), current once a route or partition call synced state.
 const uint64_t* ctx_wire_tcd(const orl_ctx* c);
-// Host-rank count sink of the context's route launches (DirView::hc_*); d_slots = nullptr turns it off.
-void ctx_set_host_count_sink(orl_ctx* c, const uint8_t* d_ros, uint32_t me, uint64_t* d_slots);
-// counts[8] = the sum of the 64 slots' counts (zeroes nothing: the slots are cleared by the caller before a batch).
-int launch_host_slots_reduce(const uint64_t* d_slots, uint64_t* d_counts, void* stream);
-constexpr uint32_t kHostCountSlots = 64;
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

@@ -119,7 +119,6 @@ struct orl_node {
     uint8_t* d_recv = nullptr;                    // owned records, chunk after chunk (max_recv x 32 B)
     uint32_t *d_route = nullptr, *d_act = nullptr, *d_order = nullptr, *d_off = nullptr;
     uint64_t* d_hcount = nullptr;                 // [8] hop-2 counts by host rank
-    uint64_t* d_hslots = nullptr;                 // [kHostCountSlots][8] the route launches' host-rank counts
     // hop 2 (allocated on first use)
     uint64_t f_cap = 0;
     uint8_t* d_fsend = nullptr;
@@ -240,7 +239,7 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
 void free_node(orl_node* nd) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(nd->d_ros); f(nd->d_send[0]); f(nd->d_send[1]); f(nd->d_head); f(nd->d_heads); f(nd->d_recv); f(nd->d_route); f(nd->d_act);
-    f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_hslots); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
+    f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
     f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts); f(nd->d_fan);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     if (nd->h_form) (void)hipHostFree(nd->h_form);
@@ -343,7 +342,6 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipMalloc((void**)&nd->d_order, mr * 4));
     ok(hipMalloc((void**)&nd->d_off, ((size_t)nd->n_act + 2) * 4));
     ok(hipMalloc((void**)&nd->d_hcount, 16 * 8));
-    ok(hipMalloc((void**)&nd->d_hslots, kHostCountSlots * 8 * 8));
     if (e != hipSuccess) return bail(ORL_E_NOMEM);
     // head words no call writes (counts past nranks, [10, 16)) travel with the all-gathers: keep them zero
     ok(hipMemset(nd->d_head, 0, 2 * kHeadWords * 8));
@@ -408,13 +406,6 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     NODE_HIP(nd, hipEventRecord(nd->ev_in, caller));  // the caller's batch is ready
     NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_in, 0));
     nd->segs.clear();
-    // hop 2's host-rank counts come from the owner's route launches (k_route counts into d_hslots while the sink is set)
-    NODE_HIP(nd, hipMemsetAsync(nd->d_hslots, 0, kHostCountSlots * 8 * 8, nd->sr));
-    ctx_set_host_count_sink(nd->ctx, nd->d_ros, me, nd->d_hslots);
-    struct SinkOff {  // no return path leaves the context counting into this node's slots
-        orl_ctx* c;
-        ~SinkOff() { ctx_set_host_count_sink(c, nullptr, 0, nullptr); }
-    } sink_off{nd->ctx};
     const uint64_t cs = (n + K - 1) / K;
     uint64_t owned = 0;                       // messages received so far (this rank)
     uint64_t owned_bytes = 0;
@@ -527,9 +518,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         owned_bytes += got * width;
     }
     // ---- hop 2: does any rank host activations of messages another rank owns? -----------------------------------
-    ctx_set_host_count_sink(nd->ctx, nullptr, 0, nullptr);
     {
-        int e = launch_host_slots_reduce(nd->d_hslots, nd->d_hcount, nd->sr);
+        int e = launch_host_rank_count(nd->d_route, owned, nd->d_ros, me, nd->d_hcount, nd->sr);
         if (e) return nfail(nd, ORL_E_DEVICE, "host rank count launch: %s", hipGetErrorString((hipError_t)e));
         NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
     }

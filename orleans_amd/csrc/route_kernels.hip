@@ -545,16 +545,7 @@ template <int HB>
 struct RouteSmem {
     RouteParams P;
     uint32_t hist[HB ? (1u << HB) : 1u];
-    uint8_t ros[256];  // host-rank count (hc_slots != nullptr): rank of each silo
-    uint32_t hc[8];
 };
-
-// Host rank of a routed message for the node's hop-2 counts (orl_node): the activation's silo's rank, or this rank
-// when the message has no host.
-__device__ __forceinline__ uint32_t route_host_rank(const uint8_t* ros, uint32_t route, uint32_t me) {
-    const uint32_t host = ORL_ROUTE_HOST(route);
-    return host == 0xFFu ? me : ros[host];
-}
 
 // FMT: the input is orl_msg_hdr (32), or exchange records: orl_wire_msg (16) or orl_wire8 (8, decoded with the
 // context's wire types).
@@ -575,20 +566,13 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
-                                                         uint32_t bins, uint32_t shift, uint32_t items,
-                                                         const uint8_t* __restrict__ hc_ros, uint32_t hc_me,
-                                                         unsigned long long* __restrict__ hc_slots) {
+                                                         uint32_t bins, uint32_t shift, uint32_t items) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
-    if (hc_slots) {
-        sm.ros[threadIdx.x] = hc_ros[threadIdx.x];
-        if (threadIdx.x < 8) sm.hc[threadIdx.x] = 0;
-    }
     __syncthreads();
-    uint64_t hpk = 0;  // this thread's host-rank counts, 8 bits per rank (items <= 16 messages per thread)
     const uint32_t n_act = sm.P.n_act;
     const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
@@ -626,7 +610,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
-                if (hc_slots) hpk += 1ull << (8u * route_host_rank(sm.ros, rr, hc_me));
                 if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
             }
             continue;
@@ -657,7 +640,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
-                if (hc_slots) hpk += 1ull << (8u * route_host_rank(sm.ros, rr, hc_me));
                 if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
             }
             continue;
@@ -688,34 +670,14 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
             store_drop(route + e, rr);
             store_drop(act_out + e, act);
-            if (hc_slots) hpk += 1ull << (8u * route_host_rank(sm.ros, rr, hc_me));
             if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
         }
-    }
-    if (hc_slots) {  // wave sums -> LDS -> one slot of 8 device counters per workgroup (64 slots spread the atomics)
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            uint32_t v = (uint32_t)(hpk >> (8u * k)) & 0xFFu;
-            for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if ((threadIdx.x & 63u) == 0 && v) atomicAdd(&sm.hc[k], v);
-        }
-        __syncthreads();
-        if (threadIdx.x < 8 && sm.hc[threadIdx.x])
-            atomicAdd(hc_slots + (blockIdx.x % kHostCountSlots) * 8u + threadIdx.x, (unsigned long long)sm.hc[threadIdx.x]);
     }
     if (HIST) {
         __syncthreads();
         uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
     }
-}
-
-__global__ __launch_bounds__(64) void k_host_slots_reduce(const unsigned long long* __restrict__ slots,
-                                                          unsigned long long* __restrict__ counts) {
-    if (threadIdx.x >= 8) return;
-    unsigned long long t = 0;
-    for (uint32_t s = 0; s < kHostCountSlots; ++s) t += slots[s * 8u + threadIdx.x];
-    counts[threadIdx.x] = t;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -3339,14 +3301,13 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
-                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, dv.hc_ros, dv.hc_me,   \
-                                              dv.hc_slots)
+                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
-                                            shift, items, dv.hc_ros, dv.hc_me, dv.hc_slots)
+                                            shift, items)
         if (hist) {
             if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
         } else {
@@ -3616,12 +3577,6 @@ int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_r
     const uint32_t g = std::min<uint32_t>(ceil_div(n, 256 * 16), 2048);
     hipLaunchKernelGGL(k_host_rank_count, dim3(g), dim3(256), 0, st, d_route, (uint32_t)n, d_ros, my_rank,
                        reinterpret_cast<unsigned long long*>(d_counts));
-    return (int)hipGetLastError();
-}
-
-int launch_host_slots_reduce(const uint64_t* d_slots, uint64_t* d_counts, void* stream) {
-    hipLaunchKernelGGL(k_host_slots_reduce, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                       reinterpret_cast<const unsigned long long*>(d_slots), reinterpret_cast<unsigned long long*>(d_counts));
     return (int)hipGetLastError();
 }
 
