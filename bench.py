@@ -74,9 +74,6 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--wire16", action="store_true",
                     help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
-    ap.add_argument("--router", action="store_true",
-                    help="configs 2/3 at N=1: go through the pipelined multi-GPU router (partition + routing on two "
-                         "streams; exercises the N>1 code path on one GPU)")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "route_kernel_pmc.json"))
     args = ap.parse_args()
@@ -164,7 +161,7 @@ def read_traffic(path, msgs_per_launch, world):
 def run_single_target(args, torch, dist, rank, world, local_rank):
     from orleans_amd import workloads as W
     from orleans_amd.engine import GrainDirectoryEngine
-    from orleans_amd.node import GrainNode, HipExecutor, PipelinedRouter, local_silos, rank_of_silo
+    from orleans_amd.node import GrainNode, local_silos, rank_of_silo
 
     zipf = args.config == 3
     n_grains = args.grains or (16_000_000 if zipf else 1_000_000)
@@ -185,11 +182,11 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     d_msgs = W.device_messages(torch, cl, n_grains, n_msgs, seed, start=rank * n_msgs,
                                sender_silos=mine if world > 1 else None, zipf=ztab)
     torch.cuda.synchronize()
-    node = part_eng = None
+    node = None
     cap = n_msgs
     local_mask = None
     n_act = n_grains
-    if world > 1 or args.router:
+    if world > 1:
         # receive capacity: every rank's per-destination counts, summed over ranks (Zipf: the hot owners get more)
         d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
         d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
@@ -216,7 +213,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     stats = {}
     if args.host_io:
         return run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains)
-    if world == 1 and not args.router:
+    if world == 1:
         route = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         act = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
         order = torch.empty(n_msgs, dtype=torch.int32, device="cuda")
@@ -225,7 +222,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         def step():
             eng.address_messages_device(d_msgs, n_msgs, route, act, order, offsets, stream=stream)
             return n_msgs
-    elif world > 1 and not args.router:
+    else:
         # the node exchange behind the C ABI: owner partition, counts all-gather, grouped send/recv over RCCL, routing
         # at the owner, hop 2 when activations live elsewhere, stage 4 at the host (orl_node_route_batch_device)
         gid = torch.zeros(L_NODE_ID_BYTES, dtype=torch.uint8, device="cuda")
@@ -242,16 +239,6 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
             stats["fwd"] = stats.get("fwd", 0) + res.n_forwarded
             stats.setdefault("widths", set()).update(w for _, c, w in res.segments if c)
             return res.n_owned
-    else:
-        # the Python torch.distributed reference protocol (orleans_amd/node.py PipelinedRouter), two batches in flight
-        part_eng = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=cap, device=local_rank)
-        W.setup_engine(part_eng, cl, local_silos=mine if world > 1 else None)
-        router = PipelinedRouter(HipExecutor(eng, cap, torch, part_eng=part_eng, slots=2, nranks=world,
-                                             part_capacity=n_msgs), rank, world, ros, cap, torch)
-
-        def step():  # partition + exchange this batch, route the previous one (two batches in flight)
-            res = router.submit(d_msgs, n_msgs)
-            return 0 if res is None else res.n_recv
     log(f"setup {time.perf_counter() - t_setup:.1f}s; warmup {args.warmup}")
     eng.set_timing(False)
 
@@ -259,7 +246,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         eng.sync()
 
     # timing events are enabled after warmup so the summary covers the timed steps only
-    for _ in range(max(args.warmup, 1 if (world > 1 or args.router) else 0)):  # the router's first step fills its pipeline
+    for _ in range(max(args.warmup, 1 if world > 1 else 0)):  # the node's first step allocates its buffers
         step()
     sync()
     torch.cuda.synchronize()
@@ -273,7 +260,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     # route kernel launches per step: 1 (one GPU), or one per received chunk (node)
     launches = max(1, nb // args.steps)
     per_launch_msgs = recv_total / args.steps / launches
-    wire = node is not None or args.router
+    wire = node is not None
     rec_w = max(stats.get("widths") or {16 if wire else 32})  # the exchange record the owner's route kernel reads
     kbytes = ROUTE_KERNEL_BYTES_PER_MSG - (32 - rec_w)  # 8-B / 16-B exchange records instead of 32-B headers
     achieved = kbytes * per_launch_msgs / (route_ms * 1e-3) / 1e9
@@ -286,16 +273,13 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     if node is not None:
         node.close()
     eng.close()
-    if part_eng is not None:
-        part_eng.close()
-    name = (f"config3: Zipf(1.1) over {n_grains >> 20}M long-key grains, {n_total >> 20}M messages in total "
+    name = (f"config3: Zipf(1.1) over {n_grains / 1e6:g}M long-key grains, {n_total >> 20}M messages in total "
             f"({n_msgs >> 20}M per GPU)" if zipf else
             f"config2: uniform {n_grains // 1_000_000}M long-key grains, {n_msgs >> 20}M single-target messages per GPU")
     name += ", 8-silo ring, stages 1-4"
     if world > 1:
         name += (", + owner partition, RCCL counts all-gather + grouped send/recv, routing at the owner, hop 2, "
-                 f"stage 4 at the host (orl_node, {args.chunks} chunks)" if node is not None else
-                 ", + Python torch.distributed exchange (PipelinedRouter)")
+                 f"stage 4 at the host (orl_node, {args.chunks} chunks)")
     out = {
         "metric": "routed grain messages/sec (node)",
         "value": value,

@@ -452,7 +452,13 @@ int orl_partition_by_owner_padded_device(orl_ctx* ctx, const orl_msg_hdr* d_in, 
                                          orl_msg_hdr* d_out, uint32_t* d_src_index, uint64_t* d_counts, void* stream);
 /* As orl_partition_by_owner_padded_device, writing 16-byte orl_wire_msg records (half the exchange
  * bytes).  *d_status (device u32) is set to 0, or to 1 if some message of the batch has no compact form
- * (then the records are invalid and the caller uses the 32-byte form for this batch). */
+ * (then the records are invalid and the caller uses the 32-byte form for this batch); | ORL_PART_LOOKBACK_FAILED when the
+ * partition's decoupled look-back gave up waiting on an earlier tile (record positions and counts invalid: a device
+ * fault, not a property of the batch).
+ * Every one-pass partition of a context (orl_partition_*_padded/compact/narrow_device) must be enqueued on ONE stream:
+ * the look-back state is reused launch after launch (tile tickets and epochs are mirrored on the host).  A look-back
+ * failure of the 32-byte form, which has no status word, is reported by orl_ctx_query(ORL_Q_PART_ERROR). */
+#define ORL_PART_LOOKBACK_FAILED 0x4u
 int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                                  const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
                                  orl_wire_msg* d_out, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_status,
@@ -560,8 +566,17 @@ int orl_node_unique_id(uint8_t id[ORL_NODE_ID_BYTES]);
 int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out);
 int orl_node_destroy(orl_node* node);
 const char* orl_node_last_error(const orl_node* node);
+/* Deadline of every host wait of the exchange, in ms (> 0).  Every rank should use the same value. */
+int orl_node_set_timeout(orl_node* node, uint32_t ms);
 /* One batch (device headers, n <= max_batch).  The outputs are complete on `stream` when the call returns (the call
- * waits on the host for each chunk's counts; the routing work may still run). */
+ * waits on the host for each chunk's counts; the routing work may still run).
+ * Failure is collective and bounded: every host wait of the exchange (the counts all-gathers, the hop-2 exchange, the
+ * LOCAL transport's barriers) has a deadline (orl_node_set_timeout; default 120 s, ORL_NODE_TIMEOUT_MS overrides) and
+ * RCCL's asynchronous error is polled while waiting.  A rank that misses it, or sees an RCCL error, aborts the
+ * communicator (ncclCommAbort) and returns ORL_E_STATE, naming the chunk and the head words it saw in
+ * orl_node_last_error; the node is then broken (every later batch returns ORL_E_STATE; destroy it and build a new one).
+ * A partition look-back failure on any rank (ORL_PART_LOOKBACK_FAILED, carried in the all-gathered status words) makes
+ * every rank return ORL_E_DEVICE for that chunk. */
 int orl_node_route_batch_device(orl_node* node, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* out,
                                 void* stream);
 /* A multicast batch across the node (config 4 sharded by publisher): every rank expands its own publishes
@@ -572,8 +587,42 @@ int orl_node_fanout_batch_device(orl_node* node, const uint64_t* d_csr_off, cons
                                  const uint8_t* d_pub_silo, size_t n_pub, uint32_t opts, uint64_t* d_pub_offsets,
                                  uint64_t* total, orl_node_result* out, void* stream);
 /* Record segment i of the last batch's hosted messages: device pointer, message count, record width (8 = orl_wire8 in
- * the context's wire types, 16 = orl_wire_msg, 32 = orl_msg_hdr). */
+ * the context's wire types, 16 = orl_wire_msg, 32 = orl_msg_hdr).  Segments start 32-byte aligned. */
 int orl_node_segment(const orl_node* node, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width);
+
+/* The protocol's host decisions, as orl_node_route_batch_device takes them after each all-gather: exposed for hosts that
+ * run the exchange over a transport of their own (orl_partition_*_padded/compact/narrow_device, the route entry points,
+ * orl_bucket_device + these two), and for the multi-process CPU tests.  ORL_NODE_HEAD_WORDS u64 per rank are
+ * all-gathered before each exchange.  Hop 1 (one per chunk): [0, nranks) records for each destination rank, [8] the
+ * partition status word (bit 0 = a message lacks the 16-B form, bit 1 = lacks the 8-B form, ORL_PART_LOOKBACK_FAILED),
+ * [9] the record width the rank wrote (bits 56-63: 8 / 16 / 32) | its wire-type digest (bits 0-55, ORL_Q_WIRE_DIGEST),
+ * the rest zero.  Hop 2: [0, nranks) routed messages whose activation each rank hosts (ORL_ROUTE_HOST's rank; no host:
+ * the owner), the rest zero.  heads = nranks x ORL_NODE_HEAD_WORDS words in rank order. */
+#define ORL_NODE_HEAD_WORDS 16u
+typedef struct orl_node_chunk_plan {
+    uint32_t width;                      /* every rank exchanges the chunk in this record width: 8, 16 or 32 */
+    uint32_t rewrite;                    /* this rank wrote another width: partition the chunk again in `width` */
+    uint64_t send[ORL_NODE_MAX_RANKS];   /* records to each rank */
+    uint64_t recv[ORL_NODE_MAX_RANKS];   /* records from each rank, received back to back in rank order */
+    uint64_t n_recv;
+} orl_node_chunk_plan;
+/* written = the width this rank partitioned the chunk in; owned_total[nranks] = every rank's receive total over the
+ * batch's earlier chunks (zero before chunk 0; updated).  ORL_E_CAPACITY when a rank would own more than max_recv and
+ * ORL_E_DEVICE when a rank's partition look-back failed: every rank gets the same result. */
+int orl_node_plan_chunk(const uint64_t* heads, uint32_t nranks, uint32_t me, uint32_t written, uint64_t max_recv,
+                        uint64_t* owned_total, orl_node_chunk_plan* out);
+typedef struct orl_node_hop2_plan {
+    uint32_t forward;                    /* 1 if any rank forwards messages (else every rank buckets its owned set) */
+    uint32_t width;                      /* record width of a forwarded set */
+    uint64_t send[ORL_NODE_MAX_RANKS];   /* forwarded {record, route word, activation} to each rank (own: kept) */
+    uint64_t recv[ORL_NODE_MAX_RANKS];
+    uint64_t n_hosted;                   /* messages this rank buckets */
+    uint64_t n_forwarded;                /* of its owned set, sent to another rank */
+} orl_node_hop2_plan;
+/* n_owned = this rank's owned (routed) messages; width_mask = the widths of its owned segments (bit 0 = 8, 1 = 16,
+ * 2 = 32).  ORL_E_CAPACITY (on every rank) when a rank would host more than max_recv. */
+int orl_node_plan_hop2(const uint64_t* heads, uint32_t nranks, uint32_t me, uint64_t n_owned, uint32_t width_mask,
+                       uint64_t max_recv, orl_node_hop2_plan* out);
 
 int orl_sync(orl_ctx* ctx);
 
@@ -595,6 +644,8 @@ int orl_sync(orl_ctx* ctx);
 #define ORL_Q_RANK_MODE 7u    /* stage-4 stable ranking on this device: bit 0 = ballot match (else LDS atomics), bit 1 = the
                                  lane-order self-check failed (ballot forced) */
 #define ORL_Q_WIRE_DIGEST 8u  /* FNV-1a digest of the wire types (orl_wire_types_set), 0 when the 8-B form is off */
+#define ORL_Q_PART_ERROR 9u   /* 1 if a one-pass partition's look-back gave up since the last query (read and cleared;
+                                 synchronises the context's device) */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 /* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
  * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */

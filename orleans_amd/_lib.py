@@ -60,7 +60,9 @@ MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_U
 
 Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_RANK_MODE = 1, 2, 3, 4, 5, 6, 7
 Q_WIRE_DIGEST = 8
+Q_PART_ERROR = 9
 MAX_WIRE_TYPES = 16
+PART_LOOKBACK_FAILED = 0x4
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -81,6 +83,7 @@ TRANSPORT_RCCL, TRANSPORT_LOCAL = 0, 1
 NODE_WIDE_ONLY = 0x1
 NODE_MAX_RANKS = 8
 NODE_MAX_CHUNKS = 16
+NODE_HEAD_WORDS = 16
 
 
 class orl_node_config(C.Structure):
@@ -93,6 +96,16 @@ class orl_node_result(C.Structure):
     _fields_ = [("n_owned", C.c_uint64), ("n_hosted", C.c_uint64), ("n_forwarded", C.c_uint64),
                 ("n_sent_remote", C.c_uint64), ("hop2", C.c_uint32), ("n_segments", C.c_uint32), ("route", C.c_void_p),
                 ("act", C.c_void_p), ("order", C.c_void_p), ("bucket_offsets", C.c_void_p)]
+
+
+class orl_node_chunk_plan(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("rewrite", C.c_uint32), ("send", C.c_uint64 * NODE_MAX_RANKS),
+                ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_recv", C.c_uint64)]
+
+
+class orl_node_hop2_plan(C.Structure):
+    _fields_ = [("forward", C.c_uint32), ("width", C.c_uint32), ("send", C.c_uint64 * NODE_MAX_RANKS),
+                ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_hosted", C.c_uint64), ("n_forwarded", C.c_uint64)]
 
 
 # Every symbol include/orleans_route.h declares, with its ctypes signature.
@@ -178,6 +191,11 @@ _SIGS = {
     "orl_node_create": (C.c_int, [_P, C.POINTER(orl_node_config), C.POINTER(_P)]),
     "orl_node_destroy": (C.c_int, [_P]),
     "orl_node_last_error": (C.c_char_p, [_P]),
+    "orl_node_set_timeout": (C.c_int, [_P, C.c_uint32]),
+    "orl_node_plan_chunk": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, _P,
+                                      C.POINTER(orl_node_chunk_plan)]),
+    "orl_node_plan_hop2": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64,
+                                     C.POINTER(orl_node_hop2_plan)]),
     "orl_node_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.POINTER(orl_node_result), _P]),
     "orl_node_segment": (C.c_int, [_P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "orl_node_fanout_batch_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P,

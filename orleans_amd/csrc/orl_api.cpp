@@ -167,7 +167,7 @@ int ensure_rank_mode(int device) {
     if (g_rank_state[device] >= 0) return 0;
     const char* m = getenv("ORL_RANK_MODE");
     uint32_t st = 0;
-    int e = launch_rank_selfcheck(m && std::strcmp(m, "ballot") == 0 ? 1 : 0, &st);
+    int e = launch_rank_selfcheck(device, m && std::strcmp(m, "ballot") == 0 ? 1 : 0, &st);
     if (e) return e;
     g_rank_state[device] = (int)st;
     return 0;
@@ -784,6 +784,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         const uint64_t tiles = (mb + kTile - 1) / kTile;
         c->s.max_batch = mb;
         c->s.max_tiles = tiles;
+        c->s.device = cfg->device;
         // histogram rows: one per 4096-element radix tile, or one per route workgroup for small batches (route
         // tiles shrink to 256 messages while a batch has < 2048 x 256 x 2 messages: at most 4096 rows)
         const uint64_t rows = std::max<uint64_t>(tiles, std::min<uint64_t>(4096, (mb + 255) / 256));
@@ -1035,6 +1036,7 @@ namespace {
 int route_impl(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                uint32_t* d_order, uint32_t* d_off, void* stream) {
     if (!c) return ORL_E_INVALID;
+    if (fmt != 8 && fmt != 16 && fmt != 32) return fail(c, ORL_E_INVALID, "record width %d (8, 16 or 32)", fmt);
     if (n && (!d_in || !d_route || !d_act)) return fail(c, ORL_E_INVALID, "null device buffer");
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     if (buckets && (!d_off || (n && !d_order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
@@ -1104,7 +1106,7 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
         ORL_HIP(c, hipMemcpyAsync(c->st_in + lo * sizeof(orl_msg_hdr), in + lo, len * sizeof(orl_msg_hdr), hipMemcpyHostToDevice, up));
         ORL_HIP(c, hipEventRecord(ev_up, up));
         ORL_HIP(c, hipStreamWaitEvent(c->stream, ev_up, 0));
-        if ((r = route_impl(c, d_in + lo, false, len, opts | ORL_OPT_NO_BUCKETS, d_route + lo, d_act + lo, nullptr, nullptr, c->stream)))
+        if ((r = route_impl(c, d_in + lo, 32, len, opts | ORL_OPT_NO_BUCKETS, d_route + lo, d_act + lo, nullptr, nullptr, c->stream)))
             return r;
         ORL_HIP(c, hipEventRecord(ev_rt, c->stream));
         ORL_HIP(c, hipStreamWaitEvent(down, ev_rt, 0));
@@ -1262,6 +1264,27 @@ int orl_partition_by_owner_padded_device(orl_ctx* c, const orl_msg_hdr* d_in, si
     if (e) return hipfail(c, (hipError_t)e, "padded partition launch");
     return ORL_OK;
 }
+
+}  // extern "C"
+namespace orl {
+// The node's hop-1 partition: any record width, with the status word (look-back failures included) for every width.
+int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                         uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
+                         uint32_t* d_status, void* stream) {
+    if (!c || !rank_of_silo || !d_status) return ORL_E_INVALID;
+    if (fmt != 8 && fmt != 16 && fmt != 32) return fail(c, ORL_E_INVALID, "record width %d", fmt);
+    if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
+    if (fmt == 8 && c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
+    if (r) return r;
+    int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, fmt, nullptr,
+                                    d_counts, d_status, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "node partition launch");
+    return ORL_OK;
+}
+}  // namespace orl
+extern "C" {
 
 int orl_partition_compact_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
                                  uint32_t nranks, uint32_t my_rank, size_t stride, orl_wire_msg* d_out, uint32_t* d_src,
@@ -1869,10 +1892,21 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
         case ORL_Q_DEVICE: *v = (uint64_t)(int64_t)c->cfg.device; return ORL_OK;
         case ORL_Q_N_ACT: *v = c->cfg.n_act; return ORL_OK;
         case ORL_Q_MAX_BATCH: *v = c->s.max_batch; return ORL_OK;
+        case ORL_Q_WIRE_DIGEST: *v = c->hp.wire_digest; return ORL_OK;  // host state: set by orl_wire_types_set
         case ORL_Q_RANK_MODE: {
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             std::lock_guard<std::mutex> lk(g_rank_mu);
             *v = (uint64_t)(int64_t)g_rank_state[c->cfg.device];
+            return ORL_OK;
+        }
+        case ORL_Q_PART_ERROR: {  // the look-back state's error word (lb_state[1]), read and cleared
+            if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+            ORL_HIP(c, hipSetDevice(c->cfg.device));
+            ORL_HIP(c, hipDeviceSynchronize());
+            uint32_t w = 0;
+            ORL_HIP(c, hipMemcpy(&w, c->s.lb_state + 1, 4, hipMemcpyDeviceToHost));
+            if (w) ORL_HIP(c, hipMemset(c->s.lb_state + 1, 0, 4));
+            *v = w ? 1u : 0u;
             return ORL_OK;
         }
         default: break;
@@ -1883,7 +1917,6 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             *v = c->probe8_valid ? 8 : c->probe_valid ? 16 : (c->probe_dev || c->probe_dev_stale) ? 17 : 32;
             return ORL_OK;
         case ORL_Q_FULL_UPLOADS: *v = c->n_full_uploads; return ORL_OK;
-        case ORL_Q_WIRE_DIGEST: *v = c->hp.wire_digest; return ORL_OK;
         case ORL_Q_SLOT_PATCHES: *v = c->n_patches; return ORL_OK;
         default: return fail(c, ORL_E_INVALID, "unknown query %u", what);
     }
@@ -1897,7 +1930,7 @@ int orl_ctx_set_rank_mode(orl_ctx* c, uint32_t mode) {
     if (mode == 0 && (st & 2)) return fail(c, ORL_E_STATE, "the LDS lane-order self-check failed on this device: ballot ranking only");
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     ORL_HIP(c, hipDeviceSynchronize());  // kernels in flight keep the mode they started with
-    ORL_HIP(c, (hipError_t)set_rank_mode(mode));
+    ORL_HIP(c, (hipError_t)set_rank_mode(c->cfg.device, mode));
     g_rank_state[c->cfg.device] = (int)(mode | (st & 2));
     return ORL_OK;
 }

@@ -244,13 +244,16 @@ struct Scratch {
     uint32_t lb_epoch = 0;  // launches so far: the granules of launch k carry epoch k (earlier ones read as unpublished)
     uint64_t max_batch;
     uint64_t max_tiles;
+    int device = -1;        // the context's HIP device: picks the ranking variant of its stage-4 launches (host_rm)
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
-// Stage-4 ranking self-check on the current device (k_rank_selfcheck): selects the LDS-atomic rank (0) or the ballot
-// fallback (1) for every kernel of this process on the device; mode 1 forces the fallback.  *ballot_out = mode | err << 1.
-int launch_rank_selfcheck(int mode, uint32_t* ballot_out);
-int set_rank_mode(uint32_t ballot);
+// Stage-4 ranking self-check on `device` (the current device; k_rank_selfcheck): selects the LDS-atomic rank (0) or the
+// ballot fallback (1) for every kernel of this process on that device; mode 1 forces the fallback.  *ballot_out = mode | err << 1.
+int launch_rank_selfcheck(int device, int mode, uint32_t* ballot_out);
+// Sets `device`'s mode (the current device must be `device`): its kernels' flag word and the host mirror that picks the
+// ranking-kernel variants of launches on contexts of that device.
+int set_rank_mode(int device, uint32_t ballot);
 // Host-changed slots of the partition: dir[idx[k]] = slots[k]; probe / probe8 (when non-null) patched alike.
 int launch_dir_patch(const uint32_t* d_idx, const DirSlot* d_slots, const ProbeSlot* d_p16, const uint2* d_p8, uint32_t n,
                      DirSlot* d_dir, ProbeSlot* d_probe, uint2* d_probe8, void* stream);
@@ -327,14 +330,22 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
 int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_ros, uint32_t my_rank, uint64_t* d_counts,
                            void* stream);
 size_t part_state_bytes(size_t n);
+// Node fault injection: a one-lane kernel on `stream` that waits (bounded, seconds) until the host-visible *flag != 0.
+int launch_node_stall(const uint32_t* flag, void* stream);
 // d_base_in (optional, device u64[nranks]): positions continue after an earlier partition into the same regions
-// (its totals); d_counts receives base + this input's counts.
+// (its totals); d_counts receives base + this input's counts.  d_err (optional): |= ORL_PART_LOOKBACK_FAILED when a
+// tile's look-back gave up (accumulates over launches; the caller zeroes it).
 int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
                        size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
                        uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts,
-                       const uint64_t* d_wire_tcd, void* stream);
+                       const uint64_t* d_wire_tcd, uint32_t* d_err, void* stream);
 // Device address of a context's wire types (RouteParams::wire_tcd), current once a route or partition call synced state.
 const uint64_t* ctx_wire_tcd(const orl_ctx* c);
+// The node's hop-1 partition (orl_api.cpp): records of `fmt` bytes (8 / 16 / 32) into padded per-rank regions, per-rank
+// counts into d_counts, and the status word (no 16-B form | no 8-B form | ORL_PART_LOOKBACK_FAILED) for every width.
+int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                         uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
+                         uint32_t* d_status, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

@@ -26,6 +26,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orl_internal.h"
@@ -34,10 +35,10 @@ using namespace orl;
 
 namespace {
 
-constexpr uint32_t kHeadWords = 16;  // [0, nranks) per-rank counts, [8] wire status (bit 0 = no 16-B form, bit 1 = no 8-B
-                                     // form), [9] record form of the partition (bits 56-63) | wire-type digest (bits 0-55)
+constexpr uint32_t kHeadWords = ORL_NODE_HEAD_WORDS;  // layout: include/orleans_route.h (orl_node_plan_chunk)
+static_assert(ORL_NODE_HEAD_WORDS == 16, "head words: counts [0, 8), status [8], form | digest [9], zero [10, 16)");
 constexpr uint64_t kDigestMask = (1ull << 56) - 1;
-constexpr int kBarrierSeconds = 120;
+constexpr uint32_t kDefaultTimeoutMs = 120000;  // every host wait of the exchange (orl_node_set_timeout)
 
 // ORL_TRANSPORT_LOCAL: the ranks are node objects of one process.  All-gathers and exchanges are host barriers around
 // published host words / device pointers; the data moves with device-to-device copies.
@@ -53,9 +54,13 @@ struct LocalGroup {
         uint64_t stride;      // bytes
     };
     std::vector<std::vector<Lane>> lanes;      // per rank: the send regions of the current exchange
-    // false on timeout (a rank stopped calling): the caller reports an error instead of hanging
-    bool barrier() {
+    bool broken = false;                       // a barrier timed out: the group is unusable (every barrier fails)
+    // false on timeout (a rank stopped calling) or once the group is broken: the caller reports an error instead of
+    // hanging.  A timeout breaks the group for every rank, so a late rank cannot pass a later barrier without the one
+    // that gave up and read its stale words or freed buffers.
+    bool barrier(uint32_t timeout_ms) {
         std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
         const uint64_t g = gen;
         if (++arrived == nranks) {
             arrived = 0;
@@ -63,7 +68,10 @@ struct LocalGroup {
             cv.notify_all();
             return true;
         }
-        return cv.wait_for(lk, std::chrono::seconds(kBarrierSeconds), [&] { return gen != g; });
+        if (cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return gen != g || broken; }) && !broken) return true;
+        broken = true;
+        cv.notify_all();
+        return false;
     }
 };
 std::mutex g_groups_mu;
@@ -99,6 +107,10 @@ struct orl_node {
     orl_node_config cfg{};
     std::string err;
     int device = 0;
+    uint32_t timeout_ms = kDefaultTimeoutMs;
+    bool broken = false;      // a bounded wait expired or RCCL failed: the communicator was aborted
+    int stall_chunk = -1;     // ORL_NODE_INJECT_STALL: the all-gather of this chunk waits on h_stall (fault injection)
+    uint32_t* h_stall = nullptr;  // pinned, device-visible release word of the injected stall
     uint32_t n_act = 0, nr = 1, me = 0;
     uint64_t chunk_cap = 0;
     ncclComm_t comm = nullptr;
@@ -126,7 +138,7 @@ struct orl_node {
     uint8_t* d_frecv = nullptr;
     uint32_t *d_frecv_route = nullptr, *d_frecv_act = nullptr, *d_forder = nullptr, *d_foff = nullptr;
     uint32_t* d_fstate = nullptr;
-    uint64_t* d_fcounts = nullptr;                // [ORL_NODE_MAX_CHUNKS][8] chained partition totals
+    uint64_t* d_fcounts = nullptr;                // [ORL_NODE_MAX_CHUNKS][8] chained partition totals, then [1] u32 error word
     struct Seg {
         const void* p;
         uint64_t count;
@@ -164,28 +176,96 @@ int nfail(orl_node* nd, int code, const char* fmt, ...) {
         if (_r != ORL_OK) return nfail((nd), _r, "%s: %s", #call, orl_last_error((nd)->ctx));           \
     } while (0)
 
+// The communicator is unusable (a peer missed a deadline or RCCL reported an error): abort it so RCCL kernels still
+// waiting on peers exit, release an injected stall, and let the streams drain (bounded).  The node stays broken.
+void break_node(orl_node* nd) {
+    nd->broken = true;
+    if (nd->comm) {
+        (void)ncclCommAbort(nd->comm);
+        nd->comm = nullptr;
+    }
+    if (nd->h_stall) __atomic_store_n(nd->h_stall, 1u, __ATOMIC_RELEASE);
+}
+
+// Bounded wait for stream `s` (instead of hipStreamSynchronize): polls the stream and, with RCCL, the communicator's
+// asynchronous error; on an RCCL error or at the deadline the node is broken (break_node) and ORL_E_STATE returned with
+// `what` and this rank's head words `d_own` (when the stream drained after the abort) in orl_node_last_error.
+int wait_bounded(orl_node* nd, hipStream_t s, const char* what, int chunk, const uint64_t* d_own) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto deadline = t0 + std::chrono::milliseconds(nd->timeout_ms);
+    uint32_t polls = 0;
+    ncclResult_t ar = ncclSuccess;
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return ORL_OK;
+        if (q != hipErrorNotReady) return nfail(nd, ORL_E_DEVICE, "%s (chunk %d): %s", what, chunk, hipGetErrorString(q));
+        if (nd->comm && (++polls & 63u) == 0u) {
+            if (ncclCommGetAsyncError(nd->comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) break;
+            ar = ncclSuccess;
+        }
+        if (std::chrono::steady_clock::now() > deadline) break;
+        if (polls > 4096) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::yield();
+    }
+    break_node(nd);
+    // the aborted communicator's kernels exit: give the stream a moment to drain before reading this rank's words
+    const auto drain = std::chrono::steady_clock::now() + std::chrono::milliseconds(2000);
+    bool drained = false;
+    while (!(drained = hipStreamQuery(s) == hipSuccess) && std::chrono::steady_clock::now() < drain)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    char words[256] = "unavailable (the stream did not drain)";
+    uint64_t own[kHeadWords] = {};
+    if (drained && d_own && hipMemcpy(own, d_own, sizeof own, hipMemcpyDeviceToHost) == hipSuccess) {
+        int k = 0;
+        for (uint32_t r = 0; r < nd->nr && k < (int)sizeof words - 24; ++r)
+            k += snprintf(words + k, sizeof words - k, "%s%llu", r ? "," : "", (unsigned long long)own[r]);
+        snprintf(words + k, sizeof words - k, " status %llu", (unsigned long long)own[8]);
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ar != ncclSuccess)
+        return nfail(nd, ORL_E_STATE, "%s (chunk %d): RCCL error %s after %.0f ms; communicator aborted; rank %u head words %s",
+                     what, chunk, ncclGetErrorString(ar), ms, nd->me, words);
+    return nfail(nd, ORL_E_STATE, "%s (chunk %d): no completion within %u ms (a rank did not take part?); communicator aborted; "
+                 "rank %u head words %s", what, chunk, nd->timeout_ms, nd->me, words);
+}
+
 // All-gather of kHeadWords u64 per rank from device `d_src` (ready once `ready` has fired) into nd->h_heads.
-int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready) {
+int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready, int chunk) {
     NODE_HIP(nd, hipStreamWaitEvent(nd->sx, ready, 0));
     if (nd->comm) {
         NODE_NCCL(nd, ncclAllGather(d_src, nd->d_heads, kHeadWords, ncclUint64, nd->comm, nd->sx));
         NODE_HIP(nd, hipMemcpyAsync(nd->h_heads, nd->d_heads, (size_t)nd->nr * kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
-        NODE_HIP(nd, hipStreamSynchronize(nd->sx));
-        return ORL_OK;
+        if (chunk == nd->stall_chunk && nd->h_stall) {
+            int e = launch_node_stall(nd->h_stall, nd->sx);
+            if (e) return nfail(nd, ORL_E_DEVICE, "stall injection: %s", hipGetErrorString((hipError_t)e));
+        }
+        return wait_bounded(nd, nd->sx, chunk >= 0 ? "node counts all-gather" : "node hop-2 counts all-gather", chunk, d_src);
     }
     LocalGroup& g = *nd->group;
     NODE_HIP(nd, hipMemcpyAsync(nd->h_heads + (size_t)nd->me * kHeadWords, d_src, kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
-    NODE_HIP(nd, hipStreamSynchronize(nd->sx));
+    if (chunk == nd->stall_chunk && nd->h_stall) {
+        int e = launch_node_stall(nd->h_stall, nd->sx);
+        if (e) return nfail(nd, ORL_E_DEVICE, "stall injection: %s", hipGetErrorString((hipError_t)e));
+    }
+    if (int r = wait_bounded(nd, nd->sx, "node all-gather", chunk, d_src)) return r;
     {
         std::lock_guard<std::mutex> lk(g.mu);
         std::memcpy(g.words[nd->me].data(), nd->h_heads + (size_t)nd->me * kHeadWords, kHeadWords * 8);
     }
-    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node all-gather: a rank did not arrive (barrier timeout)");
+    if (!g.barrier(nd->timeout_ms)) {
+        nd->broken = true;
+        return nfail(nd, ORL_E_STATE, "node all-gather (chunk %d): a rank did not arrive within %u ms (barrier timeout)", chunk,
+                     nd->timeout_ms);
+    }
     {
         std::lock_guard<std::mutex> lk(g.mu);
         for (uint32_t r = 0; r < nd->nr; ++r) std::memcpy(nd->h_heads + (size_t)r * kHeadWords, g.words[r].data(), kHeadWords * 8);
     }
-    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node all-gather: a rank did not arrive (barrier timeout)");
+    if (!g.barrier(nd->timeout_ms)) {
+        nd->broken = true;
+        return nfail(nd, ORL_E_STATE, "node all-gather (chunk %d): a rank did not arrive within %u ms (barrier timeout)", chunk,
+                     nd->timeout_ms);
+    }
     return ORL_OK;
 }
 
@@ -212,13 +292,16 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
         return ORL_OK;
     }
     LocalGroup& g = *nd->group;
-    NODE_HIP(nd, hipStreamSynchronize(nd->sx));  // my send regions are complete
+    if (int r = wait_bounded(nd, nd->sx, "node exchange: send regions", -1, nullptr)) return r;  // my send regions are complete
     {
         std::lock_guard<std::mutex> lk(g.mu);
         g.lanes[me].clear();
         for (const Lane& L : lanes) g.lanes[me].push_back(LocalGroup::Lane{L.send, L.stride});
     }
-    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive (barrier timeout)");
+    if (!g.barrier(nd->timeout_ms)) {
+        nd->broken = true;
+        return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive within %u ms (barrier timeout)", nd->timeout_ms);
+    }
     std::vector<std::vector<LocalGroup::Lane>> peers;
     {
         std::lock_guard<std::mutex> lk(g.mu);
@@ -231,8 +314,11 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
                 NODE_HIP(nd, hipMemcpyAsync(lanes[k].recv + roff[r] * lanes[k].elem, peers[r][k].base + me * peers[r][k].stride,
                                             recv[r] * lanes[k].elem, hipMemcpyDeviceToDevice, nd->sx));
             }
-    NODE_HIP(nd, hipStreamSynchronize(nd->sx));
-    if (!g.barrier()) return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive (barrier timeout)");  // regions free
+    if (int r = wait_bounded(nd, nd->sx, "node exchange: copies", -1, nullptr)) return r;
+    if (!g.barrier(nd->timeout_ms)) {  // every rank has copied out of my regions: they are free
+        nd->broken = true;
+        return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive within %u ms (barrier timeout)", nd->timeout_ms);
+    }
     return ORL_OK;
 }
 
@@ -243,11 +329,13 @@ void free_node(orl_node* nd) {
     f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts); f(nd->d_fan);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     if (nd->h_form) (void)hipHostFree(nd->h_form);
+    if (nd->h_stall) (void)hipHostFree(nd->h_stall);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr})
         if (s) (void)hipStreamDestroy(s);
     if (nd->comm) (void)ncclCommDestroy(nd->comm);
+    nd->comm = nullptr;
 }
 
 // Hop-2 buffers for an owned set of up to `owned` messages (regions of that stride), grown on demand.
@@ -270,7 +358,7 @@ int ensure_hop2(orl_node* nd, uint64_t owned) {
         NODE_HIP(nd, hipMalloc((void**)&nd->d_frecv_act, m * 4));
         NODE_HIP(nd, hipMalloc((void**)&nd->d_forder, m * 4));
         NODE_HIP(nd, hipMalloc((void**)&nd->d_foff, ((size_t)nd->n_act + 2) * 4));
-        NODE_HIP(nd, hipMalloc((void**)&nd->d_fcounts, ORL_NODE_MAX_CHUNKS * 8 * 8));
+        NODE_HIP(nd, hipMalloc((void**)&nd->d_fcounts, ORL_NODE_MAX_CHUNKS * 8 * 8 + 8));
     }
     nd->f_cap = cap;
     return ORL_OK;
@@ -279,6 +367,76 @@ int ensure_hop2(orl_node* nd, uint64_t owned) {
 }  // namespace
 
 extern "C" {
+
+// The protocol's host decisions.  Every rank evaluates them on the same all-gathered words, so every rank reaches the
+// same width, the same sizes and the same errors without another round trip.
+int orl_node_plan_chunk(const uint64_t* H, uint32_t nr, uint32_t me, uint32_t written, uint64_t max_recv, uint64_t* owned_total,
+                        orl_node_chunk_plan* out) {
+    if (!H || !owned_total || !out || nr == 0 || nr > ORL_NODE_MAX_RANKS || me >= nr) return ORL_E_INVALID;
+    if (written != 8 && written != 16 && written != 32) return ORL_E_INVALID;
+    const uint64_t W = kHeadWords;
+    std::memset(out, 0, sizeof *out);
+    for (uint32_t r = 0; r < nr; ++r)
+        if ((uint32_t)H[r * W + 8] & ORL_PART_LOOKBACK_FAILED) return ORL_E_DEVICE;
+    // 8-B when every rank wrote that form with one wire-type digest and no message lacked it, 16-B when no message lacked
+    // that, else 32-B headers (a rank that wrote 32-B, ORL_NODE_WIDE_ONLY, makes the chunk 32-B)
+    bool all8 = true, no16 = false, no8 = false, wide = false;
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t st = (uint32_t)H[r * W + 8];
+        const uint32_t f = (uint32_t)(H[r * W + 9] >> 56);
+        no16 |= (st & 1u) != 0;
+        no8 |= (st & 2u) != 0;
+        wide |= f == 32u;
+        all8 &= f == 8u && (H[r * W + 9] & kDigestMask) == (H[0 * W + 9] & kDigestMask);
+    }
+    out->width = (wide || no16) ? 32u : (all8 && !no8) ? 8u : 16u;
+    out->rewrite = out->width != written;
+    for (uint32_t r = 0; r < nr; ++r) {
+        out->send[r] = H[me * W + r];
+        out->recv[r] = H[r * W + me];
+        out->n_recv += out->recv[r];
+    }
+    int rc = ORL_OK;
+    for (uint32_t d = 0; d < nr; ++d) {  // every rank checks every rank: all return the same error, none waits
+        uint64_t in = 0;
+        for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
+        owned_total[d] += in;
+        if (owned_total[d] > max_recv) rc = ORL_E_CAPACITY;
+    }
+    return rc;
+}
+
+int orl_node_plan_hop2(const uint64_t* H, uint32_t nr, uint32_t me, uint64_t n_owned, uint32_t width_mask, uint64_t max_recv,
+                       orl_node_hop2_plan* out) {
+    if (!H || !out || nr == 0 || nr > ORL_NODE_MAX_RANKS || me >= nr || width_mask > 7) return ORL_E_INVALID;
+    const uint64_t W = kHeadWords;
+    std::memset(out, 0, sizeof *out);
+    for (uint32_t s = 0; s < nr; ++s)
+        for (uint32_t d = 0; d < nr; ++d)
+            if (s != d && H[s * W + d]) {
+                out->forward = 1;
+                if (s == me) out->n_forwarded += H[s * W + d];
+            }
+    // one record width for a forwarded set: the common width of the owned segments, or 32-B headers for a mix
+    const bool w8 = width_mask & 1u, w16 = width_mask & 2u, w32 = width_mask & 4u;
+    out->width = (w32 || (w8 && w16)) ? 32u : w16 ? 16u : 8u;
+    if (!out->forward) {
+        out->n_hosted = n_owned;
+        return ORL_OK;
+    }
+    int rc = ORL_OK;
+    for (uint32_t d = 0; d < nr; ++d) {
+        uint64_t in = 0;
+        for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
+        if (in > max_recv) rc = ORL_E_CAPACITY;
+        if (d == me) out->n_hosted = in;
+    }
+    for (uint32_t r = 0; r < nr; ++r) {
+        out->send[r] = H[me * W + r];
+        out->recv[r] = H[r * W + me];
+    }
+    return rc;
+}
 
 int orl_node_unique_id(uint8_t id[ORL_NODE_ID_BYTES]) {
     if (!id) return ORL_E_INVALID;
@@ -289,6 +447,12 @@ int orl_node_unique_id(uint8_t id[ORL_NODE_ID_BYTES]) {
 }
 
 const char* orl_node_last_error(const orl_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+
+int orl_node_set_timeout(orl_node* nd, uint32_t ms) {
+    if (!nd || ms == 0) return ORL_E_INVALID;
+    nd->timeout_ms = ms;
+    return ORL_OK;
+}
 
 int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     if (!ctx || !cfg || !out) return ORL_E_INVALID;
@@ -348,6 +512,15 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipMemset(nd->d_hcount, 0, 16 * 8));
     if (e != hipSuccess) return bail(ORL_E_DEVICE);
     for (hipEvent_t ev : {nd->ev_slot[0], nd->ev_slot[1]}) (void)hipEventRecord(ev, nd->sx);  // both slots free
+    if (const char* t = getenv("ORL_NODE_TIMEOUT_MS")) {
+        const long v = atol(t);
+        if (v > 0) nd->timeout_ms = (uint32_t)std::min<long>(v, 0x7FFFFFFF);
+    }
+    if (const char* st = getenv("ORL_NODE_INJECT_STALL")) {  // fault injection: "<chunk>" (hop 1) or "hop2"
+        nd->stall_chunk = std::strcmp(st, "hop2") == 0 ? -2 : atoi(st);
+        if (!ok(hipHostMalloc((void**)&nd->h_stall, 64, hipHostMallocMapped | hipHostMallocCoherent))) return bail(ORL_E_NOMEM);
+        *nd->h_stall = 0;
+    }
     if (cfg->transport == ORL_TRANSPORT_RCCL) {
         ncclUniqueId u;
         std::memcpy(u.internal, cfg->group_id, ORL_NODE_ID_BYTES);
@@ -395,6 +568,8 @@ int orl_node_segment(const orl_node* nd, uint32_t i, const void** d_records, uin
 int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* res,
                                 void* stream) {
     if (!nd || !res) return ORL_E_INVALID;
+    if (nd->broken) return nfail(nd, ORL_E_STATE, "node is broken (an earlier exchange failed; its communicator was aborted): %s",
+                                 nd->err.c_str());
     if (n && !d_in) return nfail(nd, ORL_E_INVALID, "null device buffer");
     if (n > nd->cfg.max_batch) return nfail(nd, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)nd->cfg.max_batch);
     std::memset(res, 0, sizeof *res);
@@ -411,7 +586,7 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     uint64_t owned_bytes = 0;
     std::vector<uint64_t> owned_all(nr, 0);   // every rank's running receive total (capacity checks agree)
     uint64_t sent_remote = 0;
-    bool seen[3] = {false, false, false};     // record widths 8 / 16 / 32 among the owned segments
+    uint32_t width_mask = 0;                  // record widths among the owned segments: bit 0 = 8, 1 = 16, 2 = 32
     // ---- hop 1 -------------------------------------------------------------------------------------------
     // Record form per chunk: every rank first writes the narrowest form it can (8-B when its context has wire types,
     // else 16-B; 32-B with ORL_NODE_WIDE_ONLY) and reports it with its wire-type digest in head word 9.  After the counts
@@ -443,18 +618,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             nd->form_word[slot] = fw;
             nd->form_valid[slot] = true;
         }
-        if (form == 32)
-            NODE_CTX(nd, orl_partition_by_owner_padded_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
-                                                              nd->chunk_cap, reinterpret_cast<orl_msg_hdr*>(send), nullptr,
-                                                              head, nd->sp));
-        else if (form == 16)
-            NODE_CTX(nd, orl_partition_compact_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
-                                                      nd->chunk_cap, reinterpret_cast<orl_wire_msg*>(send), nullptr, head,
-                                                      status, nd->sp));
-        else
-            NODE_CTX(nd, orl_partition_narrow_device(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me,
-                                                     nd->chunk_cap, reinterpret_cast<orl_wire8*>(send), nullptr, head,
-                                                     status, nd->sp));
+        NODE_CTX(nd, ctx_partition_padded(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me, nd->chunk_cap, send,
+                                          (int)form, head, status, nd->sp));
         NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
         return ORL_OK;
     };
@@ -466,39 +631,41 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         uint8_t* send = nd->d_send[slot];
         if (c + 1 < K)
             if (int r = partition(c + 1, first_form)) return r;
-        if (int r = allgather_heads(nd, head, nd->ev_part[slot])) return r;
+        if (int r = allgather_heads(nd, head, nd->ev_part[slot], (int)c)) return r;
         const uint64_t* H = nd->h_heads;
-        bool all8 = true, no16 = false, no8 = false, wide = false;
-        for (uint32_t r = 0; r < nr; ++r) {
-            const uint32_t st = (uint32_t)H[r * W + 8];
-            const uint32_t f = (uint32_t)(H[r * W + 9] >> 56);
-            no16 |= (st & 1u) != 0;
-            no8 |= (st & 2u) != 0;
-            wide |= f == 32u;
-            all8 &= f == 8u && (H[r * W + 9] & kDigestMask) == (H[0 * W + 9] & kDigestMask);
+        orl_node_chunk_plan plan;
+        const int pr = orl_node_plan_chunk(H, nr, me, first_form, nd->cfg.max_recv, owned_all.data(), &plan);
+        if (pr == ORL_E_DEVICE) {
+            for (uint32_t r = 0; r < nr; ++r)  // every rank sees every rank's status: all fail together
+                if ((uint32_t)H[r * W + 8] & ORL_PART_LOOKBACK_FAILED)
+                    return nfail(nd, ORL_E_DEVICE, "chunk %u: rank %u's partition look-back gave up (device fault)", c, r);
         }
-        const uint32_t width = (wide || no16) ? 32u : (all8 && !no8) ? 8u : 16u;
-        if (width != first_form)  // some rank's records do not fit the form: every rank rewrites the chunk in `width`
+        if (pr == ORL_E_CAPACITY) {
+            for (uint32_t d = 0; d < nr; ++d)
+                if (owned_all[d] > nd->cfg.max_recv)
+                    return nfail(nd, ORL_E_CAPACITY, "rank %u receives %llu > max_recv %llu messages", d,
+                                 (unsigned long long)owned_all[d], (unsigned long long)nd->cfg.max_recv);
+        }
+        if (pr) return nfail(nd, pr, "chunk %u: node plan failed", c);
+        const uint32_t width = plan.width;
+        if (plan.rewrite) {  // some rank's records do not fit the form: every rank rewrites the chunk in `width`
             if (int r = partition(c, width)) return r;
-        seen[width == 8 ? 0 : width == 16 ? 1 : 2] = true;
-        std::vector<uint64_t> sendc(nr), recvc(nr);
-        uint64_t got = 0;
-        for (uint32_t r = 0; r < nr; ++r) {
-            sendc[r] = H[me * W + r];
-            recvc[r] = H[r * W + me];
-            got += recvc[r];
-            if (r != me) sent_remote += sendc[r];
+            // the rewrite's look-back is checked on this rank only (its counts are those already all-gathered)
+            uint32_t st = 0;
+            if (int r = wait_bounded(nd, nd->sp, "re-partition", (int)c, nullptr)) return r;
+            NODE_HIP(nd, hipMemcpy(&st, head + 8, 4, hipMemcpyDeviceToHost));
+            if (st & ORL_PART_LOOKBACK_FAILED)
+                return nfail(nd, ORL_E_DEVICE, "chunk %u: the %u-byte re-partition's look-back gave up (device fault)", c, width);
         }
-        for (uint32_t d = 0; d < nr; ++d) {  // every rank checks every rank: all return the same error, none waits
-            uint64_t in = 0;
-            for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
-            owned_all[d] += in;
-            if (owned_all[d] > nd->cfg.max_recv)
-                return nfail(nd, ORL_E_CAPACITY, "rank %u receives %llu > max_recv %llu messages", d,
-                             (unsigned long long)owned_all[d], (unsigned long long)nd->cfg.max_recv);
-        }
+        width_mask |= width == 8 ? 1u : width == 16 ? 2u : 4u;
+        const uint64_t got = plan.n_recv;
+        for (uint32_t r = 0; r < nr; ++r)
+            if (r != me) sent_remote += plan.send[r];
+        // segments start 32-B aligned, whatever the widths before them (an odd count of 8-B records, then wider ones);
+        // the padding fits max_recv x 32 B: a chunk of 8- or 16-B records never fills its 32-B share
+        owned_bytes = (owned_bytes + 31) & ~uint64_t(31);
         uint8_t* recv = nd->d_recv + owned_bytes;
-        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, sendc.data(), recvc.data(), nd->ev_part[slot]))
+        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, plan.send, plan.recv, nd->ev_part[slot]))
             return r;
         NODE_HIP(nd, hipEventRecord(nd->ev_slot[slot], nd->sx));
         nd->segs.push_back(orl_node::Seg{recv, got, width});
@@ -529,18 +696,23 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     // buffers) and costs one stage 4.
     const bool spec = !nd->last_forward;
     if (spec) NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
-    if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_r)) return r;
+    if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_r, -2)) return r;
     const uint64_t* H = nd->h_heads;
-    bool forward = false;
-    uint64_t fwd = 0;
-    for (uint32_t s = 0; s < nr; ++s)
-        for (uint32_t d = 0; d < nr; ++d)
-            if (s != d && H[s * W + d]) {
-                forward = true;
-                if (s == me) fwd += H[s * W + d];
-            }
+    orl_node_hop2_plan h2;
+    const int pr = orl_node_plan_hop2(H, nr, me, owned, width_mask, nd->cfg.max_recv, &h2);
+    if (pr == ORL_E_CAPACITY) {
+        for (uint32_t d = 0; d < nr; ++d) {
+            uint64_t in = 0;
+            for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
+            if (in > nd->cfg.max_recv)
+                return nfail(nd, ORL_E_CAPACITY, "rank %u hosts %llu > max_recv %llu messages", d, (unsigned long long)in,
+                             (unsigned long long)nd->cfg.max_recv);
+        }
+    }
+    if (pr) return nfail(nd, pr, "hop-2 plan failed");
+    const bool forward = h2.forward != 0;
     res->n_owned = owned;
-    res->n_forwarded = fwd;
+    res->n_forwarded = h2.n_forwarded;
     res->n_sent_remote = sent_remote;
     nd->last_forward = forward;
     if (!forward) {  // every routed message is hosted where it was routed: stage 4 over the owned set
@@ -551,40 +723,37 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         res->order = nd->d_order;
         res->bucket_offsets = nd->d_off;
     } else {
-        uint64_t hosted = 0;
-        for (uint32_t d = 0; d < nr; ++d) {
-            uint64_t in = 0;
-            for (uint32_t s = 0; s < nr; ++s) in += H[s * W + d];
-            if (in > nd->cfg.max_recv)
-                return nfail(nd, ORL_E_CAPACITY, "rank %u hosts %llu > max_recv %llu messages", d, (unsigned long long)in,
-                             (unsigned long long)nd->cfg.max_recv);
-            if (d == me) hosted = in;
-        }
+        const uint64_t hosted = h2.n_hosted;
         if (int r = ensure_hop2(nd, owned)) return r;
-        // one record width for the forwarded set: the common width of the owned segments, or headers for a mix
-        const uint32_t wout = (seen[2] || (seen[0] && seen[1])) ? 32u : seen[1] ? 16u : 8u;
+        const uint32_t wout = h2.width;
+        uint32_t* d_ferr = reinterpret_cast<uint32_t*>(nd->d_fcounts + ORL_NODE_MAX_CHUNKS * 8);
+        NODE_HIP(nd, hipMemsetAsync(d_ferr, 0, 4, nd->sr));
         uint64_t off = 0;
         for (size_t k = 0; k < nd->segs.size(); ++k) {  // one partition per segment, positions chained through the totals
             const orl_node::Seg& sg = nd->segs[k];
             int e = launch_part_routed(nd->d_ros, sg.p, (int)sg.width, (int)wout, nd->d_route + off, nd->d_act + off, sg.count, me,
                                        nr, nd->f_cap, nd->d_fsend, nd->d_fsend_route, nd->d_fsend_act, nd->d_fstate,
                                        k ? nd->d_fcounts + 8 * (k - 1) : nullptr, nd->d_fcounts + 8 * k,
-                                       ctx_wire_tcd(nd->ctx), nd->sr);
+                                       ctx_wire_tcd(nd->ctx), d_ferr, nd->sr);
             if (e) return nfail(nd, ORL_E_DEVICE, "hop-2 partition launch: %s", hipGetErrorString((hipError_t)e));
             off += sg.count;
         }
         NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
-        std::vector<uint64_t> sendc(nr), recvc(nr);
-        for (uint32_t r = 0; r < nr; ++r) {
-            sendc[r] = H[me * W + r];
-            recvc[r] = H[r * W + me];
+        {  // the hop-2 partition's look-back error word (its state is zeroed per launch): checked before anything is sent
+            uint32_t lb_err = 0;
+            if (int r = wait_bounded(nd, nd->sr, "hop-2 partition", -2, nullptr)) return r;
+            NODE_HIP(nd, hipMemcpy(&lb_err, d_ferr, 4, hipMemcpyDeviceToHost));
+            if (lb_err) return nfail(nd, ORL_E_DEVICE, "hop-2 partition look-back gave up (device fault)");
         }
         const std::vector<Lane> lanes = {Lane{nd->d_fsend, nd->f_cap * wout, nd->d_frecv, wout},
                                          Lane{reinterpret_cast<uint8_t*>(nd->d_fsend_route), nd->f_cap * 4,
                                               reinterpret_cast<uint8_t*>(nd->d_frecv_route), 4},
                                          Lane{reinterpret_cast<uint8_t*>(nd->d_fsend_act), nd->f_cap * 4,
                                               reinterpret_cast<uint8_t*>(nd->d_frecv_act), 4}};
-        if (int r = exchange(nd, lanes, sendc.data(), recvc.data(), nd->ev_r)) return r;
+        if (int r = exchange(nd, lanes, h2.send, h2.recv, nd->ev_r)) return r;
+        // nothing after this exchange waits on the host: bound it here, so a missing peer fails this call instead of
+        // hanging the caller's stream
+        if (int r = wait_bounded(nd, nd->sx, "hop-2 exchange", -2, nullptr)) return r;
         NODE_HIP(nd, hipEventRecord(nd->ev_x, nd->sx));
         NODE_HIP(nd, hipStreamWaitEvent(nd->sr, nd->ev_x, 0));
         NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_frecv_act, hosted, nd->d_forder, nd->d_foff, nd->sr));

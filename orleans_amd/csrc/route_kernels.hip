@@ -329,10 +329,20 @@ __device__ uint32_t g_rank_flags = kRankUniform;
 
 __device__ __forceinline__ uint32_t rank_flags() { return __builtin_amdgcn_readfirstlane(g_rank_flags); }
 
-// Host mirror of g_rank_flags (last set on any device: the modes are set process-wide in practice), which picks the
-// ranking-kernel variant of each launch.
-uint32_t g_host_rank_flags = kRankUniform;
-int host_rm() { return (g_host_rank_flags & kRankBallot) ? kRmBallot : (g_host_rank_flags & kRankUniform) ? kRmHot : kRmPlain; }
+// Host mirror of each device's g_rank_flags, which picks the ranking-kernel variant of a launch from the launching
+// context's device (Scratch::device): a device whose lane-order self-check failed keeps the ballot variant whatever
+// the other devices of the process use.
+// kRankSet marks a device whose mode was set (by its self-check); an unset or unknown device gets the ballot variant,
+// which is correct whatever the LDS atomics' lane order.
+constexpr int kMaxDevices = 64;
+constexpr uint32_t kRankSet = 0x100u;
+uint32_t g_host_rank_flags[kMaxDevices];
+int host_rm(int device) {
+    if (device < 0 || device >= kMaxDevices) return kRmBallot;
+    const uint32_t f = __atomic_load_n(&g_host_rank_flags[device], __ATOMIC_ACQUIRE);
+    if (!(f & kRankSet)) return kRmBallot;
+    return (f & kRankBallot) ? kRmBallot : (f & kRankUniform) ? kRmHot : kRmPlain;
+}
 
 __device__ __forceinline__ uint64_t lanes_below() {
     const uint32_t lane = __lane_id();
@@ -2136,9 +2146,10 @@ __device__ __forceinline__ uint32_t rank_group_bits(uint64_t m, uint32_t r) {  /
 // Granule tag word: epoch << 2 | kind (1 aggregate, 2 inclusive).  A granule of another epoch reads as unpublished, so a
 // state buffer reused launch after launch needs no zeroing when each launch has its own epoch (k_part_lb); epoch 0 with a
 // zeroed buffer is the plain form (k_part_routed).
+// err_word (optional): also gets ORL_PART_LOOKBACK_FAILED when the look-back gives up (state[1] always does).
 __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restrict__ state, uint32_t nranks, uint32_t ntiles,
                                                uint64_t* __restrict__ counts, const uint64_t* __restrict__ base_in,
-                                               uint32_t epoch) {
+                                               uint32_t epoch, uint32_t* __restrict__ err_word = nullptr) {
     if (threadIdx.x >= 64) return;
     uint64_t* status = reinterpret_cast<uint64_t*>(state + 4);
     const uint32_t lane = threadIdx.x, r = lane & 7u, k = lane >> 3, t = lb.tile;
@@ -2187,7 +2198,10 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
                 done = true;
             } else if (f0 == 0u) {
                 if (++spins > kLbSpinLimit) {  // cannot happen with every earlier tile started; never hang the GPU
-                    if (k == 0) atomicOr(&state[1], 1u);
+                    if (k == 0) {
+                        atomicOr(&state[1], 1u);
+                        if (err_word) atomicOr(err_word, ORL_PART_LOOKBACK_FAILED);
+                    }
                     done = true;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -2203,7 +2217,8 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
 }
 
 // FMT: the record written — 32 = orl_msg_hdr, 16 = orl_wire_msg (*wire_status |= 1 if a message has no 16-B form),
-// 8 = orl_wire8 (|= 1 as for 16, |= 2 if a message has no 8-B form).
+// 8 = orl_wire8 (|= 1 as for 16, |= 2 if a message has no 8-B form).  wire_status (optional for FMT 32) also gets
+// ORL_PART_LOOKBACK_FAILED when a tile's look-back gave up (the record positions are then not valid).
 template <int FMT>
 __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
@@ -2246,7 +2261,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
     }
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
-    lookback_ranks(sm.lb, state, nranks, ntiles, counts, nullptr, epoch);
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts, nullptr, epoch, wire_status);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
@@ -2344,7 +2359,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
                                                                void* __restrict__ out, uint32_t* __restrict__ route_out,
                                                                uint32_t* __restrict__ act_out, uint32_t* __restrict__ state,
                                                                uint32_t ntiles, const uint64_t* __restrict__ base_in,
-                                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ wire_tcd) {
+                                                               uint64_t* __restrict__ counts, const uint64_t* __restrict__ wire_tcd,
+                                                               uint32_t* __restrict__ err_word) {
     static_assert((WIN == 8 || WIN == 16 || WIN == 32) && WOUT >= WIN && (WIN != 8 || WOUT != 16), "record widths");
     __shared__ PartRoutedSmem sm;
     if (WIN == 8 && WOUT == 32 && threadIdx.x < ORL_MAX_WIRE_TYPES) sm.wire_tcd[threadIdx.x] = wire_tcd[threadIdx.x];
@@ -2380,7 +2396,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_routed(const uint8_t* __
     }
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
-    lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in, 0u);
+    lookback_ranks(sm.lb, state, nranks, ntiles, counts, base_in, 0u, err_word);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPartItems; ++j) {
@@ -3062,12 +3078,12 @@ uint32_t route_items(uint64_t n, uint32_t max_items) {
 }
 
 template <int BITS>
-void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
+void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
                                                 row_step, ntiles, pout, order, keys)
-#define ORL_RP(I, O, IT) do { const int rm_ = host_rm(); if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
+#define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
         switch (out) {
@@ -3086,10 +3102,10 @@ void launch_pass_bits(int in, int out, const void* kin, uint32_t n, uint32_t n_a
 #undef ORL_RP3
 }
 
-void launch_pass(int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
+void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
     switch (bits) {
-#define ORL_CASE(B) case B: launch_pass_bits<B>(in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st); break;
+#define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3128,7 +3144,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
                                      s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
                                          s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
-#define ORL_SS(I) do { const int rm_ = host_rm(); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
+#define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
     if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
     else ORL_SC(IN_SOA16);
@@ -3191,10 +3207,10 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
             col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st);
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
-                launch_pass(bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
+                launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
-                launch_pass(bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
+                launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
                             nullptr, nullptr, st);
             }
             kin = s.pairs_a;
@@ -3217,7 +3233,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         col_scan(s.tile_hist, nrows, bins, row_step, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
-        launch_pass(plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
+        launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
                     s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
     hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
@@ -3233,7 +3249,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
 
 }  // namespace
 
-int launch_rank_selfcheck(int mode, uint32_t* ballot_out) {
+int launch_rank_selfcheck(int device, int mode, uint32_t* ballot_out) {
     uint32_t* d_err = nullptr;
     uint32_t err = 0;
     hipError_t e = hipMalloc((void**)&d_err, 4);
@@ -3246,16 +3262,19 @@ int launch_rank_selfcheck(int mode, uint32_t* ballot_out) {
     if (d_err) (void)hipFree(d_err);
     if (e != hipSuccess) return (int)e;
     const uint32_t ballot = (mode == 1 || err) ? 1u : 0u;
-    e = (hipError_t)set_rank_mode(ballot);
+    e = (hipError_t)set_rank_mode(device, ballot);
     *ballot_out = ballot | (err << 1);
     return (int)e;
 }
 
-int set_rank_mode(uint32_t ballot) {
+int set_rank_mode(int device, uint32_t ballot) {
+    if (device < 0 || device >= kMaxDevices) return (int)hipErrorInvalidDevice;
     const char* u = getenv("ORL_RANK_UNIFORM");
     const uint32_t flags = (ballot ? kRankBallot : 0u) | ((u && u[0] == '0') ? 0u : kRankUniform);
-    g_host_rank_flags = flags;
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rank_flags), &flags, 4);
+    // the device symbol first: a launch that reads the host mirror afterwards finds the device flags already set
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_rank_flags), &flags, 4);
+    if (e == hipSuccess) __atomic_store_n(&g_host_rank_flags[device], flags | kRankSet, __ATOMIC_RELEASE);
+    return (int)e;
 }
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream) {
@@ -3288,6 +3307,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     hipStream_t st = (hipStream_t)stream;
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    if (fmt != 8 && fmt != 16 && fmt != 32) return (int)hipErrorInvalidValue;  // record widths: orl_msg_hdr / wire16 / wire8
     if (n == 0) {
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
@@ -3302,7 +3322,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
-#define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)
+#define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
@@ -3582,10 +3602,25 @@ int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_r
 
 size_t part_state_bytes(size_t n) { return 16 + (size_t)ceil_div(n, kPartTile) * 64; }
 
+// Fault injection for the node's bounded waits (ORL_NODE_INJECT_STALL): one lane polls a host-visible word (system-scope
+// vector loads) until it is nonzero, and gives up by itself after ~2^21 sleeps (seconds), so the kernel always ends.
+__global__ void k_node_stall(const uint32_t* __restrict__ flag) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t i = 0; i < (1u << 21); ++i) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+
+int launch_node_stall(const uint32_t* flag, void* stream) {
+    hipLaunchKernelGGL(k_node_stall, dim3(1), dim3(64), 0, (hipStream_t)stream, flag);
+    return (int)hipGetLastError();
+}
+
 int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout, const uint32_t* d_route, const uint32_t* d_act,
                        size_t n, uint32_t my_rank, uint32_t nranks, uint64_t stride, void* d_out, uint32_t* d_route_out,
                        uint32_t* d_act_out, uint32_t* d_state, const uint64_t* d_base_in, uint64_t* d_counts,
-                       const uint64_t* d_wire_tcd, void* stream) {
+                       const uint64_t* d_wire_tcd, uint32_t* d_err, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = d_base_in ? hipMemcpyAsync(d_counts, d_base_in, sizeof(uint64_t) * nranks, hipMemcpyDeviceToDevice, st)
                              : hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);
@@ -3594,7 +3629,7 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
     if ((e = hipMemsetAsync(d_state, 0, part_state_bytes(n), st)) != hipSuccess) return (int)e;
 #define ORL_PR(WI, WO) hipLaunchKernelGGL((k_part_routed<WI, WO>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_ros, d_in, d_route,  \
                                           d_act, (uint32_t)n, my_rank, nranks, stride, d_out, d_route_out, d_act_out, d_state,   \
-                                          ntiles, d_base_in, d_counts, d_wire_tcd)
+                                          ntiles, d_base_in, d_counts, d_wire_tcd, d_err)
     if (win == 8 && wout == 8) ORL_PR(8, 8);
     else if (win == 8) ORL_PR(8, 32);
     else if (win == 16 && wout == 16) ORL_PR(16, 16);
@@ -3610,7 +3645,9 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
                             Scratch& s, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipSuccess;
-    if (fmt != 32) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
+    if (fmt != 8 && fmt != 16 && fmt != 32) return (int)hipErrorInvalidValue;
+    if (fmt != 32 && !d_wire_status) return (int)hipErrorInvalidValue;
+    if (d_wire_status) e = hipMemsetAsync(d_wire_status, 0, sizeof(uint32_t), st);
     if (e == hipSuccess && n == 0) e = hipMemsetAsync(d_counts, 0, sizeof(uint64_t) * nranks, st);  // else the last tile writes them
     if (e != hipSuccess || n == 0) return (int)e;
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;

@@ -1,239 +1,72 @@
 """Multi-GPU silo node: one process per GPU, the directory sharded by ring range.
 
-Per batch (messages originate on the rank that hosts their sending silo):
-  1. stages 1-2 + stable partition of the local batch by the rank holding each message's directory owner,
-     in one pass into padded per-rank send regions (``orl_partition_by_owner_padded_device``);
-  2. all-to-all of the per-rank counts, then grouped send/recv of the 32-B headers (torch.distributed
-     batch_isend_irecv: RCCL over xGMI on GPUs, gloo on CPU) — the reference's per-target-silo sender
-     queues + TCP (OutboundMessageQueue.cs:113-145) collapsed into one grouped exchange;
-  3. on the owner rank: stages 1-4 over the received messages (``orl_route_batch_device``).
-Received messages are concatenated in source-rank order and each source's block keeps its arrival
-order, so the per-activation FIFO order is the stable order by (source rank, source index): per-sender
-order holds because a sender's messages all originate on one rank.
+The exchange lives behind the C ABI (``orl_node_*``, orleans_amd/csrc/orl_node.cpp): per batch, every rank partitions its
+local messages by the rank of their directory owner, all-gathers the per-rank counts, exchanges the records with a grouped
+RCCL send/recv (or, ORL_TRANSPORT_LOCAL, device copies between the ranks of one process), routes what it owns, forwards
+messages whose activation lives on another rank (hop 2) and buckets what it hosts.  ``GrainNode`` is a thin ctypes wrapper
+of that; there is no Python collective on the data path.
 
-PipelinedRouter keeps two batches in flight so the exchange of one overlaps the routing of the previous.
-The exchange logic is independent of what computes the two local steps: ``HipExecutor`` drives the HIP
-library; tests substitute a CPU executor built on the oracle to run the same protocol over gloo.
+``plan_chunk`` / ``plan_hop2`` bind the protocol's host decisions (``orl_node_plan_chunk`` / ``orl_node_plan_hop2``: the
+record width of a chunk, the send / receive sizes, the collective capacity errors, whether hop 2 forwards) — the same
+functions orl_node_route_batch_device calls after each all-gather.  They are plain host code, so the multi-process CPU
+tests (tests/test_distributed.py) run the protocol over gloo with them and check every rank's result against the
+single-process replay.
 """
 from __future__ import annotations
 
-import contextlib
 from dataclasses import dataclass
-from typing import List, Optional, Protocol, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
 from . import _lib as L
 
-HDR_WORDS = 8   # orl_msg_hdr as 8 int32 words
-WIRE_WORDS = 4  # orl_wire_msg (compact exchange record) as 4 int32 words
-
-
-HEAD_LEN = 9     # partition head: per-rank counts at [0, nranks), wire status at [8]
-
-
-class Executor(Protocol):
-    def partition(self, msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int, slot: int = 0,
-                  stream=None, compact: bool = True):
-        """-> (per-rank send regions: list of [>= count_r, W] int32 tensors (W = 8: orl_msg_hdr, 4: orl_wire_msg),
-               head: int64 [HEAD_LEN] = per-rank counts, then at [8] 1 if the batch has no compact form)"""
-
-    def route(self, msgs, n: int, slot: int = 0, stream=None):
-        """-> (route [n], act [n], order [n], offsets [n_act+2]) for the received records ([n, W] int32)"""
+HEAD_WORDS = L.NODE_HEAD_WORDS
 
 
 @dataclass
-class StepResult:
-    recv_splits: List[int]   # messages received from each source rank
-    send_splits: List[int]   # messages sent to each destination rank
-    route: object
-    act: object
-    order: object
-    offsets: object
+class ChunkPlan:
+    width: int          # record width every rank exchanges the chunk in (8 / 16 / 32)
+    rewrite: bool       # this rank wrote another width: partition again in `width`
+    send: List[int]     # records to each rank
+    recv: List[int]     # records from each rank (back to back, rank order)
     n_recv: int
 
 
-class HipExecutor:
-    """Drives liborleans_route.so on this rank's GPU with preallocated device buffers.
-
-    `part_eng` (default: `eng`) runs the owner partition; giving it its own context (ring only) lets a partition
-    and a route run concurrently on two streams without sharing scratch.  `slots` output sets let the
-    pipelined router keep two batches in flight.  Send regions: `nranks` x `part_capacity` records per slot
-    (the largest local batch; HBM is plentiful, so the one-pass partition needs no totals first).  `compact`
-    sends 16-B orl_wire_msg records (half the exchange bytes) whenever the batch has that form."""
-
-    def __init__(self, eng, capacity: int, torch_mod, device: str = "cuda", opts: int = 0, part_eng=None,
-                 slots: int = 1, nranks: int = 1, part_capacity: Optional[int] = None, compact: bool = True):
-        t = torch_mod
-        self.t = t
-        self.eng = eng
-        self.part_eng = part_eng or eng
-        self.opts = opts
-        self.cap = capacity
-        self.pcap = part_capacity or capacity
-        self.nranks = nranks
-        self.compact = compact
-        mk = lambda *shape, dt=t.int32: t.empty(shape, dtype=dt, device=device)  # noqa: E731
-        self.part = [mk(nranks * self.pcap * HDR_WORDS) for _ in range(slots)]  # flat: either record width
-        self.head = [mk(HEAD_LEN, dt=t.int64) for _ in range(slots)]
-        self.route_buf = [mk(capacity) for _ in range(slots)]
-        self.act = [mk(capacity) for _ in range(slots)]
-        self.order = [mk(capacity) for _ in range(slots)]
-        self.offsets = [mk(eng.n_act + 2) for _ in range(slots)]
-
-    def _stream(self, stream):
-        return (stream or self.t.cuda.current_stream()).cuda_stream
-
-    def partition(self, msgs, n, rank_of_silo, nranks, my_rank, slot: int = 0, stream=None, compact: bool = True):
-        assert n <= self.pcap and nranks <= self.nranks
-        head = self.head[slot]
-        st = self._stream(stream)
-        wide = not (compact and self.compact)
-        width = HDR_WORDS if wide else WIRE_WORDS
-        out = self.part[slot][:nranks * self.pcap * width].view(-1, width)
-        if wide:
-            self.part_eng.partition_by_owner_padded_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap, out,
-                                                           head, stream=st, opts=self.opts)
-            head[8:].zero_()
-        else:
-            head[8:].zero_()  # the kernel sets the low word of [8]
-            self.part_eng.partition_compact_device(msgs, n, rank_of_silo, nranks, my_rank, self.pcap, out, head,
-                                                   head[8:], stream=st, opts=self.opts)
-        regions = [out[r * self.pcap:(r + 1) * self.pcap] for r in range(nranks)]
-        return regions, head
-
-    def route(self, msgs, n, slot: int = 0, stream=None):
-        assert n <= self.cap
-        fn = self.eng.address_compact_device if msgs.shape[1] == WIRE_WORDS else self.eng.address_messages_device
-        fn(msgs, n, self.route_buf[slot], self.act[slot], self.order[slot], self.offsets[slot],
-           stream=self._stream(stream), opts=self.opts)
-        return self.route_buf[slot][:n], self.act[slot][:n], self.order[slot][:n], self.offsets[slot]
+@dataclass
+class Hop2Plan:
+    forward: bool
+    width: int
+    send: List[int]
+    recv: List[int]
+    n_hosted: int
+    n_forwarded: int
 
 
-class PipelinedRouter:
-    """The exchange protocol of one rank, with two batches in flight (overlap the exchange
-    with stages 1-4).
+def plan_chunk(heads: np.ndarray, me: int, written: int, max_recv: int, owned_total: np.ndarray) -> ChunkPlan:
+    """orl_node_plan_chunk over all-gathered head words (uint64 [nranks, HEAD_WORDS]); owned_total (uint64 [nranks]) is
+    updated in place.  Raises OrleansRouteError with the code every rank gets (E_CAPACITY, E_DEVICE)."""
+    import ctypes as C
+    h = np.ascontiguousarray(heads, np.uint64)
+    nr = h.shape[0]
+    assert h.shape == (nr, HEAD_WORDS) and owned_total.dtype == np.uint64 and owned_total.flags["C_CONTIGUOUS"]
+    out = L.orl_node_chunk_plan()
+    rc = L.load().orl_node_plan_chunk(L.ptr(h), nr, int(me), int(written), int(max_recv), L.ptr(owned_total), C.byref(out))
+    if rc != L.OK:
+        raise L.OrleansRouteError(rc, "orl_node_plan_chunk")
+    return ChunkPlan(out.width, bool(out.rewrite), list(out.send)[:nr], list(out.recv)[:nr], out.n_recv)
 
-    submit(batch k) enqueues, in this order:
-      1. route(k-1) on stream R, after the exchange of batch k-1 (its Works' wait() on R);
-      2. owner partition(k) on stream P, after route(k-2) released slot k % 2;
-      3. an all-gather of every rank's per-rank counts and wire status (the host reads them: the exchange
-         sizes, and whether the batch travels as 16-B compact records or, if any rank cannot, as 32-B headers);
-      4. the grouped send/recv of batch k's records (async; RCCL's stream, after P).
-    So on a GPU the RCCL exchange of batch k overlaps the routing of batch k-1, and the partition of batch
-    k+1 overlaps the exchange of batch k.  submit returns batch k-1's StepResult (None for the first batch);
-    flush() routes the last one; step() = submit + flush (one batch, nothing in flight).  Batch k's outputs
-    live in slot k % 2 and stay valid until submit(k + 2); on a GPU they are complete once stream R is
-    (flush() makes the current stream wait for it).  The executor needs 2 slots and, on a GPU, separate
-    contexts for partition and route (HipExecutor(part_eng=...)).  On the CPU (gloo) it all runs in order."""
 
-    def __init__(self, executor, rank: int, world: int, rank_of_silo: Sequence[int], capacity: int, torch_mod,
-                 device: str = "cuda", group=None):
-        t = torch_mod
-        self.ex = executor
-        self.rank = rank
-        self.world = world
-        self.ros = list(rank_of_silo)
-        self.t = t
-        self.group = group
-        self.cap = capacity
-        self.gpu = device != "cpu"
-        self.recv_flat = [t.empty(capacity * HDR_WORDS, dtype=t.int32, device=device) for _ in range(2)]
-        self.recv = [None, None]  # [n_recv, W] view of the received records of each slot
-        self.heads = [t.empty((world, HEAD_LEN), dtype=t.int64, device=device) for _ in range(2)]
-        if self.gpu:
-            self.sp, self.sr = t.cuda.Stream(), t.cuda.Stream()
-        self.route_done = [None, None]
-        self.pending = None  # (slot, works, exchanged event, n_recv, send_splits, recv_splits)
-        self.k = 0
-
-    def _on(self, stream):
-        return self.t.cuda.stream(stream) if self.gpu else contextlib.nullcontext()
-
-    def _route_pending(self) -> Optional[StepResult]:
-        if self.pending is None:
-            return None
-        slot, works, exchanged, n_recv, send_splits, recv_splits = self.pending
-        self.pending = None
-        with self._on(self.sr if self.gpu else None):
-            for w in works:
-                w.wait()
-            if exchanged is not None:
-                self.sr.wait_event(exchanged)
-            r = self.ex.route(self.recv[slot], n_recv, slot=slot, stream=self.sr if self.gpu else None)
-            if self.gpu:
-                ev = self.t.cuda.Event()
-                ev.record(self.sr)
-                self.route_done[slot] = ev
-        return StepResult(recv_splits, send_splits, *r, n_recv=n_recv)
-
-    def _exchange(self, slot, regions, send_splits, recv_splits):
-        """Grouped send/recv of every rank's region (self: a device copy).  Returns the Works to wait on."""
-        dist = self.t.distributed
-        recv_views, o = [], 0
-        for c in recv_splits:
-            recv_views.append(self.recv[slot][o:o + c])
-            o += c
-        ops = []
-        for r in range(self.world):
-            if r == self.rank:
-                if send_splits[r]:
-                    recv_views[r].copy_(regions[r][:send_splits[r]])
-                continue
-            if send_splits[r]:
-                ops.append(dist.P2POp(dist.isend, regions[r][:send_splits[r]], r, self.group))
-            if recv_splits[r]:
-                ops.append(dist.P2POp(dist.irecv, recv_views[r], r, self.group))
-        return dist.batch_isend_irecv(ops) if ops else []
-
-    def submit(self, msgs, n: int) -> Optional[StepResult]:
-        dist = self.t.distributed
-        slot = self.k % 2
-        self.k += 1
-        prev = self._route_pending()
-        exchanged = None
-        with self._on(self.sp if self.gpu else None):
-            if self.gpu:
-                self.sp.wait_stream(self.t.cuda.current_stream())  # the caller's batch is ready
-                if self.route_done[slot] is not None:
-                    self.sp.wait_event(self.route_done[slot])
-            st = self.sp if self.gpu else None
-            regions, head = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot, stream=st)
-            # every rank's counts + wire status in one collective: the exchange sizes, and whether all ranks
-            # can send compact records this batch (if one cannot, everyone re-partitions in the 32-B form)
-            if self.world == 1:
-                heads = [[int(x) for x in head.tolist()]]
-            else:
-                dist.all_gather_into_tensor(self.heads[slot], head.contiguous().view(1, -1), group=self.group)
-                heads = self.heads[slot].tolist()
-            if any(h[8] for h in heads):
-                regions, head = self.ex.partition(msgs, n, self.ros, self.world, self.rank, slot=slot, stream=st,
-                                                  compact=False)
-            send_splits = [int(x) for x in heads[self.rank][:self.world]]
-            recv_splits = [int(h[self.rank]) for h in heads]
-            n_recv = sum(recv_splits)
-            if n_recv > self.cap:
-                raise RuntimeError(f"rank {self.rank}: received {n_recv} messages > capacity {self.cap}")
-            width = regions[0].shape[1]
-            self.recv[slot] = self.recv_flat[slot][:n_recv * width].view(n_recv, width)
-            works = self._exchange(slot, regions, send_splits, recv_splits)
-            if self.gpu:
-                exchanged = self.t.cuda.Event()
-                exchanged.record(self.sp)
-        self.pending = (slot, works, exchanged, n_recv, send_splits, recv_splits)
-        return prev
-
-    def flush(self) -> Optional[StepResult]:
-        r = self._route_pending()
-        if self.gpu:
-            self.t.cuda.current_stream().wait_stream(self.sr)
-        return r
-
-    def step(self, msgs, n: int) -> StepResult:
-        """One batch with nothing in flight (submit + flush)."""
-        assert self.pending is None, "step() with a batch in flight: flush() first"
-        self.submit(msgs, n)
-        return self.flush()
+def plan_hop2(heads: np.ndarray, me: int, n_owned: int, width_mask: int, max_recv: int) -> Hop2Plan:
+    """orl_node_plan_hop2 over the all-gathered hop-2 words (uint64 [nranks, HEAD_WORDS])."""
+    import ctypes as C
+    h = np.ascontiguousarray(heads, np.uint64)
+    nr = h.shape[0]
+    out = L.orl_node_hop2_plan()
+    rc = L.load().orl_node_plan_hop2(L.ptr(h), nr, int(me), int(n_owned), int(width_mask), int(max_recv), C.byref(out))
+    if rc != L.OK:
+        raise L.OrleansRouteError(rc, "orl_node_plan_hop2")
+    return Hop2Plan(bool(out.forward), out.width, list(out.send)[:nr], list(out.recv)[:nr], out.n_hosted, out.n_forwarded)
 
 
 def narrow_records_to_headers(raw: np.ndarray, wire_types) -> np.ndarray:
@@ -322,6 +155,12 @@ class GrainNode:
         if rc != L.OK:
             raise L.OrleansRouteError(rc, "orl_node_unique_id failed")
         return bytes(buf)
+
+    def set_timeout(self, ms: int) -> None:
+        """Deadline of every host wait of the exchange (orl_node_set_timeout)."""
+        rc = self._lib.orl_node_set_timeout(self._node, int(ms))
+        if rc != L.OK:
+            raise L.OrleansRouteError(rc, "orl_node_set_timeout")
 
     def route_batch_device(self, d_msgs, n: int, stream=None, opts: int = 0) -> NodeResult:
         C = self._C

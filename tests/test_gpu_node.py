@@ -12,10 +12,11 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import pytest
 
+import node_replay as R
 from oracle import cpu_ref
 from orleans_amd import _lib as L
 from orleans_amd import workloads as W
-from orleans_amd.engine import GrainDirectoryEngine, decode_route
+from orleans_amd.engine import GrainDirectoryEngine
 from orleans_amd.node import GrainNode
 
 pytestmark = pytest.mark.gpu
@@ -30,101 +31,38 @@ def torch():
 
 class World:
     """W ranks: directory partitions by owner rank, activations on a host silo (owner or another), dense handles per
-    host rank (each rank's catalog numbers its own activations)."""
+    host rank (each rank's catalog numbers its own activations) — node_replay.population, one engine + one oracle per
+    rank."""
 
-    def __init__(self, nranks, n_grains=40_000, seed=3, host_mix=0.3, ros=None):
-        cl = W.default_cluster()
-        self.cl = cl
-        self.nr = nranks
-        self.ros = cl.rank_of_silo(nranks) if ros is None else np.asarray(ros, np.uint8)
-        keys, uni, owner, reg = W.grain_population(cl, n_grains, 0.9, seed)
-        rng = np.random.default_rng(seed)
-        host = np.where(rng.random(n_grains) < 1.0 - host_mix, owner, rng.integers(0, 8, n_grains)).astype(np.uint8)
-        hrank = self.ros[host]
-        act = np.zeros(n_grains, np.uint32)
-        cnt = []
-        for r in range(nranks):
-            idx = np.nonzero((hrank == r) & reg)[0]
-            act[idx] = np.arange(len(idx), dtype=np.uint32)
-            cnt.append(len(idx))
-        self.n_act = max(cnt) + 8
-        self.n_grains = n_grains
+    def __init__(self, nranks, n_grains=40_000, seed=3, host_mix=0.3, ros=None, cl=None, max_batch=1 << 20, reg_frac=0.9):
+        p = R.population(nranks, n_grains, seed, host_mix, ros, cl, reg_frac)
+        self.p = p
+        self.cl, self.nr, self.ros, self.n_act, self.n_grains = p.cl, nranks, p.ros, p.n_act, n_grains
         self.engs, self.oracles = [], []
         for r in range(nranks):
             local = (self.ros == r).astype(np.uint8)
-            e = GrainDirectoryEngine(n_act=self.n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+            sel = R.rank_selection(p, r)
+            e = GrainDirectoryEngine(n_act=self.n_act, dir_capacity=max(len(sel), 1024), max_batch=max_batch, device=0)
             e.set_silos(8, local=local)
-            o = cpu_ref.Oracle(8, local=list(local))
             for s in range(8):
-                e.add_server(s, int(cl.hashes[s]))
-                o.add_server(s, int(cl.hashes[s]))
-            sel = np.nonzero(reg & (self.ros[owner] == r))[0]
-            st, _, _ = e.register_single_activation(keys[sel], act[sel], host[sel])
+                e.add_server(s, int(self.cl.hashes[s]))
+            st, _, _ = e.register_single_activation(p.keys[sel], p.act[sel], p.host[sel])
             assert (st == L.INS_INSERTED).all()
-            o.register(keys[sel], act[sel], host[sel])
             self.engs.append(e)
-            self.oracles.append(o)
+            self.oracles.append(R.rank_oracle(p, r))
 
     def set_wire_types(self, mode):
-        """8-B exchange form: None (off), "both" (grain + system-target types on every rank), "grain_only" (system-target
-        messages lack the form), "mismatch" (the last rank's list differs: the digests disagree)."""
-        if mode is None:
-            return
-        grain_t = (L.CAT_GRAIN << 56) + (self.cl.type_code & 0x00FFFFFFFFFFFFFF)
-        sys_t = (L.CAT_SYSTEM_TARGET << 56) | 12
-        for r, e in enumerate(self.engs):
-            types = [grain_t] if mode == "grain_only" else [grain_t, sys_t]
-            if mode == "mismatch" and r == self.nr - 1:
-                types = [sys_t, grain_t]
-            e.set_wire_types(types)
+        """8-B exchange form per node_replay.wire_types(mode)."""
+        for e, types in zip(self.engs, R.wire_types(self.p, mode)):
+            if types:
+                e.set_wire_types(types)
 
     def messages(self, rank, n, seed, wide_at=None):
-        silos = np.nonzero(self.ros == rank)[0].astype(np.uint8)
-        m = W.uniform_messages(self.cl, self.n_grains + 3000, n, seed=seed, sender_silos=silos)
-        rng = np.random.default_rng(seed)
-        c = rng.random(n)
-        m["flags"][c < 0.03] = L.HDR_ADDRESS_COMPLETE  # responses: complete addresses, routed to the target silo
-        m["target_silo"][c < 0.03] = rng.integers(0, 8, int((c < 0.03).sum()))
-        st = (c >= 0.03) & (c < 0.05)
-        m["tcd"][st] = (np.uint64(L.CAT_SYSTEM_TARGET) << np.uint64(56)) | np.uint64(12)
-        if wide_at is not None:  # a Guid-keyed target: this chunk has no compact form
-            m["n0"][wide_at] = 0x1234
-        return m
+        return R.messages(self.p, rank, n, seed, wide_at)
 
     def expected(self, batches, chunks):
         """The oracle's replay of one batch per rank: per-rank (route, act, order, offsets, hosted headers)."""
-        nr, ros = self.nr, self.ros
-        owned = [[] for _ in range(nr)]
-        for c in range(chunks):
-            for s in range(nr):
-                ms = batches[s]
-                cs = -(-len(ms) // chunks)
-                lo = min(c * cs, len(ms))
-                ch = ms[lo:min(lo + cs, len(ms))]
-                src, cnt = self.oracles[0].partition(ch, ros, nr, s)
-                o0 = 0
-                for d in range(nr):
-                    owned[d].append(ch[src[o0:o0 + int(cnt[d])]])
-                    o0 += int(cnt[d])
-        owned = [np.concatenate(x) if x else np.zeros(0, L.MSG_DTYPE) for x in owned]
-        routed = [self.oracles[d].route(owned[d]) for d in range(nr)]
-        hostr = []
-        for d in range(nr):
-            h = decode_route(routed[d][0]).host
-            hostr.append(np.where(h == 0xFF, d, ros[np.minimum(h, 7).astype(np.int64)]))
-        forward = any((hostr[d] != d).any() for d in range(nr))
-        out = []
-        for hr in range(nr):
-            if forward:
-                sel = [hostr[o] == hr for o in range(nr)]
-                hdr = np.concatenate([owned[o][sel[o]] for o in range(nr)])
-                route = np.concatenate([routed[o][0][sel[o]] for o in range(nr)])
-                act = np.concatenate([routed[o][1][sel[o]] for o in range(nr)])
-            else:
-                hdr, (route, act) = owned[hr], routed[hr]
-            order, off = self.oracles[hr].bucket(act, self.n_act)
-            out.append((route, act, order, off, hdr))
-        return out, forward
+        return R.expected(self.oracles, self.ros, batches, chunks, self.n_act)
 
     def close(self):
         for e in self.engs:
@@ -188,7 +126,54 @@ def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix, wire):
     world.close()
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("host_mix", [0.0, 0.3])
+def test_node_config3_8ranks_vs_oracle(torch, host_mix):
+    """Config 3's 8-GPU split, as bench.py --gpus 8 runs it, on one GPU: 8 ranks over ORL_TRANSPORT_LOCAL (the same
+    protocol code as RCCL), the balanced ring, Zipf(1.1) over 16M grains (all registered), > 2M messages originated per
+    rank from its own silos, 4 chunks of 8-B orl_wire8 records; host_mix = 0.3 puts 30 % of the activations on another
+    silo, so hop 2 forwards.  Every rank's hosted route words, handles, order, offsets and headers == the oracle's replay.
+    Reference: OutboundMessageQueue.cs:113-145, LocalGrainDirectory.cs:439-497, ActivationData.cs:483-514."""
+    import time
+    t = torch
+    t0 = time.perf_counter()
+    log = lambda *a: print(f"[c3x8 {time.perf_counter() - t0:6.1f}s]", *a, flush=True)  # noqa: E731 (progress: long test)
+    nr, n_grains, chunks = 8, 16_000_000, 4
+    world = World(nr, n_grains=n_grains, seed=W.SEED_C3, host_mix=host_mix, cl=W.balanced_cluster(), max_batch=10 << 20,
+                  reg_frac=1.0)
+    world.set_wire_types("grain_only")
+    log("8 engines + 8 oracle directories registered")
+    batches = [W.zipf_messages(world.cl, n_grains, 2_000_003 + 1111 * r, seed=W.SEED_C3, start=r * 2_100_000,
+                               sender_silos=np.nonzero(world.ros == r)[0]) for r in range(nr)]
+    log("messages generated")
+    max_recv = 9 << 20
+    nodes = [GrainNode(world.engs[r], nr, r, world.ros, max_batch=len(batches[r]), max_recv=max_recv,
+                       transport=L.TRANSPORT_LOCAL, group_id=b"node-c3-8-%d" % int(host_mix * 10), chunks=chunks)
+             for r in range(nr)]
+    streams = [t.cuda.Stream() for _ in range(nr)]
+    got = _run(t, world, nodes, batches, streams)
+    log("node batch routed on the GPU")
+    exp, forward = world.expected(batches, chunks)
+    log("oracle replay done")
+    assert forward == (host_mix > 0)
+    owned = [g[0].n_owned for g in got]
+    assert max(owned) > 1.3 * (sum(owned) / nr), owned  # the Zipf-hot grain's owner (the imbalance the bench sees)
+    for r in range(nr):
+        res, (route, act, order, off, hdrs) = got[r]
+        er, ea, eo, ef, eh = exp[r]
+        assert {w for _, c, w in res.segments if c} == {8}
+        assert res.hop2 == forward and res.n_hosted == len(er)
+        np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} headers")
+        np.testing.assert_array_equal(route, er, err_msg=f"rank {r} route")
+        np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} act")
+        np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} order")
+        np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} offsets")
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_node_fanout_batch_vs_oracle(torch, nranks):
     """Config 4 sharded by publisher: every rank expands its own publishes (orl_node_fanout_batch_device) and the
     emitted messages are routed across the node; each rank's hosted output == the oracle's replay of the protocol over
@@ -281,4 +266,119 @@ def test_node_rccl_single_rank(torch):
     np.testing.assert_array_equal(order, eo)
     np.testing.assert_array_equal(off, ef)
     node.close()
+    world.close()
+
+
+def test_node_rccl_bounded_wait_aborts(torch, monkeypatch):
+    """A counts all-gather that cannot complete (fault injection: chunk 1's all-gather is followed on the exchange stream
+    by a kernel that waits for a host word nobody sets) fails within the node's deadline with ORL_E_STATE naming the chunk
+    and this rank's head words; the communicator is aborted, the node reports itself broken on the next call, and the
+    stalled stream drains (the injected kernel is released, so close() returns)."""
+    import time
+    t = torch
+    monkeypatch.setenv("ORL_NODE_INJECT_STALL", "1")
+    world = World(1, n_grains=30_000, host_mix=0.0)
+    node = GrainNode(world.engs[0], 1, 0, world.ros, max_batch=300_000, max_recv=300_000, transport=L.TRANSPORT_RCCL,
+                     group_id=GrainNode.unique_id(), chunks=3)
+    node.set_timeout(1500)
+    m = world.messages(0, 250_000, seed=9)
+    d_in = t.from_numpy(m.view(np.int32).reshape(-1, 8)).cuda()
+    t.cuda.synchronize()
+    t0 = time.perf_counter()
+    with pytest.raises(L.OrleansRouteError) as ei:
+        node.route_batch_device(d_in, len(m))
+    took = time.perf_counter() - t0
+    msg = str(ei.value)
+    assert ei.value.code == L.E_STATE, msg
+    assert "chunk 1" in msg and "communicator aborted" in msg and "head words" in msg, msg
+    assert took < 12, took
+    with pytest.raises(L.OrleansRouteError) as ei2:
+        node.route_batch_device(d_in, len(m))
+    assert ei2.value.code == L.E_STATE and "broken" in str(ei2.value)
+    node.close()
+    world.close()
+
+
+def test_node_local_barrier_timeout_breaks_group(torch):
+    """LOCAL transport: when one rank of two never calls, the other's barrier times out (ORL_E_STATE within the
+    deadline) and the group is broken, so the late rank fails at once instead of pairing with a later barrier."""
+    import time
+    t = torch
+    world = World(2, n_grains=20_000, host_mix=0.0)
+    nodes = [GrainNode(world.engs[r], 2, r, world.ros, max_batch=100_000, max_recv=200_000, transport=L.TRANSPORT_LOCAL,
+                       group_id=b"node-timeout", chunks=2) for r in range(2)]
+    for nd in nodes:
+        nd.set_timeout(1000)
+    batches = [world.messages(r, 50_000, seed=r) for r in range(2)]
+    d_in = [t.from_numpy(b.view(np.int32).reshape(-1, 8)).cuda() for b in batches]
+    t.cuda.synchronize()
+    t0 = time.perf_counter()
+    with pytest.raises(L.OrleansRouteError) as ei:
+        nodes[0].route_batch_device(d_in[0], len(batches[0]))
+    assert ei.value.code == L.E_STATE and "barrier timeout" in str(ei.value)
+    assert time.perf_counter() - t0 < 10
+    t1 = time.perf_counter()
+    with pytest.raises(L.OrleansRouteError) as ei:
+        nodes[1].route_batch_device(d_in[1], len(batches[1]))
+    assert ei.value.code == L.E_STATE
+    assert time.perf_counter() - t1 < 5
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
+@pytest.mark.parametrize("chunks", [3])
+def test_node_mixed_width_segments_aligned(torch, chunks):
+    """An odd number of 8-B records received in one chunk, then a 32-B chunk (a Guid-keyed target): every hosted segment
+    starts 32-B aligned and the hosted output still equals the oracle's replay (hop 2 forwards the mix as headers)."""
+    t = torch
+    world = World(2, n_grains=30_000, host_mix=0.3)
+    world.set_wire_types("both")
+    nodes = [GrainNode(world.engs[r], 2, r, world.ros, max_batch=100_000, max_recv=300_000, transport=L.TRANSPORT_LOCAL,
+                       group_id=b"node-align", chunks=chunks) for r in range(2)]
+    streams = [t.cuda.Stream() for _ in range(2)]
+    for b in range(3):
+        batches = [world.messages(r, 60_001 + 2 * r + 2 * b, seed=500 + 10 * b + r,
+                                  wide_at=(45_000 if (b >= 1 and r == 0) else None)) for r in range(2)]
+        got = _run(t, world, nodes, batches, streams)
+        exp, forward = world.expected(batches, chunks)
+        for r in range(2):
+            res, (route, act, order, off, hdrs) = got[r]
+            er, ea, eo, ef, eh = exp[r]
+            np.testing.assert_array_equal(hdrs, eh)
+            np.testing.assert_array_equal(route, er)
+            np.testing.assert_array_equal(act, ea)
+            np.testing.assert_array_equal(order, eo)
+            np.testing.assert_array_equal(off, ef)
+    for nd in nodes:
+        nd.close()
+    world.close()
+    # segment addresses: a world with no forwarding keeps the owned segments as the hosted ones.  Seeds are tried until
+    # the unpadded layout (segments back to back) would have left a wide segment misaligned on some rank.
+    world = World(2, n_grains=30_000, host_mix=0.0)
+    world.set_wire_types("both")
+    nodes = [GrainNode(world.engs[r], 2, r, world.ros, max_batch=100_000, max_recv=300_000, transport=L.TRANSPORT_LOCAL,
+                       group_id=b"node-align2", chunks=chunks) for r in range(2)]
+    hit = False
+    for seed in range(700, 716, 2):
+        batches = [world.messages(r, 60_001 + 2 * r, seed=seed + r, wide_at=(45_000 if r == 0 else None)) for r in range(2)]
+        got = _run(t, world, nodes, batches, streams)
+        exp, forward = world.expected(batches, chunks)
+        assert not forward
+        for r in range(2):
+            res, (route, act, order, off, hdrs) = got[r]
+            assert [w for _, c, w in res.segments] == [8, 8, 32], res.segments
+            assert all(p % 32 == 0 for p, c, w in res.segments), [(p % 32, c, w) for p, c, w in res.segments]
+            unpadded = np.cumsum([0] + [c * w for _, c, w in res.segments[:-1]])
+            hit |= bool((unpadded % 32 != 0).any())
+            np.testing.assert_array_equal(hdrs, exp[r][4])
+            np.testing.assert_array_equal(route, exp[r][0])
+            np.testing.assert_array_equal(act, exp[r][1])
+            np.testing.assert_array_equal(order, exp[r][2])
+            np.testing.assert_array_equal(off, exp[r][3])
+        if hit:
+            break
+    assert hit, "no seed produced an odd 8-B segment before a wide one"
+    for nd in nodes:
+        nd.close()
     world.close()

@@ -536,38 +536,6 @@ def test_route_batch_graph_replay(torch):
     eng.close()
 
 
-def test_pipelined_router_single_rank(torch):
-    """The N>1 code path on one GPU: PipelinedRouter with separate partition / route contexts on two streams,
-    two batches in flight; every batch's results equal the direct call's (world 1: the partition keeps the order)."""
-    from orleans_amd.node import HipExecutor, PipelinedRouter, rank_of_silo
-
-    t = torch
-    cl, eng, o = _random_setup(20_000, 20_000)
-    part_eng = GrainDirectoryEngine(n_act=1, dir_capacity=1, max_batch=1 << 20, device=0)
-    W.setup_engine(part_eng, cl)
-    cap = 300_000
-    router = PipelinedRouter(HipExecutor(eng, cap, t, part_eng=part_eng, slots=2, nranks=1), 0, 1, rank_of_silo(8, 1),
-                             cap, t)
-    batches = [W.uniform_messages(cl, 22_000, 250_000 - 1000 * b, seed=40 + b) for b in range(4)]
-    d_in = [t.from_numpy(m.view(np.int32).reshape(-1, 8)).cuda() for m in batches]
-    got = []
-    for b in range(len(batches) + 1):
-        res = router.submit(d_in[b], len(batches[b])) if b < len(batches) else router.flush()
-        if res is not None:
-            t.cuda.synchronize()
-            got.append([x.cpu().numpy().view(np.uint32).copy() for x in (res.route, res.act, res.order, res.offsets)])
-    assert len(got) == len(batches)
-    for m, (r, a, od, off) in zip(batches, got):
-        r_ref, a_ref = o.route(m)
-        np.testing.assert_array_equal(r, r_ref)
-        np.testing.assert_array_equal(a, a_ref)
-        o_ref, f_ref = o.bucket(a_ref, 20_000)
-        np.testing.assert_array_equal(od, o_ref)
-        np.testing.assert_array_equal(off, f_ref)
-    part_eng.close()
-    eng.close()
-
-
 def test_device_directory_mutation_vs_oracle(torch):
     """batched RegisterSingleActivation / Unregister on the device table == the oracle applying
     the same batches one message at a time (statuses, winners, removed flags), then routing over the mutated
