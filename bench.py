@@ -42,6 +42,12 @@ ROUTE_KERNEL_BYTES_PER_MSG = 72  # 32 B header + 32 B directory slot + 4 B route
 PIPELINE_BYTES_PER_MSG = 76      # + 4 B stable position
 FANOUT_BYTES_PER_MSG = 48        # 4 B CSR target + 32 B slot + 12 B outputs per emitted message
 FANOUT_BYTES_PER_PUB = 40        # + 32 B header + 8 B CSR offset per publish
+# config 5 (one mixed batch, Guid keys: the 32-B directory table): a direct game message reads its 32-B header and a 32-B
+# slot and writes 8 B; a player message reads its 4-B CSR target, its 24-B key-table entry and a 32-B slot and writes 8 B;
+# a publish reads its publisher id, silo and CSR start (4 + 1 + 8 B) and its u32 offset
+PRESENCE_BYTES_DIRECT = 72
+PRESENCE_BYTES_FANOUT = 68
+PRESENCE_BYTES_PER_PUB = 17
 
 
 def log(*a):
@@ -69,9 +75,13 @@ def main():
     ap.add_argument("--local-ranks", type=int, default=0,
                     help="rehearse the N-rank node exchange on ONE GPU: N ranks as threads over the in-process transport "
                          "(orl_node LOCAL); measures the protocol, not xGMI scaling")
-    ap.add_argument("--host-io", choices=["pinned", "pageable"], default=None,
-                    help="config 2 at N=1: time the host-array P/Invoke call (orl_route_batch: PCIe in and out) instead")
+    ap.add_argument("--host-io", choices=["pinned", "pageable", "narrow"], default=None,
+                    help="config 2 at N=1: time the host-array P/Invoke call instead (orl_route_batch: 32-B headers in over "
+                         "PCIe, route / act / order out; narrow = orl_route_batch_narrow: 8-B orl_wire8 records in, pinned)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--unregistered", type=float, default=0.0,
+                    help="configs 2/3: fraction of the grains never registered (SURVEY §8(d) config 2's 10%% variant: "
+                         "their messages miss the directory and are placed PreferLocal)")
     ap.add_argument("--wire16", action="store_true",
                     help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
@@ -175,7 +185,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     ros = rank_of_silo(cl.n_silos, world)
     mine = local_silos(cl.n_silos, world, rank)
     t_setup = time.perf_counter()
-    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    keys, uni, owner, reg = W.grain_population(cl, n_grains, 1.0 - args.unregistered)
     seed = W.SEED_C3 if zipf else W.SEED_C2
     ztab = W.zipf_tables(torch, n_grains, seed) if zipf else None
     # this rank's share of the workload's message stream, generated on the device (== the numpy generators)
@@ -269,13 +279,15 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     traffic = read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf)
+        cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf, 1.0 - args.unregistered)
     if node is not None:
         node.close()
     eng.close()
     name = (f"config3: Zipf(1.1) over {n_grains / 1e6:g}M long-key grains, {n_total >> 20}M messages in total "
             f"({n_msgs >> 20}M per GPU)" if zipf else
             f"config2: uniform {n_grains // 1_000_000}M long-key grains, {n_msgs >> 20}M single-target messages per GPU")
+    if args.unregistered:
+        name += f", {args.unregistered:.0%} of the grains unregistered (misses placed PreferLocal)"
     name += ", 8-silo ring, stages 1-4"
     if world > 1:
         name += (", + owner partition, RCCL counts all-gather + grouped send/recv, routing at the owner, hop 2, "
@@ -293,7 +305,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": f"synthetic (seeded splitmix64 on the device; config {args.config} of SURVEY §8(d))",
-        "config": {"workload": name, "grains": n_grains, "messages_total": n_total, "messages_per_gpu": n_msgs,
+        "config": {"workload": name, "grains": n_grains, "unregistered_frac": args.unregistered,
+                   "messages_total": n_total, "messages_per_gpu": n_msgs,
                    "silos": cl.n_silos, "ring": "balanced (silo generations %s)" % W.balanced_generations(cl.n_silos),
                    "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
@@ -406,29 +419,50 @@ def run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains):
     from orleans_amd import _lib as L
     msgs = d_msgs.cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
     outs = [np.empty(n_msgs, np.uint32) for _ in range(3)] + [np.empty(n_act + 2, np.uint32)]
-    pinned = args.host_io == "pinned"
+    narrow = args.host_io == "narrow"
+    pinned = args.host_io in ("pinned", "narrow")
+    rec_bytes = 8 if narrow else 32
+    if narrow:  # the silo's batch as 8-B records {N1 low 32 bits, meta} with the grain class as wire type 0
+        from orleans_amd import workloads as W
+        eng.set_wire_types([W.grain_tcd(cl)])
+        recs = np.empty((n_msgs, 2), np.uint32)
+        recs[:, 0] = msgs["n1"].astype(np.uint32)
+        recs[:, 1] = (msgs["sending_silo"].astype(np.uint32) | (msgs["category"].astype(np.uint32) << 8) |
+                      (msgs["flags"].astype(np.uint32) << 10) | (msgs["target_silo"].astype(np.uint32) << 24))
+        assert (msgs["n1"] < (1 << 32)).all() and (msgs["n0"] == 0).all()
+        src = recs
+
+        def call():
+            eng.route_batch_narrow_host(recs, *outs)
+    else:
+        src = msgs
+
+        def call():
+            eng.route_batch_host(msgs, *outs)
     if pinned:
-        for a in [msgs] + outs:
+        for a in [src] + outs:
             eng.host_register(a)
     for _ in range(max(1, args.warmup)):
-        eng.route_batch_host(msgs, *outs)
+        call()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.route_batch_host(msgs, *outs)
+        call()
     el = time.perf_counter() - t0
     if pinned:
-        for a in [msgs] + outs:
+        for a in [src] + outs:
             eng.host_unregister(a)
     eng.close()
-    pcie = n_msgs * (32 + 12) + 4 * (n_act + 2)
+    pcie = n_msgs * (rec_bytes + 12) + 4 * (n_act + 2)
     log(f"host io ({args.host_io}): {el * 1e3 / args.steps:.2f} ms per {n_msgs} messages, {pcie / (el / args.steps) / 1e9:.1f} GB/s PCIe")
     return {"metric": "routed grain messages/sec (node), host arrays over PCIe", "value": n_msgs * args.steps / el,
             "unit": "messages/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u32/u64 integer", "data": "synthetic (config 2)",
-            "config": {"workload": f"config2 through orl_route_batch with {args.host_io} host arrays: 32 B in, 12 B + offsets "
-                                   "out per message over PCIe, chunked upload / route / download overlap"},
-            "pcie_bytes_per_step": pcie, "pcie_GBs": pcie / (el / args.steps) / 1e9, "roofline": None, "cpu_baseline": None}
+            "config": {"workload": f"config2 through {'orl_route_batch_narrow' if narrow else 'orl_route_batch'} with "
+                                   f"{'pinned' if pinned else 'pageable'} host arrays: {rec_bytes} B in, 12 B + offsets out per "
+                                   "message over PCIe, chunked upload / route / download overlap"},
+            "pcie_bytes_per_step": pcie, "pcie_bytes_per_msg": pcie / n_msgs, "pcie_GBs": pcie / (el / args.steps) / 1e9,
+            "roofline": None, "cpu_baseline": None}
 
 
 def cpu_info():
@@ -443,7 +477,7 @@ def cpu_info():
     return model, os.cpu_count() or 1, len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf):
+def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf, reg_frac=1.0):
     """The oracle (C++ restatement of the reference per-message path: linear FindLast ring scan, unordered_map partition,
     per-activation FIFO) on the host cores, as the reference's CPU path stand-in (.NET cannot run here): on the box's CPU
     share (OMP_NUM_THREADS threads, the cores this job may use), on every CPU the OS lists (a bounded sample; the threads
@@ -455,11 +489,12 @@ def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf):
     model, ncpu, navail = cpu_info()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or navail
     share = max(1, min(share, navail))
-    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    keys, uni, owner, reg = W.grain_population(cl, n_grains, reg_frac)
     o = cpu_ref.Oracle(cl.n_silos)
     for s in range(cl.n_silos):
         o.add_server(s, int(cl.hashes[s]))
-    o.register(keys, np.arange(n_grains, dtype=np.uint32), owner)
+    idx = np.nonzero(reg)[0]
+    o.register(keys[idx], idx.astype(np.uint32), owner[idx])
     n_all = d_msgs.shape[0]
 
     def host(k):
@@ -494,6 +529,33 @@ def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf):
                       f"{' (the whole batch)' if n_mt == n_all else ''} on {share} threads (the box's CPU share) and on "
                       f"{runs.get('all_cpus', runs['share'])['threads']} threads, the first {n_1} on 1 thread; same "
                       f"directory, stages 1-4, oracle/cpu_ref.cpp ref_route_bucket_mt"}
+
+
+def cpu_step_baseline(o, make_msgs, n_act, target_wall, what):
+    """The oracle's stages 1-4 (ref_route_bucket_mt) over one step's messages, made by make_msgs() (the oracle's own
+    expansion for fan-out steps, timed with it), on the box's CPU share and on 1 thread."""
+    from oracle import cpu_ref  # noqa: F401  (the checker; outside every timed GPU region)
+    model, ncpu, navail = cpu_info()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or navail
+    share = max(1, min(share, navail))
+    runs = {}
+    for key, threads in (("share", share), ("one", 1)):
+        reps, n_done = 0, 0
+        t0 = time.perf_counter()
+        while True:
+            msgs = make_msgs()
+            o.route_bucket_mt(msgs, n_act, threads)
+            reps += 1
+            n_done += len(msgs)
+            if time.perf_counter() - t0 > target_wall / 2:
+                break
+        el = time.perf_counter() - t0
+        runs[key] = {"threads": threads, "messages": n_done, "seconds": el, "value": n_done / el, "steps": reps}
+    log("cpu baseline: " + ", ".join(f"{k} {r['threads']} threads {r['value'] / 1e6:.2f} M msgs/s" for k, r in runs.items()))
+    return {"value": runs["share"]["value"], "unit": "messages/s", "cores": share, "kind": "port", "cpu_model": model,
+            "threads_share": runs["share"], "threads_1": runs["one"], "box_thread_share_env": os.environ.get("OMP_NUM_THREADS"),
+            "sample": f"{runs['share']['steps']} whole steps ({what}) on {share} threads (the box's CPU share), "
+                      f"{runs['one']['steps']} on 1 thread; oracle/cpu_ref.cpp expansion + ref_route_bucket_mt"}
 
 
 # ---- config 1: Chirper generator graph, one silo --------------------------------------------------------------
@@ -626,6 +688,15 @@ def run_fanout(args, torch):
     eng.close()
     per_step = emitted / args.steps
     bytes_launch = FANOUT_BYTES_PER_MSG * per_step + FANOUT_BYTES_PER_PUB * n_pub
+    cpu = None
+    if not args.no_cpu:  # the oracle: the step's 1M publishes expanded (ref_fanout_expand) + stages 1-4, host cores
+        from oracle import cpu_ref
+        o = cpu_ref.Oracle(cl.n_silos)
+        for s_ in range(cl.n_silos):
+            o.add_server(s_, int(cl.hashes[s_]))
+        o.register(keys, np.arange(n_acc, dtype=np.uint32), owner)
+        cpu = cpu_step_baseline(o, lambda: cpu_ref.fanout_expand(csr_off, csr_tgt, pub_sets[0], owner[pub_sets[0]], tcd)[0],
+                                n_acc, args.cpu_wall * 2, f"{n_pub} publishes -> {totals[0]} messages")
     achieved = bytes_launch / (route_ms * 1e-3) / 1e9
     log(f"config 4: {elapsed * 1e3 / args.steps:.3f} ms/step, fan-out route kernel {route_ms:.3f} ms, "
         f"bucketing {bucket_ms:.3f} ms")
@@ -641,7 +712,7 @@ def run_fanout(args, torch):
                          "bytes_per_msg": FANOUT_BYTES_PER_MSG, "bytes_per_publish": FANOUT_BYTES_PER_PUB,
                          "avg_launch_ms": route_ms},
             "pipeline": {"route_kernel_ms": route_ms, "bucketing_ms": bucket_ms, "call_ms": total_ms},
-            "cpu_baseline": None}
+            "cpu_baseline": cpu}
 
 
 def run_fanout_node(args, torch, dist, rank, world, local_rank, rehearsal=False):
@@ -1128,9 +1199,40 @@ def run_presence(args, torch):
     s.synchronize()
     reps = max(1, steps // n_sets)
     thr_graph_all = thr_run(lambda i: g_all.replay(), reps)
+    # the route kernel's own time (HIP events around it on stream s), eager steps after the timed runs
+    roof = None
+    if mixed:
+        eng.set_timing(True)
+        with torch.cuda.stream(s):
+            for i in range(steps):
+                one(i % n_sets)
+        s.synchronize()
+        nb, route_ms, bucket_ms, total_ms = eng.timing_summary()
+        eng.set_timing(False)
+        bytes_launch = PRESENCE_BYTES_DIRECT * n_hb + PRESENCE_BYTES_FANOUT * n_fan + PRESENCE_BYTES_PER_PUB * n_hb
+        achieved = bytes_launch / (route_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_fanout_route (direct + fan-out, stages 5 + 1-3)", "achieved": achieved,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "bytes_per_launch": bytes_launch, "avg_launch_ms": route_ms, "bucketing_ms": bucket_ms, "call_ms": total_ms,
+                "note": "a 590k-message step fills the chip for ~10 us per kernel: launch- and latency-bound, not HBM-bound"}
     eng.close()
     if eng2 is not eng:
         eng2.close()
+    cpu = None
+    if not args.no_cpu:  # the oracle over the same step: game messages + the player fan-out named by the key table
+        from oracle import cpu_ref
+        o = cpu_ref.Oracle(cl.n_silos)
+        for s_ in range(cl.n_silos):
+            o.add_server(s_, int(cl.hashes[s_]))
+        o.register(all_keys, np.arange(n_keys, dtype=np.uint32), owner)
+        g0, m0 = batches[0]
+
+        def make_msgs():
+            exp, _ = cpu_ref.fanout_expand(pr.csr_off, pr.csr_tgt, g0, owner[g0.astype(np.int64)], 0)
+            k = pr.player_keys[exp["n1"].astype(np.int64)]
+            exp["tcd"], exp["n0"], exp["n1"] = k["tcd"], k["n0"], k["n1"]
+            return np.concatenate([m0, exp])
+        cpu = cpu_step_baseline(o, make_msgs, n_keys, args.cpu_wall, f"{n_hb} game messages + {n_fan} player messages")
     value = per_step * steps / thr_graph
     log(f"config 5: eager {thr_eager * 1e3 / steps:.3f} ms/step (p50 {np.percentile(lat_eager, 50):.3f}, "
         f"p99 {np.percentile(lat_eager, 99):.3f} ms); graph {thr_graph * 1e3 / steps:.3f} ms/step "
@@ -1150,7 +1252,7 @@ def run_presence(args, torch):
                            "graph_p99": float(np.percentile(lat_graph, 99))},
             "throughput_msgs_per_s": {"eager": per_step * steps / thr_eager, "graph": value,
                                       f"graph_{n_sets}_steps_per_launch": per_step * reps * n_sets / thr_graph_all},
-            "roofline": None, "cpu_baseline": None}
+            "roofline": roof, "cpu_baseline": cpu}
 
 
 if __name__ == "__main__":

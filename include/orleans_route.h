@@ -258,6 +258,13 @@ int orl_hash_batch(orl_ctx* ctx, const orl_grain_key* keys, size_t n, uint32_t* 
  * Host-buffer form (P/Invoke): copies in/out over PCIe and synchronises. */
 int orl_route_batch(orl_ctx* ctx, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
                     uint32_t* order, uint32_t* bucket_offsets);
+/* Host-array form over 8-byte orl_wire8 records in the context's wire types (orl_wire_types_set): the narrow P/Invoke
+ * call a silo makes per batch when its targets are long-key grains of known classes with 32-bit keys (the common case:
+ * GrainId.GetGrainId(typeCode, long key), GrainId.cs:90-97).  PCIe carries 8 B in and 8 B out per message (+ 4 B of
+ * order) instead of 32 + 8 (+ 4); outputs as orl_route_batch.  Replaces the per-message Dispatcher.AddressMessage
+ * (src/OrleansRuntime/Core/Dispatcher.cs:555-579). */
+int orl_route_batch_narrow(orl_ctx* ctx, const orl_wire8* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                           uint32_t* order, uint32_t* bucket_offsets);
 /* Device-resident form: all pointers in HBM; enqueued on `stream` (hipStream_t, NULL = default). */
 int orl_route_batch_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route,
                            uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
@@ -646,6 +653,9 @@ int orl_sync(orl_ctx* ctx);
 #define ORL_Q_WIRE_DIGEST 8u  /* FNV-1a digest of the wire types (orl_wire_types_set), 0 when the 8-B form is off */
 #define ORL_Q_PART_ERROR 9u   /* 1 if a one-pass partition's look-back gave up since the last query (read and cleared;
                                  synchronises the context's device) */
+#define ORL_Q_HOT_KEY 10u     /* stage 4's hot key: the activation handle (n_act = the unresolved bucket) whose messages the
+                                 next batch of >= 2^20 messages places without sorting, picked from the last such batch
+                                 (>= 1/32 of its messages); 0xFFFFFFFF = none.  Outputs never depend on it.  Synchronises. */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 /* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
  * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */

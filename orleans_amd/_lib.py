@@ -61,6 +61,7 @@ MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_U
 Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_RANK_MODE = 1, 2, 3, 4, 5, 6, 7
 Q_WIRE_DIGEST = 8
 Q_PART_ERROR = 9
+Q_HOT_KEY = 10
 MAX_WIRE_TYPES = 16
 PART_LOOKBACK_FAILED = 0x4
 
@@ -130,6 +131,7 @@ _SIGS = {
     "orl_dir_lookup_host": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_hash_batch": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "orl_route_batch": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
+    "orl_route_batch_narrow": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
     "orl_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
     "orl_fanout_route_device": (C.c_int, [_P, _P, _P, _P, _P, C.c_size_t, C.c_uint64, C.c_uint32, _P, _P, _P, _P, _P,
                                           C.POINTER(C.c_uint64), _P]),

@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.hot);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->hev) if (e) (void)hipEventDestroy(e);
@@ -788,7 +788,7 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         // histogram rows: one per 4096-element radix tile, or one per route workgroup for small batches (route
         // tiles shrink to 256 messages while a batch has < 2048 x 256 x 2 messages: at most 4096 rows)
         const uint64_t rows = std::max<uint64_t>(tiles, std::min<uint64_t>(4096, (mb + 255) / 256));
-        const uint64_t hist_words = (1ull << kMaxDigitBits) * rows;
+        const uint64_t hist_words = ((1ull << kMaxDigitBits) + 1) * rows;  // + the hot-key column
         if ((e = hipMalloc((void**)&c->s.pairs_a, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_a)");
         if ((e = hipMalloc((void**)&c->s.pairs_b, mb * 8)) != hipSuccess) return bail(e, "hipMalloc(pairs_b)");
         if ((e = hipMalloc((void**)&c->s.idx_a, (mb + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(idx)");
@@ -815,9 +815,14 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         c->s.lb_ticket = 0;
         c->s.lb_epoch = 0;
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
-        if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * (1ull << kMaxDigitBits) * 4)) != hipSuccess)
+        if ((e = hipMalloc((void**)&c->s.col_sums, ((rows + 63) / 64) * ((1ull << kMaxDigitBits) + 1) * 4)) != hipSuccess)
             return bail(e, "hipMalloc(col_sums)");
-        if ((e = hipMalloc((void**)&c->s.col_tot, (1ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMalloc(col_tot)");
+        if ((e = hipMalloc((void**)&c->s.col_tot, ((1ull << kMaxDigitBits) + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(col_tot)");
+        if ((e = hipMalloc((void**)&c->s.hot, 16)) != hipSuccess) return bail(e, "hipMalloc(hot)");
+        {
+            const uint32_t init[4] = {0xFFFFFFFFu, 0u, 0u, 0u};  // no hot key yet; pick counter and accumulator zero
+            if ((e = hipMemcpy(c->s.hot, init, 16, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "hipMemcpy(hot)");
+        }
         if ((e = hipMalloc((void**)&c->st_off, ((size_t)cfg->n_act + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(offsets)");
     }
     *out = c;
@@ -1077,15 +1082,17 @@ int orl_route_narrow_device(orl_ctx* c, const orl_wire8* d_in, size_t n, uint32_
 // (the context's stream) and the download of its route words / handles (second copy stream) overlap with the
 // neighbouring chunks', and stage 4 runs once over the whole batch at the end.  Caller arrays registered with
 // orl_host_register (pinned) are copied asynchronously at full PCIe rate; pageable ones go through the runtime's
-// staging (correct, slower).
-int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
-                    uint32_t* order, uint32_t* offsets) {
+// staging (correct, slower).  fmt = the input record width (32 = orl_msg_hdr, 8 = orl_wire8).
+namespace {
+int route_batch_host(orl_ctx* c, const void* in, int fmt, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                     uint32_t* order, uint32_t* offsets) {
     if (!c) return ORL_E_INVALID;
     if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     if (n && (!in || !route || !act)) return fail(c, ORL_E_INVALID, "null host buffer");
     if (buckets && (!offsets || (n && !order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
     if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    if (fmt == 8 && c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     int r = ensure_staging(c, std::max<size_t>(n, 1) * sizeof(orl_msg_hdr), std::max<size_t>(n, 1) * 3);
     if (r) return r;
@@ -1096,17 +1103,19 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
     uint32_t* d_route = c->st_out;
     uint32_t* d_act = d_route + n;
     uint32_t* d_order = d_act + n;
-    const orl_msg_hdr* d_in = reinterpret_cast<const orl_msg_hdr*>(c->st_in);
+    const uint8_t* h_in = static_cast<const uint8_t*>(in);
+    const size_t esz = (size_t)fmt;
     const size_t chunk = std::max<size_t>(kHostChunk, (n + kHostChunks - 1) / kHostChunks);
     hipStream_t up = c->hstream[0], down = c->hstream[1];
     size_t k = 0;
     for (size_t lo = 0; lo < n; lo += chunk, ++k) {
         const size_t len = std::min(chunk, n - lo);
         hipEvent_t ev_up = c->hev[2 * (k % (kHostChunks + 1))], ev_rt = c->hev[2 * (k % (kHostChunks + 1)) + 1];
-        ORL_HIP(c, hipMemcpyAsync(c->st_in + lo * sizeof(orl_msg_hdr), in + lo, len * sizeof(orl_msg_hdr), hipMemcpyHostToDevice, up));
+        ORL_HIP(c, hipMemcpyAsync(c->st_in + lo * esz, h_in + lo * esz, len * esz, hipMemcpyHostToDevice, up));
         ORL_HIP(c, hipEventRecord(ev_up, up));
         ORL_HIP(c, hipStreamWaitEvent(c->stream, ev_up, 0));
-        if ((r = route_impl(c, d_in + lo, 32, len, opts | ORL_OPT_NO_BUCKETS, d_route + lo, d_act + lo, nullptr, nullptr, c->stream)))
+        if ((r = route_impl(c, c->st_in + lo * esz, fmt, len, opts | ORL_OPT_NO_BUCKETS, d_route + lo, d_act + lo, nullptr, nullptr,
+                            c->stream)))
             return r;
         ORL_HIP(c, hipEventRecord(ev_rt, c->stream));
         ORL_HIP(c, hipStreamWaitEvent(down, ev_rt, 0));
@@ -1123,6 +1132,17 @@ int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, 
     ORL_HIP(c, hipStreamSynchronize(down));
     ORL_HIP(c, hipStreamSynchronize(up));
     return ORL_OK;
+}
+}  // namespace
+
+int orl_route_batch(orl_ctx* c, const orl_msg_hdr* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                    uint32_t* order, uint32_t* offsets) {
+    return route_batch_host(c, in, 32, n, opts, route, act, order, offsets);
+}
+
+int orl_route_batch_narrow(orl_ctx* c, const orl_wire8* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
+                           uint32_t* order, uint32_t* offsets) {
+    return route_batch_host(c, in, 8, n, opts, route, act, order, offsets);
 }
 
 namespace {
@@ -1897,6 +1917,15 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             std::lock_guard<std::mutex> lk(g_rank_mu);
             *v = (uint64_t)(int64_t)g_rank_state[c->cfg.device];
+            return ORL_OK;
+        }
+        case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
+            if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+            ORL_HIP(c, hipSetDevice(c->cfg.device));
+            ORL_HIP(c, hipDeviceSynchronize());
+            uint32_t w = 0;
+            ORL_HIP(c, hipMemcpy(&w, c->s.hot, 4, hipMemcpyDeviceToHost));
+            *v = w;
             return ORL_OK;
         }
         case ORL_Q_PART_ERROR: {  // the look-back state's error word (lb_state[1]), read and cleared

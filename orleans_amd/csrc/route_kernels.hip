@@ -413,20 +413,23 @@ __device__ __forceinline__ uint32_t wave_hot_digit(uint32_t d) {
 // input); the hot-digit peel when one digit covers many lanes of the first step (an unsorted Zipf stream); else one
 // returning LDS atomic per element.
 
-template <int BITS, bool PACKED, int N, int RM = kRmRuntime>
-__device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
-                                           uint32_t flags) {
+// SKIP: elements with skip[j] set are not ranked (stage 4's hot-key path places them apart); every mode ranks the
+// active lanes of a step under the exec mask, so skipped lanes never touch a counter.
+template <int BITS, bool PACKED, int N, int RM, bool SKIP>
+__device__ __forceinline__ void rank_steps_impl(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
+                                                uint32_t flags, const bool* skip) {
     const uint32_t lane = __lane_id();
+#define ORL_ON(j) ((j) * 64u + lane < lim && !(SKIP && skip[j]))
     if (RM == kRmPlain) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            if (j * 64u + lane < lim) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
+            if (ORL_ON(j)) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
         return;
     }
     if (RM == kRmBallot || (RM == kRmRuntime && (flags & kRankBallot))) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            if (j * 64u + lane < lim) rank[j] = wave_rank_ballot<BITS, PACKED>(cnt, d[j], __builtin_amdgcn_read_exec(), lanes_below());
+            if (ORL_ON(j)) rank[j] = wave_rank_ballot<BITS, PACKED>(cnt, d[j], __builtin_amdgcn_read_exec(), lanes_below());
         return;
     }
     bool hot = false;
@@ -434,19 +437,32 @@ __device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N]
     if (hot) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            if (j * 64u + lane < lim) rank[j] = rank_step_uniform<PACKED>(cnt, d[j]);
+            if (ORL_ON(j)) rank[j] = rank_step_uniform<PACKED>(cnt, d[j]);
         return;
     }
     const uint32_t dh = ((RM == kRmHot || (flags & kRankUniform)) && lim >= 64u) ? wave_hot_digit(d[0]) : kNoHot;
     if (dh != kNoHot) {
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            if (j * 64u + lane < lim) rank[j] = rank_step_peel<PACKED>(cnt, d[j], dh);
+            if (ORL_ON(j)) rank[j] = rank_step_peel<PACKED>(cnt, d[j], dh);
         return;
     }
 #pragma unroll
     for (int j = 0; j < N; ++j)
-        if (j * 64u + lane < lim) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
+        if (ORL_ON(j)) rank[j] = counter_add<PACKED>(cnt, d[j], 1u);
+#undef ORL_ON
+}
+
+template <int BITS, bool PACKED, int N, int RM = kRmRuntime>
+__device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
+                                           uint32_t flags) {
+    rank_steps_impl<BITS, PACKED, N, RM, false>(cnt, d, lim, rank, flags, nullptr);
+}
+
+template <int BITS, bool PACKED, int N, int RM = kRmRuntime>
+__device__ __forceinline__ void rank_steps(uint32_t* cnt, const uint32_t (&d)[N], uint32_t lim, uint32_t (&rank)[N],
+                                           uint32_t flags, const bool (&skip)[N]) {
+    rank_steps_impl<BITS, PACKED, N, RM, true>(cnt, d, lim, rank, flags, skip);
 }
 
 // The lane-order self-check: every wave ranks pseudo-random digit streams (uniform 10-bit, 8 hot of 1024, 4 distinct,
@@ -555,7 +571,29 @@ template <int HB>
 struct RouteSmem {
     RouteParams P;
     uint32_t hist[HB ? (1u << HB) : 1u];
+    uint32_t hot;  // messages of the batch's hot activation (stage 4's hot-key path): counted apart from their digit
 };
+
+// Stage 4's hot-key path (bucket_after_route): the messages of ONE activation the previous batch found hot (>= 1/32 of
+// a batch) skip the two-level sort.  The histogram pass counts them in an extra column (stride bins + 1) instead of
+// their digit, the MSD pass writes their indices straight to a contiguous run in arrival order, and after the offsets
+// scan one copy puts that run at the activation's place in `order`: 16 instead of 32 bytes of stage-4 traffic per
+// message (the Zipf-hot grain: half of the hot rank's messages at 8 ranks; the unresolved bucket of a batch with misses).
+// hot words (Scratch::hot): [0] the key in use (kNoHotKey: none), [1] the pick kernel's done counter, [2..3] u64 max of
+// (count << 32 | key) accumulated by the pick.
+constexpr uint32_t kNoHotKey = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t hot_key_of(const uint32_t* hot) {
+    return hot ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(hot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : kNoHotKey;
+}
+
+// Adds this lane's hot count to *dst with one LDS atomic per wave.
+__device__ __forceinline__ void wave_add_hot(uint32_t* dst, uint32_t mine) {
+    uint32_t v = mine;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d, 64);
+    if ((threadIdx.x & 63u) == 0 && v) atomicAdd(dst, v);
+}
 
 // FMT: the input is orl_msg_hdr (32), or exchange records: orl_wire_msg (16) or orl_wire8 (8, decoded with the
 // context's wire types).
@@ -576,14 +614,18 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
-                                                         uint32_t bins, uint32_t shift, uint32_t items) {
+                                                         uint32_t bins, uint32_t shift, uint32_t items,
+                                                         const uint32_t* __restrict__ hot_words) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
+    if (threadIdx.x == 0) sm.hot = 0;
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
+    const uint32_t hk = HIST ? hot_key_of(hot_words) : kNoHotKey;  // hot_words != null: rows of bins + 1 (the hot column)
+    uint32_t hot_mine = 0;
     const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
     for (uint32_t j = 0; j < items; ++j) {
@@ -620,7 +662,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
-                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+                if (HIST) {
+                    const uint32_t k = bucket_key(act, n_act);
+                    if (k == hk) ++hot_mine;
+                    else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
+                }
             }
             continue;
         }
@@ -650,7 +696,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
-                if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+                if (HIST) {
+                    const uint32_t k = bucket_key(act, n_act);
+                    if (k == hk) ++hot_mine;
+                    else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
+                }
             }
             continue;
         }
@@ -680,13 +730,20 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
             store_drop(route + e, rr);
             store_drop(act_out + e, act);
-            if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+            if (HIST) {
+                const uint32_t k = bucket_key(act, n_act);
+                if (k == hk) ++hot_mine;
+                else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
+            }
         }
     }
     if (HIST) {
+        if (hot_words) wave_add_hot(&sm.hot, hot_mine);
         __syncthreads();
-        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
+        const uint32_t stride = bins + (hot_words ? 1u : 0u);
+        uint32_t* row = tile_hist + (size_t)blockIdx.x * stride;
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
+        if (hot_words && threadIdx.x == 0) row[bins] = sm.hot;
     }
 }
 
@@ -855,10 +912,15 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 // first digit's histogram for stage 4 over messages routed earlier (orl_bucket_device, the host side of hop 2).
 template <bool ACTS>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
-                                                    uint32_t bins, uint32_t* __restrict__ tile_hist) {
+                                                    uint32_t bins, uint32_t* __restrict__ tile_hist,
+                                                    const uint32_t* __restrict__ hot_words = nullptr) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
+    __shared__ uint32_t hot;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
+    if (threadIdx.x == 0) hot = 0;
     __syncthreads();
+    const uint32_t hk = ACTS ? hot_key_of(hot_words) : kNoHotKey;  // hot_words != null: rows of bins + 1
+    uint32_t hot_mine = 0;
     const uint32_t base = blockIdx.x * kTile;
     uint32_t k[kItems];
     if (ACTS) {  // arrival order: element j * 256 + x (coalesced)
@@ -869,7 +931,11 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
-            if (base + j * 256 + threadIdx.x < n) atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
+            if (base + j * 256 + threadIdx.x < n) {
+                if (k[j] == hk) ++hot_mine;
+                else atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
+            }
+        if (hot_words) wave_add_hot(&hot, hot_mine);
     } else {
         // pairs of an LSD pass: sorted by the previous digit, so a hot key's pairs sit in consecutive lanes.  Loads stay
         // coalesced (element j * 256 + x); each run of equal digits inside a 64-lane step adds its length with one
@@ -895,8 +961,10 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
         }
     }
     __syncthreads();
-    uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
+    const uint32_t stride = bins + ((ACTS && hot_words) ? 1u : 0u);
+    uint32_t* row = tile_hist + (size_t)blockIdx.x * stride;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
+    if (ACTS && hot_words && threadIdx.x == 0) row[bins] = hot;
 }
 
 // Column scan of the [ntiles][bins] count matrix, in chunks of kScanRows tiles.
@@ -1078,15 +1146,20 @@ struct PassSmem : PassSmemCore<BITS, ITEMS> {
 
 // ITEMS: elements per thread; the tile is 256 * ITEMS (the MSD pass of the two-level path takes kMsdItems: half the
 // digit-histogram rows of 4096-element tiles and twice the run length per digit in its scattered writes).
+// hot_words (IN_ACT + OUT_PAIR only; rows of B + 1 words): the hot key's elements are not ranked; their indices go to
+// hot_idx[row's hot column base + rank among the tile's hot elements] (arrival order), a run at the end of hot_idx.
 template <int BITS, int IN, int OUT, int ITEMS, int RM>
 __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
-                                                    uint32_t* __restrict__ key_out) {
+                                                    uint32_t* __restrict__ key_out, const uint32_t* __restrict__ hot_words,
+                                                    uint32_t* __restrict__ hot_idx) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
+    constexpr bool HOTP = IN == IN_ACT && OUT == OUT_PAIR;
     __shared__ PassSmem<BITS, ITEMS> sm;
+    __shared__ uint32_t hotw[kWaves];
     const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
@@ -1110,17 +1183,47 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             idx[j] = v.y;
         }
     }
+    const uint32_t hk = HOTP ? hot_key_of(hot_words) : kNoHotKey;
+    bool ishot[ITEMS];
+    uint32_t hrank[ITEMS];
+    if (HOTP && hk != kNoHotKey) {  // the hot key's elements: ranked among themselves by lane prefix, in arrival order
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < ITEMS; ++j) {
+            ishot[j] = wbase + j * 64u + lane < n && key[j] == hk;
+            const uint64_t b = __ballot(ishot[j]);
+            hrank[j] = run + (uint32_t)__popcll(b & lanes_below());
+            run += (uint32_t)__popcll(b);
+        }
+        if (lane == 0) hotw[w] = run;
+    }
     __syncthreads();
     {
         uint32_t dg[ITEMS];
 #pragma unroll
         for (uint32_t j = 0; j < ITEMS; ++j) dg[j] = (key[j] >> shift) & (B - 1u);
-        rank_steps<BITS, true, ITEMS, RM>(&sm.cnt[w][0], dg, n > wbase ? n - wbase : 0u, rank, rflags);
+        if (HOTP && hk != kNoHotKey) rank_steps<BITS, true, ITEMS, RM>(&sm.cnt[w][0], dg, n > wbase ? n - wbase : 0u, rank, rflags, ishot);
+        else rank_steps<BITS, true, ITEMS, RM>(&sm.cnt[w][0], dg, n > wbase ? n - wbase : 0u, rank, rflags);
     }
     __syncthreads();
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
-    // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
-    const uint32_t* orow = tile_off + (size_t)tile * row_step * B;
+    // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base); with the hot
+    // path the rows have one more column, the hot key's
+    const uint32_t row_stride = (HOTP && hot_words) ? B + 1u : B;
+    const uint32_t* orow = tile_off + (size_t)tile * row_step * row_stride;
+    uint32_t tile_hot = 0;
+    if (HOTP && hk != kNoHotKey) {
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kWaves; ++q) {
+            before += q < w ? hotw[q] : 0u;
+            tile_hot += hotw[q];
+        }
+        const uint32_t hb = orow[B] + before;  // absolute: the hot run fills hot_idx[n - hot total, n)
+#pragma unroll
+        for (uint32_t j = 0; j < ITEMS; ++j)
+            if (ishot[j] && hb + hrank[j] < n) hot_idx[hb + hrank[j]] = idx[j];
+    }
     uint32_t tot[PER], start[PER], dl[PER];
     round_starts<BITS>(sm.cnt, reinterpret_cast<uint32_t*>(&sm.stage[0]), tot, start);  // the scan's wave sums: stage is free here
 #pragma unroll
@@ -1131,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
-        if (wbase + j * 64u + lane < n) {
+        if (wbase + j * 64u + lane < n && !(HOTP && hk != kNoHotKey && ishot[j])) {
             const uint32_t d = (key[j] >> shift) & (B - 1u);
             const uint32_t lpos = packed_get(sm.cnt[w], d) + rank[j];
             sm.stage[lpos] = make_uint2(key[j], idx[j]);
@@ -1143,7 +1246,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     for (uint32_t q = 0; q < PER; ++q)
         if (threadIdx.x * PER + q < B) delta[threadIdx.x * PER + q] = dl[q];
     __syncthreads();
-    const uint32_t cnt = (n - tbase) < TILE ? (n - tbase) : TILE;
+    const uint32_t cnt = ((n - tbase) < TILE ? (n - tbase) : TILE) - tile_hot;
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t i = j * 256u + threadIdx.x;
@@ -3054,6 +3157,61 @@ int scan_inplace(uint32_t* a, uint64_t m, const Scratch& s, hipStream_t st) {
 // (32 = 8192-element tiles measured slower: route 1297 -> 1321 us, MSD pass 221 -> 256 us; profiles/r02_stage4_ab.txt)
 constexpr uint32_t kMsdItems = 16;
 
+// ---- stage 4's hot-key path: the three small steps around the two-level sort (see kNoHotKey) -------------------------
+// After the segment scan wrote per-key counts into offsets (the hot key's is 0: its elements were not in any segment),
+// before the offsets scan: the hot key's count (the hot column's total) is added.
+__global__ void k_hot_finish(const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total, uint32_t nb,
+                             uint32_t* __restrict__ offsets) {
+    const uint32_t hk = hot_key_of(hot_words);
+    if (threadIdx.x == 0 && hk < nb) offsets[hk] += *hot_total;
+}
+
+// After the offsets scan: the hot run (hot_idx[n - total, n), arrival order) is copied to order[offsets[hk] ...).
+__global__ __launch_bounds__(256) void k_hot_copy(const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
+                                                  uint32_t n, uint32_t nb, const uint32_t* __restrict__ hot_idx,
+                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
+    const uint32_t hk = hot_key_of(hot_words);
+    if (hk >= nb) return;
+    const uint32_t cnt = *hot_total, off = offsets[hk];
+    if (cnt > n || off > n - cnt) return;  // inconsistent counts: never write out of bounds
+    const uint32_t* src = hot_idx + (n - cnt);
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = src[i];
+}
+
+// After the batch's offsets are final: the most frequent key of this batch becomes the next batch's hot key when it holds
+// >= 1/32 of the batch (and >= 2 segments' worth); else none.  Keys [0, nkeys) from offsets[k + 1] - offsets[k]; one u64
+// atomicMax of (count << 32 | key) per block, and the last block to finish decides and resets the accumulator.
+constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
+__global__ __launch_bounds__(256) void k_hot_pick(const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t n,
+                                                  uint32_t* __restrict__ hot_words) {
+    __shared__ unsigned long long bmax[kWaves];
+    unsigned long long best = 0;
+    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nkeys; k += gridDim.x * 256u) {
+        const uint32_t c = offsets[k + 1] - offsets[k];
+        const unsigned long long v = ((unsigned long long)c << 32) | k;
+        best = v > best ? v : best;
+    }
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(best, (int)d, 64);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63u) == 0) bmax[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (uint32_t q = 1; q < kWaves; ++q) best = bmax[q] > best ? bmax[q] : best;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(hot_words + 2);
+    atomicMax(acc, best);
+    __threadfence();
+    if (atomicAdd(&hot_words[1], 1u) != gridDim.x - 1) return;
+    __threadfence();
+    const unsigned long long v = atomicExch(acc, 0ull);
+    const uint32_t c = (uint32_t)(v >> 32), k = (uint32_t)v;
+    const bool hot = (uint64_t)c * kHotShare >= n && c >= kHotMinCount;
+    __hip_atomic_store(&hot_words[0], hot ? k : kNoHotKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&hot_words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Messages per thread of a route launch feeding stage 4 for n_act activations: the MSD tile of the two-level path,
 // else the LSD tile.
 uint32_t max_route_items(uint32_t n_act) {
@@ -3079,10 +3237,11 @@ uint32_t route_items(uint64_t n, uint32_t max_items) {
 
 template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
-                      uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
+                      uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
+                      const uint32_t* hot_words, uint32_t* hot_idx) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
-                                                row_step, ntiles, pout, order, keys)
+                                                row_step, ntiles, pout, order, keys, hot_words, hot_idx)
 #define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
@@ -3103,9 +3262,11 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
 }
 
 void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
-                 uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st) {
+                 uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
+                 const uint32_t* hot_words = nullptr, uint32_t* hot_idx = nullptr) {
     switch (bits) {
-#define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st); break;
+#define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
+                                                hot_words, hot_idx); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3138,7 +3299,7 @@ RouteHist route_hist(uint32_t n_act) {
 
 template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
+                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
     const uint32_t nb = n_act + 2;
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
@@ -3156,18 +3317,25 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
                        s.seg_meta, d_offsets);
     hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
                        d_offsets);
+    if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, s.hot, s.col_tot + nbk, nb, d_offsets);
     scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
+    if (hot) {
+        hipLaunchKernelGGL(k_hot_copy, dim3(std::min<uint32_t>(ceil_div(n, 256u * 8u), 2048u)), dim3(256), 0, st, s.hot,
+                           s.col_tot + nbk, n, nb, s.sorted_keys, d_offsets, d_order);
+        hipLaunchKernelGGL(k_hot_pick, dim3(std::min<uint32_t>(ceil_div(n_act + 1, 256u * 8u), 512u)), dim3(256), 0, st,
+                           d_offsets, n_act + 1, n, s.hot);
+    }
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
+                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
     switch (lb) {
-#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st); break;
+#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3186,11 +3354,24 @@ bool stage4_soa() {
     return soa;
 }
 
+// The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair
+// layout; ORL_NO_HOT=1 turns it off (A/B).
+bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
+    static const bool off = [] {
+        const char* e = getenv("ORL_NO_HOT");
+        return e && e[0] == '1';
+    }();
+    if (off || !s.hot || n < kHotMinBatch || stage4_soa()) return false;
+    const BucketPlan bp = make_bucket_plan(n_act);
+    return bp.two_level && bp.hb > 0;
+}
+
 // Stage 4 after a route kernel that already wrote route_hist()'s tile histogram into s.tile_hist.
 //   two-level: [MSD pass by the high digit → pairs_a] → segment count → segment scan → offsets scan → scatter;
 //   LSD fallback: passes act → pairs_a → pairs_b → ... → (order, sorted keys); offsets from the sorted keys.
+// hot: the histogram pass wrote rows of 2^hb + 1 words (the hot column, hot_words != null in it): the hot-key path.
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t route_items, uint32_t* d_order,
-                       uint32_t* d_offsets, const Scratch& s, hipStream_t st) {
+                       uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
     const BucketPlan bp = make_bucket_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
@@ -3204,20 +3385,20 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st);
+            col_scan(s.tile_hist, nrows0, nbk + (hot ? 1u : 0u), row_step0, s, st);
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
-                            nullptr, nullptr, st);
+                            nullptr, nullptr, st, hot ? s.hot : nullptr, hot ? s.sorted_keys : nullptr);
             }
             kin = s.pairs_a;
         }
         hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
         const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
-        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st);
+        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
@@ -3317,17 +3498,19 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const RouteHist rh = route_hist(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     const bool hist = buckets && rh.on;
+    const bool hot = hist && hot_path_on(n, n_act, s);
+    const uint32_t* hw = hot ? s.hot : nullptr;
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
-                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items)
+                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
-                                            shift, items)
+                                            shift, items, hw)
         if (hist) {
             if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
         } else {
@@ -3345,7 +3528,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     int e = (int)hipGetLastError();
     if (e) return e;
     if (!buckets) return 0;
-    return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st);
+    return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st, hot);
 }
 
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
@@ -3408,7 +3591,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     if (ev_route_end) (void)hipEventRecord((hipEvent_t)ev_route_end, st);
     int e = (int)hipGetLastError();
     if (e || !buckets) return e;
-    return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st);
+    return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st, false);
 }
 
 int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
@@ -3581,12 +3764,13 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
     if (n == 0) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
     const RouteHist rh = route_hist(n_act);
     const uint32_t ntiles = ceil_div(n, kTile);
+    const bool hot = rh.on && hot_path_on(n, n_act, s);
     if (rh.on)
         hipLaunchKernelGGL(k_hist_pairs<true>, dim3(ntiles), dim3(256), 0, st, d_act, (uint32_t)n, n_act, rh.shift, rh.bins,
-                           s.tile_hist);
+                           s.tile_hist, hot ? s.hot : nullptr);
     int e = (int)hipGetLastError();
     if (e) return e;
-    return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st);
+    return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st, hot);
 }
 
 int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_ros, uint32_t my_rank, uint64_t* d_counts,

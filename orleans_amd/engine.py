@@ -264,6 +264,16 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_route_batch(self._ctx, ptr(msgs), len(msgs), int(opts), ptr(route), ptr(act), ptr(order),
                                            ptr(offsets)))
 
+    def route_batch_narrow_host(self, recs: np.ndarray, route: np.ndarray, act: np.ndarray, order: Optional[np.ndarray],
+                                offsets: Optional[np.ndarray], opts: int = 0) -> None:
+        """orl_route_batch_narrow: 8-B orl_wire8 records (uint32 pairs {n1, meta}) in host memory, outputs into caller
+        arrays (order / offsets None: ORL_OPT_NO_BUCKETS)."""
+        if order is None:
+            opts |= L.OPT_NO_BUCKETS
+        n = recs.size * recs.itemsize // 8
+        self._ck(self._lib.orl_route_batch_narrow(self._ctx, ptr(recs), n, int(opts), ptr(route), ptr(act), ptr(order),
+                                                  ptr(offsets)))
+
     def host_register(self, a: np.ndarray) -> None:
         """Page-lock a host array for asynchronous full-rate copies (a pinned GCHandle buffer on the C# side)."""
         self._ck(self._lib.orl_host_register(self._ctx, ptr(a), a.nbytes))

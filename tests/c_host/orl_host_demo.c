@@ -5,10 +5,12 @@
  *   1. context + silo table + ring from SiloAddress consistent hashes (orl_silo_consistent_hash of "10.0.0.s:11111")
  *   2. RegisterSingleActivation of 50k long-key grains (orl_dir_insert_single), type code = CalculateIdHash(class name)
  *   3. a batch of 200k headers (~9 % never registered, some complete addresses) through
- *      a. orl_route_batch on page-locked host arrays (orl_host_register), and
+ *      a. orl_route_batch on page-locked host arrays (orl_host_register),
  *      b. device buffers it allocates through the library (orl_device_alloc / orl_copy_to_device /
- *         orl_route_batch_device / orl_copy_to_host / orl_stream_sync)
- *   4. both compared word for word with the oracle's route + stable bucketing of the same batch.
+ *         orl_route_batch_device / orl_copy_to_host / orl_stream_sync), and
+ *      c. the narrow call: the same batch as 8-byte orl_wire8 records (orl_wire_types_set with the grain class),
+ *         orl_route_batch_narrow on page-locked arrays
+ *   4. all three compared word for word with the oracle's route + stable bucketing of the same batch.
  *
  * Build: gcc -std=c11 -O2 -I include tests/c_host/orl_host_demo.c -L orleans_amd -lorleans_route
  *        -L oracle -lorleans_cpu_ref -Wl,-rpath,<dirs> -o tools/orl_host_demo        (tests/test_c_host.py does this)
@@ -159,10 +161,32 @@ int main(void) {
     void* bufs[] = {d_in, d_route, d_act, d_order, d_off};
     for (size_t k = 0; k < sizeof bufs / sizeof bufs[0]; ++k) check(ctx, orl_device_free(ctx, bufs[k]), "orl_device_free");
 
+    /* c: the narrow call — {N1 low 32 bits, sending silo | category << 8 | flags << 10 | wire type << 16 | target silo
+     * << 24} per message, the grain class as wire type 0 (include/orleans_route.h orl_wire8) */
+    check(ctx, orl_wire_types_set(ctx, 1, &tcd), "orl_wire_types_set");
+    orl_wire8* recs = calloc(N_MSGS, sizeof *recs);
+    for (size_t i = 0; i < N_MSGS; ++i) {
+        recs[i].n1 = (uint32_t)msgs[i].target.n1;
+        recs[i].meta = (uint32_t)msgs[i].sending_silo | ((uint32_t)msgs[i].category << 8) | ((uint32_t)msgs[i].flags << 10) |
+                       ((uint32_t)msgs[i].target_silo << 24);
+    }
+    memset(route, 0, N_MSGS * 4);
+    memset(act, 0, N_MSGS * 4);
+    memset(order, 0, N_MSGS * 4);
+    memset(off, 0, nb * 4);
+    void* pinned[] = {recs, route, act, order};
+    for (size_t k = 0; k < 4; ++k)
+        check(ctx, orl_host_register(ctx, pinned[k], N_MSGS * (k == 0 ? sizeof *recs : 4)), "orl_host_register");
+    check(ctx, orl_route_batch_narrow(ctx, recs, N_MSGS, 0, route, act, order, off), "orl_route_batch_narrow");
+    for (size_t k = 0; k < 4; ++k) check(ctx, orl_host_unregister(ctx, pinned[k]), "orl_host_unregister");
+    bad |= compare("route (narrow)", route, er, N_MSGS) | compare("act (narrow)", act, ea, N_MSGS) |
+           compare("order (narrow)", order, eo, N_MSGS) | compare("offsets (narrow)", off, ef, nb);
+    free(recs);
+
     ref_dir_free(dir);
     check(ctx, orl_ctx_destroy(ctx), "orl_ctx_destroy");
     if (bad) return 1;
-    printf("c host ok: %d messages through orl_route_batch (pinned host arrays) and orl_route_batch_device "
-           "(library-allocated buffers), bit-exact vs the oracle\n", N_MSGS);
+    printf("c host ok: %d messages through orl_route_batch (pinned host arrays), orl_route_batch_device "
+           "(library-allocated buffers) and orl_route_batch_narrow (8-B records), bit-exact vs the oracle\n", N_MSGS);
     return 0;
 }

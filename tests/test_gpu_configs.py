@@ -576,3 +576,69 @@ def test_stage4_rank_modes_vs_oracle(torch, n_act):
     finally:
         eng.set_rank_mode(0)
     eng.close()
+
+
+@pytest.mark.parametrize("n_act", [1_000_000, 2_000_000])
+def test_stage4_hot_key_path_vs_oracle(torch, n_act):
+    """Stage 4's hot-key path (route_kernels.hip kNoHotKey): a batch of >= 2^20 messages picks its most frequent key when
+    it holds >= 1/32 of the batch; the next batch places that key's messages without sorting them.  Every batch, with
+    the hot key right, wrong, absent or the unresolved bucket, is bit-exact vs the oracle's stable bucketing
+    (ActivationData.EnqueueMessage FIFO, ActivationData.cs:483-514).  n_act 1M: 10 + 10-bit plan; 2M: 11 + 10 (the hot
+    rank of config 3 at 8 ranks)."""
+    t = torch
+    rng = np.random.default_rng(n_act)
+    o = cpu_ref.Oracle(8)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=5_000_000, device=0)
+    W.setup_engine(eng, W.default_cluster())
+
+    def batch(n, hot=None, share=0.0, unresolved=0.0):
+        a = rng.integers(0, n_act, n, dtype=np.int64).astype(np.uint32)
+        u = rng.random(n)
+        if hot is not None:
+            a[u < share] = hot
+        a[(u >= share) & (u < share + unresolved)] = L.NO_ACT
+        return a
+
+    hot1, hot2 = 123_457 % n_act, n_act - 3
+    plan = [(batch(4_000_003, hot1, 0.30), hot1),          # picks hot1
+            (batch(3_000_001, hot1, 0.55), hot1),          # uses hot1 (the hot rank's share), picks it again
+            (batch(2_500_000, hot2, 0.20), hot2),          # uses hot1 (now rare), picks hot2
+            (batch(2_000_000), None),                       # uses hot2 (absent), picks none
+            (batch(2_000_000, unresolved=0.10), n_act),     # no hot key; picks the unresolved bucket (misses)
+            (batch(1_500_000, unresolved=0.10), n_act),     # uses the unresolved bucket
+            (batch(900_000, hot1, 0.9), n_act)]             # below 2^20 messages: no hot path, pick unchanged
+    off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
+    for k, (a, expect_next) in enumerate(plan):
+        d_act = t.from_numpy(a.view(np.int32)).cuda()
+        order = t.empty(len(a), dtype=t.int32, device="cuda")
+        eng.bucket_device(d_act, len(a), order, off)
+        t.cuda.synchronize()
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), eo, err_msg=f"batch {k} order")
+        np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), ef, err_msg=f"batch {k} offsets")
+        nxt = eng.query(L.Q_HOT_KEY)
+        assert nxt == (0xFFFFFFFF if expect_next is None else expect_next), (k, nxt)
+    # the route path (stage 4 after k_route's histogram) with misses: 10 % unregistered targets, two batches
+    cl = W.default_cluster()
+    n_grains = 200_000
+    keys, uni, owner, reg = W.grain_population(cl, n_grains, 0.9)
+    eng2 = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=3_000_000, device=0)
+    W.setup_engine(eng2, cl)
+    W.register_population(eng2, keys, owner, reg)
+    o2 = _oracle_for(cl, keys[reg], np.nonzero(reg)[0].astype(np.uint32), owner[reg])
+    for b in range(2):
+        m = W.uniform_messages(cl, n_grains, 2_100_000 + b, seed=77 + b)
+        d_in = t.from_numpy(m.view(np.uint8).reshape(-1, 32)).cuda()
+        outs = [t.empty(len(m), dtype=t.int32, device="cuda") for _ in range(3)]
+        off2 = t.empty(n_grains + 2, dtype=t.int32, device="cuda")
+        eng2.address_messages_device(d_in, len(m), *outs, off2)
+        t.cuda.synchronize()
+        r, a = o2.route(m)
+        eo, ef = o2.bucket(a, n_grains)
+        np.testing.assert_array_equal(outs[0].cpu().numpy().view(np.uint32), r)
+        np.testing.assert_array_equal(outs[1].cpu().numpy().view(np.uint32), a)
+        np.testing.assert_array_equal(outs[2].cpu().numpy().view(np.uint32), eo, err_msg=f"route batch {b} order")
+        np.testing.assert_array_equal(off2.cpu().numpy().view(np.uint32), ef)
+        assert eng2.query(L.Q_HOT_KEY) == n_grains  # the unresolved bucket (PreferLocal placements) is hot
+    eng2.close()
+    eng.close()

@@ -143,31 +143,35 @@ def test_node_config3_8ranks_vs_oracle(torch, host_mix):
                   reg_frac=1.0)
     world.set_wire_types("grain_only")
     log("8 engines + 8 oracle directories registered")
-    batches = [W.zipf_messages(world.cl, n_grains, 2_000_003 + 1111 * r, seed=W.SEED_C3, start=r * 2_100_000,
-                               sender_silos=np.nonzero(world.ros == r)[0]) for r in range(nr)]
-    log("messages generated")
     max_recv = 9 << 20
-    nodes = [GrainNode(world.engs[r], nr, r, world.ros, max_batch=len(batches[r]), max_recv=max_recv,
+    nodes = [GrainNode(world.engs[r], nr, r, world.ros, max_batch=2_200_000, max_recv=max_recv,
                        transport=L.TRANSPORT_LOCAL, group_id=b"node-c3-8-%d" % int(host_mix * 10), chunks=chunks)
              for r in range(nr)]
     streams = [t.cuda.Stream() for _ in range(nr)]
-    got = _run(t, world, nodes, batches, streams)
-    log("node batch routed on the GPU")
-    exp, forward = world.expected(batches, chunks)
-    log("oracle replay done")
-    assert forward == (host_mix > 0)
-    owned = [g[0].n_owned for g in got]
-    assert max(owned) > 1.3 * (sum(owned) / nr), owned  # the Zipf-hot grain's owner (the imbalance the bench sees)
-    for r in range(nr):
-        res, (route, act, order, off, hdrs) = got[r]
-        er, ea, eo, ef, eh = exp[r]
-        assert {w for _, c, w in res.segments if c} == {8}
-        assert res.hop2 == forward and res.n_hosted == len(er)
-        np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} headers")
-        np.testing.assert_array_equal(route, er, err_msg=f"rank {r} route")
-        np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} act")
-        np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} order")
-        np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} offsets")
+    for b in range(2):  # the second batch runs stage 4's hot-key path at the hot rank (its key picked by the first)
+        batches = [W.zipf_messages(world.cl, n_grains, 2_000_003 + 1111 * r - 77 * b, seed=W.SEED_C3,
+                                   start=(8 * b + r) * 2_100_000, sender_silos=np.nonzero(world.ros == r)[0])
+                   for r in range(nr)]
+        log(f"batch {b}: messages generated")
+        got = _run(t, world, nodes, batches, streams)
+        log(f"batch {b}: node batch routed on the GPU")
+        exp, forward = world.expected(batches, chunks)
+        log(f"batch {b}: oracle replay done")
+        assert forward == (host_mix > 0)
+        owned = [g[0].n_owned for g in got]
+        assert max(owned) > 1.3 * (sum(owned) / nr), owned  # the Zipf-hot grain's owner (the imbalance the bench sees)
+        for r in range(nr):
+            res, (route, act, order, off, hdrs) = got[r]
+            er, ea, eo, ef, eh = exp[r]
+            assert {w for _, c, w in res.segments if c} == {8}
+            assert res.hop2 == forward and res.n_hosted == len(er)
+            np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} batch {b} headers")
+            np.testing.assert_array_equal(route, er, err_msg=f"rank {r} batch {b} route")
+            np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} batch {b} act")
+            np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} batch {b} order")
+            np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} batch {b} offsets")
+    hot_rank = int(np.argmax([g[0].n_hosted for g in got]))
+    assert world.engs[hot_rank].query(L.Q_HOT_KEY) != 0xFFFFFFFF  # the hot rank's stage 4 found its hot activation
     for nd in nodes:
         nd.close()
     world.close()
@@ -362,6 +366,9 @@ def test_node_mixed_width_segments_aligned(torch, chunks):
     hit = False
     for seed in range(700, 716, 2):
         batches = [world.messages(r, 60_001 + 2 * r, seed=seed + r, wide_at=(45_000 if r == 0 else None)) for r in range(2)]
+        for m in batches:  # no complete addresses: nothing is forwarded, the owned segments are the hosted ones
+            m["flags"][:] = 0
+            m["target_silo"][:] = 0
         got = _run(t, world, nodes, batches, streams)
         exp, forward = world.expected(batches, chunks)
         assert not forward
