@@ -670,7 +670,7 @@ bool keys_equal(const DirSlot& s, const orl_grain_key& k) {
 // Probe the mirror: returns slot index of the key, or -1; *free_slot = first reusable slot on the chain.
 int64_t dir_find(const orl_ctx* c, const orl_grain_key& k, int64_t* free_slot) {
     const uint32_t h = jenkins3(k.type_code_data, k.n0, k.n1);
-    uint64_t i = fmix32(h) & c->mask;
+    uint64_t i = dir_slot(h, c->mask);
     int64_t fr = -1;
     for (uint64_t step = 0; step <= c->mask; ++step) {
         const DirSlot& s = c->table[i];
@@ -1464,7 +1464,7 @@ int orl_dir_compact(orl_ctx* c) {
     c->count = c->tombs = 0;
     for (const DirSlot& d : old) {  // re-insert every live entry in slot order (lookups are layout-independent)
         if (d.state != SLOT_FULL) continue;
-        uint64_t i = fmix32(jenkins3(d.tcd, d.n0, d.n1)) & c->mask;
+        uint64_t i = dir_slot(jenkins3(d.tcd, d.n0, d.n1), c->mask);
         while (c->table[i].state != SLOT_EMPTY) i = (i + 1) & c->mask;
         c->table[i] = d;
         ++c->count;

@@ -64,6 +64,13 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     return h;
 }
 
+// Start slot of a key in a directory table of mask + 1 (a power of two, <= 2^32) slots: the HIGH bits of fmix32(uniform
+// hash) (multiply-shift), so the table's eighths are fmix32(h) >> 29 whatever its size — the slice a node rank can name
+// for a message without knowing the owner's table size.
+__host__ __device__ inline uint64_t dir_slot(uint32_t h, uint64_t mask) {
+    return ((uint64_t)fmix32(h) * (mask + 1)) >> 32;
+}
+
 // ---- Jenkins lookup2, 24-byte form (JenkinsHash.cs:54-65, 126-144) ---------------------------------
 #define ORL_MIX(a, b, c)                 \
     do {                                 \

@@ -268,7 +268,7 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
     const bool vc = r == kNeedProbeCache;
     const u32x4* dir4 = reinterpret_cast<const u32x4*>(vc ? cache : dir);
     const uint64_t mask = vc ? cmask : dmask;
-    uint64_t slot = fmix32(h) & mask;
+    uint64_t slot = dir_slot(h, mask);
     uint32_t fact = 0, fsilo = 0;
     int st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
     for (uint64_t step = 0; st == 2 && step < mask; ++step) {
@@ -293,7 +293,7 @@ __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirS
     const uint32_t mk = probe_type(P, m);
     if (mk != kNoType) {
         const u32x4* p4 = reinterpret_cast<const u32x4*>(probe);
-        uint64_t slot = fmix32(h) & dmask;
+        uint64_t slot = dir_slot(h, dmask);
         st = probe_slot16(p4[slot], m.n1, mk, fact, fsilo);
         for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
             slot = (slot + 1) & dmask;
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
                 if (r == kNeedProbe) {
                     can = probe8_key(sm.P, m);
-                    slot = fmix32(h) & dmask;
+                    slot = dir_slot(h, dmask);
                     if (can) q = reinterpret_cast<const uint2*>(probe)[slot];
                 }
             }
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
                 if (r == kNeedProbe) {
                     mk = probe_type(sm.P, m);
-                    slot = fmix32(h) & dmask;
+                    slot = dir_slot(h, dmask);
                     if (mk != kNoType) sa = reinterpret_cast<const u32x4*>(probe)[slot];
                 }
             }
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                     dir4 = reinterpret_cast<const u32x4*>(cache);
                     mask = cmask;
                 }
-                slot = fmix32(h) & mask;
+                slot = dir_slot(h, mask);
                 sa = dir4[2 * slot];
                 sb = dir4[2 * slot + 1];
             }
@@ -2585,7 +2585,7 @@ constexpr uint32_t kRetryLimit = 1u << 22;
 template <bool LAST_WINS>
 __device__ __forceinline__ int find_or_claim(DirSlot* __restrict__ dir, uint64_t mask, uint32_t* __restrict__ claim,
                                              const orl_grain_key& k, uint32_t tag, uint64_t& slot_out, bool& was_tomb_out) {
-    const uint64_t start = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
+    const uint64_t start = dir_slot(jenkins3(k.type_code_data, k.n0, k.n1), mask);
     int outcome = -1;  // 0 = existing FULL entry, 1 = candidate for a claimed slot
     uint64_t slot = start;
     bool was_tomb = false;
@@ -2878,7 +2878,7 @@ __global__ __launch_bounds__(256) void k_dir_rm_probe(const DirSlot* __restrict_
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const orl_grain_key k = keys[i];
-    uint64_t slot = fmix32(jenkins3(k.type_code_data, k.n0, k.n1)) & mask;
+    uint64_t slot = dir_slot(jenkins3(k.type_code_data, k.n0, k.n1), mask);
     uint32_t out = kSlotNone;
     for (uint64_t step = 0; step <= mask; ++step) {
         const uint8_t state = dir[slot].state;

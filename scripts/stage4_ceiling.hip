@@ -9,6 +9,8 @@
 //   scatter  read pairs (8 B, stream) -> write index (4 B) to its final position: runs of 4 (16 B) per key per
 //            segment, keys 64 elements apart (each 64-B line gets 16 B from 4 segments)
 //   + the streaming floors of the same byte counts (contiguous writes).
+// "occ3": the launch reserves dynamic LDS so at most 3 workgroups share a CU, the occupancy the real scatter kernels run
+// at (4 per CU made config 2's stage 4 slower — more partial lines in flight per L2).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/stage4_ceiling scripts/stage4_ceiling.hip
 #include <hip/hip_runtime.h>
 
@@ -162,14 +164,19 @@ int main() {
         fflush(stdout);
     };
     const dim3 b(256), gs(8192);
+    const size_t occ3 = 50 * 1024, occ3_lds = 18 * 1024;  // 3 x 50 KB <= 160 KB < 4 x 50 KB
     timeit("stream: read 4 B, write 8 B (MSD bytes, contiguous)", 12.0 * n, [&] { hipLaunchKernelGGL((k_stream<4, 8>), gs, b, 0, 0, act, n, reinterpret_cast<uint32_t*>(pairs2)); });
     timeit("msd floor: read act, 8-B runs of 4/digit/tile, linear tiles", 12.0 * n, [&] { hipLaunchKernelGGL(k_msd_floor<false>, dim3(ntiles), b, 0, 0, act, n, ntiles, pairs2); });
     timeit("msd floor: same, XCD-aware tile order", 12.0 * n, [&] { hipLaunchKernelGGL(k_msd_floor<true>, dim3(ntiles), b, 0, 0, act, n, ntiles, pairs2); });
+    timeit("msd floor: XCD order, occ3", 12.0 * n, [&] { hipLaunchKernelGGL(k_msd_floor<true>, dim3(ntiles), b, occ3, 0, act, n, ntiles, pairs2); });
     timeit("msd floor + LDS staging image (XCD order)", 12.0 * n, [&] { hipLaunchKernelGGL(k_msd_floor_lds, dim3(ntiles), b, 0, 0, act, n, ntiles, pairs2); });
+    timeit("msd floor + LDS staging image (XCD order), occ3", 12.0 * n, [&] { hipLaunchKernelGGL(k_msd_floor_lds, dim3(ntiles), b, occ3_lds, 0, act, n, ntiles, pairs2); });
     timeit("stream: read 8 B (count bytes)", 8.0 * n, [&] { hipLaunchKernelGGL((k_stream<8, 0>), gs, b, 0, 0, reinterpret_cast<uint32_t*>(pairs), n, order); });
     timeit("count floor: read pairs per segment, no LDS", 8.0 * n, [&] { hipLaunchKernelGGL(k_count_floor<false>, dim3(ntiles), b, 0, 0, pairs, n, hist); });
     timeit("count floor + 1 LDS atomic per element (1024 bins)", 8.0 * n, [&] { hipLaunchKernelGGL(k_count_floor<true>, dim3(ntiles), b, 0, 0, pairs, n, hist); });
+    timeit("count floor + LDS atomics, occ3", 8.0 * n, [&] { hipLaunchKernelGGL(k_count_floor<true>, dim3(ntiles), b, occ3, 0, pairs, n, hist); });
     timeit("stream: read 8 B, write 4 B (scatter bytes)", 12.0 * n, [&] { hipLaunchKernelGGL((k_stream<8, 4>), gs, b, 0, 0, reinterpret_cast<uint32_t*>(pairs), n, order); });
     timeit("scatter floor: 16-B runs per key per segment", 12.0 * n, [&] { hipLaunchKernelGGL(k_scatter_floor, dim3(ntiles), b, 0, 0, pairs, n, order); });
+    timeit("scatter floor, occ3", 12.0 * n, [&] { hipLaunchKernelGGL(k_scatter_floor, dim3(ntiles), b, occ3, 0, pairs, n, order); });
     return 0;
 }
