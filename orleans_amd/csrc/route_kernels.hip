@@ -3166,25 +3166,24 @@ __global__ void k_hot_finish(const uint32_t* __restrict__ hot_words, const uint3
     if (threadIdx.x == 0 && hk < nb) offsets[hk] += *hot_total;
 }
 
-// After the offsets scan: the hot run (hot_idx[n - total, n), arrival order) is copied to order[offsets[hk] ...).
-__global__ __launch_bounds__(256) void k_hot_copy(const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
-                                                  uint32_t n, uint32_t nb, const uint32_t* __restrict__ hot_idx,
-                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
-    const uint32_t hk = hot_key_of(hot_words);
-    if (hk >= nb) return;
-    const uint32_t cnt = *hot_total, off = offsets[hk];
-    if (cnt > n || off > n - cnt) return;  // inconsistent counts: never write out of bounds
-    const uint32_t* src = hot_idx + (n - cnt);
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = src[i];
-}
-
-// After the batch's offsets are final: the most frequent key of this batch becomes the next batch's hot key when it holds
-// >= 1/32 of the batch (and >= 2 segments' worth); else none.  Keys [0, nkeys) from offsets[k + 1] - offsets[k]; one u64
-// atomicMax of (count << 32 | key) per block, and the last block to finish decides and resets the accumulator.
+// The end of a batch's stage 4, one launch: (1) the hot run (hot_idx[n - total, n), arrival order) is copied to
+// order[offsets[hk] ...); (2) the most frequent key of this batch becomes the next batch's hot key when it holds >= 1/32
+// of the batch (and >= 2 segments' worth), else none: keys [0, nkeys) from offsets[k + 1] - offsets[k], one u64 atomicMax
+// of (count << 32 | key) per block; the last block to finish (every block has read the current key by then) decides and
+// resets the accumulator.
 constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
-__global__ __launch_bounds__(256) void k_hot_pick(const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t n,
-                                                  uint32_t* __restrict__ hot_words) {
+__global__ __launch_bounds__(256) void k_hot_tail(uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
+                                                  uint32_t n, uint32_t nkeys, const uint32_t* __restrict__ hot_idx,
+                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
     __shared__ unsigned long long bmax[kWaves];
+    const uint32_t hk = hot_key_of(hot_words);
+    if (hk < nkeys) {  // the copy: hk is one of the offsets' keys [0, n_act]
+        const uint32_t cnt = *hot_total, off = offsets[hk];
+        if (cnt <= n && off <= n - cnt) {  // inconsistent counts: never write out of bounds
+            const uint32_t* src = hot_idx + (n - cnt);
+            for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = src[i];
+        }
+    }
     unsigned long long best = 0;
     for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nkeys; k += gridDim.x * 256u) {
         const uint32_t c = offsets[k + 1] - offsets[k];
@@ -3321,12 +3320,9 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
-    if (hot) {
-        hipLaunchKernelGGL(k_hot_copy, dim3(std::min<uint32_t>(ceil_div(n, 256u * 8u), 2048u)), dim3(256), 0, st, s.hot,
-                           s.col_tot + nbk, n, nb, s.sorted_keys, d_offsets, d_order);
-        hipLaunchKernelGGL(k_hot_pick, dim3(std::min<uint32_t>(ceil_div(n_act + 1, 256u * 8u), 512u)), dim3(256), 0, st,
-                           d_offsets, n_act + 1, n, s.hot);
-    }
+    if (hot)
+        hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(std::max<uint32_t>(n, n_act + 1), 256u * 8u), 1024u)),
+                           dim3(256), 0, st, s.hot, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
