@@ -359,16 +359,21 @@ def test_node_mixed_width_segments_aligned(torch, chunks):
     world.close()
     # segment addresses: a world with no forwarding keeps the owned segments as the hosted ones.  Seeds are tried until
     # the unpadded layout (segments back to back) would have left a wide segment misaligned on some rank.
-    world = World(2, n_grains=30_000, host_mix=0.0)
+    world = World(2, n_grains=30_000, host_mix=0.0, reg_frac=1.0)
     world.set_wire_types("both")
     nodes = [GrainNode(world.engs[r], 2, r, world.ros, max_batch=100_000, max_recv=300_000, transport=L.TRANSPORT_LOCAL,
                        group_id=b"node-align2", chunks=chunks) for r in range(2)]
     hit = False
     for seed in range(700, 716, 2):
-        batches = [world.messages(r, 60_001 + 2 * r, seed=seed + r, wide_at=(45_000 if r == 0 else None)) for r in range(2)]
-        for m in batches:  # no complete addresses: nothing is forwarded, the owned segments are the hosted ones
-            m["flags"][:] = 0
-            m["target_silo"][:] = 0
+        # registered targets only, activations on their owners, no complete addresses: nothing is forwarded, so the
+        # owned segments are the hosted ones
+        batches = [W.uniform_messages(world.cl, world.n_grains, 60_001 + 2 * r, seed=seed + r,
+                                      sender_silos=np.nonzero(world.ros == r)[0]) for r in range(2)]
+        # a header carrying its precomputed uniform hash (ORL_HDR_HASH_VALID, the KeyExt form) has no compact record: chunk 2
+        # goes as 32-B headers; the hash is the target's own, so it routes like the others
+        m0 = batches[0][45_000:45_001]
+        batches[0]["aux"][45_000] = int(W.jenkins3_np(m0["tcd"], m0["n0"], m0["n1"])[0])
+        batches[0]["flags"][45_000] = L.HDR_HASH_VALID
         got = _run(t, world, nodes, batches, streams)
         exp, forward = world.expected(batches, chunks)
         assert not forward
