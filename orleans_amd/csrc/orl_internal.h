@@ -236,10 +236,10 @@ struct Scratch {
     uint2* pairs_b;         // [max_batch]
     uint32_t* idx_a;        // [max_batch + 1] fan-out publish offsets
     uint32_t* sorted_keys;  // [max_batch] (LSD fallback only)
-    uint32_t* tile_hist;    // [(2048 + 1) * rows]: + the hot-key column
+    uint32_t* tile_hist;    // [2048 * rows]
     uint32_t* scan_sums;    // [scan blocks]
     uint32_t* col_sums;     // [ceil(max_tiles/64) * 2048] column-scan chunk sums
-    uint32_t* col_tot;      // [2048 + 1] column totals (+ the hot key's)
+    uint32_t* col_tot;      // [2048 + 1] column totals (+ the hot key's at [bins])
     uint8_t* digits;        // [max_batch] (partition by owner)
     uint32_t* seg_hist;     // [max segments][2^lb] two-level path: per-segment low-digit counts → bases
     uint32_t* seg_carry;    // [ceil(max segments / 64)][2^lb] chunked segment scan: chunk sums, then carry-ins
@@ -253,6 +253,9 @@ struct Scratch {
     uint64_t max_tiles;
     int device = -1;        // the context's HIP device: picks the ranking variant of its stage-4 launches (host_rm)
     uint32_t* hot = nullptr;  // stage 4's hot-key words: [0] key in use (0xFFFFFFFF none), [1] pick counter, [2..3] u64 max
+    uint32_t* hot_rows = nullptr;      // [rows] the hot key's count per histogram row, then its exclusive prefix
+    uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
+    uint32_t* hot_host_dev = nullptr;  // its device address
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);

@@ -615,7 +615,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
                                                          uint32_t bins, uint32_t shift, uint32_t items,
-                                                         const uint32_t* __restrict__ hot_words) {
+                                                         const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     if (threadIdx.x == 0) sm.hot = 0;
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
-    const uint32_t hk = HIST ? hot_key_of(hot_words) : kNoHotKey;  // hot_words != null: rows of bins + 1 (the hot column)
+    const uint32_t hk = (HIST && hot_rows) ? hot_key_of(hot_words) : kNoHotKey;  // hot_rows: the hot key's count per row
     uint32_t hot_mine = 0;
     const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
@@ -738,12 +738,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         }
     }
     if (HIST) {
-        if (hot_words) wave_add_hot(&sm.hot, hot_mine);
+        if (hot_rows) wave_add_hot(&sm.hot, hot_mine);
         __syncthreads();
-        const uint32_t stride = bins + (hot_words ? 1u : 0u);
-        uint32_t* row = tile_hist + (size_t)blockIdx.x * stride;
+        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
-        if (hot_words && threadIdx.x == 0) row[bins] = sm.hot;
+        if (hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = sm.hot;
     }
 }
 
@@ -913,13 +912,14 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 template <bool ACTS>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     uint32_t bins, uint32_t* __restrict__ tile_hist,
-                                                    const uint32_t* __restrict__ hot_words = nullptr) {
+                                                    const uint32_t* __restrict__ hot_words = nullptr,
+                                                    uint32_t* __restrict__ hot_rows = nullptr) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
     __shared__ uint32_t hot;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
     if (threadIdx.x == 0) hot = 0;
     __syncthreads();
-    const uint32_t hk = ACTS ? hot_key_of(hot_words) : kNoHotKey;  // hot_words != null: rows of bins + 1
+    const uint32_t hk = (ACTS && hot_rows) ? hot_key_of(hot_words) : kNoHotKey;  // hot_rows: the hot key's count per row
     uint32_t hot_mine = 0;
     const uint32_t base = blockIdx.x * kTile;
     uint32_t k[kItems];
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
                 if (k[j] == hk) ++hot_mine;
                 else atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
             }
-        if (hot_words) wave_add_hot(&hot, hot_mine);
+        if (hot_rows) wave_add_hot(&hot, hot_mine);
     } else {
         // pairs of an LSD pass: sorted by the previous digit, so a hot key's pairs sit in consecutive lanes.  Loads stay
         // coalesced (element j * 256 + x); each run of equal digits inside a 64-lane step adds its length with one
@@ -961,10 +961,9 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
         }
     }
     __syncthreads();
-    const uint32_t stride = bins + ((ACTS && hot_words) ? 1u : 0u);
-    uint32_t* row = tile_hist + (size_t)blockIdx.x * stride;
+    uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
-    if (ACTS && hot_words && threadIdx.x == 0) row[bins] = hot;
+    if (ACTS && hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = hot;
 }
 
 // Column scan of the [ntiles][bins] count matrix, in chunks of kScanRows tiles.
@@ -988,9 +987,26 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M,
 // 16 columns per block; 16 threads per column each own a contiguous run of chunks.  (Running k_seg_plan in the last
 // block to finish, to save its launch, measured slower: 5.1 + 4.9 -> 12.0 us at config 5 — the fences and the
 // serialised plan cost more than the launch.)
+// hot_rows (stage 4's hot-key path): one more block turns the per-row hot counts into their exclusive prefix, in place,
+// and writes their total to T[bins].
 __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
-                                                  uint32_t* __restrict__ T) {
+                                                  uint32_t* __restrict__ T, uint32_t* __restrict__ hot_rows, uint32_t nrows) {
     __shared__ uint32_t part[16][17];
+    if (hot_rows && blockIdx.x == gridDim.x - 1) {  // contiguous runs of rows per thread, then one block scan
+        uint32_t* wsum = &part[0][0];
+        const uint32_t per = (nrows + 255) / 256, r0 = threadIdx.x * per, r1 = min(r0 + per, nrows);
+        uint32_t acc = 0;
+        for (uint32_t r = r0; r < r1; ++r) acc += hot_rows[r];
+        uint32_t total;
+        uint32_t run = block_excl_scan(acc, wsum, total);
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t v = hot_rows[r];
+            hot_rows[r] = run;
+            run += v;
+        }
+        if (threadIdx.x == 0) T[bins] = total;
+        return;
+    }
     const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
     const uint32_t d = blockIdx.x * 16 + col;
     const uint32_t per = (nchunks + 15) / 16;
@@ -1146,14 +1162,15 @@ struct PassSmem : PassSmemCore<BITS, ITEMS> {
 
 // ITEMS: elements per thread; the tile is 256 * ITEMS (the MSD pass of the two-level path takes kMsdItems: half the
 // digit-histogram rows of 4096-element tiles and twice the run length per digit in its scattered writes).
-// hot_words (IN_ACT + OUT_PAIR only; rows of B + 1 words): the hot key's elements are not ranked; their indices go to
-// hot_idx[row's hot column base + rank among the tile's hot elements] (arrival order), a run at the end of hot_idx.
+// hot_rows (IN_ACT + OUT_PAIR only; col_scan'ed per-row hot counts): the hot key's elements are not ranked; their indices
+// go to hot_idx[hot_rows[the tile's first row] + rank among the tile's hot elements] (arrival order): one run at the front
+// of hot_idx.
 template <int BITS, int IN, int OUT, int ITEMS, int RM>
 __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out, const uint32_t* __restrict__ hot_words,
-                                                    uint32_t* __restrict__ hot_idx) {
+                                                    const uint32_t* __restrict__ hot_rows, uint32_t* __restrict__ hot_idx) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
@@ -1183,7 +1200,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             idx[j] = v.y;
         }
     }
-    const uint32_t hk = HOTP ? hot_key_of(hot_words) : kNoHotKey;
+    const uint32_t hk = (HOTP && hot_rows) ? hot_key_of(hot_words) : kNoHotKey;
     bool ishot[ITEMS];
     uint32_t hrank[ITEMS];
     if (HOTP && hk != kNoHotKey) {  // the hot key's elements: ranked among themselves by lane prefix, in arrival order
@@ -1207,10 +1224,8 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     }
     __syncthreads();
     // row of this tile's global bases: tile-major rows, row_step rows per tile (the route kernel writes one row per
-    // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base); with the hot
-    // path the rows have one more column, the hot key's
-    const uint32_t row_stride = (HOTP && hot_words) ? B + 1u : B;
-    const uint32_t* orow = tile_off + (size_t)tile * row_step * row_stride;
+    // 256 * items messages; col_scan's exclusive column prefix at a tile's first row is the tile's base)
+    const uint32_t* orow = tile_off + (size_t)tile * row_step * B;
     uint32_t tile_hot = 0;
     if (HOTP && hk != kNoHotKey) {
         uint32_t before = 0;
@@ -1219,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             before += q < w ? hotw[q] : 0u;
             tile_hot += hotw[q];
         }
-        const uint32_t hb = orow[B] + before;  // absolute: the hot run fills hot_idx[n - hot total, n)
+        const uint32_t hb = hot_rows[(size_t)tile * row_step] + before;
 #pragma unroll
         for (uint32_t j = 0; j < ITEMS; ++j)
             if (ishot[j] && hb + hrank[j] < n) hot_idx[hb + hrank[j]] = idx[j];
@@ -3172,17 +3187,18 @@ __global__ void k_hot_finish(const uint32_t* __restrict__ hot_words, const uint3
 // of (count << 32 | key) per block; the last block to finish (every block has read the current key by then) decides and
 // resets the accumulator.
 constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
+// copy = 0: this batch did not take the path (only the pick runs).  host_word: a mapped host copy of the next key (the
+// launcher's hint whether a batch should take the path; results never depend on it).
 __global__ __launch_bounds__(256) void k_hot_tail(uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
-                                                  uint32_t n, uint32_t nkeys, const uint32_t* __restrict__ hot_idx,
-                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
+                                                  uint32_t n, uint32_t nkeys, uint32_t copy, const uint32_t* __restrict__ hot_idx,
+                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
+                                                  uint32_t* __restrict__ host_word) {
     __shared__ unsigned long long bmax[kWaves];
     const uint32_t hk = hot_key_of(hot_words);
-    if (hk < nkeys) {  // the copy: hk is one of the offsets' keys [0, n_act]
+    if (copy && hk < nkeys) {  // the copy: hk is one of the offsets' keys [0, n_act]; the run is hot_idx[0, cnt)
         const uint32_t cnt = *hot_total, off = offsets[hk];
-        if (cnt <= n && off <= n - cnt) {  // inconsistent counts: never write out of bounds
-            const uint32_t* src = hot_idx + (n - cnt);
-            for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = src[i];
-        }
+        if (cnt <= n && off <= n - cnt)  // inconsistent counts: never write out of bounds
+            for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = hot_idx[i];
     }
     unsigned long long best = 0;
     for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nkeys; k += gridDim.x * 256u) {
@@ -3209,6 +3225,7 @@ __global__ __launch_bounds__(256) void k_hot_tail(uint32_t* __restrict__ hot_wor
     const bool hot = (uint64_t)c * kHotShare >= n && c >= kHotMinCount;
     __hip_atomic_store(&hot_words[0], hot ? k : kNoHotKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&hot_words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_word) __hip_atomic_store(host_word, hot ? k : kNoHotKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Messages per thread of a route launch feeding stage 4 for n_act activations: the MSD tile of the two-level path,
@@ -3237,10 +3254,10 @@ uint32_t route_items(uint64_t n, uint32_t max_items) {
 template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
-                      const uint32_t* hot_words, uint32_t* hot_idx) {
+                      const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
-                                                row_step, ntiles, pout, order, keys, hot_words, hot_idx)
+                                                row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx)
 #define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
@@ -3262,10 +3279,10 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
 
 void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
-                 const uint32_t* hot_words = nullptr, uint32_t* hot_idx = nullptr) {
+                 const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr) {
     switch (bits) {
 #define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
-                                                hot_words, hot_idx); break;
+                                                hot_words, hot_rows, hot_idx); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3275,11 +3292,13 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
 
 // Column scan of a tile-major [ntiles][bins] histogram into per-(tile, bin) output bases, in place.
 // row_step: the reading pass uses rows t % row_step == 0 only.
-void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st) {
+void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
+              uint32_t* hot_rows = nullptr) {
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
     hipLaunchKernelGGL(k_col_sum, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums);
-    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot);
+    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + (hot_rows ? 1u : 0u)), dim3(256), 0, st, s.col_sums, nch, bins,
+                       s.col_tot, hot_rows, ntiles);
     hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot, row_step);
 }
 
@@ -3298,7 +3317,7 @@ RouteHist route_hist(uint32_t n_act) {
 
 template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
+                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     const uint32_t nb = n_act + 2;
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
@@ -3320,18 +3339,20 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
-    if (hot)
-        hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(std::max<uint32_t>(n, n_act + 1), 256u * 8u), 1024u)),
-                           dim3(256), 0, st, s.hot, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
+    if (hot || pick)  // the copy (when the batch took the path) + the next batch's key
+        hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(std::max<uint32_t>(hot ? n : 0u, n_act + 1), 256u * 16u),
+                                                               256u)),
+                           dim3(256), 0, st, s.hot, s.col_tot + nbk, n, n_act + 1, hot ? 1u : 0u, s.sorted_keys, d_offsets,
+                           d_order, s.hot_host_dev);
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
+                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     switch (lb) {
-#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot); break;
+#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot, pick); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3362,12 +3383,19 @@ bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
     return bp.two_level && bp.hb > 0;
 }
 
+// Whether the last pick (the tail kernel of an earlier batch, mirrored to mapped host memory) found a hot key: a batch
+// takes the path only then, so a batch without one pays just the pick.  A stale answer costs time, never correctness.
+bool hot_known(const Scratch& s) {
+    return s.hot_host && __atomic_load_n(s.hot_host, __ATOMIC_ACQUIRE) != kNoHotKey;
+}
+
 // Stage 4 after a route kernel that already wrote route_hist()'s tile histogram into s.tile_hist.
 //   two-level: [MSD pass by the high digit → pairs_a] → segment count → segment scan → offsets scan → scatter;
 //   LSD fallback: passes act → pairs_a → pairs_b → ... → (order, sorted keys); offsets from the sorted keys.
-// hot: the histogram pass wrote rows of 2^hb + 1 words (the hot column, hot_words != null in it): the hot-key path.
+// hot: the histogram pass wrote the hot key's per-row counts (s.hot_rows): this batch takes the hot-key path.  pick: the
+// batch is large enough for the path: the tail kernel picks the next batch's key (hot implies pick).
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t route_items, uint32_t* d_order,
-                       uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot) {
+                       uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick = false) {
     const BucketPlan bp = make_bucket_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
@@ -3381,20 +3409,20 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk + (hot ? 1u : 0u), row_step0, s, st);
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr);
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
-                            nullptr, nullptr, st, hot ? s.hot : nullptr, hot ? s.sorted_keys : nullptr);
+                            nullptr, nullptr, st, hot ? s.hot : nullptr, hot ? s.hot_rows : nullptr, hot ? s.sorted_keys : nullptr);
             }
             kin = s.pairs_a;
         }
         hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
         const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
-        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0);
+        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
@@ -3494,19 +3522,21 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const RouteHist rh = route_hist(n_act);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     const bool hist = buckets && rh.on;
-    const bool hot = hist && hot_path_on(n, n_act, s);
+    const bool pick = hist && hot_path_on(n, n_act, s);
+    const bool hot = pick && hot_known(s);
     const uint32_t* hw = hot ? s.hot : nullptr;
+    uint32_t* hr = hot ? s.hot_rows : nullptr;
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
-                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw)
+                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
-                                            shift, items, hw)
+                                            shift, items, hw, hr)
         if (hist) {
             if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
         } else {
@@ -3524,7 +3554,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     int e = (int)hipGetLastError();
     if (e) return e;
     if (!buckets) return 0;
-    return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st, hot);
+    return bucket_after_route(d_act, (uint32_t)n, n_act, items, d_order, d_offsets, s, st, hot, pick);
 }
 
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
@@ -3760,13 +3790,14 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
     if (n == 0) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
     const RouteHist rh = route_hist(n_act);
     const uint32_t ntiles = ceil_div(n, kTile);
-    const bool hot = rh.on && hot_path_on(n, n_act, s);
+    const bool pick = rh.on && hot_path_on(n, n_act, s);
+    const bool hot = pick && hot_known(s);
     if (rh.on)
         hipLaunchKernelGGL(k_hist_pairs<true>, dim3(ntiles), dim3(256), 0, st, d_act, (uint32_t)n, n_act, rh.shift, rh.bins,
-                           s.tile_hist, hot ? s.hot : nullptr);
+                           s.tile_hist, hot ? s.hot : nullptr, hot ? s.hot_rows : nullptr);
     int e = (int)hipGetLastError();
     if (e) return e;
-    return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st, hot);
+    return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st, hot, pick);
 }
 
 int launch_host_rank_count(const uint32_t* d_route, size_t n, const uint8_t* d_ros, uint32_t my_rank, uint64_t* d_counts,

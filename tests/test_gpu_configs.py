@@ -618,6 +618,18 @@ def test_stage4_hot_key_path_vs_oracle(torch, n_act):
         np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), ef, err_msg=f"batch {k} offsets")
         nxt = eng.query(L.Q_HOT_KEY)
         assert nxt == (0xFFFFFFFF if expect_next is None else expect_next), (k, nxt)
+    # the same batches enqueued back to back: the launcher's host copy of the pick lags the device (it decides whether a
+    # batch runs the path from an earlier batch's pick), which may cost time but never changes a result
+    d_acts = [t.from_numpy(a.view(np.int32)).cuda() for a, _ in plan]
+    outs = [(t.empty(len(a), dtype=t.int32, device="cuda"), t.empty(n_act + 2, dtype=t.int32, device="cuda"))
+            for a, _ in plan]
+    for k, (a, _) in enumerate(plan):
+        eng.bucket_device(d_acts[k], len(a), outs[k][0], outs[k][1])
+    t.cuda.synchronize()
+    for k, (a, _) in enumerate(plan):
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(outs[k][0].cpu().numpy().view(np.uint32), eo, err_msg=f"queued batch {k} order")
+        np.testing.assert_array_equal(outs[k][1].cpu().numpy().view(np.uint32), ef, err_msg=f"queued batch {k} offsets")
     # the route path (stage 4 after k_route's histogram) with misses: 10 % unregistered targets, two batches
     cl = W.default_cluster()
     n_grains = 200_000
