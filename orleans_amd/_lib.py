@@ -62,6 +62,7 @@ Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_
 Q_WIRE_DIGEST = 8
 Q_PART_ERROR = 9
 Q_HOT_KEY = 10
+Q_HOT_BATCHES = 11
 MAX_WIRE_TYPES = 16
 PART_LOOKBACK_FAILED = 0x4
 

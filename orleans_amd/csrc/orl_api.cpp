@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.hot); f(c->s.hot_rows);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -821,10 +821,13 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.col_tot, ((1ull << kMaxDigitBits) + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(col_tot)");
         if ((e = hipMalloc((void**)&c->s.hot, 16)) != hipSuccess) return bail(e, "hipMalloc(hot)");
         {
-            const uint32_t init[4] = {0xFFFFFFFFu, 0u, 0u, 0u};  // no hot key yet; pick counter and accumulator zero
+            const uint32_t init[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u};  // no hot key in either slot
             if ((e = hipMemcpy(c->s.hot, init, 16, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "hipMemcpy(hot)");
         }
-        if ((e = hipMalloc((void**)&c->s.hot_rows, rows * 4)) != hipSuccess) return bail(e, "hipMalloc(hot_rows)");
+        // the hot column's rows, then its 64-row chunk sums
+        if ((e = hipMalloc((void**)&c->s.hot_bmax, (((uint64_t)cfg->n_act + 2 + 4095) / 4096 + 1) * 8)) != hipSuccess)
+            return bail(e, "hipMalloc(hot_bmax)");
+        if ((e = hipMalloc((void**)&c->s.hot_rows, (rows + (rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(hot_rows)");
         if ((e = hipHostMalloc((void**)&c->s.hot_host, 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e, "hipHostMalloc(hot_host)");
         *c->s.hot_host = 0xFFFFFFFFu;
@@ -1926,12 +1929,15 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             *v = (uint64_t)(int64_t)g_rank_state[c->cfg.device];
             return ORL_OK;
         }
+        case ORL_Q_HOT_BATCHES:
+            *v = c->s.hot_batches;
+            return ORL_OK;
         case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             ORL_HIP(c, hipSetDevice(c->cfg.device));
             ORL_HIP(c, hipDeviceSynchronize());
             uint32_t w = 0;
-            ORL_HIP(c, hipMemcpy(&w, c->s.hot, 4, hipMemcpyDeviceToHost));
+            ORL_HIP(c, hipMemcpy(&w, c->s.hot + (c->s.hot_parity & 1u), 4, hipMemcpyDeviceToHost));
             *v = w;
             return ORL_OK;
         }

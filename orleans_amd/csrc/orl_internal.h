@@ -252,10 +252,13 @@ struct Scratch {
     uint64_t max_batch;
     uint64_t max_tiles;
     int device = -1;        // the context's HIP device: picks the ranking variant of its stage-4 launches (host_rm)
-    uint32_t* hot = nullptr;  // stage 4's hot-key words: [0] key in use (0xFFFFFFFF none), [1] pick counter, [2..3] u64 max
-    uint32_t* hot_rows = nullptr;      // [rows] the hot key's count per histogram row, then its exclusive prefix
+    uint32_t* hot = nullptr;  // stage 4's hot-key slots: [parity] the key in use (0xFFFFFFFF none), [parity ^ 1] the next pick
+    mutable uint32_t hot_parity = 0;   // flips with every batch that picks (scan_offsets_pick)
+    unsigned long long* hot_bmax = nullptr;  // [offset-scan chunks] per-chunk max of (count << 32 | key)
+    uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
     uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
     uint32_t* hot_host_dev = nullptr;  // its device address
+    mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
 };
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);

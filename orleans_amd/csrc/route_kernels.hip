@@ -579,8 +579,8 @@ struct RouteSmem {
 // their digit, the MSD pass writes their indices straight to a contiguous run in arrival order, and after the offsets
 // scan one copy puts that run at the activation's place in `order`: 16 instead of 32 bytes of stage-4 traffic per
 // message (the Zipf-hot grain: half of the hot rank's messages at 8 ranks; the unresolved bucket of a batch with misses).
-// hot words (Scratch::hot): [0] the key in use (kNoHotKey: none), [1] the pick kernel's done counter, [2..3] u64 max of
-// (count << 32 | key) accumulated by the pick.
+// hot words (Scratch::hot): two key slots (kNoHotKey: none), alternating per batch that picks: a batch reads its key
+// from one slot and the offsets scan writes its pick into the other (hot_cur / hot_next).
 constexpr uint32_t kNoHotKey = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t hot_key_of(const uint32_t* hot) {
@@ -778,22 +778,49 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     return pre + incl - v;
 }
 
-// SRC 0: sums of a[0..m).  SRC 1: the fan-out publish offsets' input: element p < m-1 is the out-degree of publisher
+// SRC 0: sums of a[0..m).  SRC 2: the same, and bmax[block] = the block's max of (a[e] << 32 | e) over e < nkeys (stage
+// 4's hot-key pick over the per-key counts).  SRC 1: the fan-out publish offsets' input: element p < m-1 is the out-degree of publisher
 // pubs[p] (csr_off[pubs[p]+1] - csr_off[pubs[p]]), element m-1 is 0; written to a, with pstart[p] = csr_off[pubs[p]]
 // (the publisher's first CSR entry, so the route kernel skips two dependent loads).
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(v, (int)d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 template <int SRC>
 __global__ __launch_bounds__(256) void k_scan_reduce(uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums,
                                                      const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
-                                                     uint64_t* __restrict__ pstart) {
+                                                     uint64_t* __restrict__ pstart, unsigned long long* __restrict__ bmax = nullptr,
+                                                     uint32_t nkeys = 0) {
     __shared__ uint32_t wsum[kWaves];
+    __shared__ unsigned long long wmax[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
     constexpr uint32_t J = kScanChunk / 256;
     uint32_t s = 0;
-    if (SRC == 0) {
+    if (SRC != 1) {
+        unsigned long long best = 0;
 #pragma unroll
         for (uint32_t j = 0; j < J; ++j) {
             const uint64_t e = base + j * 256 + threadIdx.x;
-            if (e < m) s += a[e];
+            const uint32_t v = e < m ? a[e] : 0u;
+            s += v;
+            if (SRC == 2 && e < nkeys) {
+                const unsigned long long c = ((unsigned long long)v << 32) | (uint32_t)e;
+                best = c > best ? c : best;
+            }
+        }
+        if (SRC == 2) {
+            best = wave_max_u64(best);
+            if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = best;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                for (uint32_t q = 1; q < kWaves; ++q) best = wmax[q] > best ? wmax[q] : best;
+                bmax[blockIdx.x] = best;
+            }
         }
     } else {  // staged so every level of loads is in flight at once: publishers, then both CSR offsets
         uint32_t p[J];
@@ -872,10 +899,32 @@ __device__ __forceinline__ void store16(uint32_t* __restrict__ a, uint64_t base,
 // Each thread owns 16 consecutive elements of the block's 4096-chunk.  DIRECT: the block adds up the earlier chunks'
 // sums itself (a few hundred at most: no k_scan_sums launch); else sums[] holds the scanned chunk prefixes.  WIDEN:
 // also out64[e] = add64 + a[e] (the fan-out's u64 publish offsets).
-template <bool DIRECT, bool WIDEN>
+// PICK (stage 4's hot-key pick): block 0 also reduces the chunks' bmax and stores the next batch's hot key into
+// next_key (and the mapped host word): the most frequent key when it holds >= 1/kHotShare of the batch's n messages and
+// >= kHotMinCount, else kNoHotKey.
+constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
+template <bool DIRECT, bool WIDEN, bool PICK = false>
 __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums,
-                                                   uint64_t* __restrict__ out64, uint64_t add64) {
+                                                   uint64_t* __restrict__ out64, uint64_t add64,
+                                                   const unsigned long long* __restrict__ bmax = nullptr, uint32_t n = 0,
+                                                   uint32_t* __restrict__ next_key = nullptr,
+                                                   uint32_t* __restrict__ host_word = nullptr) {
     __shared__ uint32_t wsum[kWaves];
+    if (PICK && blockIdx.x == 0) {
+        __shared__ unsigned long long wmax[kWaves];
+        unsigned long long best = 0;
+        for (uint32_t i = threadIdx.x; i < gridDim.x; i += 256) best = bmax[i] > best ? bmax[i] : best;
+        best = wave_max_u64(best);
+        if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t q = 1; q < kWaves; ++q) best = wmax[q] > best ? wmax[q] : best;
+            const uint32_t c = (uint32_t)(best >> 32), k = (uint32_t)best;
+            const uint32_t key = ((uint64_t)c * kHotShare >= n && c >= kHotMinCount) ? k : kNoHotKey;
+            __hip_atomic_store(next_key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16u;
     uint32_t v[16];
     load16(a, base, m, 0u, v);
@@ -972,8 +1021,17 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 //   k_col_apply: M[t][d] = base(d) + S[c][d] + rows of chunk c before t (grid: chunks x ceil(bins/256))
 constexpr uint32_t kScanRows = 64;
 
+// hot_rows (stage 4's hot-key path): the hot key's per-row counts, one more column kept apart: the last grid row of each
+// kernel handles it (chunk sums at hot_rows[ntiles + chunk]; the scan and the apply turn them into exclusive bases).
 __global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
-                                                 uint32_t* __restrict__ S) {
+                                                 uint32_t* __restrict__ S, uint32_t* __restrict__ hot_rows) {
+    if (hot_rows && blockIdx.y == gridDim.y - 1) {  // one wave: kScanRows = 64 rows, one per lane
+        if (threadIdx.x >= 64) return;
+        const uint32_t t = blockIdx.x * kScanRows + threadIdx.x;
+        const uint32_t v = wave_incl_scan(t < ntiles ? hot_rows[t] : 0u);
+        if (threadIdx.x == 63) hot_rows[ntiles + blockIdx.x] = v;
+        return;
+    }
     const uint32_t d = blockIdx.y * 256 + threadIdx.x;
     if (d >= bins) return;
     const uint32_t t0 = blockIdx.x * kScanRows;
@@ -987,21 +1045,22 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M,
 // 16 columns per block; 16 threads per column each own a contiguous run of chunks.  (Running k_seg_plan in the last
 // block to finish, to save its launch, measured slower: 5.1 + 4.9 -> 12.0 us at config 5 — the fences and the
 // serialised plan cost more than the launch.)
-// hot_rows (stage 4's hot-key path): one more block turns the per-row hot counts into their exclusive prefix, in place,
+// hot_rows (stage 4's hot-key path): one more block scans the hot column's chunk sums (hot_rows[nrows + c]) in place
 // and writes their total to T[bins].
 __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
                                                   uint32_t* __restrict__ T, uint32_t* __restrict__ hot_rows, uint32_t nrows) {
     __shared__ uint32_t part[16][17];
-    if (hot_rows && blockIdx.x == gridDim.x - 1) {  // contiguous runs of rows per thread, then one block scan
+    if (hot_rows && blockIdx.x == gridDim.x - 1) {  // contiguous runs of chunks per thread, then one block scan
         uint32_t* wsum = &part[0][0];
-        const uint32_t per = (nrows + 255) / 256, r0 = threadIdx.x * per, r1 = min(r0 + per, nrows);
+        uint32_t* hs = hot_rows + nrows;
+        const uint32_t per = (nchunks + 255) / 256, c0 = threadIdx.x * per, c1 = min(c0 + per, nchunks);
         uint32_t acc = 0;
-        for (uint32_t r = r0; r < r1; ++r) acc += hot_rows[r];
+        for (uint32_t c = c0; c < c1; ++c) acc += hs[c];
         uint32_t total;
         uint32_t run = block_excl_scan(acc, wsum, total);
-        for (uint32_t r = r0; r < r1; ++r) {
-            const uint32_t v = hot_rows[r];
-            hot_rows[r] = run;
+        for (uint32_t c = c0; c < c1; ++c) {
+            const uint32_t v = hs[c];
+            hs[c] = run;
             run += v;
         }
         if (threadIdx.x == 0) T[bins] = total;
@@ -1036,9 +1095,17 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
 // only those are written.
 __global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
-                                                   uint32_t row_step) {
+                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
+    if (hot_rows && blockIdx.y == gridDim.y - 1) {  // the hot column: chunk base + the exclusive prefix of its 64 rows
+        if (threadIdx.x >= 64) return;
+        const uint32_t t = blockIdx.x * kScanRows + threadIdx.x;
+        const uint32_t v = t < ntiles ? hot_rows[t] : 0u;
+        const uint32_t ex = wave_incl_scan(v) - v + hot_rows[ntiles + blockIdx.x];
+        if (t < ntiles) hot_rows[t] = ex;
+        return;
+    }
     const uint32_t d0 = blockIdx.y * 256;
     const uint32_t d = d0 + threadIdx.x;
     // base(d) = sum of column totals before d: columns before this block's 256, then an in-block scan
@@ -3155,13 +3222,36 @@ constexpr uint32_t kScanDirectChunks = 1024;
 int scan_inplace(uint32_t* a, uint64_t m, const Scratch& s, hipStream_t st) {
     const uint32_t nb = ceil_div(m, kScanChunk);
     if (nb == 0) return 0;
-    hipLaunchKernelGGL(k_scan_reduce<0>, dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_scan_reduce<0>, dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, nullptr, nullptr, nullptr, 0u);
     if (nb <= kScanDirectChunks) {
-        hipLaunchKernelGGL((k_scan_down<true, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull);
+        hipLaunchKernelGGL((k_scan_down<true, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull, nullptr, 0u,
+                           nullptr, nullptr);
     } else {
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nb);
-        hipLaunchKernelGGL((k_scan_down<false, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull);
+        hipLaunchKernelGGL((k_scan_down<false, false>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull, nullptr, 0u,
+                           nullptr, nullptr);
     }
+    return (int)hipGetLastError();
+}
+
+// The bucket offsets' scan with stage 4's hot-key pick folded in (counts of keys [0, nkeys) → the next batch's key into
+// hot_next(s), for a batch of n messages); flips the slots.
+uint32_t* hot_cur(const Scratch& s) { return s.hot + (s.hot_parity & 1u); }
+
+int scan_offsets_pick(uint32_t* a, uint64_t m, uint32_t nkeys, uint32_t n, const Scratch& s, hipStream_t st) {
+    const uint32_t nb = ceil_div(m, kScanChunk);
+    if (nb == 0) return 0;
+    uint32_t* next = s.hot + ((s.hot_parity + 1u) & 1u);
+    hipLaunchKernelGGL(k_scan_reduce<2>, dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, nullptr, nullptr, s.hot_bmax, nkeys);
+    if (nb <= kScanDirectChunks) {
+        hipLaunchKernelGGL((k_scan_down<true, false, true>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull,
+                           s.hot_bmax, n, next, s.hot_host_dev);
+    } else {
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nb);
+        hipLaunchKernelGGL((k_scan_down<false, false, true>), dim3(nb), dim3(256), 0, st, a, m, s.scan_sums, nullptr, 0ull,
+                           s.hot_bmax, n, next, s.hot_host_dev);
+    }
+    s.hot_parity ^= 1u;
     return (int)hipGetLastError();
 }
 
@@ -3181,51 +3271,26 @@ __global__ void k_hot_finish(const uint32_t* __restrict__ hot_words, const uint3
     if (threadIdx.x == 0 && hk < nb) offsets[hk] += *hot_total;
 }
 
-// The end of a batch's stage 4, one launch: (1) the hot run (hot_idx[n - total, n), arrival order) is copied to
-// order[offsets[hk] ...); (2) the most frequent key of this batch becomes the next batch's hot key when it holds >= 1/32
-// of the batch (and >= 2 segments' worth), else none: keys [0, nkeys) from offsets[k + 1] - offsets[k], one u64 atomicMax
-// of (count << 32 | key) per block; the last block to finish (every block has read the current key by then) decides and
-// resets the accumulator.
-constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
-// copy = 0: this batch did not take the path (only the pick runs).  host_word: a mapped host copy of the next key (the
-// launcher's hint whether a batch should take the path; results never depend on it).
-__global__ __launch_bounds__(256) void k_hot_tail(uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
-                                                  uint32_t n, uint32_t nkeys, uint32_t copy, const uint32_t* __restrict__ hot_idx,
-                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order,
-                                                  uint32_t* __restrict__ host_word) {
-    __shared__ unsigned long long bmax[kWaves];
+// The end of a hot batch's stage 4: the hot run (hot_idx[0, total), arrival order) is copied to order[offsets[hk] ...),
+// kTailUnroll loads in flight per thread (a grid-stride loop of single loads is latency-bound).
+constexpr uint32_t kTailUnroll = 8;
+__global__ __launch_bounds__(256) void k_hot_tail(const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
+                                                  uint32_t n, uint32_t nkeys, const uint32_t* __restrict__ hot_idx,
+                                                  const uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
     const uint32_t hk = hot_key_of(hot_words);
-    if (copy && hk < nkeys) {  // the copy: hk is one of the offsets' keys [0, n_act]; the run is hot_idx[0, cnt)
-        const uint32_t cnt = *hot_total, off = offsets[hk];
-        if (cnt <= n && off <= n - cnt)  // inconsistent counts: never write out of bounds
-            for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) order[off + i] = hot_idx[i];
-    }
-    unsigned long long best = 0;
-    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nkeys; k += gridDim.x * 256u) {
-        const uint32_t c = offsets[k + 1] - offsets[k];
-        const unsigned long long v = ((unsigned long long)c << 32) | k;
-        best = v > best ? v : best;
-    }
+    if (hk >= nkeys) return;  // hk is one of the offsets' keys [0, n_act]
+    const uint32_t cnt = *hot_total, off = offsets[hk];
+    if (cnt > n || off > n - cnt) return;  // inconsistent counts: never write out of bounds
+    const uint32_t stride = gridDim.x * 256u;
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    for (; i + (kTailUnroll - 1) * stride < cnt; i += kTailUnroll * stride) {
+        uint32_t v[kTailUnroll];
 #pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) {
-        const unsigned long long o = __shfl_xor(best, (int)d, 64);
-        best = o > best ? o : best;
+        for (uint32_t u = 0; u < kTailUnroll; ++u) v[u] = hot_idx[i + u * stride];
+#pragma unroll
+        for (uint32_t u = 0; u < kTailUnroll; ++u) order[off + i + u * stride] = v[u];
     }
-    if ((threadIdx.x & 63u) == 0) bmax[threadIdx.x >> 6] = best;
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    for (uint32_t q = 1; q < kWaves; ++q) best = bmax[q] > best ? bmax[q] : best;
-    unsigned long long* acc = reinterpret_cast<unsigned long long*>(hot_words + 2);
-    atomicMax(acc, best);
-    __threadfence();
-    if (atomicAdd(&hot_words[1], 1u) != gridDim.x - 1) return;
-    __threadfence();
-    const unsigned long long v = atomicExch(acc, 0ull);
-    const uint32_t c = (uint32_t)(v >> 32), k = (uint32_t)v;
-    const bool hot = (uint64_t)c * kHotShare >= n && c >= kHotMinCount;
-    __hip_atomic_store(&hot_words[0], hot ? k : kNoHotKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&hot_words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (host_word) __hip_atomic_store(host_word, hot ? k : kNoHotKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (; i < cnt; i += stride) order[off + i] = hot_idx[i];
 }
 
 // Messages per thread of a route launch feeding stage 4 for n_act activations: the MSD tile of the two-level path,
@@ -3296,10 +3361,12 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, co
               uint32_t* hot_rows = nullptr) {
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
-    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums);
-    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + (hot_rows ? 1u : 0u)), dim3(256), 0, st, s.col_sums, nch, bins,
-                       s.col_tot, hot_rows, ntiles);
-    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot, row_step);
+    const uint32_t hy = hot_rows ? 1u : 0u;  // the hot column's extra grid row / block
+    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, M, ntiles, bins, s.col_sums, hot_rows);
+    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
+                       ntiles);
+    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
+                       hot_rows);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -3335,15 +3402,17 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
                        s.seg_meta, d_offsets);
     hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
                        d_offsets);
-    if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, s.hot, s.col_tot + nbk, nb, d_offsets);
-    scan_inplace(d_offsets, nb, s, st);  // per-key counts → bucket offsets
+    const uint32_t* hw = hot_cur(s);
+    if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
+    if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
+        scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
+    else
+        scan_inplace(d_offsets, nb, s, st);
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
-    if (hot || pick)  // the copy (when the batch took the path) + the next batch's key
-        hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(std::max<uint32_t>(hot ? n : 0u, n_act + 1), 256u * 16u),
-                                                               256u)),
-                           dim3(256), 0, st, s.hot, s.col_tot + nbk, n, n_act + 1, hot ? 1u : 0u, s.sorted_keys, d_offsets,
-                           d_order, s.hot_host_dev);
+    if (hot)  // the hot run's copy (this batch's key: hw)
+        hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0, st,
+                           hw, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
@@ -3386,7 +3455,9 @@ bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
 // Whether the last pick (the tail kernel of an earlier batch, mirrored to mapped host memory) found a hot key: a batch
 // takes the path only then, so a batch without one pays just the pick.  A stale answer costs time, never correctness.
 bool hot_known(const Scratch& s) {
-    return s.hot_host && __atomic_load_n(s.hot_host, __ATOMIC_ACQUIRE) != kNoHotKey;
+    const bool on = s.hot_host && __atomic_load_n(s.hot_host, __ATOMIC_ACQUIRE) != kNoHotKey;
+    s.hot_batches += on ? 1u : 0u;
+    return on;
 }
 
 // Stage 4 after a route kernel that already wrote route_hist()'s tile histogram into s.tile_hist.
@@ -3416,7 +3487,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
-                            nullptr, nullptr, st, hot ? s.hot : nullptr, hot ? s.hot_rows : nullptr, hot ? s.sorted_keys : nullptr);
+                            nullptr, nullptr, st, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr, hot ? s.sorted_keys : nullptr);
             }
             kin = s.pairs_a;
         }
@@ -3524,7 +3595,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const bool hist = buckets && rh.on;
     const bool pick = hist && hot_path_on(n, n_act, s);
     const bool hot = pick && hot_known(s);
-    const uint32_t* hw = hot ? s.hot : nullptr;
+    const uint32_t* hw = hot ? hot_cur(s) : nullptr;
     uint32_t* hr = hot ? s.hot_rows : nullptr;
     uint32_t* th = hist ? s.tile_hist : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
@@ -3794,7 +3865,7 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
     const bool hot = pick && hot_known(s);
     if (rh.on)
         hipLaunchKernelGGL(k_hist_pairs<true>, dim3(ntiles), dim3(256), 0, st, d_act, (uint32_t)n, n_act, rh.shift, rh.bins,
-                           s.tile_hist, hot ? s.hot : nullptr, hot ? s.hot_rows : nullptr);
+                           s.tile_hist, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr);
     int e = (int)hipGetLastError();
     if (e) return e;
     return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st, hot, pick);

@@ -105,7 +105,8 @@ def main(R=8, chunks=4, width=8):
         t_all = timed(lambda: addr(recs, n, route, act, order_o, offs, stream=st))
         xgmi_mb = n * (R - 1) / R * width / 1e6
         print(f"{label} rank {r}: {n / 2**20:.1f}M messages received; route {t_route:.3f} ms, route + stage 4 "
-              f"{t_all:.3f} ms; n_act {n_act}; receives ~{xgmi_mb:.0f} MB over xGMI", flush=True)
+              f"{t_all:.3f} ms; n_act {n_act}; receives ~{xgmi_mb:.0f} MB over xGMI; hot key {eng.query(L.Q_HOT_KEY)}, "
+              f"{eng.query(L.Q_HOT_BATCHES)} batches on the hot-key path", flush=True)
         eng.close()
         del recs
     part.close()

@@ -618,6 +618,8 @@ def test_stage4_hot_key_path_vs_oracle(torch, n_act):
         np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), ef, err_msg=f"batch {k} offsets")
         nxt = eng.query(L.Q_HOT_KEY)
         assert nxt == (0xFFFFFFFF if expect_next is None else expect_next), (k, nxt)
+    # with a sync after every batch the launcher's hint is current: batches 1, 2, 3 and 5 ran the path
+    assert eng.query(L.Q_HOT_BATCHES) == 4
     # the same batches enqueued back to back: the launcher's host copy of the pick lags the device (it decides whether a
     # batch runs the path from an earlier batch's pick), which may cost time but never changes a result
     d_acts = [t.from_numpy(a.view(np.int32)).cuda() for a, _ in plan]
