@@ -151,6 +151,7 @@ static_assert(sizeof(RouteParams) % 16 == 0, "params must be 16-B granular");
 constexpr uint32_t kRouteThreads = 256;
 constexpr uint32_t kItems = 16;                               // messages per thread per tile
 constexpr uint32_t kTile = kRouteThreads * kItems;            // 4096 messages per tile
+constexpr uint32_t kMaxRouteRows = 8192;  // route tiles (= stage-4 histogram rows) of a small batch's finer grid
 constexpr uint32_t kMaxDigitBits = 11;                        // radix digit width cap (2048 bins)
 
 // Radix plan for keys in [0, n_buckets): passes of <= kMaxDigitBits bits, low digit first (LSD).
@@ -181,6 +182,8 @@ inline RadixPlan make_plan(uint32_t max_key) {
 // most seg_elems() messages; the per-key counts of that second level ARE the bucket offsets (one scan).
 // Wider keys fall back to LSD passes (`lsd`) + offsets from the sorted keys.
 constexpr uint32_t kSegChunk = kTile;  // messages per LDS round inside a segment
+// LSD path's bucket offsets: queue of long empty-bucket gaps (k_offsets_gaps / k_offsets_long), 4096 pieces
+constexpr size_t kGapQueueWords = 2 + 3 * 4096;
 
 struct BucketPlan {
     bool two_level;
@@ -246,6 +249,7 @@ struct Scratch {
     uint32_t* seg_meta;     // [ceil(max segments / 64)] chunked segment scan: each chunk's first bucket + shape bits
     uint32_t* bstart;       // [4097] bucket starts (two-level path; k_seg_plan handles up to 4096)
     uint32_t* sstart;       // [4098] first segment of each bucket; [4097] = a bucket has > 64 segments (skew flag)
+    uint32_t* gap_q;        // [kGapQueueWords] LSD offsets: long-gap queue (zeroed once; k_offsets_long empties it)
     uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile (zeroed once)
     uint32_t lb_ticket = 0; // host mirror of lb_state's ticket counter after the launches so far (tile = ticket - base)
     uint32_t lb_epoch = 0;  // launches so far: the granules of launch k carry epoch k (earlier ones read as unpublished)

@@ -1481,6 +1481,108 @@ __global__ __launch_bounds__(256) void k_sufmin_down(uint32_t* __restrict__ a, u
     store16(a, base, m, v);
 }
 
+// Bucket offsets from the sorted keys in one pass, every entry written exactly once (replaces fill + mark + the three
+// suffix-min launches: 5 -> 2 launches, 40 -> 8 B of offsets traffic per bucket).  Position i in [0, n] starts every
+// bucket b in (key[i-1], key[i]] (key[-1] = -1, key[n] = nb - 1): the buckets no earlier key occupies up to key[i], so
+// offsets[b] = i = lower_bound(sorted, b).  A thread owns 8 consecutive positions, a workgroup 2048.  When the
+// workgroup's buckets span <= kGapLds entries (the common case: about 2048 x nb / n) its threads fill them in LDS and
+// the workgroup writes the span with whole-wave coalesced stores (one lane per position writing its gap straight to
+// HBM made every store instruction touch 64 lines: 55 us at config 4).  Otherwise gaps go to global memory: short ones
+// by their thread, one of more than kGapWave buckets by the whole wave (64 entries per store), and one of more than
+// kGapChunk buckets queued in kGapChunk pieces for k_offsets_long (a workgroup per piece).  Queue: q[0] = count, q[1] =
+// finished workgroups of k_offsets_long (which zeroes both at its end), then {lo, len, value} triples; a full queue
+// leaves the gap to the wave.
+constexpr uint32_t kGapWave = 16, kGapChunk = 32768, kGapCap = 4096, kGapLds = 4096, kGapPer = 8, kGapBlock = 256 * kGapPer;
+static_assert(kGapQueueWords == 2 + 3 * (size_t)kGapCap, "gap queue size");
+
+__global__ __launch_bounds__(256) void k_offsets_gaps(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
+                                                      uint32_t* __restrict__ offsets, uint32_t* __restrict__ q, uint32_t cap) {
+    __shared__ uint32_t span[kGapLds];
+    __shared__ uint32_t range[2];
+    const uint64_t p0 = (uint64_t)blockIdx.x * kGapBlock, i0 = p0 + threadIdx.x * kGapPer;
+    const uint32_t lane = threadIdx.x & 63u, top = nb - 1u;
+    if (threadIdx.x == 0) {  // the workgroup's buckets [r0, r1): from its first position's gap to its last position's key
+        const uint64_t pl = min<uint64_t>(p0 + kGapBlock - 1u, n);
+        range[0] = p0 == 0 ? 0u : min(sorted[p0 - 1], top) + 1u;
+        range[1] = (pl < n ? min(sorted[pl], top) : top) + 1u;
+    }
+    uint32_t k[kGapPer];
+    if (i0 + kGapPer <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(sorted + i0);
+#pragma unroll
+        for (uint32_t j = 0; j < kGapPer / 4; ++j) {
+            const uint4 v = p[j];
+            k[4 * j] = v.x; k[4 * j + 1] = v.y; k[4 * j + 2] = v.z; k[4 * j + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kGapPer; ++j) k[j] = (i0 + j < n) ? sorted[i0 + j] : top;  // position n (and past it) closes at nb - 1
+    }
+    // lo = first bucket not yet started before position i0 (nb: nothing left, the thread is past position n)
+    uint32_t lo = i0 == 0 ? 0u : i0 <= n ? min(sorted[i0 - 1], top) + 1u : nb;
+    __syncthreads();
+    const uint32_t r0 = range[0], r1 = range[1];
+    const bool in_lds = r1 - r0 <= kGapLds;  // workgroup-uniform
+    auto put = [&](uint32_t b, uint32_t v) {   // bucket b's offset: into the span, or straight to HBM
+        if (in_lds) span[b - r0] = v; else offsets[b] = v;
+    };
+#pragma unroll
+    for (uint32_t j = 0; j < kGapPer; ++j) {
+        const uint32_t hi = min(k[j], top) + 1u;  // exclusive
+        const uint32_t len = hi > lo ? hi - lo : 0u, val = (uint32_t)(i0 + j);
+        if (len <= kGapWave)
+            for (uint32_t b = 0; b < len; ++b) put(lo + b, val);
+        uint64_t m = __ballot(len > kGapWave);
+        while (m) {  // long gaps: the whole wave writes them, one lane's gap at a time
+            const uint32_t src = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t glo = (uint32_t)__shfl((int)lo, (int)src, 64);
+            const uint32_t gl = (uint32_t)__shfl((int)len, (int)src, 64);
+            const uint32_t gv = (uint32_t)__shfl((int)val, (int)src, 64);
+            uint32_t done = 0;
+            if (!in_lds && gl > kGapChunk) {  // queue whole pieces while there is room; the wave writes the rest
+                const uint32_t pieces = gl / kGapChunk;
+                uint32_t first = 0;
+                if (lane == 0) first = atomicAdd(&q[0], pieces);
+                first = (uint32_t)__shfl((int)first, 0, 64);
+                const uint32_t took = first >= cap ? 0u : min(pieces, cap - first);
+                for (uint32_t p = lane; p < took; p += 64) {
+                    uint32_t* t = q + 2 + 3 * (size_t)(first + p);
+                    t[0] = glo + p * kGapChunk;
+                    t[1] = kGapChunk;
+                    t[2] = gv;
+                }
+                done = took * kGapChunk;
+            }
+            for (uint32_t b = done + lane; b < gl; b += 64) put(glo + b, gv);
+        }
+        lo = hi > lo ? hi : lo;
+    }
+    if (in_lds) {  // the span, coalesced
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < r1 - r0; b += 256u) offsets[r0 + b] = span[b];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ offsets, uint32_t* __restrict__ q, uint32_t cap) {
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = min(__hip_atomic_load(&q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), cap);
+    __syncthreads();
+    for (uint32_t e = blockIdx.x; e < cnt; e += gridDim.x) {
+        const uint32_t* t = q + 2 + 3 * (size_t)e;
+        const uint32_t lo = t[0], len = t[1], val = t[2];
+        for (uint32_t b = threadIdx.x; b < len; b += 256) offsets[lo + b] = val;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the last workgroup to finish (every one has read the count) empties the queue
+        __threadfence();
+        if (atomicAdd(&q[1], 1u) == gridDim.x - 1u) {
+            q[0] = 0;
+            q[1] = 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
                                                       uint32_t* __restrict__ offsets) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
@@ -1970,7 +2072,11 @@ struct FanSmem {
     uint32_t prange[2];
 };
 
-template <int HB, int PW>
+// phase markers of k_fanout_route's U-message step (never route words: status bytes 0xFD / 0xFC are unused)
+constexpr uint32_t kNoAct4 = 0xFDFDFDFDu, kFanSlow = 0xFCFCFCFCu;
+constexpr int kFanIlp = 1;  // default messages per thread and step
+
+template <int HB, int PW, int U>
 __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
     uint64_t cmask, const ProbeSlot* __restrict__ probe, const uint32_t* __restrict__ probe_bad,
@@ -2009,57 +2115,106 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
     const bool use16 = PW != 0 && (probe_bad == nullptr || *probe_bad == 0u);
-    for (uint32_t j = 0; j < items; ++j) {
-        const uint32_t e = base + j * kRouteThreads + threadIdx.x;
-        if (e >= n) break;
-        if (e >= lim) {  // past the emitted total: no message
-            route[e] = pack_route(0xFFu, 0xFFu, ORL_ST_PAST_TOTAL, 0u);
-            act_out[e] = ORL_NO_ACT;
-            if (HIST) atomicAdd(&sm.hist[(n_act >> shift) & (bins - 1)], 1u);
-            continue;
-        }
-        Msg m;
-        if (e < nd) {  // a direct message of the same batch
-            m = load_hdr(direct, e);
-        } else {
-            const uint32_t f = e - nd;
-            uint32_t lo, hi, p, start;
-            if (in_lds) {
-                lo = 0; hi = span + 1;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (sm.poff[mid] <= f) lo = mid + 1; else hi = mid;
+    // U messages per thread and step, in three phases so their dependent loads overlap: (A) publisher search + CSR
+    // target load, (B) stages 1-2 + the first probe, (C) probe chain, stage-3 tail, outputs.  U = 1 is one message at a
+    // time (the round-2 loop).
+    for (uint32_t j = 0; j < items; j += U) {
+        uint32_t e[U], tgt[U], pub[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {  // (A)
+            e[q] = base + (j + q) * kRouteThreads + threadIdx.x;
+            tgt[q] = 0;
+            pub[q] = 0;
+            if (j + q < items && e[q] < lim && e[q] >= nd) {
+                const uint32_t f = e[q] - nd;
+                uint32_t lo, hi, pq, start;
+                if (in_lds) {
+                    lo = 0; hi = span + 1;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (sm.poff[mid] <= f) lo = mid + 1; else hi = mid;
+                    }
+                    pq = p_lo + lo - 1;
+                    start = sm.poff[lo - 1];
+                } else {
+                    lo = p_lo; hi = p_hi + 1;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (poff32[mid] <= f) lo = mid + 1; else hi = mid;
+                    }
+                    pq = lo - 1;
+                    start = poff32[pq];
                 }
-                p = p_lo + lo - 1;
-                start = sm.poff[lo - 1];
-            } else {
-                lo = p_lo; hi = p_hi + 1;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (poff32[mid] <= f) lo = mid + 1; else hi = mid;
-                }
-                p = lo - 1;
-                start = poff32[p];
+                pub[q] = pq;
+                tgt[q] = csr_tgt[pstart[pq] + (f - start)];
             }
-            const uint32_t tgt = csr_tgt[pstart[p] + (f - start)];
-            if (follower_keys) {  // followers named by a key table (e.g. Guid-keyed players)
-                const orl_grain_key k = follower_keys[tgt];
-                m.tcd = k.type_code_data;
-                m.n0 = k.n0;
-                m.n1 = k.n1;
+        }
+        Msg m[U];
+        uint32_t r[U], h[U], own[U], rf[U], mk[U];
+        uint64_t slot[U];
+        u32x4 sa[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {  // (B)
+            r[q] = kNoAct4;  // no message
+            mk[q] = kNoType;
+            slot[q] = 0;
+            if (j + q >= items || e[q] >= n) continue;
+            if (e[q] >= lim) {  // past the emitted total: no message
+                route[e[q]] = pack_route(0xFFu, 0xFFu, ORL_ST_PAST_TOTAL, 0u);
+                act_out[e[q]] = ORL_NO_ACT;
+                if (HIST) atomicAdd(&sm.hist[(n_act >> shift) & (bins - 1)], 1u);
+                continue;
+            }
+            if (e[q] < nd) {  // a direct message of the same batch
+                m[q] = load_hdr(direct, e[q]);
+            } else if (follower_keys) {  // followers named by a key table (e.g. Guid-keyed players)
+                const orl_grain_key k = follower_keys[tgt[q]];
+                m[q].tcd = k.type_code_data;
+                m[q].n0 = k.n0;
+                m[q].n1 = k.n1;
             } else {  // GrainId(follower_tcd, long id)
-                m.tcd = follower_tcd;
-                m.n0 = 0;
-                m.n1 = (uint64_t)tgt;
+                m[q].tcd = follower_tcd;
+                m[q].n0 = 0;
+                m[q].n1 = (uint64_t)tgt[q];
             }
-            m.meta = (uint32_t)pub_silo[p] | (2u << 8);  // Application message from the publisher's silo
-            m.aux = 0;
+            if (e[q] >= nd) {
+                m[q].meta = (uint32_t)pub_silo[pub[q]] | (2u << 8);  // Application message from the publisher's silo
+                m[q].aux = 0;
+            }
+            if (!use16) {
+                r[q] = kFanSlow;
+                continue;
+            }
+            r[q] = route_head(sm.P, m[q], excl != 0, h[q], own[q], rf[q]);
+            if (r[q] == kNeedProbe) {
+                mk[q] = probe_type(sm.P, m[q]);
+                slot[q] = dir_slot(h[q], mask);
+                if (mk[q] != kNoType) sa[q] = reinterpret_cast<const u32x4*>(probe)[slot[q]];
+            }
         }
-        uint32_t act;
-        route[e] = use16 ? route_msg16(sm.P, dir, mask, probe, cache, cmask, m, excl != 0, act)
-                       : route_msg(sm.P, dir, mask, cache, cmask, m, excl != 0, act);
-        act_out[e] = act;
-        if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+#pragma unroll
+        for (int q = 0; q < U; ++q) {  // (C)
+            if (r[q] == kNoAct4) continue;
+            uint32_t act = ORL_NO_ACT, rr = r[q];
+            if (rr == kFanSlow || rr == kNeedProbeCache) {  // the 32-B table, or a remote owner's cache
+                rr = route_msg(sm.P, dir, mask, cache, cmask, m[q], excl != 0, act);
+            } else if (rr == kNeedProbe) {
+                uint32_t fact = 0, fsilo = 0;
+                int st = 1;
+                if (mk[q] != kNoType) {
+                    st = probe_slot16(sa[q], m[q].n1, mk[q], fact, fsilo);
+                    uint64_t sl = slot[q];
+                    for (uint64_t step = 0; st == 2 && step < mask; ++step) {
+                        sl = (sl + 1) & mask;
+                        st = probe_slot16(reinterpret_cast<const u32x4*>(probe)[sl], m[q].n1, mk[q], fact, fsilo);
+                    }
+                }
+                rr = route_tail(sm.P, m[q], h[q], own[q], rf[q], st == 0, fact, fsilo, act, false);
+            }
+            route[e[q]] = rr;
+            act_out[e[q]] = act;
+            if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
+        }
     }
     if (HIST) {
         __syncthreads();
@@ -3309,10 +3464,22 @@ uint32_t route_min_wgs() {  // ORL_ROUTE_MIN_WG: A/B knob for the small-batch gr
     return v;
 }
 
-uint32_t route_items(uint64_t n, uint32_t max_items) {
+uint32_t fan_min_wgs() {  // ORL_FAN_MIN_WG: the fan-out kernel's (default 4096)
+    static const uint32_t v = [] {
+        const char* e = getenv("ORL_FAN_MIN_WG");
+        const long x = e ? atol(e) : 0;
+        return x > 0 ? (uint32_t)x : 4096u;
+    }();
+    return v;
+}
+
+uint32_t route_items(uint64_t n, uint32_t max_items, uint32_t min_wg = 0) {
     uint32_t items = max_items;
-    const uint32_t min_wg = route_min_wgs();
-    while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < min_wg) items >>= 1;
+    if (min_wg == 0) min_wg = route_min_wgs();
+    // smaller tiles until the grid has min_wg workgroups, never past kMaxRouteRows histogram rows (the scratch's)
+    while (items > 1 && ceil_div(n, (uint64_t)kRouteThreads * items) < min_wg &&
+           ceil_div(n, (uint64_t)kRouteThreads * (items >> 1)) <= kMaxRouteRows)
+        items >>= 1;
     return items;
 }
 
@@ -3440,6 +3607,32 @@ bool stage4_soa() {
     return soa;
 }
 
+// LSD path's bucket offsets: ORL_OFFSETS_SUFMIN=1 keeps the round-2 five-launch form (A/B).
+bool offsets_sufmin() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_OFFSETS_SUFMIN");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// Queue capacity of k_offsets_gaps (pieces); ORL_GAP_CAP lowers it (tests: the full-queue fallback).
+uint32_t gap_cap() {  // read per launch (a getenv per batch), so a test can change it in-process
+    const char* e = getenv("ORL_GAP_CAP");
+    const long v = e ? atol(e) : (long)kGapCap;
+    return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
+}
+
+// k_fanout_route's messages per thread and step: ORL_FAN_U = 1, 2 or 4 (A/B).
+int fan_ilp() {
+    static const int u = [] {
+        const char* e = getenv("ORL_FAN_U");
+        const int v = e ? atoi(e) : kFanIlp;
+        return v == 4 ? 4 : v == 2 ? 2 : 1;
+    }();
+    return u;
+}
+
 // The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair
 // layout; ORL_NO_HOT=1 turns it off (A/B).
 bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
@@ -3512,14 +3705,19 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
                     s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
     }
-    hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
-    hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
-    {  // empty buckets: suffix minima (the next present key's start, n after the last)
+    if (offsets_sufmin()) {  // A/B: the five-launch form (fill, mark, suffix minima)
+        hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
+        hipLaunchKernelGGL(k_offsets_mark, dim3(ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, st, s.sorted_keys, n, nb, d_offsets);
         const uint32_t nch = ceil_div(nb, kScanChunk);
         hipLaunchKernelGGL(k_sufmin_reduce, dim3(nch), dim3(256), 0, st, d_offsets, nb, s.scan_sums);
         hipLaunchKernelGGL(k_sufmin_chunks, dim3(1), dim3(256), 0, st, s.scan_sums, nch, n);
         hipLaunchKernelGGL(k_sufmin_down, dim3(nch), dim3(256), 0, st, d_offsets, nb, s.scan_sums);
+        return (int)hipGetLastError();
     }
+    // every bucket written once from the gaps between consecutive sorted keys (positions 0..n: n + 1 of them)
+    hipLaunchKernelGGL(k_offsets_gaps, dim3(ceil_div(n + 1, kGapBlock)), dim3(256), 0, st, s.sorted_keys, n, nb,
+                       d_offsets, s.gap_q, gap_cap());
+    hipLaunchKernelGGL(k_offsets_long, dim3(256), dim3(256), 0, st, d_offsets, s.gap_q, gap_cap());
     return (int)hipGetLastError();
 }
 
@@ -3668,15 +3866,21 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t items = route_items(total, max_route_items(n_act));
+    // a finer grid than k_route's (>= 4096 tiles): each tile starts with a few dependent loads (its publisher range),
+    // which later tiles overlap (config 4: 0.223 -> 0.210 ms; 8192 tiles 0.219)
+    const uint32_t items = route_items(total, max_route_items(n_act), fan_min_wgs());
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
 
 // the fan-out kernel takes the 16-B form: the 8-B form measured slower here (config 4: 0.266 vs 0.247 ms)
-#define ORL_FAN(H, TH, BINS, SHIFT) do { if (dv.probe) ORL_FAN_(H, 16, TH, BINS, SHIFT); else ORL_FAN_(H, 0, TH, BINS, SHIFT); } while (0)
-#define ORL_FAN_(H, Q, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
+// U messages per thread and step (fan_ilp(): ORL_FAN_U, A/B)
+#define ORL_FAN(H, TH, BINS, SHIFT) do { const int u_ = fan_ilp();                                                          \
+        if (dv.probe) { if (u_ == 4) ORL_FAN_(H, 16, 4, TH, BINS, SHIFT); else if (u_ == 2) ORL_FAN_(H, 16, 2, TH, BINS, SHIFT); \
+                        else ORL_FAN_(H, 16, 1, TH, BINS, SHIFT); }                                                          \
+        else ORL_FAN_(H, 0, 1, TH, BINS, SHIFT); } while (0)
+#define ORL_FAN_(H, Q, U, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q, U>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
                                                        dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
                                                        follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
                                                        excl, d_route, d_act, TH, BINS, \

@@ -656,3 +656,39 @@ def test_stage4_hot_key_path_vs_oracle(torch, n_act):
         assert eng2.query(L.Q_HOT_KEY) == n_grains  # the unresolved bucket (PreferLocal placements) is hot
     eng2.close()
     eng.close()
+
+
+# ---- stage 4, LSD plan (keys > 22 bits): bucket offsets from the gaps between sorted keys -----------------------
+@pytest.mark.parametrize("cap", [None, "3"])
+def test_lsd_offsets_long_gaps_vs_oracle(torch, monkeypatch, cap):
+    """The LSD plan's bucket offsets (k_offsets_gaps / k_offsets_long): every empty bucket gets lower_bound(sorted, b).
+    Batches over 20M handles with short gaps only (uniform), gaps the whole wave writes (sparse keys), gaps queued in
+    32768-bucket pieces (a few keys: millions of empty buckets between them, before the first and after the last) and, with
+    the queue capped at 3 pieces (ORL_GAP_CAP), the full-queue fallback where the wave writes what did not fit; the
+    offsets-only form (no messages) and a batch whose keys are all unresolved.  Order and offsets == the oracle's stable
+    bucketing (ActivationData.cs:483-514)."""
+    t = torch
+    if cap is not None:
+        monkeypatch.setenv("ORL_GAP_CAP", cap)
+    n_act = 20_000_000
+    rng = np.random.default_rng(11)
+    o = cpu_ref.Oracle(8)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=1 << 21, device=0)
+    W.setup_engine(eng, W.default_cluster())
+    batches = [rng.integers(0, n_act, 1_500_000, dtype=np.int64).astype(np.uint32),          # gaps of ~13
+               rng.integers(0, n_act // 40, 300_000, dtype=np.int64).astype(np.uint32) * 40,  # gaps of 39 and more
+               rng.choice(np.array([5, 6, 9_000_123, 9_000_124, 12_345_678], np.uint32), 700_001),
+               np.full(1000, n_act - 1, np.uint32),
+               np.full(5000, L.NO_ACT, np.uint32),
+               np.array([n_act // 2], np.uint32)]
+    off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
+    for k, a in enumerate(batches):
+        d_act = t.from_numpy(a.view(np.int32)).cuda()
+        order = t.empty(len(a), dtype=t.int32, device="cuda")
+        off.fill_(-1)
+        eng.bucket_device(d_act, len(a), order, off)
+        t.cuda.synchronize()
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(_u32(order), eo, err_msg=f"batch {k} order")
+        np.testing.assert_array_equal(_u32(off), ef, err_msg=f"batch {k} offsets")
+    eng.close()
