@@ -1,4 +1,4 @@
-"""The node exchange protocol with several processes over gloo on the CPU (world sizes 2 and 4).
+"""The node exchange protocol with several processes over gloo on the CPU (world sizes 2, 3, 4, and 8 as the SCALE run uses).
 
 Every rank runs the steps orl_node_route_batch_device takes (orleans_amd/csrc/orl_node.cpp), in the same order, with the
 product's own host decisions — orl_node_plan_chunk after each chunk's counts all-gather (record width, re-partition,
@@ -220,7 +220,7 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("world,name", [(2, "narrow_hop2"), (4, "narrow_hop2"), (2, "wire16"), (3, "grain_only"),
+@pytest.mark.parametrize("world,name", [(2, "narrow_hop2"), (4, "narrow_hop2"), (8, "narrow_hop2"), (2, "wire16"), (3, "grain_only"),
                                         (2, "mismatch")])
 def test_node_protocol_gloo(world, name):
     case = CASES[name]
