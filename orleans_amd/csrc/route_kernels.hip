@@ -2444,6 +2444,10 @@ constexpr uint32_t kPartItems = 8;
 // (3 ballots, one update per digit group) ranks them without relying on the atomics' lane order.
 constexpr int kPartRm = kRmBallot;
 constexpr uint32_t kPartTile = kRouteThreads * kPartItems;
+#ifndef ORL_PART_GROUPS
+#define ORL_PART_GROUPS 2
+#endif
+constexpr uint32_t kPartGroups = ORL_PART_GROUPS;  // k_part_lb<8>: header load groups per tile (see there)
 constexpr uint32_t kLbSpinLimit = 1u << 24;
 
 struct LbShared {
@@ -2578,27 +2582,43 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
     const uint32_t t = sm.lb.tile;
     const uint32_t wbase = t * kPartTile + w * (kPartItems * 64u);
     u32x4 h0[kPartItems], h1[kPartItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kPartItems; ++j) {  // unconditional (clamped) loads: all in flight together
-        const uint32_t e = wbase + j * 64u + lane;
-        const u32x4* sp = reinterpret_cast<const u32x4*>(in + (e < n ? e : n - 1));
-        h0[j] = __builtin_nontemporal_load(sp);
-        h1[j] = __builtin_nontemporal_load(sp + 1);
-    }
     uint32_t dig[kPartItems], rank[kPartItems];
+    uint2 nrec[kPartItems];  // FMT 8: the records, encoded before the ranking so the 32-B headers leave the registers
+    uint32_t bad = 0;
+    // FMT 8 loads and encodes the tile's headers in kPartGroups groups (a scheduling barrier keeps a group's loads from
+    // being hoisted above the previous group's encoding), so only one group's 32-B headers are live at a time: fewer
+    // VGPRs, more tiles resident per CU to cover the look-back's device round trips.  Wider records keep the headers.
+    constexpr uint32_t G = FMT == 8 ? kPartGroups : 1u, GI = kPartItems / G;
 #pragma unroll
-    for (uint32_t j = 0; j < kPartItems; ++j) {
-        dig[j] = 0;
-        if (wbase + j * 64u + lane < n) {
-            Msg m;
-            m.tcd = (uint64_t)h0[j].x | ((uint64_t)h0[j].y << 32);
-            m.n0 = (uint64_t)h0[j].z | ((uint64_t)h0[j].w << 32);
-            m.n1 = (uint64_t)h1[j].x | ((uint64_t)h1[j].y << 32);
-            m.meta = h1[j].z;
-            m.aux = h1[j].w;
-            dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+    for (uint32_t gq = 0; gq < G; ++gq) {
+#pragma unroll
+        for (uint32_t jj = 0; jj < GI; ++jj) {  // unconditional (clamped) loads: the group's in flight together
+            const uint32_t j = gq * GI + jj, e = wbase + j * 64u + lane;
+            const u32x4* sp = reinterpret_cast<const u32x4*>(in + (e < n ? e : n - 1));
+            h0[j] = __builtin_nontemporal_load(sp);
+            h1[j] = __builtin_nontemporal_load(sp + 1);
         }
+#pragma unroll
+        for (uint32_t jj = 0; jj < GI; ++jj) {
+            const uint32_t j = gq * GI + jj;
+            dig[j] = 0;
+            if (wbase + j * 64u + lane < n) {
+                Msg m;
+                m.tcd = (uint64_t)h0[j].x | ((uint64_t)h0[j].y << 32);
+                m.n0 = (uint64_t)h0[j].z | ((uint64_t)h0[j].w << 32);
+                m.n1 = (uint64_t)h1[j].x | ((uint64_t)h1[j].y << 32);
+                m.meta = h1[j].z;
+                m.aux = h1[j].w;
+                dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+                if (FMT == 8) {
+                    u32x4 wr;
+                    bad |= (encode_wire(h0[j], h1[j], wr) ? 0u : 1u) | (encode_narrow(sm.P, h0[j], h1[j], nrec[j]) ? 0u : 2u);
+                }
+            }
+        }
+        if (G > 1 && gq + 1 < G) __builtin_amdgcn_sched_barrier(0);
     }
+    if (FMT == 8 && bad) atomicOr(wire_status, bad);
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts, nullptr, epoch, wire_status);
@@ -2614,11 +2634,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __
                 if (!encode_wire(h0[j], h1[j], wr)) atomicOr(wire_status, 1u);
                 reinterpret_cast<u32x4*>(out)[g] = wr;
             } else if (FMT == 8) {
-                u32x4 wr;
-                uint2 nw;
-                const uint32_t bad = (encode_wire(h0[j], h1[j], wr) ? 0u : 1u) | (encode_narrow(sm.P, h0[j], h1[j], nw) ? 0u : 2u);
-                if (bad) atomicOr(wire_status, bad);
-                reinterpret_cast<uint2*>(out)[g] = nw;
+                reinterpret_cast<uint2*>(out)[g] = nrec[j];
             } else {
                 u32x4* dp = reinterpret_cast<u32x4*>(static_cast<orl_msg_hdr*>(out) + g);
                 dp[0] = h0[j];
