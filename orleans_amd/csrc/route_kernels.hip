@@ -2448,6 +2448,9 @@ constexpr uint32_t kPartTile = kRouteThreads * kPartItems;
 #define ORL_PART_GROUPS 2
 #endif
 constexpr uint32_t kPartGroups = ORL_PART_GROUPS;  // k_part_lb<8>: header load groups per tile (see there)
+#ifndef ORL_PART_MINWG
+#define ORL_PART_MINWG 1
+#endif
 constexpr uint32_t kLbSpinLimit = 1u << 24;
 
 struct LbShared {
@@ -2564,7 +2567,7 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
 // 8 = orl_wire8 (|= 1 as for 16, |= 2 if a message has no 8-B form).  wire_status (optional for FMT 32) also gets
 // ORL_PART_LOOKBACK_FAILED when a tile's look-back gave up (the record positions are then not valid).
 template <int FMT>
-__global__ __launch_bounds__(kRouteThreads) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
+__global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
                                                            void* __restrict__ out, uint32_t* __restrict__ src_index,
