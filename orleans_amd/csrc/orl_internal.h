@@ -239,7 +239,8 @@ struct Scratch {
     uint2* pairs_b;         // [max_batch]
     uint32_t* idx_a;        // [max_batch + 1] fan-out publish offsets
     uint32_t* sorted_keys;  // [max_batch] (LSD fallback only)
-    uint32_t* tile_hist;    // [2048 * rows]
+    uint32_t* tile_hist;    // [2048 * rows] per-(tile, digit) output bases (col_scan's output; also a u32 scan buffer)
+    uint16_t* tile_cnt;     // [2048 * rows] per-(tile, digit) counts written by the histogram passes (col_scan's input)
     uint32_t* scan_sums;    // [scan blocks]
     uint32_t* col_sums;     // [ceil(max_tiles/64) * 2048] column-scan chunk sums
     uint32_t* col_tot;      // [2048 + 1] column totals (+ the hot key's at [bins])

@@ -305,6 +305,18 @@ __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirS
 
 __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { return act < n_act ? act : n_act; }
 
+// A tile's digit counts as one u16 row of the count matrix (a tile holds <= 4096 elements, so every count fits): two
+// bins per 4-B store when the row is 4-B aligned (bins even), else one per 2-B store.  Half the bytes of u32 rows for
+// the histogram pass to write and the column sum / apply to read (k_col_sum, k_col_apply).
+__device__ __forceinline__ void store_count_row(uint16_t* __restrict__ row, const uint32_t* __restrict__ hist, uint32_t bins) {
+    if ((bins & 1u) == 0u) {
+        uint32_t* r2 = reinterpret_cast<uint32_t*>(row);
+        for (uint32_t b = threadIdx.x; b < bins / 2u; b += blockDim.x) r2[b] = hist[2u * b] | (hist[2u * b + 1u] << 16);
+    } else {
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = (uint16_t)hist[b];
+    }
+}
+
 // Stable rank of this lane's digit among the wave's earlier elements with the same digit: one returning LDS
 // atomic on the wave's private counter row.  The LDS services the same-address lanes of one ds_add_rtn_u32
 // in lane order, so lane order == arrival order inside each 64-element step, and consecutive steps of the
@@ -613,7 +625,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          const uint32_t* __restrict__ probe_bad,
                                                          const void* __restrict__ in, uint32_t n,
                                                          uint32_t excl, uint32_t* __restrict__ route,
-                                                         uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist,
+                                                         uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt,
                                                          uint32_t bins, uint32_t shift, uint32_t items,
                                                          const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows) {
     __shared__ RouteSmem<HB> sm;
@@ -740,8 +752,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
     if (HIST) {
         if (hot_rows) wave_add_hot(&sm.hot, hot_mine);
         __syncthreads();
-        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
-        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
+        store_count_row(tile_cnt + (size_t)blockIdx.x * bins, sm.hist, bins);
         if (hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = sm.hot;
     }
 }
@@ -960,7 +971,7 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 // first digit's histogram for stage 4 over messages routed earlier (orl_bucket_device, the host side of hop 2).
 template <bool ACTS>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
-                                                    uint32_t bins, uint32_t* __restrict__ tile_hist,
+                                                    uint32_t bins, uint16_t* __restrict__ tile_cnt,
                                                     const uint32_t* __restrict__ hot_words = nullptr,
                                                     uint32_t* __restrict__ hot_rows = nullptr) {
     __shared__ uint32_t hist[1u << kMaxDigitBits];
@@ -1010,8 +1021,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
         }
     }
     __syncthreads();
-    uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
-    for (uint32_t b = threadIdx.x; b < bins; b += 256) row[b] = hist[b];
+    store_count_row(tile_cnt + (size_t)blockIdx.x * bins, hist, bins);
     if (ACTS && hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = hot;
 }
 
@@ -1023,7 +1033,7 @@ constexpr uint32_t kScanRows = 64;
 
 // hot_rows (stage 4's hot-key path): the hot key's per-row counts, one more column kept apart: the last grid row of each
 // kernel handles it (chunk sums at hot_rows[ntiles + chunk]; the scan and the apply turn them into exclusive bases).
-__global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
+__global__ __launch_bounds__(256) void k_col_sum(const uint16_t* __restrict__ C, uint32_t ntiles, uint32_t bins,
                                                  uint32_t* __restrict__ S, uint32_t* __restrict__ hot_rows) {
     if (hot_rows && blockIdx.y == gridDim.y - 1) {  // one wave: kScanRows = 64 rows, one per lane
         if (threadIdx.x >= 64) return;
@@ -1038,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint32_t* __restrict__ M,
     const uint32_t t1 = min(t0 + kScanRows, ntiles);
     uint32_t acc = 0;
 #pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) acc += M[(size_t)t * bins + d];
+    for (uint32_t t = t0; t < t1; ++t) acc += C[(size_t)t * bins + d];
     S[(size_t)blockIdx.x * bins + d] = acc;
 }
 
@@ -1093,7 +1103,7 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
 
 // row_step: the pass reading the result reads only rows t % row_step == 0 (route tiles smaller than its tile), so
 // only those are written.
-__global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
+__global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ C, uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
                                                    uint32_t row_step, uint32_t* __restrict__ hot_rows) {
     __shared__ uint32_t wsum[kWaves];
@@ -1125,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_col_apply(uint32_t* __restrict__ M, uin
     for (uint32_t t = t0; t < t1; t += 8) {
         uint32_t v[8];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) v[k] = t + k < t1 ? M[(size_t)(t + k) * bins + d] : 0u;
+        for (uint32_t k = 0; k < 8; ++k) v[k] = t + k < t1 ? C[(size_t)(t + k) * bins + d] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
             if (t + k < t1 && (t + k) % row_step == 0) M[(size_t)(t + k) * bins + d] = run;
@@ -2084,7 +2094,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, const orl_msg_hdr* __restrict__ direct, uint32_t nd, uint32_t n,
     uint32_t excl, uint32_t* __restrict__ route,
-    uint32_t* __restrict__ act_out, uint32_t* __restrict__ tile_hist, uint32_t bins, uint32_t shift, uint32_t items) {
+    uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift, uint32_t items) {
     __shared__ FanSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
@@ -2218,8 +2228,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     }
     if (HIST) {
         __syncthreads();
-        uint32_t* row = tile_hist + (size_t)blockIdx.x * bins;
-        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) row[b] = sm.hist[b];
+        store_count_row(tile_cnt + (size_t)blockIdx.x * bins, sm.hist, bins);
     }
 }
 
@@ -3541,17 +3550,18 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
     }
 }
 
-// Column scan of a tile-major [ntiles][bins] histogram into per-(tile, bin) output bases, in place.
+// Column scan of a tile-major [ntiles][bins] u16 count matrix C (s.tile_cnt) into per-(tile, bin) u32 output bases M.
 // row_step: the reading pass uses rows t % row_step == 0 only.
 void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
               uint32_t* hot_rows = nullptr) {
+    const uint16_t* C = s.tile_cnt;
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
     const uint32_t hy = hot_rows ? 1u : 0u;  // the hot column's extra grid row / block
-    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, M, ntiles, bins, s.col_sums, hot_rows);
+    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, C, ntiles, bins, s.col_sums, hot_rows);
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
                        ntiles);
-    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
+    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
                        hot_rows);
 }
 
@@ -3717,7 +3727,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
         if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
-                               (uint32_t)plan.shift[p], bins, s.tile_hist);
+                               (uint32_t)plan.shift[p], bins, s.tile_cnt);
         col_scan(s.tile_hist, nrows, bins, row_step, s, st);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
@@ -3814,7 +3824,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     const bool hot = pick && hot_known(s);
     const uint32_t* hw = hot ? hot_cur(s) : nullptr;
     uint32_t* hr = hot ? s.hot_rows : nullptr;
-    uint32_t* th = hist ? s.tile_hist : nullptr;
+    uint16_t* th = hist ? s.tile_cnt : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
 #define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
@@ -3904,7 +3914,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
                                                        follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
                                                        excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items)
-    if (hist) ORL_FAN(kMaxDigitBits, s.tile_hist, rh.bins, rh.shift);
+    if (hist) ORL_FAN(kMaxDigitBits, s.tile_cnt, rh.bins, rh.shift);
     else ORL_FAN(0, nullptr, 1u, 0u);
 #undef ORL_FAN
 #undef ORL_FAN_
@@ -4088,7 +4098,7 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
     const bool hot = pick && hot_known(s);
     if (rh.on)
         hipLaunchKernelGGL(k_hist_pairs<true>, dim3(ntiles), dim3(256), 0, st, d_act, (uint32_t)n, n_act, rh.shift, rh.bins,
-                           s.tile_hist, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr);
+                           s.tile_cnt, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr);
     int e = (int)hipGetLastError();
     if (e) return e;
     return bucket_after_route(d_act, (uint32_t)n, n_act, kItems, d_order, d_offsets, s, st, hot, pick);
