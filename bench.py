@@ -54,6 +54,14 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _bincount(torch, x, n):
+    """torch.bincount in slices of 2^25 (a single call over 256M elements raised SIGFPE inside torch's histogram kernel)."""
+    out = torch.zeros(n, dtype=torch.int64, device=x.device)
+    for i in range(0, x.numel(), 1 << 25):
+        out += torch.bincount(x[i:i + (1 << 25)], minlength=n).to(torch.int64)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,7 +209,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
         d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
         n1 = d_msgs.view(torch.int64).view(-1, 4)[:, 2]
-        per_dest = torch.bincount(d_ros[d_owner[n1]], minlength=world).to(torch.int64)
+        per_dest = _bincount(torch, d_ros[d_owner[n1]], world)
         del d_owner, d_ros, n1
         if world > 1:
             dist.all_reduce(per_dest)
@@ -355,7 +363,7 @@ def run_rehearsal(args, torch):
     for r in range(R):
         m = W.device_messages(torch, cl, n_grains, n_msgs, seed, start=r * n_msgs, sender_silos=local_silos(cl.n_silos, R, r),
                               zipf=ztab)
-        per_dest += torch.bincount(d_ros[d_owner[m.view(torch.int64).view(-1, 4)[:, 2]]], minlength=R)
+        per_dest += _bincount(torch, d_ros[d_owner[m.view(torch.int64).view(-1, 4)[:, 2]]], R)
         msgs.append(m)
     cap = max(n_msgs, int(per_dest.max().item()))
     cap += cap // 64 + 4096
