@@ -308,6 +308,7 @@ __device__ __forceinline__ uint32_t bucket_key(uint32_t act, uint32_t n_act) { r
 // A tile's digit counts as one u16 row of the count matrix (a tile holds <= 4096 elements, so every count fits): two
 // bins per 4-B store when the row is 4-B aligned (bins even), else one per 2-B store.  Half the bytes of u32 rows for
 // the histogram pass to write and the column sum / apply to read (k_col_sum, k_col_apply).
+static_assert(kTile <= 65535u, "a tile's digit counts must fit the u16 count rows");
 __device__ __forceinline__ void store_count_row(uint16_t* __restrict__ row, const uint32_t* __restrict__ hist, uint32_t bins) {
     if ((bins & 1u) == 0u) {
         uint32_t* r2 = reinterpret_cast<uint32_t*>(row);
@@ -3444,6 +3445,7 @@ int scan_offsets_pick(uint32_t* a, uint64_t m, uint32_t nkeys, uint32_t n, const
 // Elements per thread of the two-level path's MSD pass (tile 8192) and of the route kernels feeding it.
 // (32 = 8192-element tiles measured slower: route 1297 -> 1321 us, MSD pass 221 -> 256 us; profiles/r02_stage4_ab.txt)
 constexpr uint32_t kMsdItems = 16;
+static_assert(kRouteThreads * kMsdItems <= 65535u, "a route tile's digit counts must fit the u16 count rows (store_count_row)");
 
 // ---- stage 4's hot-key path: the three small steps around the two-level sort (see kNoHotKey) -------------------------
 // After the segment scan wrote per-key counts into offsets (the hot key's is 0: its elements were not in any segment),
