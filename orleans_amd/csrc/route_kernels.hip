@@ -3654,14 +3654,11 @@ uint32_t gap_cap() {  // read per launch (a getenv per batch), so a test can cha
     return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
 }
 
-// k_fanout_route's messages per thread and step: ORL_FAN_U = 1, 2 or 4 (A/B).
+// k_fanout_route's messages per thread and step: ORL_FAN_U = 1, 2 or 4 (A/B; read per launch, so a test can switch it).
 int fan_ilp() {
-    static const int u = [] {
-        const char* e = getenv("ORL_FAN_U");
-        const int v = e ? atoi(e) : kFanIlp;
-        return v == 4 ? 4 : v == 2 ? 2 : 1;
-    }();
-    return u;
+    const char* e = getenv("ORL_FAN_U");
+    const int v = e ? atoi(e) : kFanIlp;
+    return v == 4 ? 4 : v == 2 ? 2 : 1;
 }
 
 // The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair

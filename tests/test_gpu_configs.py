@@ -305,11 +305,15 @@ def test_config3_full_size_zipf(torch):
 
 
 # ---- config 4: 10M-account power-law CSR fan-out --------------------------------------------------------------
-def test_config4_full_size_fanout(torch):
+@pytest.mark.parametrize("fan_u", [None, "2", "4"])
+def test_config4_full_size_fanout(torch, monkeypatch, fan_u):
     """BASELINE config 4: 10M accounts, power-law followers (exponent 2.1, 1..1e5), 1M publishers: the fan-out +
     stages 1-4 on the device; the first >= 1M emitted messages (whole publishers) bit-exact vs the oracle's CSR
-    expansion + routing, the rest by properties."""
+    expansion + routing, the rest by properties.  fan_u: the fan-out kernel's messages per thread and step (ORL_FAN_U,
+    an A/B knob: 4 messages per thread and step at this size's 1024-message tiles)."""
     t = torch
+    if fan_u is not None:
+        monkeypatch.setenv("ORL_FAN_U", fan_u)
     n_acc, n_pub = 10_000_000, 1_000_000
     cl = W.default_cluster()
     off, tgt = W.powerlaw_csr(n_acc)
