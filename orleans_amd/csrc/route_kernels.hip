@@ -1364,21 +1364,11 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     }
 }
 
-// bucket_offsets[b] = lower_bound(sorted, b) for b in [0, nb).  Block handles 256 buckets: two binary
-// searches bound its slice of the sorted keys, which it then walks once.
-__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t v) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
-// Bucket offsets in two steps over an offsets array pre-filled with kNoOffset:
+// Round-2 bucket offsets (ORL_OFFSETS_SUFMIN=1, A/B against k_offsets_gaps below), over an offsets array pre-filled
+// with kNoOffset:
 //   k_offsets_mark: one streaming read of the sorted keys; every position i whose key differs from key[i-1]
 //                   starts bucket key[i] (16 keys per thread, 4 x 16-B loads);
-//   k_offsets_fill: empty buckets (still kNoOffset) get lower_bound(sorted, b): where the next key starts.
+//   the empty buckets (still kNoOffset) then get the next present key's start by suffix minima (k_sufmin_*).
 constexpr uint32_t kNoOffset = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(256) void k_fill_u32(uint32_t* __restrict__ a, uint32_t m, uint32_t v) {
@@ -1410,7 +1400,7 @@ __global__ __launch_bounds__(256) void k_offsets_mark(const uint32_t* __restrict
     }
 }
 
-// Empty buckets by a suffix-min scan instead of one binary search per key (k_offsets_fill: 306 us at config 3, whose
+// Empty buckets by a suffix-min scan instead of one binary search per key (306 us at config 3, whose
 // 16M handles are mostly absent from a Zipf batch): present keys hold their first position and positions grow with
 // the key, so offsets[b] = min(offsets[b .. nb), n) is lower_bound(sorted, b) for every b.  In 4096-element chunks:
 // chunk minima; their exclusive suffix minima (one block); each chunk rescanned from its end.
@@ -1592,12 +1582,6 @@ __global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ off
             q[1] = 0;
         }
     }
-}
-
-__global__ __launch_bounds__(256) void k_offsets_fill(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
-                                                      uint32_t* __restrict__ offsets) {
-    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
-    if (b < nb && offsets[b] == kNoOffset) offsets[b] = lower_bound_u32(sorted, n, b);
 }
 
 // ---------------------------------------------------------------------------------------------------
