@@ -265,7 +265,12 @@ int orl_route_batch(orl_ctx* ctx, const orl_msg_hdr* in, size_t n, uint32_t opts
  * (src/OrleansRuntime/Core/Dispatcher.cs:555-579). */
 int orl_route_batch_narrow(orl_ctx* ctx, const orl_wire8* in, size_t n, uint32_t opts, uint32_t* route, uint32_t* act,
                            uint32_t* order, uint32_t* bucket_offsets);
-/* Device-resident form: all pointers in HBM; enqueued on `stream` (hipStream_t, NULL = default). */
+/* Device-resident form: all pointers in HBM; enqueued on `stream` (hipStream_t, NULL = default).
+ * Stage 4 of a context keeps per-context state from batch to batch (the hot-key slots the tail kernel of one batch
+ * writes and the next batch reads, their parity flipped by the launcher, the candidate word of the one-pass level 2,
+ * the long-gap queue of the LSD offsets): every bucketing call of one context (orl_route_*_device, orl_fanout_*_device,
+ * orl_bucket_device) must be enqueued on ONE stream, as the one-pass partitions must (below).  Two streams need two
+ * contexts. */
 int orl_route_batch_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route,
                            uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
 

@@ -264,7 +264,13 @@ struct Scratch {
     uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
+    unsigned long long* res_max = nullptr;  // one-pass level 2: the hot-key pick's candidate (zeroed once, then by k_hot_pick)
+    uint32_t gap_cap = 4096;  // LSD offsets' long-gap queue capacity (env_gap_cap() at context creation)
+    int fan_u = 1;            // fan-out messages per thread and step (env_fan_u() at context creation)
 };
+// Knobs read from the environment once per context (orl_ctx_create): ORL_GAP_CAP, ORL_FAN_U.
+uint32_t env_gap_cap();
+int env_fan_u();
 
 int launch_hash(const orl_grain_key* d_keys, size_t n, uint32_t* d_out, void* stream);
 // Stage-4 ranking self-check on `device` (the current device; k_rank_selfcheck): selects the LDS-atomic rank (0) or the

@@ -176,13 +176,20 @@ int nfail(orl_node* nd, int code, const char* fmt, ...) {
         if (_r != ORL_OK) return nfail((nd), _r, "%s: %s", #call, orl_last_error((nd)->ctx));           \
     } while (0)
 
-// The communicator is unusable (a peer missed a deadline or RCCL reported an error): abort it so RCCL kernels still
-// waiting on peers exit, release an injected stall, and let the streams drain (bounded).  The node stays broken.
+// The communicator is unusable (a peer missed a deadline, RCCL reported an error, or this rank found a device fault its
+// peers cannot see): abort it so RCCL kernels still waiting on peers exit (and the peers' own bounded waits see the
+// error at once instead of at their deadline), break a LOCAL group the same way (every barrier of every rank fails),
+// release an injected stall, and let the streams drain (bounded).  The node stays broken.
 void break_node(orl_node* nd) {
     nd->broken = true;
     if (nd->comm) {
         (void)ncclCommAbort(nd->comm);
         nd->comm = nullptr;
+    }
+    if (nd->group) {
+        std::lock_guard<std::mutex> lk(nd->group->mu);
+        nd->group->broken = true;
+        nd->group->cv.notify_all();
     }
     if (nd->h_stall) __atomic_store_n(nd->h_stall, 1u, __ATOMIC_RELEASE);
 }
@@ -199,7 +206,8 @@ int wait_bounded(orl_node* nd, hipStream_t s, const char* what, int chunk, const
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) return ORL_OK;
         if (q != hipErrorNotReady) return nfail(nd, ORL_E_DEVICE, "%s (chunk %d): %s", what, chunk, hipGetErrorString(q));
-        if (nd->comm && (++polls & 63u) == 0u) {
+        ++polls;  // (both transports: the sleep backoff below applies to LOCAL rank threads too)
+        if (nd->comm && (polls & 63u) == 0u) {
             if (ncclCommGetAsyncError(nd->comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) break;
             ar = ncclSuccess;
         }
@@ -654,8 +662,11 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             uint32_t st = 0;
             if (int r = wait_bounded(nd, nd->sp, "re-partition", (int)c, nullptr)) return r;
             NODE_HIP(nd, hipMemcpy(&st, head + 8, 4, hipMemcpyDeviceToHost));
-            if (st & ORL_PART_LOOKBACK_FAILED)
-                return nfail(nd, ORL_E_DEVICE, "chunk %u: the %u-byte re-partition's look-back gave up (device fault)", c, width);
+            if (st & ORL_PART_LOOKBACK_FAILED) {  // only this rank sees it: abort, so the peers fail now, not at their deadline
+                break_node(nd);
+                return nfail(nd, ORL_E_DEVICE, "chunk %u: the %u-byte re-partition's look-back gave up (device fault); "
+                             "communicator aborted", c, width);
+            }
         }
         width_mask |= width == 8 ? 1u : width == 16 ? 2u : 4u;
         const uint64_t got = plan.n_recv;
@@ -743,7 +754,10 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             uint32_t lb_err = 0;
             if (int r = wait_bounded(nd, nd->sr, "hop-2 partition", -2, nullptr)) return r;
             NODE_HIP(nd, hipMemcpy(&lb_err, d_ferr, 4, hipMemcpyDeviceToHost));
-            if (lb_err) return nfail(nd, ORL_E_DEVICE, "hop-2 partition look-back gave up (device fault)");
+            if (lb_err) {  // only this rank sees it: abort, so the peers fail now, not at their deadline
+                break_node(nd);
+                return nfail(nd, ORL_E_DEVICE, "hop-2 partition look-back gave up (device fault); communicator aborted");
+            }
         }
         const std::vector<Lane> lanes = {Lane{nd->d_fsend, nd->f_cap * wout, nd->d_frecv, wout},
                                          Lane{reinterpret_cast<uint8_t*>(nd->d_fsend_route), nd->f_cap * 4,

@@ -1599,10 +1599,12 @@ __global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ off
 // takes the chunked kernels, else the one-pass k_seg_scan (cheaper when every bucket is short).
 constexpr uint32_t kSkewSlot = 4097;
 
+// res_cap (the one-pass level 2, k_bucket_resident): buckets of <= res_cap messages get no segments (0: every nonempty
+// bucket is segmented).
 template <uint32_t NT>
 __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart,
-                                              uint32_t (*wsum)[16]) {
+                                              uint32_t (*wsum)[16], uint32_t res_cap) {
     constexpr uint32_t Q = 4096 / NT, NW = NT / 64;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t c[Q], p[Q], cs = 0, ps = 0, pmax = 0;
@@ -1610,7 +1612,7 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
     for (uint32_t q = 0; q < Q; ++q) {
         const uint32_t b = threadIdx.x * Q + q;
         c[q] = b < nbk ? (col_tot ? col_tot[b] : n) : 0u;
-        p[q] = (c[q] + seg - 1) / seg;
+        p[q] = c[q] > res_cap ? (c[q] + seg - 1) / seg : 0u;
         cs += c[q];
         ps += p[q];
         pmax = max(pmax, p[q]);
@@ -1655,9 +1657,9 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
 }
 
 __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
-                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
+                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart, uint32_t res_cap) {
     __shared__ uint32_t wsum[3][16];
-    seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum);
+    seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum, res_cap);
 }
 
 // Segment j of the launch: blocks [0, nseg) map XCD-contiguously onto segments (consecutive segments of one
@@ -1666,11 +1668,13 @@ struct SegRange {
     uint32_t bucket, index, lo, hi;
 };
 
+// blk: the block's k-th segment slot, blockIdx.x + k * gridDim.x (a grid smaller than the segment count loops; with a
+// grid that is a multiple of 8 every slot of a block stays on the block's XCD).
 __device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                             uint32_t nbk, uint32_t seg, SegRange& r) {
+                                             uint32_t nbk, uint32_t seg, SegRange& r, uint32_t blk) {
     const uint32_t nseg = sstart[nbk];
-    if (blockIdx.x >= nseg) return false;
-    const uint32_t j = xcd_tile(blockIdx.x, nseg);
+    if (blk >= nseg) return false;
+    const uint32_t j = xcd_tile(blk, nseg);
     uint32_t lo = 0, hi = nbk + 1;  // bucket = upper_bound(sstart, j) - 1 (skips empty buckets)
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1709,7 +1713,7 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
     SegRange r;
-    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
+    for (uint32_t blk = blockIdx.x; seg_of_block(bstart, sstart, nbk, seg, r, blk); blk += gridDim.x) {
     for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
     __syncthreads();
     for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
@@ -1749,19 +1753,24 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
     __syncthreads();
     uint32_t* row = seg_hist + (size_t)r.index * BL;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
+    __syncthreads();  // hist is zeroed again for the block's next segment
+    }
 }
 
 // Per bucket b and low digit l (every bucket has <= kScanRows segments): the segment rows become exclusive prefixes
 // inside the bucket and the column total (messages with key = b << lb | l) goes to counts[key] (keys < nb only).
+// res (k_bucket_resident runs too): only buckets with segments are written; the others' offsets and the keys past the last
+// bucket are the resident kernel's.
 template <int LB>
 __device__ __forceinline__ void seg_scan_bucket(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                 uint32_t nbk, uint32_t nb, uint32_t* __restrict__ counts, uint32_t b,
-                                                uint32_t l) {
+                                                uint32_t l, bool res) {
     constexpr uint32_t BL = 1u << LB;
-    if (b == 0 && l == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+    if (b == 0 && l == 0 && !res)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
         for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
     if (l >= BL) return;
     const uint32_t j0 = sstart[b], j1 = sstart[b + 1];
+    if (res && j0 == j1) return;
     uint32_t run = 0, j = j0;
     for (; j + 4 <= j1; j += 4) {
         uint32_t v[4];
@@ -1810,7 +1819,7 @@ template <int LB>
 __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
                                                uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t c,
-                                               uint32_t l) {
+                                               uint32_t l, bool res) {
     constexpr uint32_t BL = 1u << LB, G = 16;
     const uint32_t nseg = sstart[nbk];
     const uint32_t j0 = c * kScanRows;
@@ -1820,9 +1829,9 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
     if (l == 0)  // the chunk's shape: first bucket, it ends inside, it continues an earlier one, a bucket starts inside
         meta[c] = b | (sstart[b + 1] <= j1 ? kMetaEnds : 0u) | (sstart[b] < j0 ? kMetaCont : 0u) |
                   (sstart[b + 1] < j1 ? kMetaInside : 0u);
-    auto put = [&](uint32_t k, uint32_t v) {
+    auto put = [&](uint32_t k, uint32_t v) {  // res: buckets without segments are the resident kernel's
         const uint32_t key = (k << LB) | l;
-        if (key < nb) counts[key] = v;
+        if (key < nb && !(res && sstart[k] == sstart[k + 1])) counts[key] = v;
     };
     if (sstart[b] == j0)  // b starts this chunk: the empty buckets just before it (no other chunk meets them)
         for (uint32_t k = b; k > 0 && sstart[k - 1] == j0;) put(--k, 0u);
@@ -1852,7 +1861,7 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
         if (j1 == nseg)
             for (uint32_t k = b + 1; k < nbk; ++k) put(k, 0u);  // empty buckets after the last segment
     }
-    if (l == 0 && j1 == nseg)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+    if (l == 0 && j1 == nseg && !res)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
         for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
     carry[(size_t)c * BL + l] = run;
 }
@@ -1861,12 +1870,12 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
 template <int LB>
 __global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                   uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
-                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts) {
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t res) {
     const uint32_t l = blockIdx.y * 256u + threadIdx.x;
     if (!sstart[kSkewSlot]) {
-        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l);
+        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l, res != 0);
     } else {
-        seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l);
+        seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l, res != 0);
     }
 }
 
@@ -1960,7 +1969,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
     SegRange r;
-    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
+    for (uint32_t blk = blockIdx.x; seg_of_block(bstart, sstart, nbk, seg, r, blk); blk += gridDim.x) {
     const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t run[PER];  // global position of the next message with digit threadIdx.x * PER + q
@@ -2030,6 +2039,260 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
         }
         __syncthreads();  // LDS is reused by the next round
     }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Stage 4, level 2 in one pass (round 4): one workgroup of 1024 threads sorts a whole MSD bucket of <= kResCap messages
+// held in registers, so the pairs are read once (the segmented path reads them twice: k_seg_count, then k_seg_scatter)
+// and there is no segment plan, segment scan or offsets scan: a bucket's key counts come out of its own LDS histogram.
+// Bucket b = pairs [bstart[b], bstart[b + 1]) in arrival order (c of them):
+//   1. load: wave w owns the contiguous run [w * 64E, (w + 1) * 64E) of the bucket (E = ceil(c / 1024) steps of 64
+//      lanes), so (wave, step, lane) order is arrival order.  An element lives in ONE register: its level-2 digit (<= 10
+//      bits) and its index minus the index in lane 0 of its step (that base goes to LDS, one word per wave step); a
+//      delta past 22 bits (a sparse bucket) makes the workgroup re-read the indices from the pairs instead;
+//   2. count: one LDS histogram row per wave (u32, 16 x 1024);
+//   3. scan: per digit the waves' exclusive prefix, over digits the bucket-local starts kst -> the bucket offsets, written
+//      here (the hot key's run included: stage 4's hot-key path, whose messages are not in the pairs);
+//   4. place: the digits whose starts fall in one kResHalf-wide band form a window; its elements are ranked (one returning
+//      LDS atomic on the wave's running position of the digit, in lane order: the stable rank of k_seg_scatter, under the
+//      same rank-mode guard) into an LDS image of < kResWin positions, written out as whole runs of `order`.  A digit of
+//      more than kResHalf messages (always the last of its window) is written from registers (consecutive positions).
+// Buckets of more than kResCap messages keep the segmented path (k_seg_plan gives them segments, the others none).
+constexpr uint32_t kResThreads = 1024, kResWaves = kResThreads / 64, kResE = 80, kResCap = kResThreads * kResE;
+constexpr uint32_t kResChunk = 8;                     // loads in flight per thread while a bucket is read
+constexpr uint32_t kResKeys = 1024;                   // level-2 digits of <= 10 bits
+constexpr uint32_t kResWin = 22016, kResHalf = kResWin / 2;
+constexpr uint32_t kResMaxWin = kResCap / kResHalf + 2;
+constexpr uint32_t kResDeltaBits = 22, kResNone = 0xFFFFFFFFu;
+static_assert(kResE % kResChunk == 0, "steps per wave: whole load chunks");
+
+struct ResSmem {
+    uint32_t cnt[kResWaves][kResKeys];  // per-wave digit counts, then each wave's running position of every digit
+    uint32_t stage[kResWin];            // one window's indices in sorted order
+    uint32_t kst[kResKeys + 1];         // bucket-local start of each digit (the hot run excluded); kst[nk] = c
+    uint32_t base[kResWaves][kResE];    // index of lane 0 of each wave step (elements keep their index minus it)
+    uint32_t wsum[kResWaves];
+    uint32_t winlo[kResMaxWin], winhi[kResMaxWin];  // first / one-past-last digit of each window (winlo kResNone: empty)
+    unsigned long long wmax[kResWaves];
+};
+static_assert(sizeof(ResSmem) <= 160u * 1024u, "one resident workgroup per CU");
+
+__device__ __forceinline__ uint32_t res_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kResWaves; ++i) {
+        const uint32_t s = wsum[i];
+        pre += i < w ? s : 0u;
+        total += s;
+    }
+    __syncthreads();
+    return pre + incl - v;
+}
+
+// The hot-key pick's candidate of a bucket: max of (count << 32 | key) over its keys below nb - 1, one atomic per block.
+__device__ __forceinline__ void pick_candidate(unsigned long long best, unsigned long long* wmax, uint32_t nwaves,
+                                               unsigned long long* __restrict__ pick_max) {
+    best = wave_max_u64(best);
+    if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t q = 1; q < nwaves; ++q) best = wmax[q] > best ? wmax[q] : best;
+        if (best) atomicMax(pick_max, best);
+    }
+}
+
+template <int RM>
+__global__ __launch_bounds__(kResThreads) void k_bucket_resident(const uint2* __restrict__ pairs, const uint32_t* __restrict__ bstart,
+                                                                 uint32_t nbk, uint32_t lb, const uint32_t* __restrict__ hot_words,
+                                                                 const uint32_t* __restrict__ hot_total,
+                                                                 uint32_t* __restrict__ offsets, uint32_t nb, uint32_t n,
+                                                                 uint32_t* __restrict__ order,
+                                                                 unsigned long long* __restrict__ pick_max) {
+    __shared__ ResSmem sm;
+    const uint32_t b = blockIdx.x;
+    const uint32_t lo = bstart[b], c = bstart[b + 1] - lo;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    if (b == 0 && tid == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) start at n
+        for (uint32_t k = nbk << lb; k < nb; ++k) offsets[k] = n;
+    if (c > kResCap) return;  // a segmented bucket
+    const uint32_t nk = 1u << lb, kmask = nk - 1u;
+    const uint32_t hk = hot_key_of(hot_words);
+    const uint32_t htot = hk != kNoHotKey ? *hot_total : 0u;
+    const uint32_t hbk = hk != kNoHotKey ? hk >> lb : kResNone;
+    const uint32_t hloc = hbk == b ? hk & kmask : kResNone;                   // the hot key, when it is a digit of this bucket
+    const uint32_t out0 = lo + (hk != kNoHotKey && b > hbk ? htot : 0u);     // the bucket's first output position
+    for (uint32_t i = tid; i < kResWaves * kResKeys; i += kResThreads) (&sm.cnt[0][0])[i] = 0;
+    if (tid < kResMaxWin) {
+        sm.winlo[tid] = kResNone;
+        sm.winhi[tid] = 0;
+    }
+    // 1. load, kResChunk steps in flight
+    const uint32_t E = (c + kResThreads - 1) / kResThreads;
+    const uint32_t w0 = w * 64u * E;
+    const uint32_t cw = c > w0 ? min(c - w0, 64u * E) : 0u;  // the wave's elements
+    const uint2* wp = pairs + lo + w0;
+    uint32_t v[kResE];
+    bool ovf = false;
+#pragma unroll
+    for (uint32_t k = 0; k < kResE / kResChunk; ++k) {
+        if (k * kResChunk * 64u < cw) {
+            uint2 pr[kResChunk];
+#pragma unroll
+            for (uint32_t q = 0; q < kResChunk; ++q)  // 32-bit byte offsets from the wave's (uniform) start
+                pr[q] = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(wp) + min((k * kResChunk + q) * 64u + lane, cw - 1u) * 8u);
+#pragma unroll
+            for (uint32_t q = 0; q < kResChunk; ++q) {
+                const uint32_t j = k * kResChunk + q;
+                const uint32_t base = __builtin_amdgcn_readfirstlane(pr[q].y);
+                if (lane == 0) sm.base[w][j] = base;
+                const uint32_t d = pr[q].y - base;
+                ovf |= j * 64u + lane < cw && d >= (1u << kResDeltaBits);
+                v[j] = (pr[q].x & kmask) | (d << 10);
+            }
+        }  // (steps past the wave's elements are never read)
+    }
+    ovf = __syncthreads_or(ovf);  // (also publishes the zeroed counters)
+    // 2. count
+    uint32_t* row = sm.cnt[w];
+    {
+        const uint32_t dh = cw >= 64u ? wave_hot_digit(v[0] & kmask) : kNoHot;  // a Zipf-hot digit: one atomic per step
+#pragma unroll
+        for (uint32_t j = 0; j < kResE; ++j) {
+            if (j * 64u < cw && j * 64u + lane < cw) {
+                const uint32_t d = v[j] & kmask;
+                if (dh == kNoHot) {
+                    atomicAdd(&row[d], 1u);
+                } else {
+                    const uint64_t m = __ballot(d == dh);
+                    if (d != dh) atomicAdd(&row[d], 1u);
+                    else if ((m & lanes_below()) == 0) atomicAdd(&row[dh], (uint32_t)__popcll(m));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // 3. scan: thread t = digit t
+    const uint32_t t = tid;
+    uint32_t tot = 0;
+    if (t < nk) {
+#pragma unroll
+        for (uint32_t ww = 0; ww < kResWaves; ++ww) {
+            const uint32_t x = sm.cnt[ww][t];
+            sm.cnt[ww][t] = tot;
+            tot += x;
+        }
+    }
+    uint32_t csum;
+    const uint32_t ks = res_excl_scan(tot, sm.wsum, csum);
+    const uint32_t key = (b << lb) | t;
+    if (t < nk) {
+        sm.kst[t] = ks;
+        if (t == nk - 1u) sm.kst[nk] = ks + tot;
+#pragma unroll
+        for (uint32_t ww = 0; ww < kResWaves; ++ww) sm.cnt[ww][t] += ks;
+        if (key < nb) offsets[key] = out0 + ks + (hloc != kResNone && t > hloc ? htot : 0u);
+    }
+    if (pick_max)
+        pick_candidate((t < nk && key + 1u < nb) ? ((unsigned long long)(tot + (t == hloc ? htot : 0u)) << 32) | key : 0ull,
+                       sm.wmax, kResWaves, pick_max);
+    __syncthreads();
+    if (t < nk) {  // windows: maximal runs of digits with equal kst / kResHalf
+        const uint32_t wi = ks / kResHalf;
+        if (t == 0 || sm.kst[t - 1] / kResHalf != wi) sm.winlo[wi] = t;
+        if (t == nk - 1u || sm.kst[t + 1] / kResHalf != wi) sm.winhi[wi] = t + 1u;
+    }
+    __syncthreads();
+    // 4. place, window by window
+    const uint32_t nwin = sm.kst[nk - 1u] / kResHalf + 1u;
+    const uint32_t hpos = hloc != kResNone ? sm.kst[hloc] : kResNone;  // the hot run sits before this bucket position
+    for (uint32_t i = 0; i < nwin; ++i) {
+        const uint32_t klo = sm.winlo[i];
+        if (klo == kResNone) continue;
+        const uint32_t khi = sm.winhi[i];
+        const uint32_t big = sm.kst[khi] - sm.kst[khi - 1u] > kResHalf ? khi - 1u : kResNone;
+        const uint32_t wlo = sm.kst[klo], whi = big != kResNone ? sm.kst[big] : sm.kst[khi];
+        const uint32_t base = i * kResHalf;
+#pragma unroll
+        for (uint32_t j = 0; j < kResE; ++j) {
+            if (j * 64u < cw) {
+                uint32_t vj = v[j], ln = lane;
+                asm volatile("" : "+v"(vj), "+v"(ln));  // keeps the per-step math inside the window loop (hoisted: E more registers)
+                const uint32_t d = vj & kmask;
+                if (j * 64u + ln < cw && d >= klo && d < khi) {
+                    uint32_t pos;
+                    if (RM == kRmBallot) pos = wave_rank_ballot<10, false>(row, d, __builtin_amdgcn_read_exec(), lanes_below());
+                    else if (RM == kRmHot) pos = rank_step_uniform<false>(row, d);
+                    else pos = atomicAdd(&row[d], 1u);
+                    const uint32_t idx = ovf ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(wp) + (j * 64u + ln) * 8u + 4u)
+                                             : sm.base[w][j] + (vj >> 10);
+                    if (d == big) order[out0 + pos + (pos >= hpos ? htot : 0u)] = idx;
+                    else sm.stage[pos - base] = idx;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = wlo + tid; q < whi; q += kResThreads) order[out0 + q + (q >= hpos ? htot : 0u)] = sm.stage[q - base];
+        __syncthreads();
+    }
+}
+
+// Offsets of the segmented buckets when k_bucket_resident takes the others: the per-key counts k_seg_scan wrote into
+// `offsets` (+ the hot key's run) become the bucket's output start + bucket-local exclusive prefixes; the largest count
+// goes to the hot-key pick.
+template <int LB>
+__global__ __launch_bounds__(256) void k_bucket_keyscan(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                                        const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
+                                                        uint32_t* __restrict__ offsets, uint32_t nb,
+                                                        unsigned long long* __restrict__ pick_max) {
+    constexpr uint32_t BL = 1u << LB, Q = BL >= 256u ? BL / 256u : 1u;
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ unsigned long long wmax[kWaves];
+    const uint32_t b = blockIdx.x;
+    if (sstart[b] == sstart[b + 1]) return;  // the resident kernel's bucket
+    const uint32_t hk = hot_key_of(hot_words);
+    const uint32_t htot = hk != kNoHotKey ? *hot_total : 0u;
+    const uint32_t hbk = hk != kNoHotKey ? hk >> LB : kResNone;
+    const uint32_t hloc = hbk == b ? hk & (BL - 1u) : kResNone;
+    const uint32_t out0 = bstart[b] + (hk != kNoHotKey && b > hbk ? htot : 0u);
+    uint32_t cnt[Q], s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+        const uint32_t t = threadIdx.x * Q + q, key = (b << LB) | t;
+        cnt[q] = (t < BL && key < nb) ? offsets[key] + (t == hloc ? htot : 0u) : 0u;
+        s += cnt[q];
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, wsum, total) + out0;
+    unsigned long long best = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+        const uint32_t t = threadIdx.x * Q + q, key = (b << LB) | t;
+        if (t < BL && key < nb) {
+            offsets[key] = run;
+            if (key + 1u < nb) best = max(best, ((unsigned long long)cnt[q] << 32) | key);
+        }
+        run += cnt[q];
+    }
+    if (pick_max) pick_candidate(best, wmax, kWaves, pick_max);
+}
+
+// The hot-key pick of a batch whose level 2 ran k_bucket_resident (+ k_bucket_keyscan): the next batch's key as the offsets
+// scan's PICK form decides it; the candidate word is cleared for the next batch.
+__global__ void k_hot_pick(unsigned long long* __restrict__ pick_max, uint32_t n, uint32_t* __restrict__ next_key,
+                           uint32_t* __restrict__ host_word) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long best = *pick_max;
+    const uint32_t c = (uint32_t)(best >> 32), k = (uint32_t)best;
+    const uint32_t key = ((uint64_t)c * kHotShare >= n && c >= kHotMinCount) ? k : kNoHotKey;
+    __hip_atomic_store(next_key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *pick_max = 0;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -3564,13 +3827,21 @@ RouteHist route_hist(uint32_t n_act) {
     return {true, 1u << bp.lsd.bits[0], (uint32_t)bp.lsd.shift[0]};
 }
 
+// Segment-kernel grid when k_bucket_resident takes the buckets of <= kResCap messages: the segmented rest (hot buckets) is
+// usually small or absent, so the count and scatter kernels loop over their segments from a grid of this many blocks
+// instead of launching one (mostly idle) block per possible segment.
+constexpr uint32_t kResSegGrid = 2048;
+
+// res: k_bucket_resident already placed the buckets without segments and wrote their offsets; the segmented buckets' key
+// counts then become offsets per bucket (k_bucket_keyscan) instead of by one scan over every key.
 template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
+                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick, bool res) {
     const uint32_t nb = n_act + 2;
-#define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
+    const uint32_t lgrid = res ? std::min(grid, kResSegGrid) : grid;
+#define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(lgrid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
-#define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
+#define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(lgrid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
                                          s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
@@ -3581,29 +3852,38 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     const uint32_t cb = ceil_div(1u << LB, 256);
     const uint32_t nch = ceil_div(grid, kScanRows);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb, s.seg_carry,
-                       s.seg_meta, d_offsets);
+                       s.seg_meta, d_offsets, res ? 1u : 0u);
     hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
                        d_offsets);
     const uint32_t* hw = hot_cur(s);
-    if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
-    if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
-        scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
-    else
-        scan_inplace(d_offsets, nb, s, st);
+    if (res) {  // per-bucket offsets of the segmented buckets (+ their pick candidates)
+        hipLaunchKernelGGL((k_bucket_keyscan<LB>), dim3(nbk), dim3(256), 0, st, s.bstart, s.sstart, hot ? hw : nullptr,
+                           s.col_tot + nbk, d_offsets, nb, pick ? s.res_max : nullptr);
+    } else {
+        if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
+        if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
+            scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
+        else
+            scan_inplace(d_offsets, nb, s, st);
+    }
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
     else ORL_SS(IN_SOA16);
     if (hot)  // the hot run's copy (this batch's key: hw)
         hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0, st,
                            hw, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
+    if (res && pick) {  // the next batch's hot key (flips the slots: hw stays this batch's)
+        hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(64), 0, st, s.res_max, n, s.hot + ((s.hot_parity + 1u) & 1u), s.hot_host_dev);
+        s.hot_parity ^= 1u;
+    }
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
+                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick, bool res = false) {
     switch (lb) {
-#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot, pick); break;
+#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot, pick, res); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3622,6 +3902,15 @@ bool stage4_soa() {
     return soa;
 }
 
+// Two-level path's level 2: ORL_NO_RESIDENT=1 segments every bucket (the round-3 form, A/B against k_bucket_resident).
+bool resident_on() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_NO_RESIDENT");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 // LSD path's bucket offsets: ORL_OFFSETS_SUFMIN=1 keeps the round-2 five-launch form (A/B).
 bool offsets_sufmin() {
     static const bool on = [] {
@@ -3631,19 +3920,6 @@ bool offsets_sufmin() {
     return on;
 }
 
-// Queue capacity of k_offsets_gaps (pieces); ORL_GAP_CAP lowers it (tests: the full-queue fallback).
-uint32_t gap_cap() {  // read per launch (a getenv per batch), so a test can change it in-process
-    const char* e = getenv("ORL_GAP_CAP");
-    const long v = e ? atol(e) : (long)kGapCap;
-    return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
-}
-
-// k_fanout_route's messages per thread and step: ORL_FAN_U = 1, 2 or 4 (A/B; read per launch, so a test can switch it).
-int fan_ilp() {
-    const char* e = getenv("ORL_FAN_U");
-    const int v = e ? atoi(e) : kFanIlp;
-    return v == 4 ? 4 : v == 2 ? 2 : 1;
-}
 
 // The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair
 // layout; ORL_NO_HOT=1 turns it off (A/B).
@@ -3696,9 +3972,22 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
             }
             kin = s.pairs_a;
         }
-        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
+        // level 2: buckets of <= kResCap messages in one pass (k_bucket_resident), the rest segmented
+        const bool res = bp.hb > 0 && bp.lb <= 10 && !stage4_soa() && resident_on() && s.res_max;
+        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart,
+                           res ? kResCap : 0u);
+        const bool hot2 = hot && bp.hb > 0, pick2 = (hot || pick) && bp.hb > 0;
+        if (res) {
+            const uint32_t* hw = hot2 ? hot_cur(s) : nullptr;
+#define ORL_RES(R) hipLaunchKernelGGL((k_bucket_resident<R>), dim3(nbk), dim3(kResThreads), 0, st, s.pairs_a, s.bstart, nbk,      \
+                                      (uint32_t)bp.lb, hw, s.col_tot + nbk, d_offsets, n_act + 2, n, d_order,                    \
+                                      pick2 ? s.res_max : nullptr)
+            const int rm = host_rm(s.device);
+            if (rm == kRmPlain) ORL_RES(kRmPlain); else if (rm == kRmHot) ORL_RES(kRmHot); else ORL_RES(kRmBallot);
+#undef ORL_RES
+        }
         const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
-        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
+        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot2, pick2, res);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;
@@ -3728,12 +4017,26 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     }
     // every bucket written once from the gaps between consecutive sorted keys (positions 0..n: n + 1 of them)
     hipLaunchKernelGGL(k_offsets_gaps, dim3(ceil_div(n + 1, kGapBlock)), dim3(256), 0, st, s.sorted_keys, n, nb,
-                       d_offsets, s.gap_q, gap_cap());
-    hipLaunchKernelGGL(k_offsets_long, dim3(256), dim3(256), 0, st, d_offsets, s.gap_q, gap_cap());
+                       d_offsets, s.gap_q, s.gap_cap);
+    hipLaunchKernelGGL(k_offsets_long, dim3(256), dim3(256), 0, st, d_offsets, s.gap_q, s.gap_cap);
     return (int)hipGetLastError();
 }
 
 }  // namespace
+
+// Test / A/B knobs read once per context (orl_ctx_create), never per launch: ORL_GAP_CAP lowers the LSD offsets' long-gap
+// queue (tests: the full-queue fallback); ORL_FAN_U = 1, 2 or 4 fan-out messages per thread and step.
+uint32_t env_gap_cap() {
+    const char* e = getenv("ORL_GAP_CAP");
+    const long v = e ? atol(e) : (long)kGapCap;
+    return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
+}
+
+int env_fan_u() {
+    const char* e = getenv("ORL_FAN_U");
+    const int v = e ? atoi(e) : kFanIlp;
+    return v == 4 ? 4 : v == 2 ? 2 : 1;
+}
 
 int launch_rank_selfcheck(int device, int mode, uint32_t* ballot_out) {
     uint32_t* d_err = nullptr;
@@ -3887,8 +4190,8 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     const bool hist = buckets && rh.on;
 
 // the fan-out kernel takes the 16-B form: the 8-B form measured slower here (config 4: 0.266 vs 0.247 ms)
-// U messages per thread and step (fan_ilp(): ORL_FAN_U, A/B)
-#define ORL_FAN(H, TH, BINS, SHIFT) do { const int u_ = fan_ilp();                                                          \
+// U messages per thread and step (s.fan_u: ORL_FAN_U at context creation, A/B)
+#define ORL_FAN(H, TH, BINS, SHIFT) do { const int u_ = s.fan_u;                                                          \
         if (dv.probe) { if (u_ == 4) ORL_FAN_(H, 16, 4, TH, BINS, SHIFT); else if (u_ == 2) ORL_FAN_(H, 16, 2, TH, BINS, SHIFT); \
                         else ORL_FAN_(H, 16, 1, TH, BINS, SHIFT); }                                                          \
         else ORL_FAN_(H, 0, 1, TH, BINS, SHIFT); } while (0)

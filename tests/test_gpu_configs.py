@@ -662,6 +662,67 @@ def test_stage4_hot_key_path_vs_oracle(torch, n_act):
     eng.close()
 
 
+@pytest.mark.parametrize("rank_mode", ["hot", "plain", "ballot"])
+def test_stage4_resident_level2_vs_oracle(torch, monkeypatch, rank_mode):
+    """Stage 4's one-pass level 2 (k_bucket_resident: a bucket of <= 81920 messages sorted in one workgroup's registers)
+    beside the segmented path for larger buckets (k_seg_* + k_bucket_keyscan), in every ranking variant.  Batches: uniform;
+    a digit of more than half an LDS window in a resident bucket (written from registers); a bucket past the resident
+    capacity next to resident ones; a sparse bucket whose indices jump by > 2^22 inside one wave step (the index re-read);
+    the hot-key path with its key in a resident and in a segmented bucket; n_act + 1 == 2^20 (the key past the last
+    bucket); tiny and all-unresolved batches.  Order and offsets == the oracle's stable bucketing
+    (ActivationData.EnqueueMessage, ActivationData.cs:483-514)."""
+    t = torch
+    if rank_mode == "plain":
+        monkeypatch.setenv("ORL_RANK_UNIFORM", "0")
+    o = cpu_ref.Oracle(8)
+    for n_act in (1_000_000, (1 << 20) - 1):
+        rng = np.random.default_rng(n_act + len(rank_mode))
+        eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=7_000_000, device=0)
+        W.setup_engine(eng, W.default_cluster())
+        eng.set_rank_mode(1 if rank_mode == "ballot" else 0)
+
+        def uni(n, lo=0, hi=n_act):
+            return rng.integers(lo, hi, n, dtype=np.int64).astype(np.uint32)
+
+        def put(a, key, count):  # `count` messages of `key` at random positions
+            a[rng.choice(len(a), count, replace=False)] = key
+            return a
+
+        sparse = uni(6_000_000, 0, 500_000)
+        sparse[:100] = n_act - 5                   # the bucket of n_act - 5: 100 messages at the start ...
+        sparse[5_000_000:5_000_100] = n_act - 5    # ... and 100 five million positions later
+        big_bucket = put(uni(4_000_000), 77, 100_000)   # bucket 0: ~100k messages > the resident capacity
+        hot_seg = put(put(uni(4_000_000), 5 * 1024 + 9, 1_300_000), 5 * 1024 + 3, 100_000)
+        plan = [uni(3_000_000),
+                put(put(uni(4_000_000), 5 * 1024 + 7, 15_000), 6 * 1024 + 1, 30_000),  # digits > half a window
+                big_bucket,
+                sparse,
+                put(uni(4_000_000), 123_457, 1_300_000),   # picks 123457 (a resident bucket's digit)
+                put(uni(4_000_000), 123_457, 1_200_000),   # ... and uses it
+                hot_seg,                                   # picks 5*1024+9, whose bucket is resident
+                put(hot_seg.copy(), 5 * 1024 + 3, 1),      # uses it; its bucket (+100k of 5*1024+3) is segmented
+                uni(1000),
+                np.full(1_100_000, L.NO_ACT, np.uint32),
+                np.array([n_act - 1], np.uint32)]
+        off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
+        for k, a in enumerate(plan):
+            d_act = t.from_numpy(a.view(np.int32)).cuda()
+            order = t.empty(len(a), dtype=t.int32, device="cuda")
+            off.fill_(-1)
+            eng.bucket_device(d_act, len(a), order, off)
+            t.cuda.synchronize()
+            eo, ef = o.bucket(a, n_act)
+            np.testing.assert_array_equal(_u32(order), eo, err_msg=f"n_act {n_act} batch {k} order")
+            np.testing.assert_array_equal(_u32(off), ef, err_msg=f"n_act {n_act} batch {k} offsets")
+            if k in (4, 5):
+                assert eng.query(L.Q_HOT_KEY) == 123_457
+            if k in (6, 7):
+                assert eng.query(L.Q_HOT_KEY) == 5 * 1024 + 9
+        assert eng.query(L.Q_HOT_BATCHES) >= 2
+        eng.set_rank_mode(0)
+        eng.close()
+
+
 # ---- stage 4, LSD plan (keys > 22 bits): bucket offsets from the gaps between sorted keys -----------------------
 @pytest.mark.parametrize("cap", [None, "3"])
 def test_lsd_offsets_long_gaps_vs_oracle(torch, monkeypatch, cap):
