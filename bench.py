@@ -35,6 +35,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+from orleans_amd import _lib as L  # noqa: E402
 L_NODE_ID_BYTES = 128
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -54,12 +55,26 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def _bincount(torch, x, n):
-    """torch.bincount in slices of 2^25 (a single call over 256M elements raised SIGFPE inside torch's histogram kernel)."""
-    out = torch.zeros(n, dtype=torch.int64, device=x.device)
-    for i in range(0, x.numel(), 1 << 25):
-        out += torch.bincount(x[i:i + (1 << 25)], minlength=n).to(torch.int64)
-    return out
+def owner_rank_counts(torch, cl, d_msgs, n, ros, world, device=0, piece=1 << 22):
+    """Messages of a batch per directory-owner rank, counted by the library's own owner partition
+    (orl_partition_by_owner_device: stages 1-2 + the per-rank counts of its send queues) over 4M-message pieces, with a
+    throwaway context: the receive capacity (max_recv) of a node run is sized by the same code that routes."""
+    from orleans_amd import workloads as W
+    from orleans_amd.engine import GrainDirectoryEngine
+    e = GrainDirectoryEngine(n_act=1, dir_capacity=16, max_batch=piece, device=device)
+    W.setup_engine(e, cl)
+    out = torch.empty((piece, 8), dtype=torch.int32, device="cuda")
+    idx = torch.empty(piece, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(world, dtype=torch.int64, device="cuda")
+    total = torch.zeros(world, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for lo in range(0, n, piece):
+        k = min(piece, n - lo)
+        e.partition_by_owner_device(d_msgs[lo:lo + k], k, ros, world, 0, out, idx, cnt, stream=st)
+        total += cnt
+    torch.cuda.synchronize()
+    e.close()
+    return total
 
 
 def main():
@@ -94,6 +109,9 @@ def main():
                     help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "route_kernel_pmc.json"))
+    ap.add_argument("--check-sample", type=int, default=256 * 1024,
+                    help="N > 1 (and --local-ranks): hosted messages per rank checked against the oracle after the timed "
+                         "steps, on top of the size-independent checks of every hosted message (0: no oracle sample)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -137,6 +155,9 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if res.get("check") not in (None, "ok"):  # a failed self-check of the hosted output fails the run (every rank)
+        log(f"self-check FAILED: {res['check']}")
+        sys.exit(1)
 
 
 def timed_steps(args, torch, dist, world, step, sync):
@@ -175,6 +196,57 @@ def read_traffic(path, msgs_per_launch, world):
     return None
 
 
+# ---- the node's correctness evidence (checker: after the timed steps, outside timing) ------------------------
+def node_self_check(torch, eng, res, rank, cl, keys, owner, reg, local_mask, n_act, ros, expect_owned, sample, stream=None):
+    """One rank's hosted output of the last timed batch: the size-independent properties of every hosted message on the
+    device (orleans_amd/selfcheck.py: owner / host / status / handle per message, a permutation grouped by activation, FIFO
+    inside every bucket, offsets = the count prefix), the owned count against the workload's own per-destination count,
+    and the first `sample` hosted messages routed by the oracle (oracle/cpu_ref.py, the checker) bit for bit.  Returns
+    the list of failures (empty: ok)."""
+    from orleans_amd import selfcheck as SC
+    from orleans_amd.node import narrow_records_to_headers, wire_records_to_headers
+    errs = []
+    if res.hop2:
+        errs.append("hop 2 forwarded messages (every activation of the workload lives on its directory owner)")
+    if expect_owned is not None and res.n_owned != expect_owned:
+        errs.append(f"owned {res.n_owned} messages, the workload sends this rank {expect_owned}")
+    d = SC.fetch_node_result(torch, eng, res, n_act, stream=stream)
+    dev = d["route"].device
+    owner_t = torch.as_tensor(owner.astype(np.int64), device=dev)
+    handle_t = torch.as_tensor(SC.local_handles(owner, reg, local_mask), device=dev)
+    ros_t = torch.as_tensor(np.asarray(ros, np.int64), device=dev)
+    errs += SC.check_routes(torch, d["route"], d["act"], d["n1"], owner_t, handle_t, bool(reg.all()), ros_t, rank)
+    errs += SC.check_stage4(torch, d["act"], d["order"], d["offsets"], n_act)
+    k = min(int(sample), res.n_hosted)
+    if k:  # the oracle replays this rank's directory partition over the first k hosted records
+        from oracle import cpu_ref
+        hdr, left = [], k
+        for p, cnt, w in res.segments:
+            take = min(cnt, left)
+            if take:
+                raw = eng.copy_to_host(np.zeros(take * w, np.uint8), p, stream=stream)
+                hdr.append(raw.view(L.MSG_DTYPE) if w == 32 else wire_records_to_headers(raw) if w == 16 else
+                           narrow_records_to_headers(raw, getattr(eng, "wire_types", ())))
+                left -= take
+            if not left:
+                break
+        hdr = np.concatenate(hdr)
+        o = cpu_ref.Oracle(cl.n_silos, local=list(np.ones(cl.n_silos, np.uint8) if local_mask is None else local_mask))
+        for s in range(cl.n_silos):
+            o.add_server(s, int(cl.hashes[s]))
+        h = SC.local_handles(owner, reg, local_mask)
+        sel = np.nonzero(h >= 0)[0]
+        o.register(keys[sel], h[sel].astype(np.uint32), owner[sel])
+        r_ref, a_ref = o.route(hdr)
+        r_got = d["route"][:k].cpu().numpy().astype(np.uint32)
+        a_got = d["act"][:k].cpu().numpy().astype(np.uint32)
+        if not np.array_equal(r_got, r_ref):
+            errs.append(f"route words differ from the oracle for {int((r_got != r_ref).sum())} of {k} sampled messages")
+        if not np.array_equal(a_got, a_ref):
+            errs.append(f"handles differ from the oracle for {int((a_got != a_ref).sum())} of {k} sampled messages")
+    return errs
+
+
 # ---- configs 2 and 3: single-target messages ---------------------------------------------------------------
 def run_single_target(args, torch, dist, rank, world, local_rank):
     from orleans_amd import workloads as W
@@ -205,16 +277,13 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     local_mask = None
     n_act = n_grains
     if world > 1:
-        # receive capacity: every rank's per-destination counts, summed over ranks (Zipf: the hot owners get more)
-        d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
-        d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
-        n1 = d_msgs.view(torch.int64).view(-1, 4)[:, 2]
-        per_dest = _bincount(torch, d_ros[d_owner[n1]], world)
-        del d_owner, d_ros, n1
-        if world > 1:
-            dist.all_reduce(per_dest)
+        # receive capacity: every rank's per-destination counts (the library's owner partition), summed over ranks
+        # (Zipf: the hot owners get more)
+        per_dest = owner_rank_counts(torch, cl, d_msgs, n_msgs, ros, world, device=local_rank)
+        dist.all_reduce(per_dest)
         cap = max(n_msgs, int(per_dest.max().item()))
         cap += cap // 64 + 4096
+        expect_owned = int(per_dest[rank].item())  # the self-check's owned count (every rank's messages to my silos)
     if world > 1:  # this rank's silos hold only their own partition; their catalog numbers its activations densely
         local_mask = np.zeros(cl.n_silos, np.uint8)
         local_mask[mine] = 1
@@ -224,7 +293,9 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     if world > 1 and not args.wire16:  # the node's grain classes: 8-B exchange records
         eng.set_wire_types([W.grain_tcd(cl)])
     n_reg = W.register_population(eng, keys, owner, reg, local_mask, dense_local=world > 1)
-    del keys, uni
+    del uni
+    if world == 1:
+        del keys
     log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
         f"receive capacity {cap}")
     stream = torch.cuda.current_stream().cuda_stream
@@ -256,6 +327,12 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
             stats["remote"] = stats.get("remote", 0) + res.n_sent_remote
             stats["fwd"] = stats.get("fwd", 0) + res.n_forwarded
             stats.setdefault("widths", set()).update(w for _, c, w in res.segments if c)
+            xs = node.stats()
+            stats["wait_us"] = stats.get("wait_us", 0) + xs["host_wait_us"]
+            stats["waits"] = stats.get("waits", 0) + xs["host_waits"]
+            stats["bytes_sent"] = [a + b for a, b in zip(stats.get("bytes_sent", [0] * world), xs["bytes_sent"])]
+            stats["comm_count"] = xs["comm_count"]
+            stats["last"] = res
             return res.n_owned
     log(f"setup {time.perf_counter() - t_setup:.1f}s; warmup {args.warmup}")
     eng.set_timing(False)
@@ -288,6 +365,20 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf, 1.0 - args.unregistered)
+    check = None
+    if node is not None:  # correctness evidence of the multi-GPU run: every rank checks what it hosted (outside timing)
+        t_chk = time.perf_counter()
+        errs = node_self_check(torch, eng, stats["last"], rank, cl, keys, owner, reg, local_mask, n_act, ros, expect_owned,
+                               args.check_sample, stream=stream)
+        tot = torch.tensor([stats["last"].n_hosted], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot)
+        if int(tot.item()) != n_total:
+            errs.append(f"the ranks host {int(tot.item())} messages of {n_total}")
+        gathered = [None] * world
+        dist.all_gather_object(gathered, errs)
+        bad = [f"rank {r}: {e}" for r, es in enumerate(gathered) for e in es]
+        check = "ok" if not bad else "; ".join(bad)
+        log(f"rank {rank}: self-check {'ok' if not errs else errs} ({time.perf_counter() - t_chk:.1f}s)")
     if node is not None:
         node.close()
     eng.close()
@@ -332,7 +423,14 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
                            "rank0_forwarded_hop2_per_step": stats["fwd"] / args.steps,
                            "record_bytes": rec_w,
                            "rank0_xgmi_bytes_per_step": rec_w * stats["remote"] / args.steps,
-                           "receive_capacity": cap}
+                           "receive_capacity": cap,
+                           "ncclCommCount": stats["comm_count"],
+                           "rank0_bytes_sent_per_peer_per_step": [b / args.steps for b in stats["bytes_sent"]],
+                           "rank0_host_wait_ms_per_step": stats["wait_us"] / 1e3 / args.steps,
+                           "rank0_host_wait_ms_per_chunk": stats["wait_us"] / 1e3 / args.steps / max(1, args.chunks),
+                           "rank0_host_waits_per_step": stats["waits"] / args.steps}
+        out["check"] = check
+        out["check_sample_per_rank"] = args.check_sample
     return out
 
 
@@ -354,27 +452,27 @@ def run_rehearsal(args, torch):
     n_msgs = n_total // R
     cl = W.balanced_cluster()
     ros = rank_of_silo(cl.n_silos, R)
-    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    keys, uni, owner, reg = W.grain_population(cl, n_grains, 1.0 - args.unregistered)
     seed = W.SEED_C3 if zipf else W.SEED_C2
     ztab = W.zipf_tables(torch, n_grains, seed) if zipf else None
-    d_owner = torch.from_numpy(owner.astype(np.int64)).cuda()
-    d_ros = torch.from_numpy(ros.astype(np.int64)).cuda()
     msgs, per_dest = [], torch.zeros(R, dtype=torch.int64, device="cuda")
     for r in range(R):
         m = W.device_messages(torch, cl, n_grains, n_msgs, seed, start=r * n_msgs, sender_silos=local_silos(cl.n_silos, R, r),
                               zipf=ztab)
-        per_dest += _bincount(torch, d_ros[d_owner[m.view(torch.int64).view(-1, 4)[:, 2]]], R)
+        per_dest += owner_rank_counts(torch, cl, m, n_msgs, ros, R)
         msgs.append(m)
     cap = max(n_msgs, int(per_dest.max().item()))
     cap += cap // 64 + 4096
-    del d_owner, d_ros
-    engs, nodes, streams = [], [], []
+    engs, nodes, streams, masks, n_acts = [], [], [], [], []
     gid = b"bench-rehearsal"
+    expect_owned = [int(x) for x in per_dest.cpu().numpy()]
     for r in range(R):
         mine = local_silos(cl.n_silos, R, r)
         mask = np.zeros(cl.n_silos, np.uint8)
         mask[mine] = 1
+        masks.append(mask)
         n_act = max(1, int((reg & mask[owner].astype(bool)).sum()))
+        n_acts.append(n_act)
         e = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_act, max_batch=max(cap, n_msgs), device=0)
         W.setup_engine(e, cl, local_silos=mine)
         if not args.wire16:
@@ -385,12 +483,18 @@ def run_rehearsal(args, torch):
                                chunks=args.chunks))
         streams.append(torch.cuda.Stream())
     torch.cuda.synchronize()
-    stats = [dict(owned=0, remote=0) for _ in range(R)]
+    stats = [dict(owned=0, remote=0, wait_us=0, waits=0) for _ in range(R)]
 
     def one(r):
         res = nodes[r].route_batch_device(msgs[r], n_msgs, stream=streams[r].cuda_stream)
         stats[r]["owned"] += res.n_owned
         stats[r]["remote"] += res.n_sent_remote
+        xs = nodes[r].stats()
+        stats[r]["wait_us"] += xs["host_wait_us"]
+        stats[r]["waits"] += xs["host_waits"]
+        stats[r]["bytes_sent"] = [a + b for a, b in zip(stats[r].get("bytes_sent", [0] * R), xs["bytes_sent"])]
+        stats[r]["comm_count"] = xs["comm_count"]
+        stats[r]["last"] = res
         streams[r].synchronize()
         return res.n_owned
 
@@ -399,12 +503,23 @@ def run_rehearsal(args, torch):
             list(ex.map(one, range(R)))
         torch.cuda.synchronize()
         for st in stats:
-            st.update(owned=0, remote=0)
+            st.update(owned=0, remote=0, wait_us=0, waits=0, bytes_sent=[0] * R)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             list(ex.map(one, range(R)))
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+    # every rank's hosted output of the last batch (outside timing): the node's correctness evidence
+    t_chk = time.perf_counter()
+    bad = []
+    for r in range(R):
+        errs = node_self_check(torch, engs[r], stats[r]["last"], r, cl, keys, owner, reg, masks[r], n_acts[r], ros,
+                               expect_owned[r], args.check_sample)
+        bad += [f"rank {r}: {e}" for e in errs]
+    if sum(st["last"].n_hosted for st in stats) != n_total:
+        bad.append(f"the ranks host {sum(st['last'].n_hosted for st in stats)} messages of {n_total}")
+    check = "ok" if not bad else "; ".join(bad)
+    log(f"rehearsal self-check: {check} ({time.perf_counter() - t_chk:.1f}s)")
     for nd in nodes:
         nd.close()
     for e in engs:
@@ -418,7 +533,13 @@ def run_rehearsal(args, torch):
             "config": {"workload": f"config{args.config} split over {R} ranks ({n_msgs} messages each), orl_node LOCAL "
                                    f"transport, {args.chunks} chunks", "receive_capacity": cap},
             "owned_per_rank": owned, "max_over_mean_owned": max(owned) / (sum(owned) / R),
-            "sent_remote_per_rank": [st["remote"] / args.steps for st in stats], "roofline": None, "cpu_baseline": None}
+            "sent_remote_per_rank": [st["remote"] / args.steps for st in stats],
+            "exchange": {"ncclCommCount": stats[0]["comm_count"],
+                         "bytes_sent_per_peer_per_step": [[b / args.steps for b in st["bytes_sent"]] for st in stats],
+                         "host_wait_ms_per_step": [st["wait_us"] / 1e3 / args.steps for st in stats],
+                         "host_wait_ms_per_chunk": [st["wait_us"] / 1e3 / args.steps / max(1, args.chunks) for st in stats],
+                         "host_waits_per_step": [st["waits"] / args.steps for st in stats]},
+            "check": check, "check_sample_per_rank": args.check_sample, "roofline": None, "cpu_baseline": None}
 
 
 def run_host_io(args, torch, eng, cl, d_msgs, n_msgs, n_act, n_grains):

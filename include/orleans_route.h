@@ -507,6 +507,8 @@ int orl_device_alloc(orl_ctx* ctx, size_t bytes, void** d_out);
 int orl_device_free(orl_ctx* ctx, void* d_ptr);
 int orl_copy_to_device(orl_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream);
 int orl_copy_to_host(orl_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
+/* Device-to-device copy on `stream` (e.g. a node result's arrays into the caller's own buffers before the next batch). */
+int orl_copy_on_device(orl_ctx* ctx, void* d_dst, const void* d_src, size_t bytes, void* stream);
 int orl_stream_sync(orl_ctx* ctx, void* stream);
 int orl_host_register(orl_ctx* ctx, void* h_ptr, size_t bytes);
 int orl_host_unregister(orl_ctx* ctx, void* h_ptr);
@@ -601,6 +603,18 @@ int orl_node_fanout_batch_device(orl_node* node, const uint64_t* d_csr_off, cons
 /* Record segment i of the last batch's hosted messages: device pointer, message count, record width (8 = orl_wire8 in
  * the context's wire types, 16 = orl_wire_msg, 32 = orl_msg_hdr).  Segments start 32-byte aligned. */
 int orl_node_segment(const orl_node* node, uint32_t i, const void** d_records, uint64_t* count, uint32_t* width);
+/* What the last batch of the node moved and waited for (measurement; the silo's statistics counters).  comm_count: ranks
+ * of the RCCL communicator (ncclCommCount), or of the LOCAL group.  bytes_sent[r]: exchange bytes this rank sent to rank r
+ * in hop 1 + hop 2 (its own share, copied locally, at r = this rank).  host_wait_us: time the host spent in the exchange's
+ * bounded waits (the counts all-gathers, the LOCAL barriers, the hop-2 exchange), host_waits: how many. */
+typedef struct orl_node_stats {
+    uint32_t comm_count;
+    uint32_t chunks;                          /* hop-1 chunks of the batch */
+    uint64_t bytes_sent[ORL_NODE_MAX_RANKS];
+    uint64_t host_wait_us;
+    uint64_t host_waits;
+} orl_node_stats;
+int orl_node_get_stats(const orl_node* node, orl_node_stats* out);
 
 /* The protocol's host decisions, as orl_node_route_batch_device takes them after each all-gather: exposed for hosts that
  * run the exchange over a transport of their own (orl_partition_*_padded/compact/narrow_device, the route entry points,

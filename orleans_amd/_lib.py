@@ -100,6 +100,11 @@ class orl_node_result(C.Structure):
                 ("act", C.c_void_p), ("order", C.c_void_p), ("bucket_offsets", C.c_void_p)]
 
 
+class orl_node_stats(C.Structure):
+    _fields_ = [("comm_count", C.c_uint32), ("chunks", C.c_uint32), ("bytes_sent", C.c_uint64 * NODE_MAX_RANKS),
+                ("host_wait_us", C.c_uint64), ("host_waits", C.c_uint64)]
+
+
 class orl_node_chunk_plan(C.Structure):
     _fields_ = [("width", C.c_uint32), ("rewrite", C.c_uint32), ("send", C.c_uint64 * NODE_MAX_RANKS),
                 ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_recv", C.c_uint64)]
@@ -184,6 +189,7 @@ _SIGS = {
     "orl_device_free": (C.c_int, [_P, _P]),
     "orl_copy_to_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
     "orl_copy_to_host": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
+    "orl_copy_on_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
     "orl_stream_sync": (C.c_int, [_P, _P]),
     "orl_host_register": (C.c_int, [_P, _P, C.c_size_t]),
     "orl_host_unregister": (C.c_int, [_P, _P]),
@@ -201,6 +207,7 @@ _SIGS = {
                                      C.POINTER(orl_node_hop2_plan)]),
     "orl_node_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.POINTER(orl_node_result), _P]),
     "orl_node_segment": (C.c_int, [_P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "orl_node_get_stats": (C.c_int, [_P, C.POINTER(orl_node_stats)]),
     "orl_node_fanout_batch_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P,
                                                C.POINTER(C.c_uint64), C.POINTER(orl_node_result), _P]),
     "orl_fanout_expand_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64,

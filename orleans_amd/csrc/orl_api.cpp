@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.res_max);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.sup_base); f(c->s.seg_sup);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -810,6 +810,11 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.seg_carry, carry_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_carry)");
         if ((e = hipMalloc((void**)&c->s.seg_meta, ((seg_rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_meta)");
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
+        if (bp.two_level && bp.hb > 0 &&
+            (e = hipMalloc((void**)&c->s.sup_base, ((1ull << bp.hb) * ((mb + 65535) / 65536) + 1) * 4)) != hipSuccess)
+            return bail(e, "hipMalloc(sup_base)");
+        if (bp.two_level && bp.hb > 0 && (e = hipMalloc((void**)&c->s.seg_sup, (seg_rows + 1) * 4)) != hipSuccess)
+            return bail(e, "hipMalloc(seg_sup)");
         if ((e = hipMalloc((void**)&c->s.sstart, 4098 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
@@ -833,8 +838,6 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.hot_bmax, (((uint64_t)cfg->n_act + 2 + 4095) / 4096 + 1) * 8)) != hipSuccess)
             return bail(e, "hipMalloc(hot_bmax)");
         if ((e = hipMalloc((void**)&c->s.hot_rows, (rows + (rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(hot_rows)");
-        if ((e = hipMalloc((void**)&c->s.res_max, 16)) != hipSuccess) return bail(e, "hipMalloc(res_max)");
-        if ((e = hipMemset(c->s.res_max, 0, 16)) != hipSuccess) return bail(e, "hipMemset(res_max)");
         if ((e = hipHostMalloc((void**)&c->s.hot_host, 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e, "hipHostMalloc(hot_host)");
         *c->s.hot_host = 0xFFFFFFFFu;
@@ -1832,6 +1835,13 @@ int orl_copy_to_host(orl_ctx* c, void* h_dst, const void* d_src, size_t bytes, v
     if (!c || (bytes && (!h_dst || !d_src))) return ORL_E_INVALID;
     if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
     if (bytes) ORL_HIP(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : c->stream));
+    return ORL_OK;
+}
+
+int orl_copy_on_device(orl_ctx* c, void* d_dst, const void* d_src, size_t bytes, void* stream) {
+    if (!c || (bytes && (!d_dst || !d_src))) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "context was created without a device (device < 0)");
+    if (bytes) ORL_HIP(c, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, stream ? (hipStream_t)stream : c->stream));
     return ORL_OK;
 }
 

@@ -264,7 +264,8 @@ struct Scratch {
     uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
-    unsigned long long* res_max = nullptr;  // one-pass level 2: the hot-key pick's candidate (zeroed once, then by k_hot_pick)
+    uint32_t* sup_base = nullptr;  // [2^hb][ceil(max_batch / 65536)] narrow level-2 records: each super-tile's base per bucket
+    uint32_t* seg_sup = nullptr;   // [max segments] narrow level-2 records: the super-tile of each segment's first position
     uint32_t gap_cap = 4096;  // LSD offsets' long-gap queue capacity (env_gap_cap() at context creation)
     int fan_u = 1;            // fan-out messages per thread and step (env_fan_u() at context creation)
 };

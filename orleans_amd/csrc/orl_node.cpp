@@ -146,6 +146,7 @@ struct orl_node {
     };
     std::vector<Seg> segs;
     orl_msg_hdr* d_fan = nullptr;                 // expanded multicast records (orl_node_fanout_batch_device), max_batch
+    orl_node_stats stats{};                       // the last batch's bytes and host waits (orl_node_get_stats)
 };
 
 namespace {
@@ -194,6 +195,20 @@ void break_node(orl_node* nd) {
     if (nd->h_stall) __atomic_store_n(nd->h_stall, 1u, __ATOMIC_RELEASE);
 }
 
+// A host wait of the exchange, counted in the node's stats (orl_node_get_stats).
+void count_wait(orl_node* nd, std::chrono::steady_clock::time_point t0) {
+    nd->stats.host_wait_us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    ++nd->stats.host_waits;
+}
+
+// A LOCAL-transport barrier, its wait counted in the node's stats.
+bool timed_barrier(orl_node* nd, LocalGroup& g) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool ok = g.barrier(nd->timeout_ms);
+    count_wait(nd, t0);
+    return ok;
+}
+
 // Bounded wait for stream `s` (instead of hipStreamSynchronize): polls the stream and, with RCCL, the communicator's
 // asynchronous error; on an RCCL error or at the deadline the node is broken (break_node) and ORL_E_STATE returned with
 // `what` and this rank's head words `d_own` (when the stream drained after the abort) in orl_node_last_error.
@@ -204,7 +219,10 @@ int wait_bounded(orl_node* nd, hipStream_t s, const char* what, int chunk, const
     ncclResult_t ar = ncclSuccess;
     for (;;) {
         const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) return ORL_OK;
+        if (q == hipSuccess) {
+            count_wait(nd, t0);
+            return ORL_OK;
+        }
         if (q != hipErrorNotReady) return nfail(nd, ORL_E_DEVICE, "%s (chunk %d): %s", what, chunk, hipGetErrorString(q));
         ++polls;  // (both transports: the sleep backoff below applies to LOCAL rank threads too)
         if (nd->comm && (polls & 63u) == 0u) {
@@ -260,7 +278,7 @@ int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready, int c
         std::lock_guard<std::mutex> lk(g.mu);
         std::memcpy(g.words[nd->me].data(), nd->h_heads + (size_t)nd->me * kHeadWords, kHeadWords * 8);
     }
-    if (!g.barrier(nd->timeout_ms)) {
+    if (!timed_barrier(nd, g)) {
         nd->broken = true;
         return nfail(nd, ORL_E_STATE, "node all-gather (chunk %d): a rank did not arrive within %u ms (barrier timeout)", chunk,
                      nd->timeout_ms);
@@ -269,7 +287,7 @@ int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready, int c
         std::lock_guard<std::mutex> lk(g.mu);
         for (uint32_t r = 0; r < nd->nr; ++r) std::memcpy(nd->h_heads + (size_t)r * kHeadWords, g.words[r].data(), kHeadWords * 8);
     }
-    if (!g.barrier(nd->timeout_ms)) {
+    if (!timed_barrier(nd, g)) {
         nd->broken = true;
         return nfail(nd, ORL_E_STATE, "node all-gather (chunk %d): a rank did not arrive within %u ms (barrier timeout)", chunk,
                      nd->timeout_ms);
@@ -283,6 +301,8 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
     const uint32_t nr = nd->nr, me = nd->me;
     std::vector<uint64_t> roff(nr + 1, 0);
     for (uint32_t r = 0; r < nr; ++r) roff[r + 1] = roff[r] + recv[r];
+    for (const Lane& L : lanes)
+        for (uint32_t r = 0; r < nr; ++r) nd->stats.bytes_sent[r] += send[r] * L.elem;
     if (nd->comm) {
         NODE_NCCL(nd, ncclGroupStart());
         for (const Lane& L : lanes)
@@ -306,7 +326,7 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
         g.lanes[me].clear();
         for (const Lane& L : lanes) g.lanes[me].push_back(LocalGroup::Lane{L.send, L.stride});
     }
-    if (!g.barrier(nd->timeout_ms)) {
+    if (!timed_barrier(nd, g)) {
         nd->broken = true;
         return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive within %u ms (barrier timeout)", nd->timeout_ms);
     }
@@ -323,7 +343,7 @@ int exchange(orl_node* nd, const std::vector<Lane>& lanes, const uint64_t* send,
                                             recv[r] * lanes[k].elem, hipMemcpyDeviceToDevice, nd->sx));
             }
     if (int r = wait_bounded(nd, nd->sx, "node exchange: copies", -1, nullptr)) return r;
-    if (!g.barrier(nd->timeout_ms)) {  // every rank has copied out of my regions: they are free
+    if (!timed_barrier(nd, g)) {  // every rank has copied out of my regions: they are free
         nd->broken = true;
         return nfail(nd, ORL_E_STATE, "node exchange: a rank did not arrive within %u ms (barrier timeout)", nd->timeout_ms);
     }
@@ -536,9 +556,12 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
             nd->comm = nullptr;
             return bail(ORL_E_DEVICE);
         }
+        int cc = 0;
+        nd->stats.comm_count = ncclCommCount(nd->comm, &cc) == ncclSuccess ? (uint32_t)cc : 0u;
     } else {
         nd->group = join_group(cfg->group_id, cfg->nranks);
         if (!nd->group) return bail(ORL_E_INVALID);
+        nd->stats.comm_count = nd->group->nranks;
     }
     *out = nd;
     return ORL_OK;
@@ -573,9 +596,21 @@ int orl_node_segment(const orl_node* nd, uint32_t i, const void** d_records, uin
     return ORL_OK;
 }
 
+int orl_node_get_stats(const orl_node* nd, orl_node_stats* out) {
+    if (!nd || !out) return ORL_E_INVALID;
+    *out = nd->stats;
+    return ORL_OK;
+}
+
 int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* res,
                                 void* stream) {
     if (!nd || !res) return ORL_E_INVALID;
+    {
+        const uint32_t cc = nd->stats.comm_count;
+        nd->stats = orl_node_stats{};
+        nd->stats.comm_count = cc;
+        nd->stats.chunks = nd->cfg.chunks;
+    }
     if (nd->broken) return nfail(nd, ORL_E_STATE, "node is broken (an earlier exchange failed; its communicator was aborted): %s",
                                  nd->err.c_str());
     if (n && !d_in) return nfail(nd, ORL_E_INVALID, "null device buffer");

@@ -1104,9 +1104,12 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
 
 // row_step: the pass reading the result reads only rows t % row_step == 0 (route tiles smaller than its tile), so
 // only those are written.
+// sup (OUT_NARROW's super-tile bases, else null): sup[d * nsup + k] = the base of row k * sup_step (the first MSD tile of
+// super-tile k), digit-major so level 2 reads one bucket's bases contiguously.
 __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ C, uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
-                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows) {
+                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows,
+                                                   uint32_t* __restrict__ sup, uint32_t sup_step, uint32_t nsup) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
     if (hot_rows && blockIdx.y == gridDim.y - 1) {  // the hot column: chunk base + the exclusive prefix of its 64 rows
@@ -1140,6 +1143,7 @@ __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ 
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
             if (t + k < t1 && (t + k) % row_step == 0) M[(size_t)(t + k) * bins + d] = run;
+            if (sup && t + k < t1 && (t + k) % sup_step == 0) sup[(size_t)d * nsup + (t + k) / sup_step] = run;
             run += v[k];
         }
     }
@@ -1166,8 +1170,41 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      OUT_SOA8 / OUT_SOA16 (the MSD pass of the two-level path) write the index to `order` (an index array) and only
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
-enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4 };  // LSD_PAIR: an LSD pass's pairs
+enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3, IN_NARROW = 4 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_NARROW = 5 };  // LSD_PAIR: an LSD pass's pairs
+
+// Level-2 records of the two-level path (OUT_NARROW / IN_NARROW, round 4): ONE u32 per message instead of an 8-B {key,
+// index} pair — the key's low `lb` bits (the level-2 digit; the bucket is the high digit) and the index's low 16 bits.
+// The MSD pass writes a bucket's records in arrival order, super-tile after super-tile (kSupTile = 16 MSD tiles = 65536
+// messages), so the index's high bits are the super-tile, which level 2 recovers from the position: sup_base[b][k] =
+// where super-tile k's records of bucket b start (col_apply writes it beside the tile bases).  Half the bytes for the MSD
+// pass to write and for both level-2 kernels to read.
+constexpr uint32_t kSupShift = 16, kSupTile = 1u << kSupShift;
+__device__ __forceinline__ uint32_t narrow_rec(uint32_t key, uint32_t idx, uint32_t lb) {
+    return (key & ((1u << lb) - 1u)) | ((idx & (kSupTile - 1u)) << lb);
+}
+
+// Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
+// zero-degree publishers share an offset with the next one and are skipped).  Whole wave, same v in every lane: each
+// round samples 64 evenly spaced candidates and keeps the interval between the last one <= v and the next one.
+__device__ __forceinline__ uint32_t wave_find_pub(const uint32_t* __restrict__ poff, uint32_t n_pub, uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t lo = 0, hi = n_pub - 1;  // invariant: poff[lo] <= v, and hi = n_pub - 1 or poff[hi + 1] > v
+    while (lo < hi) {
+        const uint32_t step = (hi - lo + 64u) / 64u;  // ceil((span + 1) / 64): samples reach past hi
+        const uint32_t sl = min(lo + lane * step, hi);
+        const uint64_t le = __ballot(poff[sl] <= v);  // a prefix of lanes (lane 0 always)
+        const uint32_t L = 63u - (uint32_t)__builtin_clzll(le);
+        const uint32_t nlo = min(lo + L * step, hi);
+        if (L < 63u) {
+            const uint32_t nx = min(lo + (L + 1u) * step, hi);
+            if (nx > nlo) hi = nx - 1u;  // poff[nx] > v
+        }
+        lo = nlo;
+    }
+    return lo;
+}
+
 
 // Digits per thread in the per-round column phase: digit pairs (one packed word) are never split between threads.
 template <int BITS>
@@ -1252,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
-    constexpr bool HOTP = IN == IN_ACT && OUT == OUT_PAIR;
+    constexpr bool HOTP = IN == IN_ACT && (OUT == OUT_PAIR || OUT == OUT_NARROW);
     __shared__ PassSmem<BITS, ITEMS> sm;
     __shared__ uint32_t hotw[kWaves];
     const uint32_t rflags = rank_flags();
@@ -1350,6 +1387,8 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = kv;
+            } else if (OUT == OUT_NARROW) {
+                reinterpret_cast<uint32_t*>(pair_out)[g] = narrow_rec(k, kv.y, shift);
             } else if (OUT == OUT_SOA8) {
                 order_out[g] = kv.y;
                 reinterpret_cast<uint8_t*>(key_out)[g] = (uint8_t)(k & ((1u << shift) - 1u));
@@ -1599,12 +1638,10 @@ __global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ off
 // takes the chunked kernels, else the one-pass k_seg_scan (cheaper when every bucket is short).
 constexpr uint32_t kSkewSlot = 4097;
 
-// res_cap (the one-pass level 2, k_bucket_resident): buckets of <= res_cap messages get no segments (0: every nonempty
-// bucket is segmented).
 template <uint32_t NT>
 __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
                                               uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart,
-                                              uint32_t (*wsum)[16], uint32_t res_cap) {
+                                              uint32_t (*wsum)[16]) {
     constexpr uint32_t Q = 4096 / NT, NW = NT / 64;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t c[Q], p[Q], cs = 0, ps = 0, pmax = 0;
@@ -1612,7 +1649,7 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
     for (uint32_t q = 0; q < Q; ++q) {
         const uint32_t b = threadIdx.x * Q + q;
         c[q] = b < nbk ? (col_tot ? col_tot[b] : n) : 0u;
-        p[q] = c[q] > res_cap ? (c[q] + seg - 1) / seg : 0u;
+        p[q] = (c[q] + seg - 1) / seg;
         cs += c[q];
         ps += p[q];
         pmax = max(pmax, p[q]);
@@ -1657,9 +1694,9 @@ __device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_t
 }
 
 __global__ __launch_bounds__(1024) void k_seg_plan(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
-                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart, uint32_t res_cap) {
+                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart) {
     __shared__ uint32_t wsum[3][16];
-    seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum, res_cap);
+    seg_plan_body<1024>(col_tot, nbk, n, seg, bstart, sstart, wsum);
 }
 
 // Segment j of the launch: blocks [0, nseg) map XCD-contiguously onto segments (consecutive segments of one
@@ -1668,13 +1705,11 @@ struct SegRange {
     uint32_t bucket, index, lo, hi;
 };
 
-// blk: the block's k-th segment slot, blockIdx.x + k * gridDim.x (a grid smaller than the segment count loops; with a
-// grid that is a multiple of 8 every slot of a block stays on the block's XCD).
 __device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                             uint32_t nbk, uint32_t seg, SegRange& r, uint32_t blk) {
+                                             uint32_t nbk, uint32_t seg, SegRange& r) {
     const uint32_t nseg = sstart[nbk];
-    if (blk >= nseg) return false;
-    const uint32_t j = xcd_tile(blk, nseg);
+    if (blockIdx.x >= nseg) return false;
+    const uint32_t j = xcd_tile(blockIdx.x, nseg);
     uint32_t lo = 0, hi = nbk + 1;  // bucket = upper_bound(sstart, j) - 1 (skips empty buckets)
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1706,14 +1741,17 @@ __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n
     }
 }
 
+// IN_NARROW: also the super-tile of each segment's first position, seg_sup[segment] (for k_seg_scatter), searched by wave 0
+// while the segment's records load.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
                                                    uint32_t seg, const uint32_t* __restrict__ bstart,
-                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist) {
+                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist,
+                                                   const uint32_t* __restrict__ sup, uint32_t nsup, uint32_t* __restrict__ seg_sup) {
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
     SegRange r;
-    for (uint32_t blk = blockIdx.x; seg_of_block(bstart, sstart, nbk, seg, r, blk); blk += gridDim.x) {
+    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
     __syncthreads();
     for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
@@ -1726,6 +1764,8 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
                 const uint32_t* ix = static_cast<const uint32_t*>(in);
                 key[j] = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[ec]
                                        : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[ec];
+            } else if (IN == IN_NARROW) {  // the record's low bits
+                key[j] = static_cast<const uint32_t*>(in)[ec] & (BL - 1u);
             } else {
                 uint32_t idx;
                 seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
@@ -1733,6 +1773,10 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
         }
         // a Zipf-hot key (most of a hot bucket's segments): its lanes add with one atomic per step (the same-address
         // lanes of an LDS atomic are serviced one by one); decided per wave from its first full step
+        if (IN == IN_NARROW && c0 == r.lo && threadIdx.x < 64u) {  // (the loads above are in flight meanwhile)
+            const uint32_t klo = wave_find_pub(sup + (size_t)r.bucket * nsup, nsup, r.lo);
+            if (threadIdx.x == 0) seg_sup[r.index] = klo;
+        }
         const uint32_t dh = c0 + 256u * kItems <= r.hi ? wave_hot_digit(key[0] & (BL - 1u)) : kNoHot;
         if (dh != kNoHot) {
 #pragma unroll
@@ -1753,24 +1797,19 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
     __syncthreads();
     uint32_t* row = seg_hist + (size_t)r.index * BL;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
-    __syncthreads();  // hist is zeroed again for the block's next segment
-    }
 }
 
 // Per bucket b and low digit l (every bucket has <= kScanRows segments): the segment rows become exclusive prefixes
 // inside the bucket and the column total (messages with key = b << lb | l) goes to counts[key] (keys < nb only).
-// res (k_bucket_resident runs too): only buckets with segments are written; the others' offsets and the keys past the last
-// bucket are the resident kernel's.
 template <int LB>
 __device__ __forceinline__ void seg_scan_bucket(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                 uint32_t nbk, uint32_t nb, uint32_t* __restrict__ counts, uint32_t b,
-                                                uint32_t l, bool res) {
+                                                uint32_t l) {
     constexpr uint32_t BL = 1u << LB;
-    if (b == 0 && l == 0 && !res)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+    if (b == 0 && l == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
         for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
     if (l >= BL) return;
     const uint32_t j0 = sstart[b], j1 = sstart[b + 1];
-    if (res && j0 == j1) return;
     uint32_t run = 0, j = j0;
     for (; j + 4 <= j1; j += 4) {
         uint32_t v[4];
@@ -1819,7 +1858,7 @@ template <int LB>
 __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
                                                uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t c,
-                                               uint32_t l, bool res) {
+                                               uint32_t l) {
     constexpr uint32_t BL = 1u << LB, G = 16;
     const uint32_t nseg = sstart[nbk];
     const uint32_t j0 = c * kScanRows;
@@ -1829,9 +1868,9 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
     if (l == 0)  // the chunk's shape: first bucket, it ends inside, it continues an earlier one, a bucket starts inside
         meta[c] = b | (sstart[b + 1] <= j1 ? kMetaEnds : 0u) | (sstart[b] < j0 ? kMetaCont : 0u) |
                   (sstart[b + 1] < j1 ? kMetaInside : 0u);
-    auto put = [&](uint32_t k, uint32_t v) {  // res: buckets without segments are the resident kernel's
+    auto put = [&](uint32_t k, uint32_t v) {
         const uint32_t key = (k << LB) | l;
-        if (key < nb && !(res && sstart[k] == sstart[k + 1])) counts[key] = v;
+        if (key < nb) counts[key] = v;
     };
     if (sstart[b] == j0)  // b starts this chunk: the empty buckets just before it (no other chunk meets them)
         for (uint32_t k = b; k > 0 && sstart[k - 1] == j0;) put(--k, 0u);
@@ -1861,7 +1900,7 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
         if (j1 == nseg)
             for (uint32_t k = b + 1; k < nbk; ++k) put(k, 0u);  // empty buckets after the last segment
     }
-    if (l == 0 && j1 == nseg && !res)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+    if (l == 0 && j1 == nseg)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
         for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
     carry[(size_t)c * BL + l] = run;
 }
@@ -1870,12 +1909,12 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
 template <int LB>
 __global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                   uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
-                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t res) {
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts) {
     const uint32_t l = blockIdx.y * 256u + threadIdx.x;
     if (!sstart[kSkewSlot]) {
-        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l, res != 0);
+        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l);
     } else {
-        seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l, res != 0);
+        seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l);
     }
 }
 
@@ -1940,6 +1979,36 @@ __global__ __launch_bounds__(256) void k_seg_carry(const uint32_t* __restrict__ 
     }
 }
 
+// IN_NARROW's index recovery in k_seg_scatter.  klo = the super-tile of the segment's first position (k_seg_count found it:
+// seg_sup); bs[t] = the base of super-tile klo + 1 + t while it is inside the round [c0, c1), then kBsNone: the bases a
+// round crosses, sorted.  A position's super-tile is klo + the number of bases <= it; each lane walks forward over bs as
+// its positions grow (64 a step: about one base per step at config 2).  A round that crosses more than kBsCap - 1 bases
+// (a sparse bucket) sets `wide`, and its positions search the bucket's bases in global memory instead.
+constexpr uint32_t kBsCap = kSegChunk, kBsNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool load_bases(const uint32_t* __restrict__ srow, uint32_t nsup, uint32_t klo, uint32_t c1, uint32_t* bs) {
+    bool wide = false;
+    for (uint32_t t = threadIdx.x; t < kBsCap; t += 256u) {
+        const uint32_t k = klo + 1u + t;
+        const uint32_t p = k < nsup ? srow[k] : kBsNone;
+        const bool in = p < c1;
+        bs[t] = in && t + 1u < kBsCap ? p : kBsNone;
+        wide |= in && t + 1u == kBsCap;
+        if (!in) break;
+    }
+    return wide;
+}
+
+// The super-tile of position e, searched in the bucket's bases (the wide-round fallback).
+__device__ __forceinline__ uint32_t sup_of(const uint32_t* __restrict__ srow, uint32_t nsup, uint32_t klo, uint32_t e) {
+    uint32_t lo = klo, hi = nsup;  // last k in [klo, nsup) with srow[k] <= e
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (srow[mid] <= e) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 // One segment: LDS rounds of kSegChunk messages.  Each round ranks its messages with wave_rank (wave w owns
 // [w*1024, w*1024+1024) of the round, 16 steps of 64 lanes, so (round, wave, step, lane) order is arrival
 // order), turns the per-wave counts into round-local sorted starts, stages the indices in LDS in sorted
@@ -1964,12 +2033,14 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, const uint32_t* __restrict__ seg_carry,
-                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order) {
+                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order,
+                                                     const uint32_t* __restrict__ sup, uint32_t nsup,
+                                                     const uint32_t* __restrict__ seg_sup) {
     constexpr uint32_t BL = 1u << LB;
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
     SegRange r;
-    for (uint32_t blk = blockIdx.x; seg_of_block(bstart, sstart, nbk, seg, r, blk); blk += gridDim.x) {
+    if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
     const uint32_t rflags = rank_flags();
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t run[PER];  // global position of the next message with digit threadIdx.x * PER + q
@@ -1990,13 +2061,48 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t e = wbase + j * 64u + lane;
-            seg_load<IN>(in, n_total, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
+            const uint32_t ec = e < r.hi ? e : r.hi - 1;
+            if (IN == IN_NARROW) {  // the digit, and the index's low 16 bits (its super-tile below)
+                const uint32_t rec = static_cast<const uint32_t*>(in)[ec];
+                key[j] = rec & (BL - 1u);
+                idx[j] = rec >> LB;
+            } else {
+                seg_load<IN>(in, n_total, ec, n_act, key[j], idx[j]);
+            }
+        }
+        uint32_t klo = 0;
+        bool wide = false;
+        const uint32_t* srow = sup + (size_t)r.bucket * nsup;
+        uint32_t* bs = reinterpret_cast<uint32_t*>(&sm.stage[0]);  // free until this round's staging writes
+        if (IN == IN_NARROW) {
+            klo = seg_sup[r.index];
+            if (c0 != r.lo) klo = sup_of(srow, nsup, klo, c0);  // (a segment is one round: seg_elems() == kSegChunk)
+            wide = load_bases(srow, nsup, klo, min(c0 + kSegChunk, r.hi), bs);
         }
         for (uint32_t k = threadIdx.x; k < BL / 2u; k += 256) {
 #pragma unroll
             for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][k] = 0;
         }
-        __syncthreads();
+        if (IN == IN_NARROW) wide = __syncthreads_or(wide);
+        else __syncthreads();
+        if (IN == IN_NARROW) {  // each lane's positions grow by 64 a step: walk the bases forward
+            uint32_t lo = 0, hi = kBsCap - 1u;  // the count of bases <= wbase (uniform binary search; bs[kBsCap - 1] = none)
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (bs[mid] <= wbase) lo = mid + 1u; else hi = mid;
+            }
+            uint32_t kc = lo;
+#pragma unroll
+            for (uint32_t j = 0; j < kItems; ++j) {
+                const uint32_t e = wbase + j * 64u + lane;
+                if (!wide) {
+                    while (bs[kc] <= e) ++kc;
+                    idx[j] |= (klo + kc) << kSupShift;
+                } else if (e < r.hi) {
+                    idx[j] |= sup_of(srow, nsup, klo, e) << kSupShift;
+                }
+            }
+        }
         {
             uint32_t dg[kItems];
 #pragma unroll
@@ -2039,287 +2145,12 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
         }
         __syncthreads();  // LDS is reused by the next round
     }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
-// Stage 4, level 2 in one pass (round 4): one workgroup of 1024 threads sorts a whole MSD bucket of <= kResCap messages
-// held in registers, so the pairs are read once (the segmented path reads them twice: k_seg_count, then k_seg_scatter)
-// and there is no segment plan, segment scan or offsets scan: a bucket's key counts come out of its own LDS histogram.
-// Bucket b = pairs [bstart[b], bstart[b + 1]) in arrival order (c of them):
-//   1. load: wave w owns the contiguous run [w * 64E, (w + 1) * 64E) of the bucket (E = ceil(c / 1024) steps of 64
-//      lanes), so (wave, step, lane) order is arrival order.  An element lives in ONE register: its level-2 digit (<= 10
-//      bits) and its index minus the index in lane 0 of its step (that base goes to LDS, one word per wave step); a
-//      delta past 22 bits (a sparse bucket) makes the workgroup re-read the indices from the pairs instead;
-//   2. count: one LDS histogram row per wave (u32, 16 x 1024);
-//   3. scan: per digit the waves' exclusive prefix, over digits the bucket-local starts kst -> the bucket offsets, written
-//      here (the hot key's run included: stage 4's hot-key path, whose messages are not in the pairs);
-//   4. place: the digits whose starts fall in one kResHalf-wide band form a window; its elements are ranked (one returning
-//      LDS atomic on the wave's running position of the digit, in lane order: the stable rank of k_seg_scatter, under the
-//      same rank-mode guard) into an LDS image of < kResWin positions, written out as whole runs of `order`.  A digit of
-//      more than kResHalf messages (always the last of its window) is written from registers (consecutive positions).
-// Buckets of more than kResCap messages keep the segmented path (k_seg_plan gives them segments, the others none).
-constexpr uint32_t kResThreads = 1024, kResWaves = kResThreads / 64, kResE = 80, kResCap = kResThreads * kResE;
-constexpr uint32_t kResChunk = 8;                     // loads in flight per thread while a bucket is read
-constexpr uint32_t kResKeys = 1024;                   // level-2 digits of <= 10 bits
-constexpr uint32_t kResWin = 22016, kResHalf = kResWin / 2;
-constexpr uint32_t kResMaxWin = kResCap / kResHalf + 2;
-constexpr uint32_t kResDeltaBits = 22, kResNone = 0xFFFFFFFFu;
-static_assert(kResE % kResChunk == 0, "steps per wave: whole load chunks");
-
-struct ResSmem {
-    uint32_t cnt[kResWaves][kResKeys];  // per-wave digit counts, then each wave's running position of every digit
-    uint32_t stage[kResWin];            // one window's indices in sorted order
-    uint32_t kst[kResKeys + 1];         // bucket-local start of each digit (the hot run excluded); kst[nk] = c
-    uint32_t base[kResWaves][kResE];    // index of lane 0 of each wave step (elements keep their index minus it)
-    uint32_t wsum[kResWaves];
-    uint32_t winlo[kResMaxWin], winhi[kResMaxWin];  // first / one-past-last digit of each window (winlo kResNone: empty)
-    unsigned long long wmax[kResWaves];
-};
-static_assert(sizeof(ResSmem) <= 160u * 1024u, "one resident workgroup per CU");
-
-__device__ __forceinline__ uint32_t res_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t incl = wave_incl_scan(v);
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t pre = 0;
-    total = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kResWaves; ++i) {
-        const uint32_t s = wsum[i];
-        pre += i < w ? s : 0u;
-        total += s;
-    }
-    __syncthreads();
-    return pre + incl - v;
-}
-
-// The hot-key pick's candidate of a bucket: max of (count << 32 | key) over its keys below nb - 1, one atomic per block.
-__device__ __forceinline__ void pick_candidate(unsigned long long best, unsigned long long* wmax, uint32_t nwaves,
-                                               unsigned long long* __restrict__ pick_max) {
-    best = wave_max_u64(best);
-    if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (uint32_t q = 1; q < nwaves; ++q) best = wmax[q] > best ? wmax[q] : best;
-        if (best) atomicMax(pick_max, best);
-    }
-}
-
-template <int RM>
-__global__ __launch_bounds__(kResThreads) void k_bucket_resident(const uint2* __restrict__ pairs, const uint32_t* __restrict__ bstart,
-                                                                 uint32_t nbk, uint32_t lb, const uint32_t* __restrict__ hot_words,
-                                                                 const uint32_t* __restrict__ hot_total,
-                                                                 uint32_t* __restrict__ offsets, uint32_t nb, uint32_t n,
-                                                                 uint32_t* __restrict__ order,
-                                                                 unsigned long long* __restrict__ pick_max) {
-    __shared__ ResSmem sm;
-    const uint32_t b = blockIdx.x;
-    const uint32_t lo = bstart[b], c = bstart[b + 1] - lo;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    if (b == 0 && tid == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) start at n
-        for (uint32_t k = nbk << lb; k < nb; ++k) offsets[k] = n;
-    if (c > kResCap) return;  // a segmented bucket
-    const uint32_t nk = 1u << lb, kmask = nk - 1u;
-    const uint32_t hk = hot_key_of(hot_words);
-    const uint32_t htot = hk != kNoHotKey ? *hot_total : 0u;
-    const uint32_t hbk = hk != kNoHotKey ? hk >> lb : kResNone;
-    const uint32_t hloc = hbk == b ? hk & kmask : kResNone;                   // the hot key, when it is a digit of this bucket
-    const uint32_t out0 = lo + (hk != kNoHotKey && b > hbk ? htot : 0u);     // the bucket's first output position
-    for (uint32_t i = tid; i < kResWaves * kResKeys; i += kResThreads) (&sm.cnt[0][0])[i] = 0;
-    if (tid < kResMaxWin) {
-        sm.winlo[tid] = kResNone;
-        sm.winhi[tid] = 0;
-    }
-    // 1. load, kResChunk steps in flight
-    const uint32_t E = (c + kResThreads - 1) / kResThreads;
-    const uint32_t w0 = w * 64u * E;
-    const uint32_t cw = c > w0 ? min(c - w0, 64u * E) : 0u;  // the wave's elements
-    const uint2* wp = pairs + lo + w0;
-    uint32_t v[kResE];
-    bool ovf = false;
-#pragma unroll
-    for (uint32_t k = 0; k < kResE / kResChunk; ++k) {
-        if (k * kResChunk * 64u < cw) {
-            uint2 pr[kResChunk];
-#pragma unroll
-            for (uint32_t q = 0; q < kResChunk; ++q)  // 32-bit byte offsets from the wave's (uniform) start
-                pr[q] = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(wp) + min((k * kResChunk + q) * 64u + lane, cw - 1u) * 8u);
-#pragma unroll
-            for (uint32_t q = 0; q < kResChunk; ++q) {
-                const uint32_t j = k * kResChunk + q;
-                const uint32_t base = __builtin_amdgcn_readfirstlane(pr[q].y);
-                if (lane == 0) sm.base[w][j] = base;
-                const uint32_t d = pr[q].y - base;
-                ovf |= j * 64u + lane < cw && d >= (1u << kResDeltaBits);
-                v[j] = (pr[q].x & kmask) | (d << 10);
-            }
-        }  // (steps past the wave's elements are never read)
-    }
-    ovf = __syncthreads_or(ovf);  // (also publishes the zeroed counters)
-    // 2. count
-    uint32_t* row = sm.cnt[w];
-    {
-        const uint32_t dh = cw >= 64u ? wave_hot_digit(v[0] & kmask) : kNoHot;  // a Zipf-hot digit: one atomic per step
-#pragma unroll
-        for (uint32_t j = 0; j < kResE; ++j) {
-            if (j * 64u < cw && j * 64u + lane < cw) {
-                const uint32_t d = v[j] & kmask;
-                if (dh == kNoHot) {
-                    atomicAdd(&row[d], 1u);
-                } else {
-                    const uint64_t m = __ballot(d == dh);
-                    if (d != dh) atomicAdd(&row[d], 1u);
-                    else if ((m & lanes_below()) == 0) atomicAdd(&row[dh], (uint32_t)__popcll(m));
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // 3. scan: thread t = digit t
-    const uint32_t t = tid;
-    uint32_t tot = 0;
-    if (t < nk) {
-#pragma unroll
-        for (uint32_t ww = 0; ww < kResWaves; ++ww) {
-            const uint32_t x = sm.cnt[ww][t];
-            sm.cnt[ww][t] = tot;
-            tot += x;
-        }
-    }
-    uint32_t csum;
-    const uint32_t ks = res_excl_scan(tot, sm.wsum, csum);
-    const uint32_t key = (b << lb) | t;
-    if (t < nk) {
-        sm.kst[t] = ks;
-        if (t == nk - 1u) sm.kst[nk] = ks + tot;
-#pragma unroll
-        for (uint32_t ww = 0; ww < kResWaves; ++ww) sm.cnt[ww][t] += ks;
-        if (key < nb) offsets[key] = out0 + ks + (hloc != kResNone && t > hloc ? htot : 0u);
-    }
-    if (pick_max)
-        pick_candidate((t < nk && key + 1u < nb) ? ((unsigned long long)(tot + (t == hloc ? htot : 0u)) << 32) | key : 0ull,
-                       sm.wmax, kResWaves, pick_max);
-    __syncthreads();
-    if (t < nk) {  // windows: maximal runs of digits with equal kst / kResHalf
-        const uint32_t wi = ks / kResHalf;
-        if (t == 0 || sm.kst[t - 1] / kResHalf != wi) sm.winlo[wi] = t;
-        if (t == nk - 1u || sm.kst[t + 1] / kResHalf != wi) sm.winhi[wi] = t + 1u;
-    }
-    __syncthreads();
-    // 4. place, window by window
-    const uint32_t nwin = sm.kst[nk - 1u] / kResHalf + 1u;
-    const uint32_t hpos = hloc != kResNone ? sm.kst[hloc] : kResNone;  // the hot run sits before this bucket position
-    for (uint32_t i = 0; i < nwin; ++i) {
-        const uint32_t klo = sm.winlo[i];
-        if (klo == kResNone) continue;
-        const uint32_t khi = sm.winhi[i];
-        const uint32_t big = sm.kst[khi] - sm.kst[khi - 1u] > kResHalf ? khi - 1u : kResNone;
-        const uint32_t wlo = sm.kst[klo], whi = big != kResNone ? sm.kst[big] : sm.kst[khi];
-        const uint32_t base = i * kResHalf;
-#pragma unroll
-        for (uint32_t j = 0; j < kResE; ++j) {
-            if (j * 64u < cw) {
-                uint32_t vj = v[j], ln = lane;
-                asm volatile("" : "+v"(vj), "+v"(ln));  // keeps the per-step math inside the window loop (hoisted: E more registers)
-                const uint32_t d = vj & kmask;
-                if (j * 64u + ln < cw && d >= klo && d < khi) {
-                    uint32_t pos;
-                    if (RM == kRmBallot) pos = wave_rank_ballot<10, false>(row, d, __builtin_amdgcn_read_exec(), lanes_below());
-                    else if (RM == kRmHot) pos = rank_step_uniform<false>(row, d);
-                    else pos = atomicAdd(&row[d], 1u);
-                    const uint32_t idx = ovf ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(wp) + (j * 64u + ln) * 8u + 4u)
-                                             : sm.base[w][j] + (vj >> 10);
-                    if (d == big) order[out0 + pos + (pos >= hpos ? htot : 0u)] = idx;
-                    else sm.stage[pos - base] = idx;
-                }
-            }
-        }
-        __syncthreads();
-        for (uint32_t q = wlo + tid; q < whi; q += kResThreads) order[out0 + q + (q >= hpos ? htot : 0u)] = sm.stage[q - base];
-        __syncthreads();
-    }
-}
-
-// Offsets of the segmented buckets when k_bucket_resident takes the others: the per-key counts k_seg_scan wrote into
-// `offsets` (+ the hot key's run) become the bucket's output start + bucket-local exclusive prefixes; the largest count
-// goes to the hot-key pick.
-template <int LB>
-__global__ __launch_bounds__(256) void k_bucket_keyscan(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                                        const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total,
-                                                        uint32_t* __restrict__ offsets, uint32_t nb,
-                                                        unsigned long long* __restrict__ pick_max) {
-    constexpr uint32_t BL = 1u << LB, Q = BL >= 256u ? BL / 256u : 1u;
-    __shared__ uint32_t wsum[kWaves];
-    __shared__ unsigned long long wmax[kWaves];
-    const uint32_t b = blockIdx.x;
-    if (sstart[b] == sstart[b + 1]) return;  // the resident kernel's bucket
-    const uint32_t hk = hot_key_of(hot_words);
-    const uint32_t htot = hk != kNoHotKey ? *hot_total : 0u;
-    const uint32_t hbk = hk != kNoHotKey ? hk >> LB : kResNone;
-    const uint32_t hloc = hbk == b ? hk & (BL - 1u) : kResNone;
-    const uint32_t out0 = bstart[b] + (hk != kNoHotKey && b > hbk ? htot : 0u);
-    uint32_t cnt[Q], s = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < Q; ++q) {
-        const uint32_t t = threadIdx.x * Q + q, key = (b << LB) | t;
-        cnt[q] = (t < BL && key < nb) ? offsets[key] + (t == hloc ? htot : 0u) : 0u;
-        s += cnt[q];
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, wsum, total) + out0;
-    unsigned long long best = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < Q; ++q) {
-        const uint32_t t = threadIdx.x * Q + q, key = (b << LB) | t;
-        if (t < BL && key < nb) {
-            offsets[key] = run;
-            if (key + 1u < nb) best = max(best, ((unsigned long long)cnt[q] << 32) | key);
-        }
-        run += cnt[q];
-    }
-    if (pick_max) pick_candidate(best, wmax, kWaves, pick_max);
-}
-
-// The hot-key pick of a batch whose level 2 ran k_bucket_resident (+ k_bucket_keyscan): the next batch's key as the offsets
-// scan's PICK form decides it; the candidate word is cleared for the next batch.
-__global__ void k_hot_pick(unsigned long long* __restrict__ pick_max, uint32_t n, uint32_t* __restrict__ next_key,
-                           uint32_t* __restrict__ host_word) {
-    if (threadIdx.x != 0) return;
-    const unsigned long long best = *pick_max;
-    const uint32_t c = (uint32_t)(best >> 32), k = (uint32_t)best;
-    const uint32_t key = ((uint64_t)c * kHotShare >= n && c >= kHotMinCount) ? k : kNoHotKey;
-    __hip_atomic_store(next_key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    *pick_max = 0;
 }
 
 // ---------------------------------------------------------------------------------------------------
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
-// Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
-// zero-degree publishers share an offset with the next one and are skipped).  Whole wave, same v in every lane: each
-// round samples 64 evenly spaced candidates and keeps the interval between the last one <= v and the next one.
-__device__ __forceinline__ uint32_t wave_find_pub(const uint32_t* __restrict__ poff, uint32_t n_pub, uint32_t v) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t lo = 0, hi = n_pub - 1;  // invariant: poff[lo] <= v, and hi = n_pub - 1 or poff[hi + 1] > v
-    while (lo < hi) {
-        const uint32_t step = (hi - lo + 64u) / 64u;  // ceil((span + 1) / 64): samples reach past hi
-        const uint32_t sl = min(lo + lane * step, hi);
-        const uint64_t le = __ballot(poff[sl] <= v);  // a prefix of lanes (lane 0 always)
-        const uint32_t L = 63u - (uint32_t)__builtin_clzll(le);
-        const uint32_t nlo = min(lo + L * step, hi);
-        if (L < 63u) {
-            const uint32_t nx = min(lo + (L + 1u) * step, hi);
-            if (nx > nlo) hi = nx - 1u;  // poff[nx] > v
-        }
-        lo = nlo;
-    }
-    return lo;
-}
-
 constexpr uint32_t kFanLds = 2048;  // publishers staged per tile; beyond that fall back to global search
 
 template <int HB>
@@ -3774,6 +3605,7 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
             case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kMsdItems); break;
             case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8, kMsdItems); break;
             case OUT_SOA16: ORL_RP(IN_ACT, OUT_SOA16, kMsdItems); break;
+            case OUT_NARROW: ORL_RP(IN_ACT, OUT_NARROW, kMsdItems); break;
             case OUT_LSD_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kItems); break;
             default: ORL_RP(IN_ACT, OUT_FINAL, kItems); break;
         }
@@ -3802,7 +3634,7 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
 // Column scan of a tile-major [ntiles][bins] u16 count matrix C (s.tile_cnt) into per-(tile, bin) u32 output bases M.
 // row_step: the reading pass uses rows t % row_step == 0 only.
 void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
-              uint32_t* hot_rows = nullptr) {
+              uint32_t* hot_rows = nullptr, uint32_t* sup = nullptr, uint32_t sup_step = 1, uint32_t nsup = 0) {
     const uint16_t* C = s.tile_cnt;
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
@@ -3811,7 +3643,7 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, co
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
                        ntiles);
     hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
-                       hot_rows);
+                       hot_rows, sup, sup_step, nsup);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -3827,63 +3659,48 @@ RouteHist route_hist(uint32_t n_act) {
     return {true, 1u << bp.lsd.bits[0], (uint32_t)bp.lsd.shift[0]};
 }
 
-// Segment-kernel grid when k_bucket_resident takes the buckets of <= kResCap messages: the segmented rest (hot buckets) is
-// usually small or absent, so the count and scatter kernels loop over their segments from a grid of this many blocks
-// instead of launching one (mostly idle) block per possible segment.
-constexpr uint32_t kResSegGrid = 2048;
-
-// res: k_bucket_resident already placed the buckets without segments and wrote their offsets; the segmented buckets' key
-// counts then become offsets per bucket (k_bucket_keyscan) instead of by one scan over every key.
 template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick, bool res) {
+                     uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     const uint32_t nb = n_act + 2;
-    const uint32_t lgrid = res ? std::min(grid, kResSegGrid) : grid;
-#define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(lgrid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
-                                     s.seg_hist)
-#define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(lgrid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
-                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
+    const uint32_t nsup = ceil_div(n, kSupTile);  // IN_NARROW: super-tiles of the batch (sup_base row length)
+#define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
+                                     s.seg_hist, s.sup_base, nsup, s.seg_sup)
+#define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order, s.sup_base, nsup, \
+                                         s.seg_sup)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
-    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR); else if (in == IN_SOA8) ORL_SC(IN_SOA8);
-    else ORL_SC(IN_SOA16);
+    if (in == IN_NARROW) ORL_SC(IN_NARROW); else if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
+    else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     // the segment scan: k_seg_scan when every bucket has <= kScanRows segments, else the chunked kernels (k_seg_plan
     // sets the flag on the device; the path not taken returns at once)
     const uint32_t cb = ceil_div(1u << LB, 256);
     const uint32_t nch = ceil_div(grid, kScanRows);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb, s.seg_carry,
-                       s.seg_meta, d_offsets, res ? 1u : 0u);
+                       s.seg_meta, d_offsets);
     hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
                        d_offsets);
     const uint32_t* hw = hot_cur(s);
-    if (res) {  // per-bucket offsets of the segmented buckets (+ their pick candidates)
-        hipLaunchKernelGGL((k_bucket_keyscan<LB>), dim3(nbk), dim3(256), 0, st, s.bstart, s.sstart, hot ? hw : nullptr,
-                           s.col_tot + nbk, d_offsets, nb, pick ? s.res_max : nullptr);
-    } else {
-        if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
-        if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
-            scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
-        else
-            scan_inplace(d_offsets, nb, s, st);
-    }
-    if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR); else if (in == IN_SOA8) ORL_SS(IN_SOA8);
-    else ORL_SS(IN_SOA16);
+    if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
+    if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
+        scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
+    else
+        scan_inplace(d_offsets, nb, s, st);
+    if (in == IN_NARROW) ORL_SS(IN_NARROW); else if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR);
+    else if (in == IN_SOA8) ORL_SS(IN_SOA8); else ORL_SS(IN_SOA16);
     if (hot)  // the hot run's copy (this batch's key: hw)
         hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0, st,
                            hw, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
-    if (res && pick) {  // the next batch's hot key (flips the slots: hw stays this batch's)
-        hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(64), 0, st, s.res_max, n, s.hot + ((s.hot_parity + 1u) & 1u), s.hot_host_dev);
-        s.hot_parity ^= 1u;
-    }
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
 }
 
 void launch_seg(int lb, int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
-                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick, bool res = false) {
+                uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     switch (lb) {
-#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot, pick, res); break;
+#define ORL_CASE(B) case B: launch_seg_bits<B>(in, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot, pick); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -3902,11 +3719,12 @@ bool stage4_soa() {
     return soa;
 }
 
-// Two-level path's level 2: ORL_NO_RESIDENT=1 segments every bucket (the round-3 form, A/B against k_bucket_resident).
-bool resident_on() {
+// Two-level path's level-2 records: ORL_STAGE4_PAIRS=1 keeps the round-3 8-B {key, index} pairs (A/B against the narrow
+// 4-B records, OUT_NARROW).
+bool stage4_pairs() {
     static const bool on = [] {
-        const char* e = getenv("ORL_NO_RESIDENT");
-        return !(e && e[0] == '1');
+        const char* e = getenv("ORL_STAGE4_PAIRS");
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -3960,34 +3778,25 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t seg = seg_elems(n);
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
+        const bool narrow = bp.hb > 0 && !stage4_soa() && !stage4_pairs() && s.sup_base && s.seg_sup;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr);
+            // narrow level-2 records: col_apply also writes each super-tile's base (rows 16 MSD tiles apart)
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr, narrow ? s.sup_base : nullptr,
+                     row_step0 * (kSupTile / (kRouteThreads * kMsdItems)), ceil_div(n, kSupTile));
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
-                launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist, row_step0, ntiles, s.pairs_a,
-                            nullptr, nullptr, st, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr, hot ? s.sorted_keys : nullptr);
+                launch_pass(host_rm(s.device), bp.hb, IN_ACT, narrow ? OUT_NARROW : OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
+                            row_step0, ntiles, s.pairs_a, nullptr, nullptr, st, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr,
+                            hot ? s.sorted_keys : nullptr);
             }
             kin = s.pairs_a;
         }
-        // level 2: buckets of <= kResCap messages in one pass (k_bucket_resident), the rest segmented
-        const bool res = bp.hb > 0 && bp.lb <= 10 && !stage4_soa() && resident_on() && s.res_max;
-        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart,
-                           res ? kResCap : 0u);
-        const bool hot2 = hot && bp.hb > 0, pick2 = (hot || pick) && bp.hb > 0;
-        if (res) {
-            const uint32_t* hw = hot2 ? hot_cur(s) : nullptr;
-#define ORL_RES(R) hipLaunchKernelGGL((k_bucket_resident<R>), dim3(nbk), dim3(kResThreads), 0, st, s.pairs_a, s.bstart, nbk,      \
-                                      (uint32_t)bp.lb, hw, s.col_tot + nbk, d_offsets, n_act + 2, n, d_order,                    \
-                                      pick2 ? s.res_max : nullptr)
-            const int rm = host_rm(s.device);
-            if (rm == kRmPlain) ORL_RES(kRmPlain); else if (rm == kRmHot) ORL_RES(kRmHot); else ORL_RES(kRmBallot);
-#undef ORL_RES
-        }
-        const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
-        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot2, pick2, res);
+        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
+        const int lin = bp.hb == 0 ? IN_ACT : narrow ? IN_NARROW : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
+        launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
         return (int)hipGetLastError();
     }
     const RadixPlan& plan = bp.lsd;

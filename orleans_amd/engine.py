@@ -556,6 +556,10 @@ class GrainDirectoryEngine:
         self._ck(self._lib.orl_stream_sync(self._ctx, ptr(stream)))
         return h_dst
 
+    def copy_on_device(self, d_dst, d_src, nbytes: int, stream=None) -> None:
+        """orl_copy_on_device: device-to-device copy on `stream` (d_dst / d_src: tensors or device pointers)."""
+        self._ck(self._lib.orl_copy_on_device(self._ctx, ptr(d_dst), ptr(d_src), int(nbytes), ptr(stream)))
+
     def csr_set(self, csr_off: np.ndarray, csr_tgt: np.ndarray) -> None:
         """Upload the follower graph once (host-array fan-out, orl_fanout_batch)."""
         off = np.ascontiguousarray(csr_off, dtype=np.uint64)

@@ -214,6 +214,15 @@ class GrainNode:
         hdrs = np.concatenate(parts) if parts else np.zeros(0, L.MSG_DTYPE)
         return route, act, order, off, hdrs
 
+    def stats(self) -> dict:
+        """orl_node_get_stats: the last batch's communicator size, bytes sent per peer and host waits."""
+        st = L.orl_node_stats()
+        rc = self._lib.orl_node_get_stats(self._node, self._C.byref(st))
+        if rc != L.OK:
+            raise L.OrleansRouteError(rc, "orl_node_get_stats")
+        return {"comm_count": st.comm_count, "chunks": st.chunks, "bytes_sent": list(st.bytes_sent)[:self.nranks],
+                "host_wait_us": st.host_wait_us, "host_waits": st.host_waits}
+
     def close(self) -> None:
         if getattr(self, "_node", None):
             self._lib.orl_node_destroy(self._node)

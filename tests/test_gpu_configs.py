@@ -304,6 +304,78 @@ def test_config3_full_size_zipf(torch):
     eng.close()
 
 
+@pytest.mark.timeout(900)
+def test_config3_256M_one_gpu(torch):
+    """BASELINE config 3's whole batch on one GPU, as `bench.py --config 3` runs it: 256M messages (8 GiB of headers: every
+    byte offset past 2^32, the size no smaller test reaches), Zipf(1.1) over 16M grains, generated on the device.  Every
+    message is checked on the device by the size-independent properties (orleans_amd/selfcheck.py: owner, host, status
+    and handle per message; a permutation grouped by activation, FIFO inside buckets, offsets = the count prefix), and a
+    1M-message sample spread over the whole batch (the last 64M included) is bit-exact vs the oracle
+    (LocalGrainDirectory.cs:439-497, GrainDirectoryPartition.cs:326-344, ActivationData.cs:483-514)."""
+    import time
+    from orleans_amd import selfcheck as SC
+    t = torch
+    t0 = time.perf_counter()
+    log = lambda *a: print(f"[c3 256M {time.perf_counter() - t0:6.1f}s]", *a, flush=True)  # noqa: E731
+    n_grains, n = 16_000_000, 256 << 20
+    cl = W.balanced_cluster()
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    eng = GrainDirectoryEngine(n_act=n_grains, dir_capacity=n_grains, max_batch=n, device=0)
+    W.setup_engine(eng, cl)
+    W.register_population(eng, keys, owner, reg)
+    d_in = W.device_messages(t, cl, n_grains, n, W.SEED_C3, zipf=W.zipf_tables(t, n_grains, W.SEED_C3))
+    log("engine + 256M messages on the device")
+    outs = [t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)]
+    off = t.empty(n_grains + 2, dtype=t.int32, device="cuda")
+    eng.address_messages_device(d_in, n, *outs, off, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    log("routed")
+    m32 = 0xFFFFFFFF
+    route, act, order = (x.to(t.int64) & m32 for x in outs)
+    offs = off.to(t.int64) & m32
+    n1 = d_in.view(t.int64).view(-1, 4)[:, 2]
+    owner_t = t.as_tensor(owner.astype(np.int64), device="cuda")
+    handle_t = t.arange(n_grains, dtype=t.int64, device="cuda")  # handle of grain i is i
+    errs = SC.check_routes(t, route, act, n1, owner_t, handle_t, True)
+    errs += SC.check_stage4(t, act, order, offs, n_grains)
+    assert not errs, errs
+    log("properties of all 256M messages hold")
+    samp = np.sort(np.random.default_rng(5).choice(n, 1_000_000, replace=False))
+    samp_t = t.as_tensor(samp, device="cuda")
+    hdr = d_in.view(-1, 8)[samp_t].cpu().numpy().reshape(-1).view(L.MSG_DTYPE)
+    o = _oracle_for(cl, keys, np.arange(n_grains, dtype=np.uint32), owner)
+    ro, ao = o.route(hdr)
+    np.testing.assert_array_equal(route[samp_t].cpu().numpy().astype(np.uint32), ro)
+    np.testing.assert_array_equal(act[samp_t].cpu().numpy().astype(np.uint32), ao)
+    assert samp.max() > (192 << 20)
+    log("1M-message oracle sample bit-exact")
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_config3_8ranks_bench_size_rehearsal(torch):
+    """Config 3's 8-GPU split at the size `bench.py --gpus 8` runs it, rehearsed on one GPU (orl_node LOCAL transport, the
+    protocol code RCCL runs): 256M messages, 32M originated per rank, 4 chunks of 8-B records, Zipf(1.1) over 16M grains
+    (the hot rank owns and hosts ~55M messages, and its second batch takes stage 4's hot-key path).  After the timed batch
+    bench.py's checker (node_self_check) verifies every rank's hosted output: the owned count against the workload's own
+    per-destination count, owner / host / status / handle of every hosted message, a permutation grouped by activation,
+    FIFO inside buckets, offsets = the count prefix, and a 1M-message oracle sample per rank bit for bit
+    (OutboundMessageQueue.cs:113-145, LocalGrainDirectory.cs:439-497, ActivationData.cs:483-514)."""
+    import argparse
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = argparse.Namespace(local_ranks=8, config=3, grains=None, msgs=None, chunks=4, steps=1, warmup=1, wire16=False,
+                              unregistered=0.0, check_sample=1 << 20)
+    res = bench.run_rehearsal(args, torch)
+    print({k: res[k] for k in ("ms_per_step", "owned_per_rank", "max_over_mean_owned", "exchange")}, flush=True)
+    assert res["check"] == "ok", res["check"]
+    assert max(res["owned_per_rank"]) > 50_000_000  # the Zipf-hot grain's owner, at the bench's size
+    assert res["exchange"]["ncclCommCount"] == 8
+
+
 # ---- config 4: 10M-account power-law CSR fan-out --------------------------------------------------------------
 @pytest.mark.parametrize("fan_u", [None, "2", "4"])
 def test_config4_full_size_fanout(torch, monkeypatch, fan_u):
@@ -663,12 +735,11 @@ def test_stage4_hot_key_path_vs_oracle(torch, n_act):
 
 
 @pytest.mark.parametrize("rank_mode", ["hot", "plain", "ballot"])
-def test_stage4_resident_level2_vs_oracle(torch, monkeypatch, rank_mode):
-    """Stage 4's one-pass level 2 (k_bucket_resident: a bucket of <= 81920 messages sorted in one workgroup's registers)
-    beside the segmented path for larger buckets (k_seg_* + k_bucket_keyscan), in every ranking variant.  Batches: uniform;
-    a digit of more than half an LDS window in a resident bucket (written from registers); a bucket past the resident
-    capacity next to resident ones; a sparse bucket whose indices jump by > 2^22 inside one wave step (the index re-read);
-    the hot-key path with its key in a resident and in a segmented bucket; n_act + 1 == 2^20 (the key past the last
+def test_stage4_level2_edges_vs_oracle(torch, monkeypatch, rank_mode):
+    """Stage 4's two-level plan (MSD pass + segmented level 2) in every ranking variant, on the shapes its level-2 records
+    depend on: uniform buckets; one digit with tens of thousands of messages in a bucket; a bucket of 100k messages next to
+    small ones; a sparse bucket whose messages are five million positions apart (its level-2 records span many
+    super-tiles); the hot-key path with its key in a small and in a large bucket; n_act + 1 == 2^20 (the key past the last
     bucket); tiny and all-unresolved batches.  Order and offsets == the oracle's stable bucketing
     (ActivationData.EnqueueMessage, ActivationData.cs:483-514)."""
     t = torch
@@ -691,16 +762,16 @@ def test_stage4_resident_level2_vs_oracle(torch, monkeypatch, rank_mode):
         sparse = uni(6_000_000, 0, 500_000)
         sparse[:100] = n_act - 5                   # the bucket of n_act - 5: 100 messages at the start ...
         sparse[5_000_000:5_000_100] = n_act - 5    # ... and 100 five million positions later
-        big_bucket = put(uni(4_000_000), 77, 100_000)   # bucket 0: ~100k messages > the resident capacity
+        big_bucket = put(uni(4_000_000), 77, 100_000)   # bucket 0: ~100k messages, many segments
         hot_seg = put(put(uni(4_000_000), 5 * 1024 + 9, 1_300_000), 5 * 1024 + 3, 100_000)
         plan = [uni(3_000_000),
-                put(put(uni(4_000_000), 5 * 1024 + 7, 15_000), 6 * 1024 + 1, 30_000),  # digits > half a window
+                put(put(uni(4_000_000), 5 * 1024 + 7, 15_000), 6 * 1024 + 1, 30_000),  # heavy digits
                 big_bucket,
                 sparse,
-                put(uni(4_000_000), 123_457, 1_300_000),   # picks 123457 (a resident bucket's digit)
+                put(uni(4_000_000), 123_457, 1_300_000),   # picks 123457 (a small bucket's digit)
                 put(uni(4_000_000), 123_457, 1_200_000),   # ... and uses it
-                hot_seg,                                   # picks 5*1024+9, whose bucket is resident
-                put(hot_seg.copy(), 5 * 1024 + 3, 1),      # uses it; its bucket (+100k of 5*1024+3) is segmented
+                hot_seg,                                   # picks 5*1024+9 (its bucket: > 1.4M messages)
+                put(hot_seg.copy(), 5 * 1024 + 3, 1),      # uses it; its bucket holds 100k more of 5*1024+3
                 uni(1000),
                 np.full(1_100_000, L.NO_ACT, np.uint32),
                 np.array([n_act - 1], np.uint32)]
