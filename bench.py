@@ -67,11 +67,15 @@ def owner_rank_counts(torch, cl, d_msgs, n, ros, world, device=0, piece=1 << 22)
     idx = torch.empty(piece, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(world, dtype=torch.int64, device="cuda")
     total = torch.zeros(world, dtype=torch.int64, device="cuda")
-    st = torch.cuda.current_stream().cuda_stream
-    for lo in range(0, n, piece):
-        k = min(piece, n - lo)
-        e.partition_by_owner_device(d_msgs[lo:lo + k], k, ros, world, 0, out, idx, cnt, stream=st)
-        total += cnt
+    # one explicit stream for the partitions AND the torch adds: torch's default stream has handle 0, which the C ABI reads
+    # as "the context's own stream", and `total += cnt` would then race the partition that writes cnt
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for lo in range(0, n, piece):
+            k = min(piece, n - lo)
+            e.partition_by_owner_device(d_msgs[lo:lo + k], k, ros, world, 0, out, idx, cnt, stream=s.cuda_stream)
+            total += cnt
     torch.cuda.synchronize()
     e.close()
     return total

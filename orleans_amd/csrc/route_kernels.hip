@@ -239,6 +239,11 @@ __device__ __forceinline__ int probe_slot8(const uint2& q, uint32_t kb, uint32_t
     return 2;
 }
 
+// OnAddActivation's host under ORL_POLICY_HASH_SPREAD (a hash instead of RandomPlacementDirector's SafeRandom).
+__device__ __forceinline__ uint32_t spread_host(const RouteParams& P, uint32_t h, bool have_h) {
+    return (have_h && P.n_active) ? P.active_list[h % P.n_active] : 0xFFu;
+}
+
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
                                                bool found, uint32_t fact, uint32_t fsilo, uint32_t& act, bool via_cache) {
     const uint32_t me = m.meta & 0xFFu;
@@ -759,6 +764,203 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Stages 1-3 with the directory probes grouped by XCD (round 4; config 2: a 16-MiB 8-B probe table).  A random probe
+// into a table of T bytes hits an XCD's 4 MiB L2 with probability 4 MiB / T; otherwise it is a 64-B fill from the
+// Infinity Cache, and those fills (~57 G/s) bound k_route.  The table's eighths are the top 3 bits of the
+// probe start (dir_slot); when each XCD probes only its own eighth (2 MiB at config 2), the probes hit L2.  Three launches:
+//   k_route_slice  stages 1-2 per message (the route_head of k_route); a message that needs a probe of the 8-B table gets
+//                  the table eighth of its start as its slice, is ranked stably inside its 4096-message tile by slice and
+//                  leaves an 8-B record {N1 low 32 bits, uniform hash} in the tile's region of that slice (kSliceCap records
+//                  per (slice, tile)), and a partial route word (owner, sender, kSliceMark | client bit | slice, flags) in
+//                  route[]; every other message is finished here (route word + handle).  A tile whose slice counts pass
+//                  the cap (a Zipf-hot grain) probes its messages itself.
+//   k_probe_slice  workgroup b probes slice b % 8 (blocks dealt round-robin over the XCDs: b and b + 8 share an XCD; that
+//                  is speed only, correctness does not depend on placement) for a contiguous run of tiles: the chain walk
+//                  of k_route over the 8-B table, one 4-B outcome per record: act | silo << 24 on a hit (silo < 255), or
+//                  0xFF000000 | the hash-spread host on a miss.
+//   k_route_gather per tile: the same stable ranking of its marked messages recovers each one's outcome, route_tail's
+//                  decision (IsValidSilo, placement) finishes the route word and handle, written in message order with
+//                  the stage-4 histogram (and the hot key's column), as k_route writes them.
+// Decisions are those of k_route message for message (the same head, chain walk and tail); only where the probes run moves.
+// Regions: [slice][tile][wave] sub-regions of kSliceWaveCap records, so a wave ranks (ballots, per 64-message step) and
+// writes its records with no workgroup barrier and no per-message state kept across the tile; a message whose rank in its
+// (wave, slice) passes the cap (a Zipf-hot grain) is probed by k_route_slice itself, and later messages of that wave and
+// slice too, so the ranks k_route_gather recomputes over the marked messages are unchanged.
+constexpr uint32_t kSliceWaveCap = kSliceCapRecs / kWaves;  // 256: twice a uniform wave's 128 per slice
+constexpr uint32_t kSliceMark = 0xE0u;  // status byte of a partial route word: kSliceMark | client << 3 | slice (no real status)
+constexpr uint32_t kSliceMiss = 0xFF000000u;
+
+__device__ __forceinline__ size_t slice_region(uint32_t d, uint32_t t, uint32_t w, uint32_t ntiles) {
+    return (((size_t)d * ntiles + t) * kWaves + w) * kSliceWaveCap;
+}
+
+// The stable rank of this lane's slice d among the active lanes of its wave's step, on the wave's running counts (LDS, 8
+// words): 3 ballots, one counter update per slice group (the exchange partition's ballot match, wave_rank_ballot).
+__device__ __forceinline__ uint32_t slice_rank(uint32_t* cnt, uint32_t d) {
+    return wave_rank_ballot<3, false>(cnt, d, __builtin_amdgcn_read_exec(), lanes_below());
+}
+
+// route_tail for a partial route word w (k_route_slice) and its probe outcome v (slice_probe's encoding: a hit on a
+// functional silo, or kSliceMiss | the hash-spread host).
+__device__ __forceinline__ uint32_t slice_tail(const RouteParams& P, uint32_t w, uint32_t v, uint32_t& act) {
+    const uint32_t owner = w & 0xFFu, me = (w >> 8) & 0xFFu, client = (w >> 19) & 1u, rf = w >> 24;
+    const uint32_t fsilo = v >> 24;
+    if (fsilo != 0xFFu) {  // LookUpGrain, IsValidSilo already applied
+        act = v & 0xFFFFFFu;
+        return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u));
+    }
+    act = ORL_NO_ACT;
+    if (client) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
+    const uint32_t host = P.policy == ORL_POLICY_PREFER_LOCAL ? me : v & 0xFFu;
+    return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf | ORL_RF_NEW_PLACEMENT | (host == me ? ORL_RF_LOOPBACK : 0u));
+}
+
+// The 8-B table's chain walk for key kb from the hash's start slot: act | silo << 24, or kSliceMiss | spread host.
+__device__ __forceinline__ uint32_t slice_probe(const RouteParams& P, const uint2* __restrict__ probe8, uint64_t dmask, uint32_t kb,
+                                                uint32_t h) {
+    uint64_t slot = dir_slot(h, dmask);
+    uint32_t fact = 0, fsilo = 0;
+    int st = probe_slot8(probe8[slot], kb, fact, fsilo);
+    for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
+        slot = (slot + 1) & dmask;
+        st = probe_slot8(probe8[slot], kb, fact, fsilo);
+    }
+    // a hit on a silo IsValidSilo rejects is a miss (route_tail): the outcome then carries the hash-spread host
+    return (st == 0 && mask_bit(P.functional, fsilo)) ? (fact | (fsilo << 24)) : (kSliceMiss | spread_host(P, h, true));
+}
+
+struct SliceSmem {
+    RouteParams P;
+    uint32_t cnt[kWaves][8];  // each wave's running count per slice
+};
+
+__global__ __launch_bounds__(kRouteThreads) void k_route_slice(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
+                                                               uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
+                                                               const uint2* __restrict__ probe8, const orl_msg_hdr* __restrict__ in,
+                                                               uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
+                                                               uint32_t* __restrict__ act_out, uint2* __restrict__ recs,
+                                                               uint32_t* __restrict__ counts, uint32_t ntiles) {
+    __shared__ SliceSmem sm;
+    stage_params(&sm.P, gp);
+    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x;
+    const uint32_t wbase = t * kTile + w * (kItems * 64u);
+    uint32_t* cnt = sm.cnt[w];
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e >= n) break;  // (whole tail steps only: e grows with j)
+        const Msg m = load_hdr(in, e);
+        uint32_t h, own, rf, act = ORL_NO_ACT;
+        uint32_t r = route_head(sm.P, m, excl != 0, h, own, rf);
+        const bool probe = r == kNeedProbe && probe8_key(sm.P, m);
+        if (probe) {
+            const uint32_t d = fmix32(h) >> 29;  // the table eighth of the probe start (dir_slot's top bits)
+            const uint32_t client = (uint32_t)(m.tcd >> 56) == ORL_CAT_CLIENT ? 1u : 0u;
+            const uint32_t rank = slice_rank(cnt, d);
+            r = pack_route(own, m.meta & 0xFFu, kSliceMark | (client << 3) | d, rf);
+            if (rank < kSliceWaveCap) recs[slice_region(d, t, w, ntiles) + rank] = make_uint2((uint32_t)m.n1, h);
+            else r = slice_tail(sm.P, r, slice_probe(sm.P, probe8, dmask, (uint32_t)m.n1, h), act);  // past the cap: here
+        } else {
+            if (r == kNeedProbe) r = route_tail(sm.P, m, h, own, rf, false, 0u, 0u, act, false);  // no 8-B key: a miss
+            else if (r == kNeedProbeCache) r = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+        }
+        store_drop(route + e, r);
+        if (!probe || (r >> 16 & 0xF0u) != kSliceMark) store_drop(act_out + e, act);
+    }
+    if (lane < 8) counts[((size_t)t * kWaves + w) * 8u + lane] = min(cnt[lane], kSliceWaveCap);
+}
+
+__global__ __launch_bounds__(kRouteThreads) void k_probe_slice(const RouteParams* __restrict__ gp, const uint2* __restrict__ probe8,
+                                                               uint64_t dmask, const uint2* __restrict__ recs,
+                                                               const uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                               uint32_t* __restrict__ out) {
+    __shared__ RouteParams P;
+    stage_params(&P, gp);
+    __syncthreads();
+    const uint32_t s = blockIdx.x & 7u, g = blockIdx.x >> 3, groups = gridDim.x >> 3;
+    const uint32_t per = (ntiles + groups - 1u) / groups;
+    const uint32_t t0 = min(g * per, ntiles), t1 = min(t0 + per, ntiles);
+    const uint32_t i = threadIdx.x;  // kSliceWaveCap == kRouteThreads: one record per thread and sub-region
+    for (uint32_t t = t0; t < t1; ++t) {
+        uint2 rec[kWaves];
+        uint32_t c[kWaves];
+#pragma unroll
+        for (uint32_t q = 0; q < kWaves; ++q) {
+            c[q] = counts[((size_t)t * kWaves + q) * 8u + s];
+            if (i < c[q]) rec[q] = recs[slice_region(s, t, q, ntiles) + i];
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kWaves; ++q)
+            if (i < c[q]) out[slice_region(s, t, q, ntiles) + i] = slice_probe(P, probe8, dmask, rec[q].x, rec[q].y);
+    }
+}
+static_assert(kSliceWaveCap == kRouteThreads, "k_probe_slice: one record per thread and (tile, wave) sub-region");
+
+template <int HB>
+struct GatherSmem {
+    RouteParams P;
+    uint32_t hist[HB ? (1u << HB) : 1u];
+    uint32_t cnt[kWaves][8];
+    uint32_t hot;
+};
+
+template <int HB>
+__global__ __launch_bounds__(kRouteThreads) void k_route_gather(const RouteParams* __restrict__ gp, uint32_t n,
+                                                                uint32_t* __restrict__ route, uint32_t* __restrict__ act_out,
+                                                                const uint32_t* __restrict__ res, uint32_t ntiles,
+                                                                uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift,
+                                                                const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows) {
+    __shared__ GatherSmem<HB> sm;
+    constexpr bool HIST = HB > 0;
+    stage_params(&sm.P, gp);
+    if (HIST)
+        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
+    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sm.hot = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x;
+    const uint32_t wbase = t * kTile + w * (kItems * 64u);
+    const uint32_t n_act = sm.P.n_act;
+    const uint32_t hk = (HIST && hot_rows) ? hot_key_of(hot_words) : kNoHotKey;
+    uint32_t* cnt = sm.cnt[w];
+    uint32_t rw[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {  // all of the tile's route words in flight
+        const uint32_t e = wbase + j * 64u + lane;
+        rw[j] = e < n ? __builtin_nontemporal_load(route + e) : 0u;
+    }
+    uint32_t hot_mine = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = wbase + j * 64u + lane;
+        if (e >= n) continue;
+        uint32_t act;
+        if (((rw[j] >> 16) & 0xF0u) == kSliceMark) {  // marked: its outcome, at the rank k_route_slice gave it
+            const uint32_t d = (rw[j] >> 16) & 7u;
+            const uint32_t v = res[slice_region(d, t, w, ntiles) + slice_rank(cnt, d)];
+            store_drop(route + e, slice_tail(sm.P, rw[j], v, act));
+            store_drop(act_out + e, act);
+        } else {
+            act = HIST ? act_out[e] : 0u;  // finished by k_route_slice
+        }
+        if (HIST) {
+            const uint32_t k = bucket_key(act, n_act);
+            if (k == hk) ++hot_mine;
+            else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
+        }
+    }
+    if (HIST) {
+        if (hot_rows) wave_add_hot(&sm.hot, hot_mine);
+        __syncthreads();
+        store_count_row(tile_cnt + (size_t)blockIdx.x * bins, sm.hist, bins);
+        if (hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = sm.hot;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Device-wide exclusive scan of u32 (3 launches): per-block sums, one-block scan of the sums, and a
 // down-sweep that rescans each block's chunk with its prefix.  Chunk = 4096 elements per block.
 constexpr uint32_t kScanChunk = 4096;
@@ -915,12 +1117,17 @@ __device__ __forceinline__ void store16(uint32_t* __restrict__ a, uint64_t base,
 // next_key (and the mapped host word): the most frequent key when it holds >= 1/kHotShare of the batch's n messages and
 // >= kHotMinCount, else kNoHotKey.
 constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4096;
+// WIDEN (the fan-out's publish offsets) with fblk: also the publisher of every kFanBlk-th fan-out message,
+// fblk[k] = the p with poff[p] <= k * kFanBlk < poff[p + 1], and fblk[ceil(total / kFanBlk)] = n_pub - 1 (written by
+// the last element, m - 1 = n_pub): a fan-out tile reads its publisher range with two independent loads.
+constexpr uint32_t kFanBlkShift = 8, kFanBlk = 1u << kFanBlkShift;
 template <bool DIRECT, bool WIDEN, bool PICK = false>
 __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums,
                                                    uint64_t* __restrict__ out64, uint64_t add64,
                                                    const unsigned long long* __restrict__ bmax = nullptr, uint32_t n = 0,
                                                    uint32_t* __restrict__ next_key = nullptr,
-                                                   uint32_t* __restrict__ host_word = nullptr) {
+                                                   uint32_t* __restrict__ host_word = nullptr,
+                                                   uint32_t* __restrict__ fblk = nullptr, uint32_t fblk_cap = 0) {
     __shared__ uint32_t wsum[kWaves];
     if (PICK && blockIdx.x == 0) {
         __shared__ unsigned long long wmax[kWaves];
@@ -957,7 +1164,17 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         o[i] = run;
-        if (WIDEN && base + i < m) out64[base + i] = add64 + run;
+        if (WIDEN && base + i < m) {
+            out64[base + i] = add64 + run;
+            if (fblk) {  // the fan-out blocks this publisher's messages start
+                const uint32_t k0 = (run + kFanBlk - 1u) >> kFanBlkShift;  // (a total past fblk_cap fails the launch after
+                if (base + i + 1 < m) {                                    //  the scan: its map is never read)
+                    for (uint32_t k = k0; (k << kFanBlkShift) < run + v[i] && k < fblk_cap; ++k) fblk[k] = (uint32_t)(base + i);
+                } else if (m > 1 && k0 < fblk_cap) {
+                    fblk[k0] = (uint32_t)(m - 2);
+                }
+            }
+        }
         run += v[i];
     }
     store16(a, base, m, o);
@@ -1986,15 +2203,17 @@ __global__ __launch_bounds__(256) void k_seg_carry(const uint32_t* __restrict__ 
 // (a sparse bucket) sets `wide`, and its positions search the bucket's bases in global memory instead.
 constexpr uint32_t kBsCap = kSegChunk, kBsNone = 0xFFFFFFFFu;
 
+// Every entry is written (kBsNone past the round), so bs is non-decreasing over its whole length and bs[kBsCap - 1] is
+// kBsNone: the searches and walks over it end.
 __device__ __forceinline__ bool load_bases(const uint32_t* __restrict__ srow, uint32_t nsup, uint32_t klo, uint32_t c1, uint32_t* bs) {
-    bool wide = false;
+    bool wide = false, past = false;
     for (uint32_t t = threadIdx.x; t < kBsCap; t += 256u) {
         const uint32_t k = klo + 1u + t;
-        const uint32_t p = k < nsup ? srow[k] : kBsNone;
-        const bool in = p < c1;
-        bs[t] = in && t + 1u < kBsCap ? p : kBsNone;
-        wide |= in && t + 1u == kBsCap;
-        if (!in) break;
+        uint32_t p = kBsNone;
+        if (!past && k < nsup) p = srow[k];
+        past |= p >= c1;
+        wide |= !past && t + 1u == kBsCap;
+        bs[t] = !past && t + 1u < kBsCap ? p : kBsNone;
     }
     return wide;
 }
@@ -2096,7 +2315,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
             for (uint32_t j = 0; j < kItems; ++j) {
                 const uint32_t e = wbase + j * 64u + lane;
                 if (!wide) {
-                    while (bs[kc] <= e) ++kc;
+                    while (kc < kBsCap - 1u && bs[kc] <= e) ++kc;  // (bs[kBsCap - 1] = none: the bound is belt and braces)
                     idx[j] |= (klo + kc) << kSupShift;
                 } else if (e < r.hi) {
                     idx[j] |= sup_of(srow, nsup, klo, e) << kSupShift;
@@ -2151,15 +2370,43 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
-constexpr uint32_t kFanLds = 2048;  // publishers staged per tile; beyond that fall back to global search
+constexpr uint32_t kFanLds = 1024;  // publishers staged per tile; beyond that fall back to global search
 
 template <int HB>
 struct FanSmem {
     RouteParams P;
     uint32_t hist[HB ? (1u << HB) : 1u];
     uint32_t poff[kFanLds + 1];
+    uint64_t pdelta[kFanLds];  // pstart[p] - poff[p]: message f of publisher p reads csr_tgt[pdelta + f]
     uint32_t prange[2];
 };
+
+// A fan-out tile's publishers [p_lo, p_hi] (a superset is fine: every f of the tile has poff[p_lo] <= f < poff[p_hi + 1]):
+// from the scan's block map (two independent loads), or (fblk null) two 64-way wave searches of the offsets.  fb / fl =
+// the tile's first / last fan-out message; waves 0 and 1 search; the result is read after a barrier.
+__device__ __forceinline__ void fan_range(const uint32_t* __restrict__ poff32, const uint32_t* __restrict__ fblk, uint32_t n_pub,
+                                          uint32_t fb, uint32_t fl, uint32_t* prange) {
+    if (fblk) {
+        if (threadIdx.x == 0) {
+            const uint32_t kmax = (poff32[n_pub] + kFanBlk - 1u) >> kFanBlkShift;  // the sentinel block: n_pub - 1
+            prange[0] = fblk[fb >> kFanBlkShift];
+            prange[1] = fblk[min((fl >> kFanBlkShift) + 1u, kmax)];
+        }
+    } else if (threadIdx.x < 128) {
+        const uint32_t p = wave_find_pub(poff32, n_pub, threadIdx.x < 64 ? fb : fl);
+        if ((threadIdx.x & 63u) == 0) prange[threadIdx.x >> 6] = p;
+    }
+}
+
+// Stages the tile's publisher offsets (span + 1) and CSR starts (as pdelta) in LDS.
+__device__ __forceinline__ void fan_stage(const uint32_t* __restrict__ poff32, const uint64_t* __restrict__ pstart, uint32_t p_lo,
+                                          uint32_t span, uint32_t* poff, uint64_t* pdelta) {
+    for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) {
+        const uint32_t o = poff32[p_lo + i];
+        poff[i] = o;
+        if (i < span) pdelta[i] = pstart[p_lo + i] - o;
+    }
+}
 
 // phase markers of k_fanout_route's U-message step (never route words: status bytes 0xFD / 0xFC are unused)
 constexpr uint32_t kNoAct4 = 0xFDFDFDFDu, kFanSlow = 0xFCFCFCFCu;
@@ -2173,7 +2420,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32, uint32_t n_pub, uint64_t follower_tcd,
     const orl_grain_key* __restrict__ follower_keys, const orl_msg_hdr* __restrict__ direct, uint32_t nd, uint32_t n,
     uint32_t excl, uint32_t* __restrict__ route,
-    uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift, uint32_t items) {
+    uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift, uint32_t items,
+    const uint32_t* __restrict__ fblk) {
     __shared__ FanSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
@@ -2189,18 +2437,15 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const uint32_t last = ((lim - base) < rtile ? lim : base + rtile) - 1;
     const uint32_t fbase = base > nd ? base : nd;  // first fan-out message of the tile
     const bool fan = base < lim && last >= nd;
-    // publisher of fan-out message f = upper_bound(poff32[0..n_pub], f) - 1
-    // (waves 0 and 1, a 64-way search each: 3 dependent loads for 64k publishers instead of 17)
-    if (fan && threadIdx.x < 128) {
-        const uint32_t p = wave_find_pub(poff32, n_pub, (threadIdx.x < 64 ? fbase : last) - nd);
-        if ((threadIdx.x & 63u) == 0) sm.prange[threadIdx.x >> 6] = p;
-    }
+    // publisher of fan-out message f = upper_bound(poff32[0..n_pub], f) - 1: the tile's range, then its offsets and CSR
+    // starts in LDS (round 4: the range from the scan's block map, one load instead of two 3-deep 64-way searches; the CSR
+    // starts staged, one dependent global load per message fewer)
+    if (fan) fan_range(poff32, fblk, n_pub, fbase - nd, last - nd, sm.prange);
     __syncthreads();
     const uint32_t p_lo = fan ? sm.prange[0] : 0u, p_hi = fan ? sm.prange[1] : 0u;
     const uint32_t span = p_hi - p_lo + 1;  // publishers touching this tile
     const bool in_lds = span <= kFanLds;
-    if (in_lds && fan)
-        for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
+    if (in_lds && fan) fan_stage(poff32, pstart, p_lo, span, sm.poff, sm.pdelta);
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
     const bool use16 = PW != 0 && (probe_bad == nullptr || *probe_bad == 0u);
@@ -2216,7 +2461,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
             pub[q] = 0;
             if (j + q < items && e[q] < lim && e[q] >= nd) {
                 const uint32_t f = e[q] - nd;
-                uint32_t lo, hi, pq, start;
+                uint32_t lo, hi, pq;
+                uint64_t ci;  // the message's CSR entry
                 if (in_lds) {
                     lo = 0; hi = span + 1;
                     while (lo < hi) {
@@ -2224,7 +2470,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                         if (sm.poff[mid] <= f) lo = mid + 1; else hi = mid;
                     }
                     pq = p_lo + lo - 1;
-                    start = sm.poff[lo - 1];
+                    ci = sm.pdelta[lo - 1] + f;
                 } else {
                     lo = p_lo; hi = p_hi + 1;
                     while (lo < hi) {
@@ -2232,10 +2478,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                         if (poff32[mid] <= f) lo = mid + 1; else hi = mid;
                     }
                     pq = lo - 1;
-                    start = poff32[pq];
+                    ci = pstart[pq] + (f - poff32[pq]);
                 }
                 pub[q] = pq;
-                tgt[q] = csr_tgt[pstart[pq] + (f - start)];
+                tgt[q] = csr_tgt[ci];
             }
         }
         Msg m[U];
@@ -2317,6 +2563,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
 // None, ORL_HDR_ADDRESS_COMPLETE, target silo 0xFF (routed as a pass-through, bucketed as unresolved).
 struct ExpandSmem {
     uint32_t poff[kFanLds + 1];
+    uint64_t pdelta[kFanLds];
     uint32_t prange[2];
 };
 
@@ -2324,7 +2571,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t*
                                                                  const uint8_t* __restrict__ pub_silo, const uint32_t* __restrict__ poff32,
                                                                  uint32_t n_pub, uint64_t follower_tcd,
                                                                  const orl_grain_key* __restrict__ follower_keys, uint32_t n,
-                                                                 uint32_t items, orl_msg_hdr* __restrict__ out) {
+                                                                 uint32_t items, orl_msg_hdr* __restrict__ out,
+                                                                 const uint32_t* __restrict__ fblk) {
     __shared__ ExpandSmem sm;
     const uint32_t rtile = kRouteThreads * items;
     const uint32_t base = blockIdx.x * rtile;
@@ -2332,16 +2580,12 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t*
     const uint32_t lim = n < real ? n : real;
     const bool fan = base < lim;
     const uint32_t last = fan ? ((lim - base) < rtile ? lim : base + rtile) - 1 : 0u;
-    if (fan && threadIdx.x < 128) {
-        const uint32_t p = wave_find_pub(poff32, n_pub, threadIdx.x < 64 ? base : last);
-        if ((threadIdx.x & 63u) == 0) sm.prange[threadIdx.x >> 6] = p;
-    }
+    if (fan) fan_range(poff32, fblk, n_pub, base, last, sm.prange);
     __syncthreads();
     const uint32_t p_lo = fan ? sm.prange[0] : 0u, p_hi = fan ? sm.prange[1] : 0u;
     const uint32_t span = p_hi - p_lo + 1;
     const bool in_lds = span <= kFanLds;
-    if (in_lds && fan)
-        for (uint32_t i = threadIdx.x; i <= span; i += blockDim.x) sm.poff[i] = poff32[p_lo + i];
+    if (in_lds && fan) fan_stage(poff32, pstart, p_lo, span, sm.poff, sm.pdelta);
     __syncthreads();
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads + threadIdx.x;
@@ -2351,7 +2595,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t*
             h0 = u32x4{0u, 0u, 0u, 0u};
             h1 = u32x4{0u, 0u, 0xFFu | ((uint32_t)ORL_HDR_ADDRESS_COMPLETE << 16) | (0xFFu << 24), 0u};
         } else {
-            uint32_t lo, hi, p, start;
+            uint32_t lo, hi, p;
+            uint64_t ci;
             if (in_lds) {
                 lo = 0; hi = span + 1;
                 while (lo < hi) {
@@ -2359,7 +2604,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t*
                     if (sm.poff[mid] <= e) lo = mid + 1; else hi = mid;
                 }
                 p = p_lo + lo - 1;
-                start = sm.poff[lo - 1];
+                ci = sm.pdelta[lo - 1] + e;
             } else {
                 lo = p_lo; hi = p_hi + 1;
                 while (lo < hi) {
@@ -2367,9 +2612,9 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_expand(const uint64_t*
                     if (poff32[mid] <= e) lo = mid + 1; else hi = mid;
                 }
                 p = lo - 1;
-                start = poff32[p];
+                ci = pstart[p] + (e - poff32[p]);
             }
-            const uint32_t tgt = csr_tgt[pstart[p] + (e - start)];
+            const uint32_t tgt = csr_tgt[ci];
             uint64_t tcd = follower_tcd, n0 = 0, n1 = (uint64_t)tgt;
             if (follower_keys) {
                 const orl_grain_key k = follower_keys[tgt];
@@ -3841,6 +4086,13 @@ uint32_t env_gap_cap() {
     return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
 }
 
+uint64_t env_slice_min() {
+    const char* off = getenv("ORL_NO_SLICE");
+    if (off && off[0] == '1') return ~0ull;
+    const char* e = getenv("ORL_SLICE_MIN");
+    return e ? (uint64_t)atoll(e) : (1ull << 20);
+}
+
 int env_fan_u() {
     const char* e = getenv("ORL_FAN_U");
     const int v = e ? atoi(e) : kFanIlp;
@@ -3910,9 +4162,12 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    const uint32_t items = route_items(n, max_route_items(n_act));
+    uint32_t items = route_items(n, max_route_items(n_act));
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
+    if (dv.probe8 && fmt == 32 && s.slice_recs && n >= s.slice_min && dv.mask + 1 >= 8 && dv.mask + 1 <= kSliceMaxSlots &&
+        n <= s.max_batch)
+        items = kItems;  // the sliced route's tiles: 4096 messages, one histogram row each
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     const bool hist = buckets && rh.on;
     const bool pick = hist && hot_path_on(n, n_act, s);
@@ -3925,7 +4180,23 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
-    if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
+    const bool sliced = dv.probe8 && fmt == 32 && s.slice_recs && n >= s.slice_min && dv.mask + 1 >= 8 &&
+                        dv.mask + 1 <= kSliceMaxSlots && n <= s.max_batch;
+    if (sliced) {  // config 2: the probes grouped by table eighth, each XCD probing its own from L2
+        ++s.sliced_batches;
+        const uint32_t ntiles = ceil_div(n, kTile);
+        const uint2* p8 = static_cast<const uint2*>(dv.probe8);
+        hipLaunchKernelGGL(k_route_slice, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, dv.cache, dv.cmask, p8,
+                           static_cast<const orl_msg_hdr*>(d_in), (uint32_t)n, excl, d_route, d_act, s.slice_recs, s.slice_cnt, ntiles);
+        hipLaunchKernelGGL(k_probe_slice, dim3(kSliceProbeGroups * 8), dim3(kRouteThreads), 0, st, d_params, p8, dv.mask, s.slice_recs,
+                           s.slice_cnt, ntiles, s.slice_res);
+        if (hist)
+            hipLaunchKernelGGL(k_route_gather<kMaxDigitBits>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, (uint32_t)n, d_route,
+                               d_act, s.slice_res, ntiles, th, bins, shift, hw, hr);
+        else
+            hipLaunchKernelGGL(k_route_gather<0>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, (uint32_t)n, d_route, d_act,
+                               s.slice_res, ntiles, th, bins, shift, hw, hr);
+    } else if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
@@ -3967,13 +4238,14 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     const uint32_t m = (uint32_t)n_pub + 1;
     const uint32_t nbs = ceil_div(m, kScanChunk);
     hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+    const uint32_t fcap = s.fan_blk ? (uint32_t)std::min<uint64_t>((max_out + kFanBlk - 1) / kFanBlk + 1, s.fan_blk_cap) : 0u;
     if (nbs <= kScanDirectChunks) {
         hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
-                           d_pub_offsets, (uint64_t)n_direct);
+                           d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else {
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
         hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
-                           d_pub_offsets, (uint64_t)n_direct);
+                           d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     }
     uint64_t total = *n_out;
     if (!(opts & ORL_OPT_TOTAL_GIVEN)) {  // read the emitted count back (one stream sync)
@@ -3993,6 +4265,8 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     // a finer grid than k_route's (>= 4096 tiles): each tile starts with a few dependent loads (its publisher range),
     // which later tiles overlap (config 4: 0.223 -> 0.210 ms; 8192 tiles 0.219)
     const uint32_t items = route_items(total, max_route_items(n_act), fan_min_wgs());
+    // the scan's publisher-block map, when its capacity covered the batch (else the kernel's wave searches)
+    const uint32_t* fblk = (fcap && (total + kFanBlk - 1) / kFanBlk < fcap) ? s.fan_blk : nullptr;
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
@@ -4008,7 +4282,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
                                                        dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
                                                        follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
                                                        excl, d_route, d_act, TH, BINS, \
-                                                       SHIFT, items)
+                                                       SHIFT, items, fblk)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_cnt, rh.bins, rh.shift);
     else ORL_FAN(0, nullptr, 1u, 0u);
 #undef ORL_FAN
@@ -4029,13 +4303,14 @@ int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, c
     const uint32_t m = (uint32_t)n_pub + 1;
     const uint32_t nbs = ceil_div(m, kScanChunk);
     hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+    const uint32_t fcap = s.fan_blk ? (uint32_t)std::min<uint64_t>((cap + kFanBlk - 1) / kFanBlk + 1, s.fan_blk_cap) : 0u;
     if (nbs <= kScanDirectChunks) {
         hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
-                           0ull);
+                           0ull, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else {
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
         hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
-                           0ull);
+                           0ull, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     }
     uint64_t total = *n_out;
     if (!(opts & ORL_OPT_TOTAL_GIVEN)) {
@@ -4050,8 +4325,9 @@ int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, c
     if (total > cap) return -1;
     if (total == 0) return 0;
     const uint32_t items = route_items(total, 4);
+    const uint32_t* fblk = (fcap && (total + kFanBlk - 1) / kFanBlk < fcap) ? s.fan_blk : nullptr;
     hipLaunchKernelGGL(k_fanout_expand, dim3(ceil_div(total, kRouteThreads * items)), dim3(kRouteThreads), 0, st, pstart, d_csr_tgt,
-                       d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total, items, d_out);
+                       d_pub_silo, poff32, (uint32_t)n_pub, follower_tcd, d_follower_keys, (uint32_t)total, items, d_out, fblk);
     return (int)hipGetLastError();
 }
 

@@ -7,7 +7,8 @@
 #   BENCH_ARGS="..."           bench arguments (default --steps 20 --warmup 5 --no-cpu)
 #   CONFIGS="1 3 4 5"          extra bench lines, one per config (--config c --steps 10 --warmup 2)
 #   PROF=1                     rocprofv3 kernel trace of the default bench (PROF_ARGS; stats to $OUT/trace)
-#   PMC="g1;g2"                extra rocprofv3 --pmc passes (one per ';'-separated group) over PROF_ARGS
+#   PMC="g1;g2"                extra rocprofv3 --pmc passes (one per ';'-separated group) over PROF_ARGS (PMC_ARGS: extra
+#                              rocprofv3 options, e.g. --kernel-include-regex k_probe_slice)
 #   LAB="cmd"                  an extra command (e.g. python scripts/rank_cost_lab.py 8 4 8), 300 s limit
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -18,7 +19,7 @@ PROF_ARGS=${PROF_ARGS:---steps 5 --warmup 1 --no-cpu}
 stop() { case $1 in 0) ;; *) echo "step exit $1: stopping"; exit $1;; esac; }
 
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TLIM:-900} python -u -m pytest $TESTS -x -v -m gpu ${K:+-k "$K"} --timeout 400 --timeout-method thread \
+  timeout -k 10 ${TLIM:-900} python -u -m pytest $TESTS -x -v -m gpu ${K:+-k "$K"} --timeout 400 --timeout-method thread --capture=tee-sys \
     > $OUT/gpu_tests.log 2>&1
   rc=$?; echo "gpu tests exit $rc: $(tail -1 $OUT/gpu_tests.log)"
   [ $rc = 0 ] || { grep -E "FAILED|Error|error" $OUT/gpu_tests.log | head -20; tail -25 $OUT/gpu_tests.log; exit $rc; }
@@ -54,7 +55,7 @@ if [ -n "$PMC" ]; then
   i=0
   for grp in "${GRPS[@]}"; do
     i=$((i+1))
-    timeout -k 10 -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python3 bench.py $PROF_ARGS > $OUT/pmc$i.log 2>&1
+    timeout -k 10 -s KILL 120 rocprofv3 --pmc $grp $PMC_ARGS --output-format csv -d $OUT/pmc$i -o pmc -- python3 bench.py $PROF_ARGS > $OUT/pmc$i.log 2>&1
     rc=$?; echo "pmc$i ($grp) exit $rc"; stop $rc
   done
   python3 scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt 2>&1; head -40 $OUT/pmc_summary.txt
