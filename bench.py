@@ -519,6 +519,8 @@ def run_rehearsal(args, torch):
     for r in range(R):
         errs = node_self_check(torch, engs[r], stats[r]["last"], r, cl, keys, owner, reg, masks[r], n_acts[r], ros,
                                expect_owned[r], args.check_sample)
+        if errs:
+            log(f"rank {r}: segments (count, width) {[(c, w) for _, c, w in stats[r]['last'].segments]}")
         bad += [f"rank {r}: {e}" for e in errs]
     if sum(st["last"].n_hosted for st in stats) != n_total:
         bad.append(f"the ranks host {sum(st['last'].n_hosted for st in stats)} messages of {n_total}")

@@ -677,8 +677,6 @@ int orl_sync(orl_ctx* ctx);
                                  (>= 1/32 of its messages); 0xFFFFFFFF = none.  Outputs never depend on it.  Synchronises. */
 #define ORL_Q_HOT_BATCHES 11u /* batches that took stage 4's hot-key path so far (the launcher decides from a mapped host copy
                                  of the last pick, which may lag the device by the batches still queued) */
-#define ORL_Q_SLICED_BATCHES 12u /* route launches that grouped their directory probes by table eighth (the XCD-sliced
-                                    route: an 8-B probe table of <= 4M slots, >= 2^20 messages, ORL_SLICE_MIN) */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 /* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
  * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */

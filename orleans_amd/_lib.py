@@ -63,7 +63,6 @@ Q_WIRE_DIGEST = 8
 Q_PART_ERROR = 9
 Q_HOT_KEY = 10
 Q_HOT_BATCHES = 11
-Q_SLICED_BATCHES = 12
 MAX_WIRE_TYPES = 16
 PART_LOOKBACK_FAILED = 0x4
 

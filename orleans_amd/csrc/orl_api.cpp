@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.sup_base); f(c->s.seg_sup); f(c->s.fan_blk); f(c->s.slice_recs); f(c->s.slice_res); f(c->s.slice_cnt);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.fan_blk);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -810,20 +810,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.seg_carry, carry_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_carry)");
         if ((e = hipMalloc((void**)&c->s.seg_meta, ((seg_rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_meta)");
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
-        c->s.slice_min = env_slice_min();
-        if (slots <= kSliceMaxSlots && slots >= 8 && c->s.slice_min != ~0ull) {  // the sliced route's records and outcomes
-            const size_t nrec = (size_t)8 * tiles * kSliceCapRecs;
-            if ((e = hipMalloc((void**)&c->s.slice_recs, nrec * 8)) != hipSuccess) return bail(e, "hipMalloc(slice records)");
-            if ((e = hipMalloc((void**)&c->s.slice_res, nrec * 4)) != hipSuccess) return bail(e, "hipMalloc(slice outcomes)");
-            if ((e = hipMalloc((void**)&c->s.slice_cnt, (size_t)tiles * 4 * 8 * 4)) != hipSuccess) return bail(e, "hipMalloc(slice counts)");
-        }
         c->s.fan_blk_cap = (uint32_t)((mb + 255) / 256 + 2);
         if ((e = hipMalloc((void**)&c->s.fan_blk, (size_t)c->s.fan_blk_cap * 4)) != hipSuccess) return bail(e, "hipMalloc(fan_blk)");
-        if (bp.two_level && bp.hb > 0 &&
-            (e = hipMalloc((void**)&c->s.sup_base, ((1ull << bp.hb) * ((mb + 65535) / 65536) + 1) * 4)) != hipSuccess)
-            return bail(e, "hipMalloc(sup_base)");
-        if (bp.two_level && bp.hb > 0 && (e = hipMalloc((void**)&c->s.seg_sup, (seg_rows + 1) * 4)) != hipSuccess)
-            return bail(e, "hipMalloc(seg_sup)");
         if ((e = hipMalloc((void**)&c->s.sstart, 4098 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
@@ -1958,10 +1946,7 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
         case ORL_Q_HOT_BATCHES:
             *v = c->s.hot_batches;
             return ORL_OK;
-        case ORL_Q_SLICED_BATCHES:
-            *v = c->s.sliced_batches;
-            return ORL_OK;
-        case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
+case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             ORL_HIP(c, hipSetDevice(c->cfg.device));
             ORL_HIP(c, hipDeviceSynchronize());

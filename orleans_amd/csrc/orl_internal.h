@@ -264,27 +264,11 @@ struct Scratch {
     uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
-    uint32_t* sup_base = nullptr;  // [2^hb][ceil(max_batch / 65536)] narrow level-2 records: each super-tile's base per bucket
-    uint32_t* seg_sup = nullptr;   // [max segments] narrow level-2 records: the super-tile of each segment's first position
-    // the XCD-sliced route (k_route_slice / k_probe_slice / k_route_gather), allocated when the directory's 8-B probe table
-    // can be sliced into L2-sized eighths (<= kSliceMaxSlots slots): [8][max_tiles][4 waves][256] records and outcomes,
-    // [max_tiles][4 waves][8] counts
-    uint2* slice_recs = nullptr;
-    uint32_t* slice_res = nullptr;
-    uint32_t* slice_cnt = nullptr;
-    uint64_t slice_min = 1u << 20;  // smaller batches take k_route (ORL_SLICE_MIN at context creation; ORL_NO_SLICE=1: never)
-    mutable uint64_t sliced_batches = 0;  // route launches on the sliced path (ORL_Q_SLICED_BATCHES)
     uint32_t* fan_blk = nullptr;   // [fan_blk_cap] fan-out: the publisher of every 256th emitted message (k_scan_down WIDEN)
     uint32_t fan_blk_cap = 0;
     uint32_t gap_cap = 4096;  // LSD offsets' long-gap queue capacity (env_gap_cap() at context creation)
     int fan_u = 1;            // fan-out messages per thread and step (env_fan_u() at context creation)
 };
-// The sliced route: tables of up to 4M 8-B slots (32 MiB; eighths of <= 4 MiB, an XCD's L2), kSliceCap records per
-// (slice, 4096-message tile), k_probe_slice's grid = kSliceProbeGroups workgroups per slice.
-constexpr uint64_t kSliceMaxSlots = 4ull << 20;
-constexpr uint32_t kSliceCapRecs = 1024;
-constexpr uint32_t kSliceProbeGroups = 256;
-uint64_t env_slice_min();  // ORL_SLICE_MIN (default 2^20), or UINT64_MAX with ORL_NO_SLICE=1
 
 // Knobs read from the environment once per context (orl_ctx_create): ORL_GAP_CAP, ORL_FAN_U.
 uint32_t env_gap_cap();

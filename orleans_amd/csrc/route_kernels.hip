@@ -239,11 +239,6 @@ __device__ __forceinline__ int probe_slot8(const uint2& q, uint32_t kb, uint32_t
     return 2;
 }
 
-// OnAddActivation's host under ORL_POLICY_HASH_SPREAD (a hash instead of RandomPlacementDirector's SafeRandom).
-__device__ __forceinline__ uint32_t spread_host(const RouteParams& P, uint32_t h, bool have_h) {
-    return (have_h && P.n_active) ? P.active_list[h % P.n_active] : 0xFFu;
-}
-
 __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
                                                bool found, uint32_t fact, uint32_t fsilo, uint32_t& act, bool via_cache) {
     const uint32_t me = m.meta & 0xFFu;
@@ -764,203 +759,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Stages 1-3 with the directory probes grouped by XCD (round 4; config 2: a 16-MiB 8-B probe table).  A random probe
-// into a table of T bytes hits an XCD's 4 MiB L2 with probability 4 MiB / T; otherwise it is a 64-B fill from the
-// Infinity Cache, and those fills (~57 G/s) bound k_route.  The table's eighths are the top 3 bits of the
-// probe start (dir_slot); when each XCD probes only its own eighth (2 MiB at config 2), the probes hit L2.  Three launches:
-//   k_route_slice  stages 1-2 per message (the route_head of k_route); a message that needs a probe of the 8-B table gets
-//                  the table eighth of its start as its slice, is ranked stably inside its 4096-message tile by slice and
-//                  leaves an 8-B record {N1 low 32 bits, uniform hash} in the tile's region of that slice (kSliceCap records
-//                  per (slice, tile)), and a partial route word (owner, sender, kSliceMark | client bit | slice, flags) in
-//                  route[]; every other message is finished here (route word + handle).  A tile whose slice counts pass
-//                  the cap (a Zipf-hot grain) probes its messages itself.
-//   k_probe_slice  workgroup b probes slice b % 8 (blocks dealt round-robin over the XCDs: b and b + 8 share an XCD; that
-//                  is speed only, correctness does not depend on placement) for a contiguous run of tiles: the chain walk
-//                  of k_route over the 8-B table, one 4-B outcome per record: act | silo << 24 on a hit (silo < 255), or
-//                  0xFF000000 | the hash-spread host on a miss.
-//   k_route_gather per tile: the same stable ranking of its marked messages recovers each one's outcome, route_tail's
-//                  decision (IsValidSilo, placement) finishes the route word and handle, written in message order with
-//                  the stage-4 histogram (and the hot key's column), as k_route writes them.
-// Decisions are those of k_route message for message (the same head, chain walk and tail); only where the probes run moves.
-// Regions: [slice][tile][wave] sub-regions of kSliceWaveCap records, so a wave ranks (ballots, per 64-message step) and
-// writes its records with no workgroup barrier and no per-message state kept across the tile; a message whose rank in its
-// (wave, slice) passes the cap (a Zipf-hot grain) is probed by k_route_slice itself, and later messages of that wave and
-// slice too, so the ranks k_route_gather recomputes over the marked messages are unchanged.
-constexpr uint32_t kSliceWaveCap = kSliceCapRecs / kWaves;  // 256: twice a uniform wave's 128 per slice
-constexpr uint32_t kSliceMark = 0xE0u;  // status byte of a partial route word: kSliceMark | client << 3 | slice (no real status)
-constexpr uint32_t kSliceMiss = 0xFF000000u;
-
-__device__ __forceinline__ size_t slice_region(uint32_t d, uint32_t t, uint32_t w, uint32_t ntiles) {
-    return (((size_t)d * ntiles + t) * kWaves + w) * kSliceWaveCap;
-}
-
-// The stable rank of this lane's slice d among the active lanes of its wave's step, on the wave's running counts (LDS, 8
-// words): 3 ballots, one counter update per slice group (the exchange partition's ballot match, wave_rank_ballot).
-__device__ __forceinline__ uint32_t slice_rank(uint32_t* cnt, uint32_t d) {
-    return wave_rank_ballot<3, false>(cnt, d, __builtin_amdgcn_read_exec(), lanes_below());
-}
-
-// route_tail for a partial route word w (k_route_slice) and its probe outcome v (slice_probe's encoding: a hit on a
-// functional silo, or kSliceMiss | the hash-spread host).
-__device__ __forceinline__ uint32_t slice_tail(const RouteParams& P, uint32_t w, uint32_t v, uint32_t& act) {
-    const uint32_t owner = w & 0xFFu, me = (w >> 8) & 0xFFu, client = (w >> 19) & 1u, rf = w >> 24;
-    const uint32_t fsilo = v >> 24;
-    if (fsilo != 0xFFu) {  // LookUpGrain, IsValidSilo already applied
-        act = v & 0xFFFFFFu;
-        return pack_route(owner, fsilo, ORL_ST_HIT, rf | (fsilo == me ? ORL_RF_LOOPBACK : 0u));
-    }
-    act = ORL_NO_ACT;
-    if (client) return pack_route(owner, 0xFFu, ORL_ST_CLIENT_UNREGISTERED, rf);
-    const uint32_t host = P.policy == ORL_POLICY_PREFER_LOCAL ? me : v & 0xFFu;
-    return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf | ORL_RF_NEW_PLACEMENT | (host == me ? ORL_RF_LOOPBACK : 0u));
-}
-
-// The 8-B table's chain walk for key kb from the hash's start slot: act | silo << 24, or kSliceMiss | spread host.
-__device__ __forceinline__ uint32_t slice_probe(const RouteParams& P, const uint2* __restrict__ probe8, uint64_t dmask, uint32_t kb,
-                                                uint32_t h) {
-    uint64_t slot = dir_slot(h, dmask);
-    uint32_t fact = 0, fsilo = 0;
-    int st = probe_slot8(probe8[slot], kb, fact, fsilo);
-    for (uint64_t step = 0; st == 2 && step < dmask; ++step) {
-        slot = (slot + 1) & dmask;
-        st = probe_slot8(probe8[slot], kb, fact, fsilo);
-    }
-    // a hit on a silo IsValidSilo rejects is a miss (route_tail): the outcome then carries the hash-spread host
-    return (st == 0 && mask_bit(P.functional, fsilo)) ? (fact | (fsilo << 24)) : (kSliceMiss | spread_host(P, h, true));
-}
-
-struct SliceSmem {
-    RouteParams P;
-    uint32_t cnt[kWaves][8];  // each wave's running count per slice
-};
-
-__global__ __launch_bounds__(kRouteThreads) void k_route_slice(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
-                                                               uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
-                                                               const uint2* __restrict__ probe8, const orl_msg_hdr* __restrict__ in,
-                                                               uint32_t n, uint32_t excl, uint32_t* __restrict__ route,
-                                                               uint32_t* __restrict__ act_out, uint2* __restrict__ recs,
-                                                               uint32_t* __restrict__ counts, uint32_t ntiles) {
-    __shared__ SliceSmem sm;
-    stage_params(&sm.P, gp);
-    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t t = blockIdx.x;
-    const uint32_t wbase = t * kTile + w * (kItems * 64u);
-    uint32_t* cnt = sm.cnt[w];
-    for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = wbase + j * 64u + lane;
-        if (e >= n) break;  // (whole tail steps only: e grows with j)
-        const Msg m = load_hdr(in, e);
-        uint32_t h, own, rf, act = ORL_NO_ACT;
-        uint32_t r = route_head(sm.P, m, excl != 0, h, own, rf);
-        const bool probe = r == kNeedProbe && probe8_key(sm.P, m);
-        if (probe) {
-            const uint32_t d = fmix32(h) >> 29;  // the table eighth of the probe start (dir_slot's top bits)
-            const uint32_t client = (uint32_t)(m.tcd >> 56) == ORL_CAT_CLIENT ? 1u : 0u;
-            const uint32_t rank = slice_rank(cnt, d);
-            r = pack_route(own, m.meta & 0xFFu, kSliceMark | (client << 3) | d, rf);
-            if (rank < kSliceWaveCap) recs[slice_region(d, t, w, ntiles) + rank] = make_uint2((uint32_t)m.n1, h);
-            else r = slice_tail(sm.P, r, slice_probe(sm.P, probe8, dmask, (uint32_t)m.n1, h), act);  // past the cap: here
-        } else {
-            if (r == kNeedProbe) r = route_tail(sm.P, m, h, own, rf, false, 0u, 0u, act, false);  // no 8-B key: a miss
-            else if (r == kNeedProbeCache) r = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
-        }
-        store_drop(route + e, r);
-        if (!probe || (r >> 16 & 0xF0u) != kSliceMark) store_drop(act_out + e, act);
-    }
-    if (lane < 8) counts[((size_t)t * kWaves + w) * 8u + lane] = min(cnt[lane], kSliceWaveCap);
-}
-
-__global__ __launch_bounds__(kRouteThreads) void k_probe_slice(const RouteParams* __restrict__ gp, const uint2* __restrict__ probe8,
-                                                               uint64_t dmask, const uint2* __restrict__ recs,
-                                                               const uint32_t* __restrict__ counts, uint32_t ntiles,
-                                                               uint32_t* __restrict__ out) {
-    __shared__ RouteParams P;
-    stage_params(&P, gp);
-    __syncthreads();
-    const uint32_t s = blockIdx.x & 7u, g = blockIdx.x >> 3, groups = gridDim.x >> 3;
-    const uint32_t per = (ntiles + groups - 1u) / groups;
-    const uint32_t t0 = min(g * per, ntiles), t1 = min(t0 + per, ntiles);
-    const uint32_t i = threadIdx.x;  // kSliceWaveCap == kRouteThreads: one record per thread and sub-region
-    for (uint32_t t = t0; t < t1; ++t) {
-        uint2 rec[kWaves];
-        uint32_t c[kWaves];
-#pragma unroll
-        for (uint32_t q = 0; q < kWaves; ++q) {
-            c[q] = counts[((size_t)t * kWaves + q) * 8u + s];
-            if (i < c[q]) rec[q] = recs[slice_region(s, t, q, ntiles) + i];
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kWaves; ++q)
-            if (i < c[q]) out[slice_region(s, t, q, ntiles) + i] = slice_probe(P, probe8, dmask, rec[q].x, rec[q].y);
-    }
-}
-static_assert(kSliceWaveCap == kRouteThreads, "k_probe_slice: one record per thread and (tile, wave) sub-region");
-
-template <int HB>
-struct GatherSmem {
-    RouteParams P;
-    uint32_t hist[HB ? (1u << HB) : 1u];
-    uint32_t cnt[kWaves][8];
-    uint32_t hot;
-};
-
-template <int HB>
-__global__ __launch_bounds__(kRouteThreads) void k_route_gather(const RouteParams* __restrict__ gp, uint32_t n,
-                                                                uint32_t* __restrict__ route, uint32_t* __restrict__ act_out,
-                                                                const uint32_t* __restrict__ res, uint32_t ntiles,
-                                                                uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift,
-                                                                const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows) {
-    __shared__ GatherSmem<HB> sm;
-    constexpr bool HIST = HB > 0;
-    stage_params(&sm.P, gp);
-    if (HIST)
-        for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
-    if (threadIdx.x < kWaves * 8) (&sm.cnt[0][0])[threadIdx.x] = 0;
-    if (threadIdx.x == 0) sm.hot = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t t = blockIdx.x;
-    const uint32_t wbase = t * kTile + w * (kItems * 64u);
-    const uint32_t n_act = sm.P.n_act;
-    const uint32_t hk = (HIST && hot_rows) ? hot_key_of(hot_words) : kNoHotKey;
-    uint32_t* cnt = sm.cnt[w];
-    uint32_t rw[kItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {  // all of the tile's route words in flight
-        const uint32_t e = wbase + j * 64u + lane;
-        rw[j] = e < n ? __builtin_nontemporal_load(route + e) : 0u;
-    }
-    uint32_t hot_mine = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t e = wbase + j * 64u + lane;
-        if (e >= n) continue;
-        uint32_t act;
-        if (((rw[j] >> 16) & 0xF0u) == kSliceMark) {  // marked: its outcome, at the rank k_route_slice gave it
-            const uint32_t d = (rw[j] >> 16) & 7u;
-            const uint32_t v = res[slice_region(d, t, w, ntiles) + slice_rank(cnt, d)];
-            store_drop(route + e, slice_tail(sm.P, rw[j], v, act));
-            store_drop(act_out + e, act);
-        } else {
-            act = HIST ? act_out[e] : 0u;  // finished by k_route_slice
-        }
-        if (HIST) {
-            const uint32_t k = bucket_key(act, n_act);
-            if (k == hk) ++hot_mine;
-            else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
-        }
-    }
-    if (HIST) {
-        if (hot_rows) wave_add_hot(&sm.hot, hot_mine);
-        __syncthreads();
-        store_count_row(tile_cnt + (size_t)blockIdx.x * bins, sm.hist, bins);
-        if (hot_rows && threadIdx.x == 0) hot_rows[blockIdx.x] = sm.hot;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
 // Device-wide exclusive scan of u32 (3 launches): per-block sums, one-block scan of the sums, and a
 // down-sweep that rescans each block's chunk with its prefix.  Chunk = 4096 elements per block.
 constexpr uint32_t kScanChunk = 4096;
@@ -1321,12 +1119,9 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
 
 // row_step: the pass reading the result reads only rows t % row_step == 0 (route tiles smaller than its tile), so
 // only those are written.
-// sup (OUT_NARROW's super-tile bases, else null): sup[d * nsup + k] = the base of row k * sup_step (the first MSD tile of
-// super-tile k), digit-major so level 2 reads one bucket's bases contiguously.
 __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ C, uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
-                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows,
-                                                   uint32_t* __restrict__ sup, uint32_t sup_step, uint32_t nsup) {
+                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
     if (hot_rows && blockIdx.y == gridDim.y - 1) {  // the hot column: chunk base + the exclusive prefix of its 64 rows
@@ -1360,7 +1155,6 @@ __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ 
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
             if (t + k < t1 && (t + k) % row_step == 0) M[(size_t)(t + k) * bins + d] = run;
-            if (sup && t + k < t1 && (t + k) % sup_step == 0) sup[(size_t)d * nsup + (t + k) / sup_step] = run;
             run += v[k];
         }
     }
@@ -1387,19 +1181,8 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      OUT_SOA8 / OUT_SOA16 (the MSD pass of the two-level path) write the index to `order` (an index array) and only
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
-enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3, IN_NARROW = 4 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_NARROW = 5 };  // LSD_PAIR: an LSD pass's pairs
-
-// Level-2 records of the two-level path (OUT_NARROW / IN_NARROW, round 4): ONE u32 per message instead of an 8-B {key,
-// index} pair — the key's low `lb` bits (the level-2 digit; the bucket is the high digit) and the index's low 16 bits.
-// The MSD pass writes a bucket's records in arrival order, super-tile after super-tile (kSupTile = 16 MSD tiles = 65536
-// messages), so the index's high bits are the super-tile, which level 2 recovers from the position: sup_base[b][k] =
-// where super-tile k's records of bucket b start (col_apply writes it beside the tile bases).  Half the bytes for the MSD
-// pass to write and for both level-2 kernels to read.
-constexpr uint32_t kSupShift = 16, kSupTile = 1u << kSupShift;
-__device__ __forceinline__ uint32_t narrow_rec(uint32_t key, uint32_t idx, uint32_t lb) {
-    return (key & ((1u << lb) - 1u)) | ((idx & (kSupTile - 1u)) << lb);
-}
+enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4 };  // LSD_PAIR: an LSD pass's pairs
 
 // Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
 // zero-degree publishers share an offset with the next one and are skipped).  Whole wave, same v in every lane: each
@@ -1506,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
-    constexpr bool HOTP = IN == IN_ACT && (OUT == OUT_PAIR || OUT == OUT_NARROW);
+    constexpr bool HOTP = IN == IN_ACT && OUT == OUT_PAIR;
     __shared__ PassSmem<BITS, ITEMS> sm;
     __shared__ uint32_t hotw[kWaves];
     const uint32_t rflags = rank_flags();
@@ -1604,8 +1387,6 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = kv;
-            } else if (OUT == OUT_NARROW) {
-                reinterpret_cast<uint32_t*>(pair_out)[g] = narrow_rec(k, kv.y, shift);
             } else if (OUT == OUT_SOA8) {
                 order_out[g] = kv.y;
                 reinterpret_cast<uint8_t*>(key_out)[g] = (uint8_t)(k & ((1u << shift) - 1u));
@@ -1958,13 +1739,10 @@ __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n
     }
 }
 
-// IN_NARROW: also the super-tile of each segment's first position, seg_sup[segment] (for k_seg_scatter), searched by wave 0
-// while the segment's records load.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
                                                    uint32_t seg, const uint32_t* __restrict__ bstart,
-                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist,
-                                                   const uint32_t* __restrict__ sup, uint32_t nsup, uint32_t* __restrict__ seg_sup) {
+                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist) {
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
     SegRange r;
@@ -1981,8 +1759,6 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
                 const uint32_t* ix = static_cast<const uint32_t*>(in);
                 key[j] = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[ec]
                                        : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[ec];
-            } else if (IN == IN_NARROW) {  // the record's low bits
-                key[j] = static_cast<const uint32_t*>(in)[ec] & (BL - 1u);
             } else {
                 uint32_t idx;
                 seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
@@ -1990,10 +1766,6 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
         }
         // a Zipf-hot key (most of a hot bucket's segments): its lanes add with one atomic per step (the same-address
         // lanes of an LDS atomic are serviced one by one); decided per wave from its first full step
-        if (IN == IN_NARROW && c0 == r.lo && threadIdx.x < 64u) {  // (the loads above are in flight meanwhile)
-            const uint32_t klo = wave_find_pub(sup + (size_t)r.bucket * nsup, nsup, r.lo);
-            if (threadIdx.x == 0) seg_sup[r.index] = klo;
-        }
         const uint32_t dh = c0 + 256u * kItems <= r.hi ? wave_hot_digit(key[0] & (BL - 1u)) : kNoHot;
         if (dh != kNoHot) {
 #pragma unroll
@@ -2196,38 +1968,6 @@ __global__ __launch_bounds__(256) void k_seg_carry(const uint32_t* __restrict__ 
     }
 }
 
-// IN_NARROW's index recovery in k_seg_scatter.  klo = the super-tile of the segment's first position (k_seg_count found it:
-// seg_sup); bs[t] = the base of super-tile klo + 1 + t while it is inside the round [c0, c1), then kBsNone: the bases a
-// round crosses, sorted.  A position's super-tile is klo + the number of bases <= it; each lane walks forward over bs as
-// its positions grow (64 a step: about one base per step at config 2).  A round that crosses more than kBsCap - 1 bases
-// (a sparse bucket) sets `wide`, and its positions search the bucket's bases in global memory instead.
-constexpr uint32_t kBsCap = kSegChunk, kBsNone = 0xFFFFFFFFu;
-
-// Every entry is written (kBsNone past the round), so bs is non-decreasing over its whole length and bs[kBsCap - 1] is
-// kBsNone: the searches and walks over it end.
-__device__ __forceinline__ bool load_bases(const uint32_t* __restrict__ srow, uint32_t nsup, uint32_t klo, uint32_t c1, uint32_t* bs) {
-    bool wide = false, past = false;
-    for (uint32_t t = threadIdx.x; t < kBsCap; t += 256u) {
-        const uint32_t k = klo + 1u + t;
-        uint32_t p = kBsNone;
-        if (!past && k < nsup) p = srow[k];
-        past |= p >= c1;
-        wide |= !past && t + 1u == kBsCap;
-        bs[t] = !past && t + 1u < kBsCap ? p : kBsNone;
-    }
-    return wide;
-}
-
-// The super-tile of position e, searched in the bucket's bases (the wide-round fallback).
-__device__ __forceinline__ uint32_t sup_of(const uint32_t* __restrict__ srow, uint32_t nsup, uint32_t klo, uint32_t e) {
-    uint32_t lo = klo, hi = nsup;  // last k in [klo, nsup) with srow[k] <= e
-    while (hi - lo > 1u) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (srow[mid] <= e) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
 // One segment: LDS rounds of kSegChunk messages.  Each round ranks its messages with wave_rank (wave w owns
 // [w*1024, w*1024+1024) of the round, 16 steps of 64 lanes, so (round, wave, step, lane) order is arrival
 // order), turns the per-wave counts into round-local sorted starts, stages the indices in LDS in sorted
@@ -2252,9 +1992,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, const uint32_t* __restrict__ seg_carry,
-                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order,
-                                                     const uint32_t* __restrict__ sup, uint32_t nsup,
-                                                     const uint32_t* __restrict__ seg_sup) {
+                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order) {
     constexpr uint32_t BL = 1u << LB;
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
@@ -2280,48 +2018,13 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t e = wbase + j * 64u + lane;
-            const uint32_t ec = e < r.hi ? e : r.hi - 1;
-            if (IN == IN_NARROW) {  // the digit, and the index's low 16 bits (its super-tile below)
-                const uint32_t rec = static_cast<const uint32_t*>(in)[ec];
-                key[j] = rec & (BL - 1u);
-                idx[j] = rec >> LB;
-            } else {
-                seg_load<IN>(in, n_total, ec, n_act, key[j], idx[j]);
-            }
-        }
-        uint32_t klo = 0;
-        bool wide = false;
-        const uint32_t* srow = sup + (size_t)r.bucket * nsup;
-        uint32_t* bs = reinterpret_cast<uint32_t*>(&sm.stage[0]);  // free until this round's staging writes
-        if (IN == IN_NARROW) {
-            klo = seg_sup[r.index];
-            if (c0 != r.lo) klo = sup_of(srow, nsup, klo, c0);  // (a segment is one round: seg_elems() == kSegChunk)
-            wide = load_bases(srow, nsup, klo, min(c0 + kSegChunk, r.hi), bs);
+            seg_load<IN>(in, n_total, e < r.hi ? e : r.hi - 1, n_act, key[j], idx[j]);
         }
         for (uint32_t k = threadIdx.x; k < BL / 2u; k += 256) {
 #pragma unroll
             for (uint32_t ww = 0; ww < kWaves; ++ww) sm.cnt[ww][k] = 0;
         }
-        if (IN == IN_NARROW) wide = __syncthreads_or(wide);
-        else __syncthreads();
-        if (IN == IN_NARROW) {  // each lane's positions grow by 64 a step: walk the bases forward
-            uint32_t lo = 0, hi = kBsCap - 1u;  // the count of bases <= wbase (uniform binary search; bs[kBsCap - 1] = none)
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (bs[mid] <= wbase) lo = mid + 1u; else hi = mid;
-            }
-            uint32_t kc = lo;
-#pragma unroll
-            for (uint32_t j = 0; j < kItems; ++j) {
-                const uint32_t e = wbase + j * 64u + lane;
-                if (!wide) {
-                    while (kc < kBsCap - 1u && bs[kc] <= e) ++kc;  // (bs[kBsCap - 1] = none: the bound is belt and braces)
-                    idx[j] |= (klo + kc) << kSupShift;
-                } else if (e < r.hi) {
-                    idx[j] |= sup_of(srow, nsup, klo, e) << kSupShift;
-                }
-            }
-        }
+        __syncthreads();
         {
             uint32_t dg[kItems];
 #pragma unroll
@@ -3850,7 +3553,6 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
             case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kMsdItems); break;
             case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8, kMsdItems); break;
             case OUT_SOA16: ORL_RP(IN_ACT, OUT_SOA16, kMsdItems); break;
-            case OUT_NARROW: ORL_RP(IN_ACT, OUT_NARROW, kMsdItems); break;
             case OUT_LSD_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kItems); break;
             default: ORL_RP(IN_ACT, OUT_FINAL, kItems); break;
         }
@@ -3879,7 +3581,7 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
 // Column scan of a tile-major [ntiles][bins] u16 count matrix C (s.tile_cnt) into per-(tile, bin) u32 output bases M.
 // row_step: the reading pass uses rows t % row_step == 0 only.
 void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
-              uint32_t* hot_rows = nullptr, uint32_t* sup = nullptr, uint32_t sup_step = 1, uint32_t nsup = 0) {
+              uint32_t* hot_rows = nullptr) {
     const uint16_t* C = s.tile_cnt;
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
@@ -3888,7 +3590,7 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, co
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
                        ntiles);
     hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
-                       hot_rows, sup, sup_step, nsup);
+                       hot_rows);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -3908,15 +3610,13 @@ template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
                      uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     const uint32_t nb = n_act + 2;
-    const uint32_t nsup = ceil_div(n, kSupTile);  // IN_NARROW: super-tiles of the batch (sup_base row length)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
-                                     s.seg_hist, s.sup_base, nsup, s.seg_sup)
+                                     s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
-                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order, s.sup_base, nsup, \
-                                         s.seg_sup)
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
-    if (in == IN_NARROW) ORL_SC(IN_NARROW); else if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
+    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
     else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     // the segment scan: k_seg_scan when every bucket has <= kScanRows segments, else the chunked kernels (k_seg_plan
     // sets the flag on the device; the path not taken returns at once)
@@ -3932,7 +3632,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
         scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
     else
         scan_inplace(d_offsets, nb, s, st);
-    if (in == IN_NARROW) ORL_SS(IN_NARROW); else if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR);
+    if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR);
     else if (in == IN_SOA8) ORL_SS(IN_SOA8); else ORL_SS(IN_SOA16);
     if (hot)  // the hot run's copy (this batch's key: hw)
         hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0, st,
@@ -3962,16 +3662,6 @@ bool stage4_soa() {
         return e && e[0] == '1';
     }();
     return soa;
-}
-
-// Two-level path's level-2 records: ORL_STAGE4_PAIRS=1 keeps the round-3 8-B {key, index} pairs (A/B against the narrow
-// 4-B records, OUT_NARROW).
-bool stage4_pairs() {
-    static const bool on = [] {
-        const char* e = getenv("ORL_STAGE4_PAIRS");
-        return e && e[0] == '1';
-    }();
-    return on;
 }
 
 // LSD path's bucket offsets: ORL_OFFSETS_SUFMIN=1 keeps the round-2 five-launch form (A/B).
@@ -4023,24 +3713,21 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t seg = seg_elems(n);
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
-        const bool narrow = bp.hb > 0 && !stage4_soa() && !stage4_pairs() && s.sup_base && s.seg_sup;
         if (bp.hb > 0) {
-            // narrow level-2 records: col_apply also writes each super-tile's base (rows 16 MSD tiles apart)
-            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr, narrow ? s.sup_base : nullptr,
-                     row_step0 * (kSupTile / (kRouteThreads * kMsdItems)), ceil_div(n, kSupTile));
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr);
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
-                launch_pass(host_rm(s.device), bp.hb, IN_ACT, narrow ? OUT_NARROW : OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
+                launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, s.pairs_a, nullptr, nullptr, st, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr,
                             hot ? s.sorted_keys : nullptr);
             }
             kin = s.pairs_a;
         }
         hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
-        const int lin = bp.hb == 0 ? IN_ACT : narrow ? IN_NARROW : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
+        const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
         launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
         return (int)hipGetLastError();
     }
@@ -4086,12 +3773,6 @@ uint32_t env_gap_cap() {
     return (uint32_t)std::min<long>(std::max<long>(v, 0), (long)kGapCap);
 }
 
-uint64_t env_slice_min() {
-    const char* off = getenv("ORL_NO_SLICE");
-    if (off && off[0] == '1') return ~0ull;
-    const char* e = getenv("ORL_SLICE_MIN");
-    return e ? (uint64_t)atoll(e) : (1ull << 20);
-}
 
 int env_fan_u() {
     const char* e = getenv("ORL_FAN_U");
@@ -4162,12 +3843,9 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
         if (buckets) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
         return 0;
     }
-    uint32_t items = route_items(n, max_route_items(n_act));
+    const uint32_t items = route_items(n, max_route_items(n_act));
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
     const RouteHist rh = route_hist(n_act);
-    if (dv.probe8 && fmt == 32 && s.slice_recs && n >= s.slice_min && dv.mask + 1 >= 8 && dv.mask + 1 <= kSliceMaxSlots &&
-        n <= s.max_batch)
-        items = kItems;  // the sliced route's tiles: 4096 messages, one histogram row each
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     const bool hist = buckets && rh.on;
     const bool pick = hist && hot_path_on(n, n_act, s);
@@ -4180,23 +3858,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
                                               dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
                                               (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
-    const bool sliced = dv.probe8 && fmt == 32 && s.slice_recs && n >= s.slice_min && dv.mask + 1 >= 8 &&
-                        dv.mask + 1 <= kSliceMaxSlots && n <= s.max_batch;
-    if (sliced) {  // config 2: the probes grouped by table eighth, each XCD probing its own from L2
-        ++s.sliced_batches;
-        const uint32_t ntiles = ceil_div(n, kTile);
-        const uint2* p8 = static_cast<const uint2*>(dv.probe8);
-        hipLaunchKernelGGL(k_route_slice, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, dv.cache, dv.cmask, p8,
-                           static_cast<const orl_msg_hdr*>(d_in), (uint32_t)n, excl, d_route, d_act, s.slice_recs, s.slice_cnt, ntiles);
-        hipLaunchKernelGGL(k_probe_slice, dim3(kSliceProbeGroups * 8), dim3(kRouteThreads), 0, st, d_params, p8, dv.mask, s.slice_recs,
-                           s.slice_cnt, ntiles, s.slice_res);
-        if (hist)
-            hipLaunchKernelGGL(k_route_gather<kMaxDigitBits>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, (uint32_t)n, d_route,
-                               d_act, s.slice_res, ntiles, th, bins, shift, hw, hr);
-        else
-            hipLaunchKernelGGL(k_route_gather<0>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, (uint32_t)n, d_route, d_act,
-                               s.slice_res, ntiles, th, bins, shift, hw, hr);
-    } else if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
+    if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
 #define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
                                             dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \

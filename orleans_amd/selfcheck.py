@@ -46,11 +46,15 @@ def fetch_node_result(t, eng, res, n_act: int, stream=None) -> dict:
         return x
 
     n = res.n_hosted
+    t.cuda.synchronize()  # torch's pending work is done before its freed blocks are filled from another stream
     out = {"route": grab(res.route, n), "act": grab(res.act, n), "order": grab(res.order, n),
            "offsets": grab(res.offsets, n_act + 2)}
+    raws = [(grab(p, cnt * w // 4), w) for p, cnt, w in res.segments]
+    # the copies run on the library's stream (stream None / torch's default stream handle 0 = the context's own stream):
+    # every torch op below runs on torch's stream, so wait for the copies before the first one reads them
+    t.cuda.synchronize()
     parts = []
-    for p, cnt, w in res.segments:
-        raw = grab(p, cnt * w // 4)
+    for raw, w in raws:
         if w == 8:
             parts.append(raw.view(-1, 2)[:, 0].to(t.int64) & _M32)
         elif w == 16:
@@ -101,11 +105,16 @@ def check_routes(t, route, act, n1, owner_t, handle_t, all_registered: bool, own
         return [f"{n1.numel()} hosted records for {route.numel()} route words"]
     if not route.numel():
         return errs
+
+    def where(bad):  # count, first and last hosted index of a failing property
+        i = t.nonzero(bad).flatten()
+        return f"{i.numel()} messages (hosted index {int(i[0])} .. {int(i[-1])})"
+
     if bool((n1 >= owner_t.numel()).any()):
-        return ["a hosted record names a grain outside the population"]
+        return [f"a hosted record names a grain outside the population: {where(n1 >= owner_t.numel())}"]
     own = owner_t[n1]
     if not t.equal(route & 0xFF, own):
-        errs.append(f"owner silo differs from the grain's ring owner for {int(((route & 0xFF) != own).sum())} messages")
+        errs.append(f"owner silo differs from the grain's ring owner for {where((route & 0xFF) != own)}")
     if owner_rank_t is not None and bool((owner_rank_t[own] != rank).any()):
         errs.append("a hosted message is owned by another rank")
     if all_registered:
@@ -114,7 +123,7 @@ def check_routes(t, route, act, n1, owner_t, handle_t, all_registered: bool, own
         if bool((((route >> 16) & 0xFF) != L.ST_HIT).any()):
             errs.append(f"{int((((route >> 16) & 0xFF) != L.ST_HIT).sum())} registered targets did not hit the directory")
         if not t.equal(act, handle_t[n1]):
-            errs.append(f"activation handle differs from the registered one for {int((act != handle_t[n1]).sum())} messages")
+            errs.append(f"activation handle differs from the registered one for {where(act != handle_t[n1])}")
     return errs
 
 

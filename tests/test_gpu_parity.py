@@ -166,63 +166,6 @@ def test_membership_variants_vs_oracle(torch):
         eng.close()
 
 
-@pytest.mark.parametrize("policy", [L.POLICY_PREFER_LOCAL, L.POLICY_HASH_SPREAD])
-def test_sliced_route_vs_oracle(torch, monkeypatch, policy):
-    """The XCD-sliced route (k_route_slice / k_probe_slice / k_route_gather: directory probes grouped by table eighth),
-    forced on small batches (ORL_SLICE_MIN=0), bit-exact vs the oracle: non-running / non-functional silos (IsValidSilo
-    turns hits into placements), both placement policies, 10 % unregistered targets, system-target, address-complete and
-    Guid (N0 != 0: no 8-B key) messages, a Zipf batch whose hot grain overflows a wave's slice region (those messages are
-    probed by k_route_slice itself), client-category grains (a miss is CLIENT_UNREGISTERED), ragged batch ends, and stage 4
-    after it.  Reference: LocalGrainDirectory.cs:439-497, GrainDirectoryPartition.cs:326-344, PlacementDirectorsManager.cs:70-91."""
-    monkeypatch.setenv("ORL_SLICE_MIN", "0")
-    running = [1, 0, 1, 1, 0, 1, 1, 1]
-    functional = [1, 1, 0, 1, 1, 1, 0, 1]
-    cl, eng, o = _random_setup(20_000, 30_000, running=running, functional=functional, policy=policy)
-    assert eng.query(L.Q_PROBE_FORM) == 8
-    rng = np.random.default_rng(policy + 3)
-    uni = W.uniform_messages(cl, 22_000, 300_001, seed=31)
-    k = rng.random(len(uni))
-    uni["tcd"][k < 0.02] = (np.uint64(L.CAT_SYSTEM_TARGET) << np.uint64(56)) | np.uint64(12)
-    uni["flags"][(k >= 0.02) & (k < 0.04)] = L.HDR_ADDRESS_COMPLETE
-    uni["target_silo"][(k >= 0.02) & (k < 0.04)] = 3
-    uni["n0"][(k >= 0.04) & (k < 0.05)] = 0x1234  # Guid-shaped: no 8-B probe key
-    batches = [uni, W.zipf_messages(cl, 22_000, 400_003, s_exp=1.6, seed=7), uni[:4097], uni[:1]]  # Zipf 1.6: ~44 % hot
-    for m in batches:
-        before = eng.query(L.Q_SLICED_BATCHES)
-        for opts in (0, L.OPT_EXCLUDE_IF_STOPPING):
-            res = eng.address_messages(m, opts)
-            r, a = o.route(m, opts)
-            np.testing.assert_array_equal(res.route, r)
-            np.testing.assert_array_equal(res.act, a)
-            order, off = o.bucket(a, 30_000)
-            np.testing.assert_array_equal(res.order, order)
-            np.testing.assert_array_equal(res.offsets, off)
-        assert eng.query(L.Q_SLICED_BATCHES) > before
-    eng.close()
-    # client-category grains: the 8-B table holds client keys, so their misses go through the sliced tail
-    from orleans_amd.engine import grain_keys_from_longs
-    eng = GrainDirectoryEngine(n_act=5000, dir_capacity=5000, max_batch=1 << 20, device=0, placement=policy)
-    eng.set_silos(8, seed=0)
-    o = cpu_ref.Oracle(8, seed=0, policy=policy)
-    for s_ in range(8):
-        eng.add_server(s_, int(cl.hashes[s_]))
-        o.add_server(s_, int(cl.hashes[s_]))
-    keys = grain_keys_from_longs(cl.type_code, np.arange(4000, dtype=np.int64), category=L.CAT_CLIENT)
-    acts = np.arange(4000, dtype=np.uint32)
-    silos = (np.arange(4000) % 8).astype(np.uint8)
-    eng.register_single_activation(keys, acts, silos)
-    o.register(keys, acts, silos)
-    assert eng.query(L.Q_PROBE_FORM) == 8
-    m = W.uniform_messages(cl, 5000, 100_000, seed=9)
-    m["tcd"] = keys["tcd"][0]
-    res = eng.address_messages(m)
-    r, a = o.route(m)
-    np.testing.assert_array_equal(res.route, r)
-    np.testing.assert_array_equal(res.act, a)
-    assert (decode_route(r).status == L.ST_CLIENT_UNREGISTERED).any() and eng.query(L.Q_SLICED_BATCHES) > 0
-    eng.close()
-
-
 def test_single_silo_ring_and_empty_ring(torch):
     for n_ring in (0, 1):
         eng = GrainDirectoryEngine(n_act=64, dir_capacity=64, device=0)
