@@ -189,15 +189,18 @@ def timed_steps(args, torch, dist, world, step, sync):
 
 
 def read_traffic(path, msgs_per_launch, world):
+    """The route kernel's measured HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, scripts/make_traffic_json.py)
+    and where they come from, for the workload they were measured on only (config 2, all grains registered, one GPU, the
+    same messages per launch); (None, None) otherwise."""
     if world != 1 or not os.path.exists(path):
-        return None
+        return None, None
     try:
         tj = json.load(open(path))
         if tj.get("msgs_per_launch") == msgs_per_launch:
-            return tj.get("hbm_bytes_per_launch")
+            return tj.get("hbm_bytes_per_launch"), f"{os.path.relpath(path, ROOT)}: {tj.get('method', 'rocprofv3 --pmc')}"
     except Exception:
-        return None
-    return None
+        return None, None
+    return None, None
 
 
 # ---- the node's correctness evidence (checker: after the timed steps, outside timing) ------------------------
@@ -365,7 +368,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     achieved = kbytes * per_launch_msgs / (route_ms * 1e-3) / 1e9
     log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms x {launches}, bucketing {bucket_ms:.3f} ms, "
         f"call {total_ms:.3f} ms over {nb} launches")
-    traffic = read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 else None
+    traffic, traffic_src = (read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 and not args.unregistered
+                            else (None, None))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf, 1.0 - args.unregistered)
@@ -414,7 +418,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
                    "parallelism": f"directory sharded by ring range over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": "k_route (stages 1-3)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "bytes_per_msg": kbytes, "msgs_per_launch": per_launch_msgs, "avg_launch_ms": route_ms},
+                     "traffic_source": traffic_src, "bytes_per_msg": kbytes, "msgs_per_launch": per_launch_msgs, "avg_launch_ms": route_ms},
         "pipeline": {"bytes_per_msg": PIPELINE_BYTES_PER_MSG, "route_kernel_ms": route_ms,
                      "bucketing_ms": bucket_ms, "call_ms": total_ms,
                      "algorithmic_GBs": PIPELINE_BYTES_PER_MSG * value / world / 1e9,
