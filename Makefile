@@ -33,8 +33,16 @@ build/orl_node.o: orleans_amd/csrc/orl_node.cpp $(HDR)
 oracle:
 	$(MAKE) -C oracle
 
+# A/B build of the kernels with extra defines, for the lab scripts only (LAB_LIB=lab/liborleans_route_<NAME>.so):
+#   make lab NAME=fan512 DEFS=-DORL_FAN_LDS=512
+lab: build/wire_codec.o build/orl_api.o build/orl_node.o
+	@mkdir -p build lab
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o build/route_kernels_$(NAME).o orleans_amd/csrc/route_kernels.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o lab/liborleans_route_$(NAME).so build/route_kernels_$(NAME).o build/wire_codec.o \
+		build/orl_api.o build/orl_node.o $(LIBS)
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean lab

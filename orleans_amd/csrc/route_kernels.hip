@@ -2073,7 +2073,10 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
-constexpr uint32_t kFanLds = 1024;  // publishers staged per tile; beyond that fall back to global search
+#ifndef ORL_FAN_LDS
+#define ORL_FAN_LDS 1024
+#endif
+constexpr uint32_t kFanLds = ORL_FAN_LDS;  // publishers staged per tile; beyond that fall back to global search
 
 template <int HB>
 struct FanSmem {

@@ -13,6 +13,9 @@ from orleans_amd.engine import GrainDirectoryEngine, grain_keys_from_longs  # no
 
 
 def main(reps=10):
+    import os
+    if os.environ.get("LAB_LIB"):  # A/B: an experimental build of the library (make lab)
+        L.LIB_PATH = os.path.abspath(os.environ["LAB_LIB"])
     n_acc, n_pub = 10_000_000, 1_000_000
     cl = W.default_cluster()
     csr_off, csr_tgt = W.powerlaw_csr(n_acc)
