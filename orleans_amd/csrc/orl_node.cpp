@@ -111,6 +111,7 @@ struct orl_node {
     bool broken = false;      // a bounded wait expired or RCCL failed: the communicator was aborted
     int stall_chunk = -1;     // ORL_NODE_INJECT_STALL: the all-gather of this chunk waits on h_stall (fault injection)
     uint32_t* h_stall = nullptr;  // pinned, device-visible release word of the injected stall
+    int lb_fail = 0;          // ORL_NODE_INJECT_LB_FAIL: 1 = the hop-2 partition's, 2 = a re-partition's look-back "gives up"
     uint32_t n_act = 0, nr = 1, me = 0;
     uint64_t chunk_cap = 0;
     ncclComm_t comm = nullptr;
@@ -544,6 +545,8 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
         const long v = atol(t);
         if (v > 0) nd->timeout_ms = (uint32_t)std::min<long>(v, 0x7FFFFFFF);
     }
+    if (const char* lf = getenv("ORL_NODE_INJECT_LB_FAIL"))  // fault injection on this rank only: "hop2" or "rewrite"
+        nd->lb_fail = std::strcmp(lf, "hop2") == 0 ? 1 : std::strcmp(lf, "rewrite") == 0 ? 2 : 0;
     if (const char* st = getenv("ORL_NODE_INJECT_STALL")) {  // fault injection: "<chunk>" (hop 1) or "hop2"
         nd->stall_chunk = std::strcmp(st, "hop2") == 0 ? -2 : atoi(st);
         if (!ok(hipHostMalloc((void**)&nd->h_stall, 64, hipHostMallocMapped | hipHostMallocCoherent))) return bail(ORL_E_NOMEM);
@@ -691,12 +694,16 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         }
         if (pr) return nfail(nd, pr, "chunk %u: node plan failed", c);
         const uint32_t width = plan.width;
+        // The rewrite runs on sp behind chunk c + 1's partition and the host waits for both (not just the
+        // rewrite): the partitions share the context's look-back state (ticket counter, epoch-tagged granules), which
+        // only stream order keeps consistent, so the rewrite cannot overtake the partition queued before it.
         if (plan.rewrite) {  // some rank's records do not fit the form: every rank rewrites the chunk in `width`
             if (int r = partition(c, width)) return r;
             // the rewrite's look-back is checked on this rank only (its counts are those already all-gathered)
             uint32_t st = 0;
             if (int r = wait_bounded(nd, nd->sp, "re-partition", (int)c, nullptr)) return r;
             NODE_HIP(nd, hipMemcpy(&st, head + 8, 4, hipMemcpyDeviceToHost));
+            if (nd->lb_fail == 2) st |= ORL_PART_LOOKBACK_FAILED;
             if (st & ORL_PART_LOOKBACK_FAILED) {  // only this rank sees it: abort, so the peers fail now, not at their deadline
                 break_node(nd);
                 return nfail(nd, ORL_E_DEVICE, "chunk %u: the %u-byte re-partition's look-back gave up (device fault); "
@@ -789,6 +796,7 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             uint32_t lb_err = 0;
             if (int r = wait_bounded(nd, nd->sr, "hop-2 partition", -2, nullptr)) return r;
             NODE_HIP(nd, hipMemcpy(&lb_err, d_ferr, 4, hipMemcpyDeviceToHost));
+            if (nd->lb_fail == 1) lb_err = 1;
             if (lb_err) {  // only this rank sees it: abort, so the peers fail now, not at their deadline
                 break_node(nd);
                 return nfail(nd, ORL_E_DEVICE, "hop-2 partition look-back gave up (device fault); communicator aborted");
