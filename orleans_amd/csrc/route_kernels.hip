@@ -2154,7 +2154,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     if (in_lds && fan) fan_stage(poff32, pstart, p_lo, span, sm.poff, sm.pdelta);
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
-    const bool use16 = PW != 0 && (probe_bad == nullptr || *probe_bad == 0u);
+    // PW 8: the 8-B probe table (host-built only: no flag); PW 16: the 16-B one unless its device rebuild flagged a key
+    const bool useq = PW == 8 || (PW == 16 && (probe_bad == nullptr || *probe_bad == 0u));
     // U messages per thread and step, in three phases so their dependent loads overlap: (A) publisher search + CSR
     // target load, (B) stages 1-2 + the first probe, (C) probe chain, stage-3 tail, outputs.  U = 1 is one message at a
     // time (the round-2 loop).
@@ -2222,15 +2223,24 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                 m[q].meta = (uint32_t)pub_silo[pub[q]] | (2u << 8);  // Application message from the publisher's silo
                 m[q].aux = 0;
             }
-            if (!use16) {
+            if (!useq) {
                 r[q] = kFanSlow;
                 continue;
             }
             r[q] = route_head(sm.P, m[q], excl != 0, h[q], own[q], rf[q]);
             if (r[q] == kNeedProbe) {
-                mk[q] = probe_type(sm.P, m[q]);
                 slot[q] = dir_slot(h[q], mask);
-                if (mk[q] != kNoType) sa[q] = reinterpret_cast<const u32x4*>(probe)[slot[q]];
+                if (PW == 8) {
+                    mk[q] = probe8_key(sm.P, m[q]) ? 0u : kNoType;
+                    if (mk[q] != kNoType) {
+                        const uint2 v = reinterpret_cast<const uint2*>(probe)[slot[q]];
+                        sa[q].x = v.x;
+                        sa[q].y = v.y;
+                    }
+                } else {
+                    mk[q] = probe_type(sm.P, m[q]);
+                    if (mk[q] != kNoType) sa[q] = reinterpret_cast<const u32x4*>(probe)[slot[q]];
+                }
             }
         }
 #pragma unroll
@@ -2242,7 +2252,15 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
             } else if (rr == kNeedProbe) {
                 uint32_t fact = 0, fsilo = 0;
                 int st = 1;
-                if (mk[q] != kNoType) {
+                if (mk[q] != kNoType && PW == 8) {
+                    const uint32_t kb = (uint32_t)m[q].n1;
+                    st = probe_slot8(make_uint2(sa[q].x, sa[q].y), kb, fact, fsilo);
+                    uint64_t sl = slot[q];
+                    for (uint64_t step = 0; st == 2 && step < mask; ++step) {
+                        sl = (sl + 1) & mask;
+                        st = probe_slot8(reinterpret_cast<const uint2*>(probe)[sl], kb, fact, fsilo);
+                    }
+                } else if (mk[q] != kNoType) {
                     st = probe_slot16(sa[q], m[q].n1, mk[q], fact, fsilo);
                     uint64_t sl = slot[q];
                     for (uint64_t step = 0; st == 2 && step < mask; ++step) {
@@ -3523,6 +3541,14 @@ uint32_t route_min_wgs() {  // ORL_ROUTE_MIN_WG: A/B knob for the small-batch gr
     return v;
 }
 
+bool fan_probe16() {  // ORL_FAN_PROBE16=1: the fan-out kernel probes the 16-B table even when the 8-B one exists (A/B)
+    static const bool on = [] {
+        const char* e = getenv("ORL_FAN_PROBE16");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 uint32_t fan_min_wgs() {  // ORL_FAN_MIN_WG: the fan-out kernel's (default 4096)
     static const uint32_t v = [] {
         const char* e = getenv("ORL_FAN_MIN_WG");
@@ -3937,14 +3963,16 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
 
-// the fan-out kernel takes the 16-B form: the 8-B form measured slower here (config 4: 0.266 vs 0.247 ms)
-// U messages per thread and step (s.fan_u: ORL_FAN_U at context creation, A/B)
+// the fan-out kernel's probe table: the 8-B form when the context has one (round 4), else the 16-B form (ORL_FAN_PROBE16=1
+// forces the 16-B form: A/B); U messages per thread and step (s.fan_u: ORL_FAN_U at context creation, A/B)
 #define ORL_FAN(H, TH, BINS, SHIFT) do { const int u_ = s.fan_u;                                                          \
-        if (dv.probe) { if (u_ == 4) ORL_FAN_(H, 16, 4, TH, BINS, SHIFT); else if (u_ == 2) ORL_FAN_(H, 16, 2, TH, BINS, SHIFT); \
-                        else ORL_FAN_(H, 16, 1, TH, BINS, SHIFT); }                                                          \
-        else ORL_FAN_(H, 0, 1, TH, BINS, SHIFT); } while (0)
-#define ORL_FAN_(H, Q, U, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q, U>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
-                                                       dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
+        if (dv.probe8 && !fan_probe16()) ORL_FAN_(H, 8, 1, static_cast<const ProbeSlot*>(dv.probe8), nullptr, TH, BINS, SHIFT);        \
+        else if (dv.probe) { if (u_ == 4) ORL_FAN_(H, 16, 4, dv.probe, dv.probe_bad, TH, BINS, SHIFT);                            \
+                             else if (u_ == 2) ORL_FAN_(H, 16, 2, dv.probe, dv.probe_bad, TH, BINS, SHIFT);                       \
+                             else ORL_FAN_(H, 16, 1, dv.probe, dv.probe_bad, TH, BINS, SHIFT); }                                  \
+        else ORL_FAN_(H, 0, 1, dv.probe, dv.probe_bad, TH, BINS, SHIFT); } while (0)
+#define ORL_FAN_(H, Q, U, PROBE, PBAD, TH, BINS, SHIFT) hipLaunchKernelGGL((k_fanout_route<H, Q, U>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
+                                                       dv.mask, dv.cache, dv.cmask, PROBE, PBAD, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
                                                        follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
                                                        excl, d_route, d_act, TH, BINS, \
                                                        SHIFT, items, fblk)

@@ -42,6 +42,13 @@ def main(reps=10):
                               total=total)
         torch.cuda.synchronize()
         print(f"{name}: {reps} calls, {total} emitted messages each", flush=True)
+    # the two-kernel form for comparison: expand to 32-B headers (k_fanout_expand), then the stream route kernel over them
+    hdr = torch.empty((total, 8), dtype=torch.int32, device=dv)
+    for _ in range(reps):
+        eng.fanout_expand_device(d_off, d_tgt, None, tcd, d_pubs, d_ps, n_pub, poff, hdr, total, stream=st, total=total)
+        eng.address_messages_device(hdr, total, route, act, order, offs, stream=st)
+    torch.cuda.synchronize()
+    print(f"expand + route: {reps} calls", flush=True)
     eng.close()
 
 
