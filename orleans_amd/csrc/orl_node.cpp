@@ -115,8 +115,10 @@ struct orl_node {
     uint32_t n_act = 0, nr = 1, me = 0;
     uint64_t chunk_cap = 0;
     ncclComm_t comm = nullptr;
+    ncclComm_t comm_h = nullptr;  // the counts all-gathers' communicator (ncclCommSplit of comm), on stream sh (round 4)
     std::shared_ptr<LocalGroup> group;
     hipStream_t sp = nullptr, sx = nullptr, sr = nullptr;
+    hipStream_t sh = nullptr;  // the counts all-gathers: chunk c's runs while chunk c-1's data exchange is still on sx
     hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
     hipEvent_t ev_part[2] = {nullptr, nullptr};  // the slot's partition (and heads) are complete
     hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
@@ -184,6 +186,10 @@ int nfail(orl_node* nd, int code, const char* fmt, ...) {
 // release an injected stall, and let the streams drain (bounded).  The node stays broken.
 void break_node(orl_node* nd) {
     nd->broken = true;
+    if (nd->comm_h) {
+        (void)ncclCommAbort(nd->comm_h);
+        nd->comm_h = nullptr;
+    }
     if (nd->comm) {
         (void)ncclCommAbort(nd->comm);
         nd->comm = nullptr;
@@ -228,6 +234,8 @@ int wait_bounded(orl_node* nd, hipStream_t s, const char* what, int chunk, const
         ++polls;  // (both transports: the sleep backoff below applies to LOCAL rank threads too)
         if (nd->comm && (polls & 63u) == 0u) {
             if (ncclCommGetAsyncError(nd->comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) break;
+            if (nd->comm_h && ncclCommGetAsyncError(nd->comm_h, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
+                break;
             ar = ncclSuccess;
         }
         if (std::chrono::steady_clock::now() > deadline) break;
@@ -258,23 +266,28 @@ int wait_bounded(orl_node* nd, hipStream_t s, const char* what, int chunk, const
 
 // All-gather of kHeadWords u64 per rank from device `d_src` (ready once `ready` has fired) into nd->h_heads.
 int allgather_heads(orl_node* nd, const uint64_t* d_src, hipEvent_t ready, int chunk) {
-    NODE_HIP(nd, hipStreamWaitEvent(nd->sx, ready, 0));
+    // Stream sh (and with RCCL the split communicator comm_h): chunk c's counts travel while chunk c-1's data exchange
+    // still runs on sx, instead of queueing behind it.  Without the split communicator (ncclCommSplit
+    // failed) the all-gathers share comm and sx, as before.
+    const bool split = nd->sh && (!nd->comm || nd->comm_h);
+    hipStream_t hs = split ? nd->sh : nd->sx;
+    NODE_HIP(nd, hipStreamWaitEvent(hs, ready, 0));
     if (nd->comm) {
-        NODE_NCCL(nd, ncclAllGather(d_src, nd->d_heads, kHeadWords, ncclUint64, nd->comm, nd->sx));
-        NODE_HIP(nd, hipMemcpyAsync(nd->h_heads, nd->d_heads, (size_t)nd->nr * kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
+        NODE_NCCL(nd, ncclAllGather(d_src, nd->d_heads, kHeadWords, ncclUint64, split ? nd->comm_h : nd->comm, hs));
+        NODE_HIP(nd, hipMemcpyAsync(nd->h_heads, nd->d_heads, (size_t)nd->nr * kHeadWords * 8, hipMemcpyDeviceToHost, hs));
         if (chunk == nd->stall_chunk && nd->h_stall) {
-            int e = launch_node_stall(nd->h_stall, nd->sx);
+            int e = launch_node_stall(nd->h_stall, hs);
             if (e) return nfail(nd, ORL_E_DEVICE, "stall injection: %s", hipGetErrorString((hipError_t)e));
         }
-        return wait_bounded(nd, nd->sx, chunk >= 0 ? "node counts all-gather" : "node hop-2 counts all-gather", chunk, d_src);
+        return wait_bounded(nd, hs, chunk >= 0 ? "node counts all-gather" : "node hop-2 counts all-gather", chunk, d_src);
     }
     LocalGroup& g = *nd->group;
-    NODE_HIP(nd, hipMemcpyAsync(nd->h_heads + (size_t)nd->me * kHeadWords, d_src, kHeadWords * 8, hipMemcpyDeviceToHost, nd->sx));
+    NODE_HIP(nd, hipMemcpyAsync(nd->h_heads + (size_t)nd->me * kHeadWords, d_src, kHeadWords * 8, hipMemcpyDeviceToHost, hs));
     if (chunk == nd->stall_chunk && nd->h_stall) {
-        int e = launch_node_stall(nd->h_stall, nd->sx);
+        int e = launch_node_stall(nd->h_stall, hs);
         if (e) return nfail(nd, ORL_E_DEVICE, "stall injection: %s", hipGetErrorString((hipError_t)e));
     }
-    if (int r = wait_bounded(nd, nd->sx, "node all-gather", chunk, d_src)) return r;
+    if (int r = wait_bounded(nd, hs, "node all-gather", chunk, d_src)) return r;
     {
         std::lock_guard<std::mutex> lk(g.mu);
         std::memcpy(g.words[nd->me].data(), nd->h_heads + (size_t)nd->me * kHeadWords, kHeadWords * 8);
@@ -361,8 +374,10 @@ void free_node(orl_node* nd) {
     if (nd->h_stall) (void)hipHostFree(nd->h_stall);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : {nd->sp, nd->sx, nd->sr})
+    for (hipStream_t s : {nd->sp, nd->sx, nd->sr, nd->sh})
         if (s) (void)hipStreamDestroy(s);
+    if (nd->comm_h) (void)ncclCommDestroy(nd->comm_h);
+    nd->comm_h = nullptr;
     if (nd->comm) (void)ncclCommDestroy(nd->comm);
     nd->comm = nullptr;
 }
@@ -519,6 +534,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipStreamCreateWithFlags(&nd->sp, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
+    ok(hipStreamCreateWithFlags(&nd->sh, hipStreamNonBlocking));
     for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_slot[0], &nd->ev_slot[1]})
         ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     const uint64_t nr = cfg->nranks, mr = cfg->max_recv;
@@ -561,6 +577,9 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
         }
         int cc = 0;
         nd->stats.comm_count = ncclCommCount(nd->comm, &cc) == ncclSuccess ? (uint32_t)cc : 0u;
+        // the counts all-gathers' own communicator (collective: every rank splits here, in the same order); on failure
+        // the all-gathers share comm and its stream
+        if (ncclCommSplit(nd->comm, 0, (int)cfg->rank, &nd->comm_h, nullptr) != ncclSuccess) nd->comm_h = nullptr;
     } else {
         nd->group = join_group(cfg->group_id, cfg->nranks);
         if (!nd->group) return bail(ORL_E_INVALID);
