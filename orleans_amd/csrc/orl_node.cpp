@@ -120,6 +120,7 @@ struct orl_node {
     hipStream_t sp = nullptr, sx = nullptr, sr = nullptr;
     hipStream_t sh = nullptr;  // the counts all-gathers: chunk c's runs while chunk c-1's data exchange is still on sx
     hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
+    hipEvent_t ev_h = nullptr;  // the hop-2 host-rank counts are written (on sh)
     hipEvent_t ev_part[2] = {nullptr, nullptr};  // the slot's partition (and heads) are complete
     hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
     bool last_forward = false;  // the previous batch forwarded messages (hop 2): stage 4 then waits for the counts
@@ -372,7 +373,7 @@ void free_node(orl_node* nd) {
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     if (nd->h_form) (void)hipHostFree(nd->h_form);
     if (nd->h_stall) (void)hipHostFree(nd->h_stall);
-    for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_slot[0], nd->ev_slot[1]})
+    for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_h, nd->ev_slot[0], nd->ev_slot[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr, nd->sh})
         if (s) (void)hipStreamDestroy(s);
@@ -535,7 +536,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sh, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_slot[0], &nd->ev_slot[1]})
+    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_h, &nd->ev_slot[0], &nd->ev_slot[1]})
         ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     const uint64_t nr = cfg->nranks, mr = cfg->max_recv;
     ok(hipMalloc((void**)&nd->d_ros, 256));
@@ -757,18 +758,21 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         owned_bytes += got * width;
     }
     // ---- hop 2: does any rank host activations of messages another rank owns? -----------------------------------
-    {
-        int e = launch_host_rank_count(nd->d_route, owned, nd->d_ros, me, nd->d_hcount, nd->sr);
-        if (e) return nfail(nd, ORL_E_DEVICE, "host rank count launch: %s", hipGetErrorString((hipError_t)e));
-        NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
-    }
     // Stage 4 over the owned set is what every batch without forwarding ends with: when the previous batch forwarded
-    // nothing, launch it now, so it runs while the hop-2 counts travel (the all-gather waits on ev_r, recorded before
-    // it).  If some rank does forward after all, the owned-set result is unused (the hop-2 path writes its own
-    // buffers) and costs one stage 4.
+    // nothing, launch it now on sr, right after the last chunk's route, so it runs while the hop-2 counts are taken and
+    // travel.  The host-rank counts read the routed words on the all-gathers' stream sh (round 4: off the stage-4
+    // stream, so stage 4 does not wait for them).  If some rank does forward after all, the owned-set result is unused
+    // (the hop-2 path writes its own buffers) and costs one stage 4.
+    NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));  // every chunk is routed
     const bool spec = !nd->last_forward;
     if (spec) NODE_CTX(nd, orl_bucket_device(nd->ctx, nd->d_act, owned, nd->d_order, nd->d_off, nd->sr));
-    if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_r, -2)) return r;
+    {
+        NODE_HIP(nd, hipStreamWaitEvent(nd->sh, nd->ev_r, 0));
+        int e = launch_host_rank_count(nd->d_route, owned, nd->d_ros, me, nd->d_hcount, nd->sh);
+        if (e) return nfail(nd, ORL_E_DEVICE, "host rank count launch: %s", hipGetErrorString((hipError_t)e));
+        NODE_HIP(nd, hipEventRecord(nd->ev_h, nd->sh));
+    }
+    if (int r = allgather_heads(nd, nd->d_hcount, nd->ev_h, -2)) return r;
     const uint64_t* H = nd->h_heads;
     orl_node_hop2_plan h2;
     const int pr = orl_node_plan_hop2(H, nr, me, owned, width_mask, nd->cfg.max_recv, &h2);
