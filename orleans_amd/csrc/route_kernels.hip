@@ -1739,53 +1739,118 @@ __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n
     }
 }
 
+// Chunk [c0, min(c0 + kSegChunk, hi))'s low-digit keys, kItems per thread (clamped loads: all in flight at once).
+template <int IN>
+__device__ __forceinline__ void seg_keys(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t c0, uint32_t hi,
+                                         uint32_t (&key)[kItems]) {
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t e = c0 + j * 256u + threadIdx.x;
+        const uint32_t ec = e < hi ? e : hi - 1;
+        if (IN == IN_SOA8 || IN == IN_SOA16) {  // the digit array only
+            const uint32_t* ix = static_cast<const uint32_t*>(in);
+            key[j] = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[ec]
+                                   : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[ec];
+        } else {
+            uint32_t idx;
+            seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
+        }
+    }
+}
+
+// That chunk's keys added to hist (LDS).  A Zipf-hot key (most of a hot bucket's segments): its lanes add with one
+// atomic per step (the same-address lanes of an LDS atomic are serviced one by one); decided per wave from its first
+// full step.
+template <int LB>
+__device__ __forceinline__ void seg_add(const uint32_t (&key)[kItems], uint32_t c0, uint32_t hi, uint32_t* hist) {
+    constexpr uint32_t BL = 1u << LB;
+    const uint32_t dh = c0 + 256u * kItems <= hi ? wave_hot_digit(key[0] & (BL - 1u)) : kNoHot;
+    if (dh != kNoHot) {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+            if (c0 + j * 256u + threadIdx.x < hi) {
+                const uint32_t d = key[j] & (BL - 1u);
+                const uint64_t m = __ballot(d == dh);
+                if (d != dh) atomicAdd(&hist[d], 1u);
+                else if ((m & lanes_below()) == 0) atomicAdd(&hist[dh], (uint32_t)__popcll(m));
+            }
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+            if (c0 + j * 256u + threadIdx.x < hi) atomicAdd(&hist[key[j] & (BL - 1u)], 1u);
+    }
+}
+
+// One segment [lo, hi)'s low-digit counts added to hist (LDS, zeroed by the caller).
+template <int LB, int IN>
+__device__ __forceinline__ void seg_count_range(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t lo,
+                                                uint32_t hi, uint32_t* hist) {
+    for (uint32_t c0 = lo; c0 < hi; c0 += kSegChunk) {
+        uint32_t key[kItems];
+        seg_keys<IN>(in, n_total, n_act, c0, hi, key);
+        seg_add<LB>(key, c0, hi, hist);
+    }
+}
+
+// skew_only: the fused count + scan (k_seg_count_scan) serves plans without a skewed bucket, so this kernel exits
+// unless k_seg_plan flagged one.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
                                                    uint32_t seg, const uint32_t* __restrict__ bstart,
-                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist) {
+                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist,
+                                                   uint32_t skew_only) {
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
+    if (skew_only && !sstart[kSkewSlot]) return;
     SegRange r;
     if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
     __syncthreads();
-    for (uint32_t c0 = r.lo; c0 < r.hi; c0 += kSegChunk) {
-        uint32_t key[kItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) {  // clamped loads: all 16 in flight at once
-            const uint32_t e = c0 + j * 256u + threadIdx.x;
-            const uint32_t ec = e < r.hi ? e : r.hi - 1;
-            if (IN == IN_SOA8 || IN == IN_SOA16) {  // the digit array only
-                const uint32_t* ix = static_cast<const uint32_t*>(in);
-                key[j] = IN == IN_SOA8 ? (uint32_t) reinterpret_cast<const uint8_t*>(ix + n_total)[ec]
-                                       : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[ec];
-            } else {
-                uint32_t idx;
-                seg_load<IN>(in, n_total, ec, n_act, key[j], idx);
-            }
-        }
-        // a Zipf-hot key (most of a hot bucket's segments): its lanes add with one atomic per step (the same-address
-        // lanes of an LDS atomic are serviced one by one); decided per wave from its first full step
-        const uint32_t dh = c0 + 256u * kItems <= r.hi ? wave_hot_digit(key[0] & (BL - 1u)) : kNoHot;
-        if (dh != kNoHot) {
-#pragma unroll
-            for (uint32_t j = 0; j < kItems; ++j) {
-                if (c0 + j * 256u + threadIdx.x < r.hi) {
-                    const uint32_t d = key[j] & (BL - 1u);
-                    const uint64_t m = __ballot(d == dh);
-                    if (d != dh) atomicAdd(&hist[d], 1u);
-                    else if ((m & lanes_below()) == 0) atomicAdd(&hist[dh], (uint32_t)__popcll(m));
-                }
-            }
-        } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kItems; ++j)
-                if (c0 + j * 256u + threadIdx.x < r.hi) atomicAdd(&hist[key[j] & (BL - 1u)], 1u);
-        }
-    }
+    seg_count_range<LB, IN>(in, n_total, n_act, r.lo, r.hi, hist);
     __syncthreads();
     uint32_t* row = seg_hist + (size_t)r.index * BL;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
+}
+
+// Count and scan fused, for plans without a skewed bucket (every bucket <= kScanRows segments; round 4): one workgroup
+// per bucket counts its segments in order and writes each segment's row as the exclusive prefix of the bucket's earlier
+// segments (what k_seg_scan makes of k_seg_count's rows), then the bucket's per-key totals to counts — no second pass
+// over the segment rows.  Exits when k_seg_plan flagged a skewed bucket (the two-kernel form runs instead).
+template <int LB, int IN>
+__global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
+                                                        uint32_t nbk, uint32_t nb, uint32_t seg,
+                                                        const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                                        uint32_t* __restrict__ seg_hist, uint32_t* __restrict__ counts) {
+    static_assert(kSegChunk == 256u * kItems, "a segment is one chunk of kItems keys per thread");
+    constexpr uint32_t BL = 1u << LB;
+    __shared__ uint32_t hist[BL];  // running counts of the bucket's segments so far
+    if (sstart[kSkewSlot]) return;
+    const uint32_t b = blockIdx.x;
+    if (b >= nbk) return;
+    if (b == 0 && threadIdx.x == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
+        for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
+    const uint32_t j0 = sstart[b], j1 = sstart[b + 1], base = bstart[b], end = bstart[b + 1];
+    for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
+    uint32_t kc[kItems];
+    if (j0 < j1) seg_keys<IN>(in, n_total, n_act, base, min(base + seg, end), kc);
+    __syncthreads();
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t lo = base + (j - j0) * seg, hi = min(lo + seg, end);
+        uint32_t kn[kItems];  // the next segment's keys load while this one is counted
+        if (j + 1 < j1) seg_keys<IN>(in, n_total, n_act, hi, min(hi + seg, end), kn);
+        uint32_t* row = seg_hist + (size_t)j * BL;  // segment j's base inside the bucket: the counts before it
+        for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
+        __syncthreads();
+        seg_add<LB>(kc, lo, hi, hist);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kItems; ++q) kc[q] = kn[q];
+    }
+    for (uint32_t l = threadIdx.x; l < BL; l += 256) {
+        const uint32_t key = (b << LB) | l;
+        if (key < nb) counts[key] = hist[l];
+    }
 }
 
 // Per bucket b and low digit l (every bucket has <= kScanRows segments): the segment rows become exclusive prefixes
@@ -1898,10 +1963,10 @@ __device__ __forceinline__ void seg_csum_chunk(uint32_t* __restrict__ seg_hist, 
 template <int LB>
 __global__ __launch_bounds__(256) void k_seg_scan(uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ sstart,
                                                   uint32_t nbk, uint32_t nb, uint32_t* __restrict__ carry,
-                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts) {
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ counts, uint32_t fused) {
     const uint32_t l = blockIdx.y * 256u + threadIdx.x;
-    if (!sstart[kSkewSlot]) {
-        if (blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l);
+    if (!sstart[kSkewSlot]) {  // (fused: k_seg_count_scan already wrote the prefixed rows and the counts)
+        if (!fused && blockIdx.x < nbk) seg_scan_bucket<LB>(seg_hist, sstart, nbk, nb, counts, blockIdx.x, l);
     } else {
         seg_csum_chunk<LB>(seg_hist, sstart, nbk, nb, carry, meta, counts, blockIdx.x, l);
     }
@@ -3635,16 +3700,27 @@ RouteHist route_hist(uint32_t n_act) {
     return {true, 1u << bp.lsd.bits[0], (uint32_t)bp.lsd.shift[0]};
 }
 
+bool seg_fused();
+
 template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
                      uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     const uint32_t nb = n_act + 2;
+    // the fused count + scan (one workgroup per bucket) serves every plan without a skewed bucket; the two-kernel form
+    // (k_seg_count, then k_seg_scan's chunked scan) the skewed ones — the device flag picks, both are launched
+    const uint32_t fz = seg_fused() ? 1u : 0u;
+#define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(nbk), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
+                                     s.sstart, s.seg_hist, d_offsets)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
-                                     s.seg_hist)
+                                     s.seg_hist, fz)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
                                          s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
+    if (fz) {
+        if (in == IN_ACT) ORL_SF(IN_ACT); else if (in == IN_PAIR) ORL_SF(IN_PAIR);
+        else if (in == IN_SOA8) ORL_SF(IN_SOA8); else ORL_SF(IN_SOA16);
+    }
     if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
     else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     // the segment scan: k_seg_scan when every bucket has <= kScanRows segments, else the chunked kernels (k_seg_plan
@@ -3652,7 +3728,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     const uint32_t cb = ceil_div(1u << LB, 256);
     const uint32_t nch = ceil_div(grid, kScanRows);
     hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb, s.seg_carry,
-                       s.seg_meta, d_offsets);
+                       s.seg_meta, d_offsets, fz);
     hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
                        d_offsets);
     const uint32_t* hw = hot_cur(s);
@@ -3666,6 +3742,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     if (hot)  // the hot run's copy (this batch's key: hw)
         hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0, st,
                            hw, s.col_tot + nbk, n, n_act + 1, s.sorted_keys, d_offsets, d_order);
+#undef ORL_SF
 #undef ORL_SC
 #undef ORL_SS
 #undef ORL_SS3
@@ -3691,6 +3768,16 @@ bool stage4_soa() {
         return e && e[0] == '1';
     }();
     return soa;
+}
+
+// Level 2's count and segment scan fused for plans without a skewed bucket (k_seg_count_scan); ORL_SEG_FUSED=0 keeps the
+// two-kernel form for every plan (A/B).
+bool seg_fused() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_SEG_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // LSD path's bucket offsets: ORL_OFFSETS_SUFMIN=1 keeps the round-2 five-launch form (A/B).
