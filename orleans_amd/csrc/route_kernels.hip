@@ -1703,11 +1703,8 @@ struct SegRange {
     uint32_t bucket, index, lo, hi;
 };
 
-__device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                             uint32_t nbk, uint32_t seg, SegRange& r) {
-    const uint32_t nseg = sstart[nbk];
-    if (blockIdx.x >= nseg) return false;
-    const uint32_t j = xcd_tile(blockIdx.x, nseg);
+__device__ __forceinline__ void seg_range(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart, uint32_t nbk,
+                                          uint32_t seg, uint32_t j, SegRange& r) {
     uint32_t lo = 0, hi = nbk + 1;  // bucket = upper_bound(sstart, j) - 1 (skips empty buckets)
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1717,6 +1714,13 @@ __device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart
     r.index = j;
     r.lo = bstart[r.bucket] + (j - sstart[r.bucket]) * seg;
     r.hi = min(r.lo + seg, bstart[r.bucket + 1]);
+}
+
+__device__ __forceinline__ bool seg_of_block(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
+                                             uint32_t nbk, uint32_t seg, SegRange& r) {
+    const uint32_t nseg = sstart[nbk];
+    if (blockIdx.x >= nseg) return false;
+    seg_range(bstart, sstart, nbk, seg, xcd_tile(blockIdx.x, nseg), r);
     return true;
 }
 
@@ -1793,16 +1797,12 @@ __device__ __forceinline__ void seg_count_range(const void* __restrict__ in, uin
     }
 }
 
-// skew_only: the fused count + scan (k_seg_count_scan) serves plans without a skewed bucket, so this kernel exits
-// unless k_seg_plan flagged one.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, uint32_t n_total, uint32_t n_act, uint32_t nbk,
                                                    uint32_t seg, const uint32_t* __restrict__ bstart,
-                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist,
-                                                   uint32_t skew_only) {
+                                                   const uint32_t* __restrict__ sstart, uint32_t* __restrict__ seg_hist) {
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];
-    if (skew_only && !sstart[kSkewSlot]) return;
     SegRange r;
     if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
     for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
@@ -1816,7 +1816,8 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
 // Count and scan fused, for plans without a skewed bucket (every bucket <= kScanRows segments; round 4): one workgroup
 // per bucket counts its segments in order and writes each segment's row as the exclusive prefix of the bucket's earlier
 // segments (what k_seg_scan makes of k_seg_count's rows), then the bucket's per-key totals to counts — no second pass
-// over the segment rows.  Exits when k_seg_plan flagged a skewed bucket (the two-kernel form runs instead).
+// over the segment rows.  When k_seg_plan flagged a skewed bucket it does k_seg_count's work instead (every segment's own
+// counts, the workgroups striding over the segments) and k_seg_scan's chunked form scans them.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
                                                         uint32_t nbk, uint32_t nb, uint32_t seg,
@@ -1825,7 +1826,21 @@ __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__
     static_assert(kSegChunk == 256u * kItems, "a segment is one chunk of kItems keys per thread");
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];  // running counts of the bucket's segments so far
-    if (sstart[kSkewSlot]) return;
+    if (sstart[kSkewSlot]) {
+        const uint32_t nseg = sstart[nbk];
+        for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
+            SegRange r;
+            seg_range(bstart, sstart, nbk, seg, j, r);
+            for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
+            __syncthreads();
+            seg_count_range<LB, IN>(in, n_total, n_act, r.lo, r.hi, hist);
+            __syncthreads();
+            uint32_t* row = seg_hist + (size_t)j * BL;
+            for (uint32_t l = threadIdx.x; l < BL; l += 256) row[l] = hist[l];
+            __syncthreads();
+        }
+        return;
+    }
     const uint32_t b = blockIdx.x;
     if (b >= nbk) return;
     if (b == 0 && threadIdx.x == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
@@ -3706,13 +3721,14 @@ template <int LB>
 void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32_t nbk, uint32_t seg, uint32_t grid,
                      uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick) {
     const uint32_t nb = n_act + 2;
-    // the fused count + scan (one workgroup per bucket) serves every plan without a skewed bucket; the two-kernel form
-    // (k_seg_count, then k_seg_scan's chunked scan) the skewed ones — the device flag picks, both are launched
+    // the fused count + scan (one workgroup per bucket) serves every plan; with a skewed bucket (device flag) it only
+    // counts the segments and k_seg_scan's chunked form scans them.  ORL_SEG_FUSED=0: k_seg_count + k_seg_scan always.
     const uint32_t fz = seg_fused() ? 1u : 0u;
-#define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(nbk), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
+    const uint32_t fgrid = std::max(nbk, std::min(grid, 1024u));  // >= 1024 workgroups for a skewed plan's segment count
+#define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(fgrid), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
                                      s.sstart, s.seg_hist, d_offsets)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
-                                     s.seg_hist, fz)
+                                     s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
                                          s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
@@ -3720,9 +3736,10 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     if (fz) {
         if (in == IN_ACT) ORL_SF(IN_ACT); else if (in == IN_PAIR) ORL_SF(IN_PAIR);
         else if (in == IN_SOA8) ORL_SF(IN_SOA8); else ORL_SF(IN_SOA16);
+    } else {
+        if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
+        else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     }
-    if (in == IN_ACT) ORL_SC(IN_ACT); else if (in == IN_PAIR) ORL_SC(IN_PAIR);
-    else if (in == IN_SOA8) ORL_SC(IN_SOA8); else ORL_SC(IN_SOA16);
     // the segment scan: k_seg_scan when every bucket has <= kScanRows segments, else the chunked kernels (k_seg_plan
     // sets the flag on the device; the path not taken returns at once)
     const uint32_t cb = ceil_div(1u << LB, 256);
