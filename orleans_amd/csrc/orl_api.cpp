@@ -835,9 +835,10 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.hot_bmax, (((uint64_t)cfg->n_act + 2 + 4095) / 4096 + 1) * 8)) != hipSuccess)
             return bail(e, "hipMalloc(hot_bmax)");
         if ((e = hipMalloc((void**)&c->s.hot_rows, (rows + (rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(hot_rows)");
-        if ((e = hipHostMalloc((void**)&c->s.hot_host, 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&c->s.hot_host, 8, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e, "hipHostMalloc(hot_host)");
-        *c->s.hot_host = 0xFFFFFFFFu;
+        c->s.hot_host[0] = 0xFFFFFFFFu;
+        c->s.hot_host[1] = 1u;  // stage 4's skew hint: the first plan launches the chunked segment scan too
         if ((e = hipHostGetDevicePointer((void**)&c->s.hot_host_dev, c->s.hot_host, 0)) != hipSuccess)
             return bail(e, "hipHostGetDevicePointer(hot_host)");
         if ((e = hipMalloc((void**)&c->st_off, ((size_t)cfg->n_act + 2) * 4)) != hipSuccess) return bail(e, "hipMalloc(offsets)");

@@ -261,7 +261,8 @@ struct Scratch {
     mutable uint32_t hot_parity = 0;   // flips with every batch that picks (scan_offsets_pick)
     unsigned long long* hot_bmax = nullptr;  // [offset-scan chunks] per-chunk max of (count << 32 | key)
     uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
-    uint32_t* hot_host = nullptr;      // mapped pinned host word: the last pick's key (the launcher's hint)
+    uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key, [1] the last level-2 plan's skew
+                                       // flag (k_seg_count_scan) — the launcher's hints
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
     uint32_t* fan_blk = nullptr;   // [fan_blk_cap] fan-out: the publisher of every 256th emitted message (k_scan_down WIDEN)

@@ -1818,15 +1818,23 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
 // segments (what k_seg_scan makes of k_seg_count's rows), then the bucket's per-key totals to counts — no second pass
 // over the segment rows.  When k_seg_plan flagged a skewed bucket it does k_seg_count's work instead (every segment's own
 // counts, the workgroups striding over the segments) and k_seg_scan's chunked form scans them.
+// solo: the launcher, hinted by the last plan's flag (skew_host, mirrored here), launched no segment scan after this
+// kernel, so every plan takes the one-pass form — a skewed bucket is then counted by one workgroup, slowly but
+// correctly, and the next launch has the hint.  direct (solo, no hot-key path): the bucket's per-key totals are scanned
+// here and written as the final bucket offsets (bstart[b] + the exclusive prefix inside the bucket), so no offsets scan
+// follows either.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
                                                         uint32_t nbk, uint32_t nb, uint32_t seg,
                                                         const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
-                                                        uint32_t* __restrict__ seg_hist, uint32_t* __restrict__ counts) {
+                                                        uint32_t* __restrict__ seg_hist, uint32_t* __restrict__ counts,
+                                                        uint32_t solo, uint32_t direct, uint32_t* __restrict__ skew_host) {
     static_assert(kSegChunk == 256u * kItems, "a segment is one chunk of kItems keys per thread");
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];  // running counts of the bucket's segments so far
-    if (sstart[kSkewSlot]) {
+    __shared__ uint32_t wsum[kWaves];
+    if (skew_host && blockIdx.x == 0 && threadIdx.x == 0) skew_host[0] = sstart[kSkewSlot];  // the next launch's hint
+    if (sstart[kSkewSlot] && !solo) {
         const uint32_t nseg = sstart[nbk];
         for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
             SegRange r;
@@ -1844,7 +1852,7 @@ __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__
     const uint32_t b = blockIdx.x;
     if (b >= nbk) return;
     if (b == 0 && threadIdx.x == 0)  // keys past the last bucket (at most one: n_act + 1 when n_act + 1 == 2^bits) hold nothing
-        for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = 0;
+        for (uint32_t k = nbk << LB; k < nb; ++k) counts[k] = direct ? bstart[nbk] : 0u;
     const uint32_t j0 = sstart[b], j1 = sstart[b + 1], base = bstart[b], end = bstart[b + 1];
     for (uint32_t l = threadIdx.x; l < BL; l += 256) hist[l] = 0;
     uint32_t kc[kItems];
@@ -1862,9 +1870,28 @@ __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__
 #pragma unroll
         for (uint32_t q = 0; q < kItems; ++q) kc[q] = kn[q];
     }
-    for (uint32_t l = threadIdx.x; l < BL; l += 256) {
-        const uint32_t key = (b << LB) | l;
-        if (key < nb) counts[key] = hist[l];
+    if (!direct) {
+        for (uint32_t l = threadIdx.x; l < BL; l += 256) {
+            const uint32_t key = (b << LB) | l;
+            if (key < nb) counts[key] = hist[l];
+        }
+        return;
+    }
+    constexpr uint32_t PER = BL >= 256u ? BL / 256u : 1u;  // thread t scans digits [t * PER, t * PER + PER)
+    const uint32_t l0 = threadIdx.x * PER;
+    uint32_t v[PER], acc = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        v[q] = l0 + q < BL ? hist[l0 + q] : 0u;
+        acc += v[q];
+    }
+    uint32_t total;
+    uint32_t run = base + block_excl_scan(acc, wsum, total);
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t l = l0 + q, key = (b << LB) | l;
+        if (l < BL && key < nb) counts[key] = run;
+        run += v[q];
     }
 }
 
@@ -2072,7 +2099,8 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, const uint32_t* __restrict__ seg_carry,
-                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order) {
+                                                     const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order,
+                                                     uint32_t solo) {
     constexpr uint32_t BL = 1u << LB;
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
@@ -2084,7 +2112,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
     const uint32_t* hrow = seg_hist + (size_t)r.index * BL;
     // a hot bucket's segments (chunked segment scan): the carry-in of the chunk whose first bucket this segment is in
     const uint32_t ch = r.index / kScanRows;
-    const uint32_t cin_on = (sstart[kSkewSlot] && (seg_meta[ch] & kMetaBucket) == r.bucket) ? 1u : 0u;
+    const uint32_t cin_on = (!solo && sstart[kSkewSlot] && (seg_meta[ch] & kMetaBucket) == r.bucket) ? 1u : 0u;
     const uint32_t* cin_row = seg_carry + (cin_on ? (size_t)ch * BL : 0);
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
@@ -3724,13 +3752,18 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     // the fused count + scan (one workgroup per bucket) serves every plan; with a skewed bucket (device flag) it only
     // counts the segments and k_seg_scan's chunked form scans them.  ORL_SEG_FUSED=0: k_seg_count + k_seg_scan always.
     const uint32_t fz = seg_fused() ? 1u : 0u;
+    // solo: the last plan had no skewed bucket, so no segment scan is launched (the hint can be stale: k_seg_count_scan
+    // then counts a skewed bucket in one workgroup); direct: nor an offsets scan (not with the hot-key path)
+    const uint32_t solo = fz && s.hot_host && !__atomic_load_n(s.hot_host + 1, __ATOMIC_ACQUIRE) ? 1u : 0u;
+    const uint32_t direct = solo && !hot && !pick ? 1u : 0u;
+    uint32_t* skew_host = s.hot_host_dev ? s.hot_host_dev + 1 : nullptr;
     const uint32_t fgrid = std::max(nbk, std::min(grid, 1024u));  // >= 1024 workgroups for a skewed plan's segment count
 #define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(fgrid), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
-                                     s.sstart, s.seg_hist, d_offsets)
+                                     s.sstart, s.seg_hist, d_offsets, solo, direct, skew_host)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
-                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order)
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order, solo)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
     if (fz) {
@@ -3744,15 +3777,17 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     // sets the flag on the device; the path not taken returns at once)
     const uint32_t cb = ceil_div(1u << LB, 256);
     const uint32_t nch = ceil_div(grid, kScanRows);
-    hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb, s.seg_carry,
-                       s.seg_meta, d_offsets, fz);
-    hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta, s.seg_carry,
-                       d_offsets);
+    if (!solo) {
+        hipLaunchKernelGGL((k_seg_scan<LB>), dim3(std::max(nbk, nch), cb), dim3(256), 0, st, s.seg_hist, s.sstart, nbk, nb,
+                           s.seg_carry, s.seg_meta, d_offsets, fz);
+        hipLaunchKernelGGL((k_seg_carry<LB>), dim3(ceil_div(1u << LB, 16)), dim3(256), 0, st, s.sstart, nbk, nb, s.seg_meta,
+                           s.seg_carry, d_offsets);
+    }
     const uint32_t* hw = hot_cur(s);
     if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
     if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
         scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
-    else
+    else if (!direct)
         scan_inplace(d_offsets, nb, s, st);
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR);
     else if (in == IN_SOA8) ORL_SS(IN_SOA8); else ORL_SS(IN_SOA16);

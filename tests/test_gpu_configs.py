@@ -654,6 +654,37 @@ def test_stage4_rank_modes_vs_oracle(torch, n_act):
     eng.close()
 
 
+@pytest.mark.parametrize("n_act", [5000, 1_000_000])
+def test_stage4_skew_hint_vs_oracle(torch, n_act):
+    """Level 2's launch form follows the last plan's skew flag (a mapped host word, k_seg_count_scan): after a plan
+    without a skewed bucket no segment scan (and, below the hot-key path's batch size, no offsets scan) is launched, so
+    a skewed batch arriving then is counted by one workgroup per bucket and must still be exact; the next batch takes the
+    chunked form again.  Every batch of the sequence is bit-exact vs the oracle's stable bucketing
+    (ActivationData.cs:483-514)."""
+    cl = W.default_cluster()
+    n_grains = 50_000
+    keys, uni, owner, reg = W.grain_population(cl, n_grains)
+    acts = (np.arange(n_grains, dtype=np.uint64) * np.uint64(2654435761) % np.uint64(n_act)).astype(np.uint32)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 21, device=0)
+    W.setup_engine(eng, cl)
+    eng.register_single_activation(keys, acts, owner)
+    o = _oracle_for(cl, keys, acts, owner)
+    uni_b = W.uniform_messages(cl, n_grains + 500, 600_000, seed=11)
+    one = W.uniform_messages(cl, n_grains, 600_000, seed=12)
+    one["n1"] = 9  # one activation: a bucket of ~147 segments (> 64: the skewed plan)
+    big = W.uniform_messages(cl, n_grains, 1_200_000, seed=13)
+    big["n1"][: 900_000] = 9  # >= 2^20 messages (the hot-key path's pick: counts, then the offsets scan) and skewed
+    # hint after each: 0, then solo + direct on a skewed batch, then the chunked form, then solo on a big skewed batch
+    for m in (uni_b, one, one, uni_b, uni_b, big, big, uni_b):
+        res = eng.address_messages(m)
+        r, a = o.route(m)
+        np.testing.assert_array_equal(res.act, a)
+        order, off = o.bucket(a, n_act)
+        np.testing.assert_array_equal(res.offsets, off)
+        np.testing.assert_array_equal(res.order, order)
+    eng.close()
+
+
 @pytest.mark.parametrize("n_act", [1_000_000, 2_000_000])
 def test_stage4_hot_key_path_vs_oracle(torch, n_act):
     """Stage 4's hot-key path (route_kernels.hip kNoHotKey): a batch of >= 2^20 messages picks its most frequent key when
