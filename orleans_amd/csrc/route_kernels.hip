@@ -1117,13 +1117,26 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
     }
 }
 
+template <uint32_t NT>
+__device__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
+                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart, uint32_t (*wsum)[16]);
+
 // row_step: the pass reading the result reads only rows t % row_step == 0 (route tiles smaller than its tile), so
 // only those are written.
+// plan_bstart (the two-level stage 4 with an MSD pass): one more grid column does k_seg_plan's work over the column
+// totals T — the segment plan is ready before the MSD pass, one launch fewer (round 4).
 __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ C, uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
-                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows) {
+                                                   uint32_t row_step, uint32_t* __restrict__ hot_rows, uint32_t plan_n,
+                                                   uint32_t plan_seg, uint32_t* __restrict__ plan_bstart,
+                                                   uint32_t* __restrict__ plan_sstart) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
+    __shared__ uint32_t pw[3][16];
+    if (plan_bstart && blockIdx.x == gridDim.x - 1) {
+        if (blockIdx.y == 0) seg_plan_body<256>(T, bins, plan_n, plan_seg, plan_bstart, plan_sstart, pw);
+        return;
+    }
     if (hot_rows && blockIdx.y == gridDim.y - 1) {  // the hot column: chunk base + the exclusive prefix of its 64 rows
         if (threadIdx.x >= 64) return;
         const uint32_t t = blockIdx.x * kScanRows + threadIdx.x;
@@ -1637,9 +1650,8 @@ __global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ off
 constexpr uint32_t kSkewSlot = 4097;
 
 template <uint32_t NT>
-__device__ __forceinline__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
-                                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart,
-                                              uint32_t (*wsum)[16]) {
+__device__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk, uint32_t n, uint32_t seg,
+                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ sstart, uint32_t (*wsum)[16]) {
     constexpr uint32_t Q = 4096 / NT, NW = NT / 64;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     uint32_t c[Q], p[Q], cs = 0, ps = 0, pmax = 0;
@@ -3717,8 +3729,10 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
 
 // Column scan of a tile-major [ntiles][bins] u16 count matrix C (s.tile_cnt) into per-(tile, bin) u32 output bases M.
 // row_step: the reading pass uses rows t % row_step == 0 only.
+// plan_n > 0: the two-level plan's MSD columns — the apply kernel also writes the segment plan (k_seg_plan's work) for
+// plan_n messages in segments of plan_seg.
 void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
-              uint32_t* hot_rows = nullptr) {
+              uint32_t* hot_rows = nullptr, uint32_t plan_n = 0, uint32_t plan_seg = 0) {
     const uint16_t* C = s.tile_cnt;
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
@@ -3726,8 +3740,9 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, co
     hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, C, ntiles, bins, s.col_sums, hot_rows);
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
                        ntiles);
-    hipLaunchKernelGGL(k_col_apply, dim3(nch, cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot, row_step,
-                       hot_rows);
+    const bool plan = plan_n > 0;
+    hipLaunchKernelGGL(k_col_apply, dim3(nch + (plan ? 1u : 0u), cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot,
+                       row_step, hot_rows, plan_n, plan_seg, plan ? s.bstart : nullptr, plan ? s.sstart : nullptr);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -3882,7 +3897,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr);
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr, n, seg);  // + the segment plan
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
@@ -3894,7 +3909,8 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
             }
             kin = s.pairs_a;
         }
-        hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, bp.hb > 0 ? s.col_tot : nullptr, nbk, n, seg, s.bstart, s.sstart);
+        if (bp.hb == 0)  // one bucket: {0, n} (with an MSD pass, k_col_apply wrote the plan)
+            hipLaunchKernelGGL(k_seg_plan, dim3(1), dim3(1024), 0, st, nullptr, nbk, n, seg, s.bstart, s.sstart);
         const int lin = bp.hb == 0 ? IN_ACT : !stage4_soa() ? IN_PAIR : bp.lb <= 8 ? IN_SOA8 : IN_SOA16;
         launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
         return (int)hipGetLastError();
