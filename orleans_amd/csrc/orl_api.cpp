@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.fan_blk);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -834,6 +834,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         // the hot column's rows, then its 64-row chunk sums
         if ((e = hipMalloc((void**)&c->s.hot_bmax, (((uint64_t)cfg->n_act + 2 + 4095) / 4096 + 1) * 8)) != hipSuccess)
             return bail(e, "hipMalloc(hot_bmax)");
+        if ((e = hipMalloc((void**)&c->s.pick_word, 8)) != hipSuccess) return bail(e, "hipMalloc(pick_word)");
+        if ((e = hipMemset(c->s.pick_word, 0, 8)) != hipSuccess) return bail(e, "hipMemset(pick_word)");
         if ((e = hipMalloc((void**)&c->s.hot_rows, (rows + (rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(hot_rows)");
         if ((e = hipHostMalloc((void**)&c->s.hot_host, 8, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e, "hipHostMalloc(hot_host)");

@@ -260,6 +260,7 @@ struct Scratch {
     uint32_t* hot = nullptr;  // stage 4's hot-key slots: [parity] the key in use (0xFFFFFFFF none), [parity ^ 1] the next pick
     mutable uint32_t hot_parity = 0;   // flips with every batch that picks (scan_offsets_pick)
     unsigned long long* hot_bmax = nullptr;  // [offset-scan chunks] per-chunk max of (count << 32 | key)
+    unsigned long long* pick_word = nullptr; // the fused level-2 pick's max of (count << 32 | key), zero between batches
     uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
     uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key, [1] the last level-2 plan's skew
                                        // flag (k_seg_count_scan) — the launcher's hints

@@ -1834,17 +1834,21 @@ __global__ __launch_bounds__(256) void k_seg_count(const void* __restrict__ in, 
 // kernel, so every plan takes the one-pass form — a skewed bucket is then counted by one workgroup, slowly but
 // correctly, and the next launch has the hint.  direct (solo, no hot-key path): the bucket's per-key totals are scanned
 // here and written as the final bucket offsets (bstart[b] + the exclusive prefix inside the bucket), so no offsets scan
-// follows either.
+// follows either.  pick_word (direct, a batch large enough for the hot-key pick): each bucket also folds its most
+// frequent key of [0, nkeys) into *pick_word (max of count << 32 | key); k_seg_scatter's block 0 turns it into the next
+// batch's hot key and clears it.
 template <int LB, int IN>
 __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
                                                         uint32_t nbk, uint32_t nb, uint32_t seg,
                                                         const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                         uint32_t* __restrict__ seg_hist, uint32_t* __restrict__ counts,
-                                                        uint32_t solo, uint32_t direct, uint32_t* __restrict__ skew_host) {
+                                                        uint32_t solo, uint32_t direct, uint32_t* __restrict__ skew_host,
+                                                        unsigned long long* __restrict__ pick_word, uint32_t nkeys) {
     static_assert(kSegChunk == 256u * kItems, "a segment is one chunk of kItems keys per thread");
     constexpr uint32_t BL = 1u << LB;
     __shared__ uint32_t hist[BL];  // running counts of the bucket's segments so far
     __shared__ uint32_t wsum[kWaves];
+    __shared__ unsigned long long wmax[kWaves];
     if (skew_host && blockIdx.x == 0 && threadIdx.x == 0) skew_host[0] = sstart[kSkewSlot];  // the next launch's hint
     if (sstart[kSkewSlot] && !solo) {
         const uint32_t nseg = sstart[nbk];
@@ -1899,11 +1903,25 @@ __global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__
     }
     uint32_t total;
     uint32_t run = base + block_excl_scan(acc, wsum, total);
+    unsigned long long best = 0;
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t l = l0 + q, key = (b << LB) | l;
         if (l < BL && key < nb) counts[key] = run;
+        if (l < BL && key < nkeys) {
+            const unsigned long long c = ((unsigned long long)v[q] << 32) | key;
+            best = c > best ? c : best;
+        }
         run += v[q];
+    }
+    if (pick_word) {
+        best = wave_max_u64(best);
+        if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t q = 1; q < kWaves; ++q) best = wmax[q] > best ? wmax[q] : best;
+            if (best >> 32) atomicMax(pick_word, best);
+        }
     }
 }
 
@@ -2112,10 +2130,19 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
                                                      const uint32_t* __restrict__ seg_hist, const uint32_t* __restrict__ offsets,
                                                      uint32_t nb, uint32_t n, const uint32_t* __restrict__ seg_carry,
                                                      const uint32_t* __restrict__ seg_meta, uint32_t* __restrict__ order,
-                                                     uint32_t solo) {
+                                                     uint32_t solo, unsigned long long* __restrict__ pick_word,
+                                                     uint32_t* __restrict__ next_key, uint32_t* __restrict__ host_word) {
     constexpr uint32_t BL = 1u << LB;
     constexpr uint32_t PER = kDigitsPerThread<LB>;
     __shared__ SegSmem<LB> sm;
+    if (pick_word && blockIdx.x == 0 && threadIdx.x == 0) {  // the hot-key pick k_seg_count_scan folded (same rule as k_scan_down)
+        const unsigned long long best = *pick_word;
+        *pick_word = 0;
+        const uint32_t c = (uint32_t)(best >> 32), k = (uint32_t)best;
+        const uint32_t key = ((uint64_t)c * kHotShare >= n && c >= kHotMinCount) ? k : kNoHotKey;
+        __hip_atomic_store(next_key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     SegRange r;
     if (!seg_of_block(bstart, sstart, nbk, seg, r)) return;
     const uint32_t rflags = rank_flags();
@@ -3770,15 +3797,19 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     // solo: the last plan had no skewed bucket, so no segment scan is launched (the hint can be stale: k_seg_count_scan
     // then counts a skewed bucket in one workgroup); direct: nor an offsets scan (not with the hot-key path)
     const uint32_t solo = fz && s.hot_host && !__atomic_load_n(s.hot_host + 1, __ATOMIC_ACQUIRE) ? 1u : 0u;
-    const uint32_t direct = solo && !hot && !pick ? 1u : 0u;
+    const uint32_t direct = solo && !hot ? 1u : 0u;
+    // direct with the pick: k_seg_count_scan folds the per-bucket maxima, k_seg_scatter stores the next batch's key
+    unsigned long long* pick_word = direct && pick ? s.pick_word : nullptr;
+    uint32_t* next_key = s.hot + ((s.hot_parity + 1u) & 1u);
     uint32_t* skew_host = s.hot_host_dev ? s.hot_host_dev + 1 : nullptr;
     const uint32_t fgrid = std::max(nbk, std::min(grid, 1024u));  // >= 1024 workgroups for a skewed plan's segment count
 #define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(fgrid), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
-                                     s.sstart, s.seg_hist, d_offsets, solo, direct, skew_host)
+                                     s.sstart, s.seg_hist, d_offsets, solo, direct, skew_host, pick_word, n_act + 1)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
-                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order, solo)
+                                         s.sstart, s.seg_hist, d_offsets, nb, n, s.seg_carry, s.seg_meta, d_order, solo, \
+                                         pick_word, next_key, s.hot_host_dev)
 #define ORL_SS(I) do { const int rm_ = host_rm(s.device); if (rm_ == kRmPlain) ORL_SS3(I, kRmPlain); else if (rm_ == kRmHot)             \
                            ORL_SS3(I, kRmHot); else ORL_SS3(I, kRmBallot); } while (0)
     if (fz) {
@@ -3800,8 +3831,10 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     }
     const uint32_t* hw = hot_cur(s);
     if (hot) hipLaunchKernelGGL(k_hot_finish, dim3(1), dim3(64), 0, st, hw, s.col_tot + nbk, nb, d_offsets);
-    if (pick)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
+    if (pick && !direct)  // per-key counts → bucket offsets, + the next batch's hot key (flips the slots: hw stays this batch's)
         scan_offsets_pick(d_offsets, nb, n_act + 1, n, s, st);
+    else if (pick)  // the offsets are final already; the scatter stores the pick
+        s.hot_parity ^= 1u;
     else if (!direct)
         scan_inplace(d_offsets, nb, s, st);
     if (in == IN_ACT) ORL_SS(IN_ACT); else if (in == IN_PAIR) ORL_SS(IN_PAIR);
