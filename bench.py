@@ -1,21 +1,20 @@
 #!/usr/bin/env python3
 """bench.py — routed grain messages/sec on MI355X (BASELINE.json metric), one process per GPU.
 
-Default workload at N=1 (BASELINE.json configs[1]): 8 logical silos 10.0.0.{1..8}:11111
-(balanced generations), 1M ChirperAccount long-key grains all registered (activation on the directory owner), 64M
-single-target messages per step, targets Uniform[0,1M) (splitmix64 seed 0x5EED0002), generated on the device and
-resident in HBM before the timed region.  A step = one pass of the hot path over the batch: stages 1-4 (hash, ring owner,
-directory probe + placement, stable per-activation bucketing).
-
-Default at N>1 (torchrun; BASELINE.json configs[2], config 3): Zipf(1.1) over 16M grains, 256M messages in total split
-256M/N per GPU (strong scaling); each GPU hosts silos s*N//8 == rank and their directory partition, originates its share
-from its own silos, and a step runs the node exchange behind the C ABI (orl_node: owner partition, RCCL counts all-gather
-+ grouped send/recv, routing at the owner, hop 2, stage 4 at the host).
+Default workload at every N (one workload along the driver's 1/2/4/8-GPU curve; BASELINE.json
+configs[2], SURVEY §8(d) config 3, the batch size north_star's targets are quoted on): 8 logical silos 10.0.0.{1..8}:11111
+(balanced generations), 16M ChirperAccount long-key grains all registered (activation on the directory owner), 256M
+single-target messages per step in total, targets Zipf(1.1) (seed 0x5EED0003) through a seeded permutation, generated on
+the device and resident in HBM before the timed region.  A step = one pass of the hot path over the batch: stages 1-4
+(hash, ring owner, directory probe + placement, stable per-activation bucketing).  At N=1 the whole batch runs on one
+GPU; at N>1 (torchrun) the batch is split 256M/N per GPU (strong scaling): each GPU hosts silos s*N//8 == rank and their
+directory partition, originates its share from its own silos, and a step runs the node exchange behind the C ABI
+(orl_node: owner partition, RCCL counts all-gather + grouped send/recv, routing at the owner, hop 2, stage 4 at the host;
+SURVEY §8(e)).
 
 Other SURVEY §8(d) workloads (measurement legs recorded under profiles/; not the driver's bench line):
   --config 1   Chirper generator graph, 1k accounts x 10 followers on one silo, every account publishes (10k messages)
-  --config 2   with N > 1: 64M messages per GPU (weak scaling) through the node exchange
-  --config 3   at N = 1: the whole 256M-message Zipf batch on one GPU
+  --config 2   uniform 1M grains, 64M messages per GPU (weak scaling; BASELINE configs[1], the round-1..4 headline)
   --config 4   Chirper-scale CSR: 10M accounts, power-law followers (exp 2.1, 1..1e5), 1M publishers per step
   --config 5   Presence: 100k Guid-keyed games x 8 players, 64k heartbeats per step, eager and hipGraph-replayed
   --config 6/7/8   directory mutation (f1), stream / reminder rings (f3), receive path (f2) legs
@@ -112,7 +111,7 @@ def main():
     ap.add_argument("--wire16", action="store_true",
                     help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "route_kernel_pmc.json"))
+    ap.add_argument("--traffic-json", default=None, help="default: profiles/route_kernel_pmc[_config<N>].json")
     ap.add_argument("--check-sample", type=int, default=256 * 1024,
                     help="N > 1 (and --local-ranks): hosted messages per rank checked against the oracle after the timed "
                          "steps, on top of the size-independent checks of every hosted message (0: no oracle sample)")
@@ -128,8 +127,8 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local_rank)
-    if args.config is None:  # the headline: config 2 on one GPU; the 8-GPU config (3, strong scaling) on several
-        args.config = 2 if world == 1 else 3
+    if args.config is None:  # the headline: config 3's 256M batch at every N, so the 1/2/4/8-GPU lines share one workload
+        args.config = 3
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         if args.config in (1, 5, 6, 7, 8):
@@ -188,16 +187,24 @@ def timed_steps(args, torch, dist, world, step, sync):
     return elapsed, units
 
 
-def read_traffic(path, msgs_per_launch, world):
+def traffic_json_path(config):
+    """The route kernel's PMC traffic record of a workload (scripts/make_traffic_json.py writes it)."""
+    return os.path.join(ROOT, "profiles", "route_kernel_pmc.json" if config == 2 else f"route_kernel_pmc_config{config}.json")
+
+
+def read_traffic(path, msgs_per_launch, world, config):
     """The route kernel's measured HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, scripts/make_traffic_json.py)
-    and where they come from, for the workload they were measured on only (config 2, all grains registered, one GPU, the
-    same messages per launch); (None, None) otherwise."""
+    and where they come from, for the workload they were measured on only (the same config, all grains registered, one GPU,
+    the same messages per launch); (None, None) otherwise."""
     if world != 1 or not os.path.exists(path):
         return None, None
     try:
         tj = json.load(open(path))
-        if tj.get("msgs_per_launch") == msgs_per_launch:
-            return tj.get("hbm_bytes_per_launch"), f"{os.path.relpath(path, ROOT)}: {tj.get('method', 'rocprofv3 --pmc')}"
+        if tj.get("msgs_per_launch") == msgs_per_launch and tj.get("config", 2) == config:
+            src = f"{os.path.relpath(path, ROOT)}: {tj.get('method', 'rocprofv3 --pmc')}"
+            if tj.get("build"):
+                src += f"; measured at build {tj['build']}"
+            return tj.get("hbm_bytes_per_launch"), src
     except Exception:
         return None, None
     return None, None
@@ -339,6 +346,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
             stats["waits"] = stats.get("waits", 0) + xs["host_waits"]
             stats["bytes_sent"] = [a + b for a, b in zip(stats.get("bytes_sent", [0] * world), xs["bytes_sent"])]
             stats["comm_count"] = xs["comm_count"]
+            stats["exchange_mode"] = xs["exchange_mode"]
             stats["last"] = res
             return res.n_owned
     log(f"setup {time.perf_counter() - t_setup:.1f}s; warmup {args.warmup}")
@@ -368,8 +376,8 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     achieved = kbytes * per_launch_msgs / (route_ms * 1e-3) / 1e9
     log(f"rank {rank}: {ms_per_step:.3f} ms/step; route kernel {route_ms:.3f} ms x {launches}, bucketing {bucket_ms:.3f} ms, "
         f"call {total_ms:.3f} ms over {nb} launches")
-    traffic, traffic_src = (read_traffic(args.traffic_json, per_launch_msgs, world) if args.config == 2 and not args.unregistered
-                            else (None, None))
+    traffic, traffic_src = (read_traffic(args.traffic_json or traffic_json_path(args.config), per_launch_msgs, world,
+                                         args.config) if not args.unregistered else (None, None))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cl, n_grains, d_msgs, args.cpu_wall, zipf, 1.0 - args.unregistered)
@@ -433,6 +441,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
                            "rank0_xgmi_bytes_per_step": rec_w * stats["remote"] / args.steps,
                            "receive_capacity": cap,
                            "ncclCommCount": stats["comm_count"],
+                           "mode": stats["exchange_mode"],
                            "rank0_bytes_sent_per_peer_per_step": [b / args.steps for b in stats["bytes_sent"]],
                            "rank0_host_wait_ms_per_step": stats["wait_us"] / 1e3 / args.steps,
                            "rank0_host_wait_ms_per_chunk": stats["wait_us"] / 1e3 / args.steps / max(1, args.chunks),
@@ -502,6 +511,7 @@ def run_rehearsal(args, torch):
         stats[r]["waits"] += xs["host_waits"]
         stats[r]["bytes_sent"] = [a + b for a, b in zip(stats[r].get("bytes_sent", [0] * R), xs["bytes_sent"])]
         stats[r]["comm_count"] = xs["comm_count"]
+        stats[r]["exchange_mode"] = xs["exchange_mode"]
         stats[r]["last"] = res
         streams[r].synchronize()
         return res.n_owned
@@ -544,7 +554,7 @@ def run_rehearsal(args, torch):
                                    f"transport, {args.chunks} chunks", "receive_capacity": cap},
             "owned_per_rank": owned, "max_over_mean_owned": max(owned) / (sum(owned) / R),
             "sent_remote_per_rank": [st["remote"] / args.steps for st in stats],
-            "exchange": {"ncclCommCount": stats[0]["comm_count"],
+            "exchange": {"ncclCommCount": stats[0]["comm_count"], "mode": stats[0]["exchange_mode"],
                          "bytes_sent_per_peer_per_step": [[b / args.steps for b in st["bytes_sent"]] for st in stats],
                          "host_wait_ms_per_step": [st["wait_us"] / 1e3 / args.steps for st in stats],
                          "host_wait_ms_per_chunk": [st["wait_us"] / 1e3 / args.steps / max(1, args.chunks) for st in stats],

@@ -547,6 +547,9 @@ int orl_fanout_batch(orl_ctx* ctx, const uint32_t* pubs, const uint8_t* pub_silo
 #define ORL_TRANSPORT_RCCL 0u
 #define ORL_TRANSPORT_LOCAL 1u
 #define ORL_NODE_WIDE_ONLY 0x1u    /* always exchange 32-B headers */
+#define ORL_NODE_SPLIT_COMM 0x2u   /* RCCL: run the counts all-gathers on a second communicator (ncclCommSplit) and stream,
+                                      concurrently with the previous chunk's send/recv; off by default.  Every rank must set
+                                      the same flags (checked at creation: ranks that disagree all fail with ORL_E_INVALID) */
 #define ORL_NODE_MAX_RANKS 8u
 #define ORL_NODE_MAX_CHUNKS 16u
 typedef struct orl_node_config {
@@ -613,7 +616,12 @@ typedef struct orl_node_stats {
     uint64_t bytes_sent[ORL_NODE_MAX_RANKS];
     uint64_t host_wait_us;
     uint64_t host_waits;
+    uint32_t exchange_mode;                   /* ORL_NODE_MODE_*: where the counts all-gathers run */
+    uint32_t reserved;
 } orl_node_stats;
+#define ORL_NODE_MODE_SPLIT_COMM 0x1u  /* RCCL: on the split communicator (ORL_NODE_SPLIT_COMM) */
+#define ORL_NODE_MODE_HEAD_STREAM 0x2u /* on a stream of their own (LOCAL always; RCCL only with the split communicator);
+                                          otherwise queued on the exchange stream behind the previous chunk's send/recv */
 int orl_node_get_stats(const orl_node* node, orl_node_stats* out);
 
 /* The protocol's host decisions, as orl_node_route_batch_device takes them after each all-gather: exposed for hosts that

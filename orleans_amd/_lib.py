@@ -83,6 +83,9 @@ class orl_config(C.Structure):
 NODE_ID_BYTES = 128
 TRANSPORT_RCCL, TRANSPORT_LOCAL = 0, 1
 NODE_WIDE_ONLY = 0x1
+NODE_SPLIT_COMM = 0x2
+NODE_MODE_SPLIT_COMM = 0x1
+NODE_MODE_HEAD_STREAM = 0x2
 NODE_MAX_RANKS = 8
 NODE_MAX_CHUNKS = 16
 NODE_HEAD_WORDS = 16
@@ -102,7 +105,8 @@ class orl_node_result(C.Structure):
 
 class orl_node_stats(C.Structure):
     _fields_ = [("comm_count", C.c_uint32), ("chunks", C.c_uint32), ("bytes_sent", C.c_uint64 * NODE_MAX_RANKS),
-                ("host_wait_us", C.c_uint64), ("host_waits", C.c_uint64)]
+                ("host_wait_us", C.c_uint64), ("host_waits", C.c_uint64), ("exchange_mode", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class orl_node_chunk_plan(C.Structure):

@@ -409,6 +409,36 @@ int ensure_hop2(orl_node* nd, uint64_t owned) {
     return ORL_OK;
 }
 
+
+// One u32 per rank summed over comm (on sx, bounded wait): the node's collective yes/no decisions at creation.
+int allreduce_u32_sum(orl_node* nd, uint32_t v, uint32_t* sum) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(nd->d_hcount);  // scratch: the hop-2 counts are not in use yet
+    NODE_HIP(nd, hipMemcpyAsync(d, &v, 4, hipMemcpyHostToDevice, nd->sx));
+    NODE_NCCL(nd, ncclAllReduce(d, d + 1, 1, ncclUint32, ncclSum, nd->comm, nd->sx));
+    if (int r = wait_bounded(nd, nd->sx, "node creation all-reduce", -3, nullptr)) return r;
+    NODE_HIP(nd, hipMemcpy(sum, d + 1, 4, hipMemcpyDeviceToHost));
+    NODE_HIP(nd, hipMemsetAsync(d, 0, 8, nd->sx));
+    return wait_bounded(nd, nd->sx, "node creation all-reduce", -3, nullptr);
+}
+
+// The optional second communicator of the counts all-gathers (ORL_NODE_SPLIT_COMM): all ranks or none.
+int setup_split_comm(orl_node* nd, bool want) {
+    uint32_t n_want = 0;
+    if (int r = allreduce_u32_sum(nd, want ? 1u : 0u, &n_want)) return r;
+    if (n_want != 0 && n_want != nd->nr)
+        return nfail(nd, ORL_E_INVALID, "ORL_NODE_SPLIT_COMM set on %u of %u ranks (every rank must use the same config)",
+                     n_want, nd->nr);
+    if (!n_want) return ORL_OK;
+    if (ncclCommSplit(nd->comm, 0, (int)nd->me, &nd->comm_h, nullptr) != ncclSuccess) nd->comm_h = nullptr;
+    uint32_t n_ok = 0;
+    if (int r = allreduce_u32_sum(nd, nd->comm_h ? 1u : 0u, &n_ok)) return r;
+    if (n_ok != nd->nr && nd->comm_h) {  // some rank's split failed: nobody uses the split communicator
+        (void)ncclCommDestroy(nd->comm_h);
+        nd->comm_h = nullptr;
+    }
+    return ORL_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -578,9 +608,12 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
         }
         int cc = 0;
         nd->stats.comm_count = ncclCommCount(nd->comm, &cc) == ncclSuccess ? (uint32_t)cc : 0u;
-        // the counts all-gathers' own communicator (collective: every rank splits here, in the same order); on failure
-        // the all-gathers share comm and its stream
-        if (ncclCommSplit(nd->comm, 0, (int)cfg->rank, &nd->comm_h, nullptr) != ncclSuccess) nd->comm_h = nullptr;
+        // The counts all-gathers' own communicator is opt-in (ORL_NODE_SPLIT_COMM): by default the
+        // all-gathers share comm and the exchange stream sx, so no two RCCL kernels of this rank ever wait on peers at the
+        // same time.  Both decisions are collective: the request is all-reduced first (ranks that disagree
+        // fail creation together instead of one rank entering ncclCommSplit alone), then the split's success, so either
+        // every rank uses comm_h or none does.
+        if (int r = setup_split_comm(nd, (cfg->flags & ORL_NODE_SPLIT_COMM) != 0)) return bail(r);
     } else {
         nd->group = join_group(cfg->group_id, cfg->nranks);
         if (!nd->group) return bail(ORL_E_INVALID);
@@ -632,6 +665,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         const uint32_t cc = nd->stats.comm_count;
         nd->stats = orl_node_stats{};
         nd->stats.comm_count = cc;
+        nd->stats.exchange_mode = (nd->comm_h ? ORL_NODE_MODE_SPLIT_COMM : 0u) |
+                                  (nd->sh && (!nd->comm || nd->comm_h) ? ORL_NODE_MODE_HEAD_STREAM : 0u);
         nd->stats.chunks = nd->cfg.chunks;
     }
     if (nd->broken) return nfail(nd, ORL_E_STATE, "node is broken (an earlier exchange failed; its communicator was aborted): %s",

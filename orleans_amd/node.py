@@ -124,8 +124,9 @@ class GrainNode:
 
     def __init__(self, eng, nranks: int, rank: int, rank_of_silo: Sequence[int], max_batch: int, max_recv: int,
                  transport: int = L.TRANSPORT_RCCL, group_id: Optional[bytes] = None, chunks: int = 4,
-                 wide_only: bool = False):
+                 wide_only: bool = False, split_comm: Optional[bool] = None):
         import ctypes as C
+        import os
         self._C = C
         self._lib = L.load()
         self.eng = eng
@@ -138,7 +139,9 @@ class GrainNode:
         ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
         C.memmove(cfg.rank_of_silo, ros.tobytes(), 256)
         cfg.max_batch, cfg.max_recv, cfg.chunks = int(max_batch), int(max_recv), int(chunks)
-        cfg.flags = L.NODE_WIDE_ONLY if wide_only else 0
+        if split_comm is None:  # opt-in: every rank must agree, which orl_node_create checks
+            split_comm = os.environ.get("ORL_NODE_SPLIT_COMM", "0") == "1"
+        cfg.flags = (L.NODE_WIDE_ONLY if wide_only else 0) | (L.NODE_SPLIT_COMM if split_comm else 0)
         h = C.c_void_p()
         rc = self._lib.orl_node_create(eng.handle, C.byref(cfg), C.byref(h))
         if rc != L.OK:
@@ -221,7 +224,7 @@ class GrainNode:
         if rc != L.OK:
             raise L.OrleansRouteError(rc, "orl_node_get_stats")
         return {"comm_count": st.comm_count, "chunks": st.chunks, "bytes_sent": list(st.bytes_sent)[:self.nranks],
-                "host_wait_us": st.host_wait_us, "host_waits": st.host_waits}
+                "host_wait_us": st.host_wait_us, "host_waits": st.host_waits, "exchange_mode": exchange_mode_name(st.exchange_mode)}
 
     def close(self) -> None:
         if getattr(self, "_node", None):
@@ -233,6 +236,15 @@ class GrainNode:
             self.close()
         except Exception:
             pass
+
+
+def exchange_mode_name(mode: int) -> str:
+    """orl_node_stats.exchange_mode as the bench JSON records it."""
+    if mode & L.NODE_MODE_SPLIT_COMM:
+        return "split communicator: counts all-gathers on their own RCCL communicator and stream"
+    if mode & L.NODE_MODE_HEAD_STREAM:
+        return "counts all-gathers on their own stream (LOCAL transport)"
+    return "one communicator: counts all-gathers queued on the exchange stream behind the previous chunk's send/recv"
 
 
 def rank_of_silo(n_silos: int, world: int) -> np.ndarray:

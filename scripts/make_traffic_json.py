@@ -7,7 +7,9 @@ coalesced) is added back once; random 32-B directory probes are one 64-B request
 WRITE_SIZE is exact for the kernel's 4-B/lane coalesced stores.  Bytes served by the Infinity Cache are included
 (the counters sit on the L2's memory side), so this is an upper bound on DRAM bytes.
 
-Usage: python scripts/make_traffic_json.py gpurun_out/prof MSGS_PER_LAUNCH [out.json]
+Usage: python scripts/make_traffic_json.py gpurun_out/prof MSGS_PER_LAUNCH [out.json] [CONFIG]
+(run here, on the pulled PMC passes: the record carries the config and the git build it was measured at, which bench.py
+checks before it quotes the traffic)
 """
 import json
 import os
@@ -20,6 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     prof, msgs = sys.argv[1], int(float(sys.argv[2]))
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "route_kernel_pmc.json")
+    config = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    try:
+        build = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                               check=True).stdout.strip()
+    except Exception:
+        build = None
     tmp = os.path.join(prof, "pmc_summary.json")
     subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), prof, "--json", tmp], check=True,
                    stdout=subprocess.DEVNULL)
@@ -29,7 +37,7 @@ def main():
     header = 32 * msgs
     fetch = c["FETCH_SIZE"] * 1024 + header / 2
     write = c["WRITE_SIZE"] * 1024
-    rec = {"kernel": k, "msgs_per_launch": float(msgs), "hbm_bytes_per_launch": fetch + write,
+    rec = {"kernel": k, "config": config, "build": build, "msgs_per_launch": float(msgs), "hbm_bytes_per_launch": fetch + write,
            "read_bytes": fetch, "write_bytes": write, "algorithmic_bytes": 72.0 * msgs,
            "tcc_ea0_rdreq": c.get("TCC_EA0_RDREQ_sum"), "tcc_hit": c.get("TCC_HIT_sum"), "tcc_miss": c.get("TCC_MISS_sum"),
            "method": "FETCH_SIZE*1024 + 16 B/msg streaming correction + WRITE_SIZE*1024 (scripts/make_traffic_json.py)"}

@@ -251,13 +251,16 @@ def test_node_capacity_error_is_consistent(torch):
     world.close()
 
 
-def test_node_rccl_single_rank(torch):
-    """The RCCL transport with a communicator of one rank: init from orl_node_unique_id, counts all-gather, grouped
-    self send; results == the direct route + bucket of the context."""
+@pytest.mark.parametrize("split", [False, True])
+def test_node_rccl_single_rank(torch, split):
+    """The RCCL transport with a communicator of one rank: init from orl_node_unique_id, the creation all-reduces (split
+    request, split success), counts all-gather, grouped self send; results == the direct route + bucket of the context.
+    The default runs the all-gathers on the one communicator and exchange stream; ORL_NODE_SPLIT_COMM opts in to the
+    second communicator, and orl_node_get_stats reports which ran."""
     t = torch
     world = World(1, n_grains=30_000, host_mix=0.0)
     node = GrainNode(world.engs[0], 1, 0, world.ros, max_batch=300_000, max_recv=300_000, transport=L.TRANSPORT_RCCL,
-                     group_id=GrainNode.unique_id(), chunks=3)
+                     group_id=GrainNode.unique_id(), chunks=3, split_comm=split)
     s = t.cuda.Stream()
     batches = [world.messages(0, 250_000, seed=9)]
     (res, (route, act, order, off, hdrs)), = _run(t, world, [node], batches, [s])
@@ -269,11 +272,14 @@ def test_node_rccl_single_rank(torch):
     np.testing.assert_array_equal(act, ea)
     np.testing.assert_array_equal(order, eo)
     np.testing.assert_array_equal(off, ef)
+    mode = node.stats()["exchange_mode"]
+    assert mode.startswith("split communicator") if split else mode.startswith("one communicator"), mode
     node.close()
     world.close()
 
 
-def test_node_rccl_bounded_wait_aborts(torch, monkeypatch):
+@pytest.mark.parametrize("split", [False, True])
+def test_node_rccl_bounded_wait_aborts(torch, monkeypatch, split):
     """A counts all-gather that cannot complete (fault injection: chunk 1's all-gather is followed on the exchange stream
     by a kernel that waits for a host word nobody sets) fails within the node's deadline with ORL_E_STATE naming the chunk
     and this rank's head words; the communicator is aborted, the node reports itself broken on the next call, and the
@@ -283,7 +289,7 @@ def test_node_rccl_bounded_wait_aborts(torch, monkeypatch):
     monkeypatch.setenv("ORL_NODE_INJECT_STALL", "1")
     world = World(1, n_grains=30_000, host_mix=0.0)
     node = GrainNode(world.engs[0], 1, 0, world.ros, max_batch=300_000, max_recv=300_000, transport=L.TRANSPORT_RCCL,
-                     group_id=GrainNode.unique_id(), chunks=3)
+                     group_id=GrainNode.unique_id(), chunks=3, split_comm=split)
     node.set_timeout(1500)
     m = world.messages(0, 250_000, seed=9)
     d_in = t.from_numpy(m.view(np.int32).reshape(-1, 8)).cuda()
