@@ -702,7 +702,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -806,9 +806,16 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         const uint64_t seg_rows = std::max<uint64_t>(max_segments(mb, bp.hb), max_segments(std::min<uint64_t>(mb, (16u << 20) - 1), bp.hb));
         const uint64_t seg_words = bp.two_level ? seg_rows << bp.lb : 1;
         if ((e = hipMalloc((void**)&c->s.seg_hist, seg_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_hist)");
-        const uint64_t carry_words = bp.two_level ? ((seg_rows + 63) / 64) << bp.lb : 1;
+        // skewed plans: per chunk of >= kSegLbMinRows segments a carry-in row and a first bucket; the fused kernel's
+        // look-back also keeps an aggregate and an inclusive row per chunk, and one flag (zeroed once: epoch-tagged)
+        const uint64_t lb_cap = bp.two_level ? (seg_rows + kSegLbMinRows - 1) / kSegLbMinRows + 1 : 1;
+        c->s.seg_lb_cap = (uint32_t)lb_cap;
+        const uint64_t carry_words = bp.two_level ? lb_cap << bp.lb : 1;
         if ((e = hipMalloc((void**)&c->s.seg_carry, carry_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_carry)");
-        if ((e = hipMalloc((void**)&c->s.seg_meta, ((seg_rows + 63) / 64 + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_meta)");
+        if ((e = hipMalloc((void**)&c->s.seg_meta, (lb_cap + 1) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_meta)");
+        if ((e = hipMalloc((void**)&c->s.seg_lb, 2 * carry_words * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_lb)");
+        if ((e = hipMalloc((void**)&c->s.seg_lbctl, (4 + lb_cap) * 4)) != hipSuccess) return bail(e, "hipMalloc(seg_lbctl)");
+        if ((e = hipMemset(c->s.seg_lbctl, 0, (4 + lb_cap) * 4)) != hipSuccess) return bail(e, "hipMemset(seg_lbctl)");
         if ((e = hipMalloc((void**)&c->s.bstart, 4097 * 4)) != hipSuccess) return bail(e, "hipMalloc(bstart)");
         c->s.fan_blk_cap = (uint32_t)((mb + 255) / 256 + 2);
         if ((e = hipMalloc((void**)&c->s.fan_blk, (size_t)c->s.fan_blk_cap * 4)) != hipSuccess) return bail(e, "hipMalloc(fan_blk)");

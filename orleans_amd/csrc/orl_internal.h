@@ -234,6 +234,10 @@ struct DirView {
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
 // All return hipError_t as int; they only enqueue on `stream`.
+// Fused level 2 on skewed plans: segments per look-back chunk (k_seg_count_scan's kLbRows, ORL_SEG_LB_ROWS for lab builds)
+// is at least this; the look-back buffers are sized for it.
+constexpr uint32_t kSegLbMinRows = 8;
+
 struct Scratch {
     uint2* pairs_a;         // [max_batch] {key, index} between radix passes
     uint2* pairs_b;         // [max_batch]
@@ -246,8 +250,12 @@ struct Scratch {
     uint32_t* col_tot;      // [2048 + 1] column totals (+ the hot key's at [bins])
     uint8_t* digits;        // [max_batch] (partition by owner)
     uint32_t* seg_hist;     // [max segments][2^lb] two-level path: per-segment low-digit counts → bases
-    uint32_t* seg_carry;    // [ceil(max segments / 64)][2^lb] chunked segment scan: chunk sums, then carry-ins
-    uint32_t* seg_meta;     // [ceil(max segments / 64)] chunked segment scan: each chunk's first bucket + shape bits
+    uint32_t* seg_carry;    // [seg_lb_cap][2^lb] skewed plans: each segment chunk's carry-in (legacy scan: chunk sums first)
+    uint32_t* seg_meta;     // [seg_lb_cap] skewed plans: each chunk's first bucket (+ shape bits in the legacy scan)
+    uint32_t* seg_lb = nullptr;     // [2][seg_lb_cap][2^lb] fused level 2, skewed plans: chunk aggregate rows, inclusive rows
+    uint32_t* seg_lbctl = nullptr;  // [4 + seg_lb_cap] ticket, done count, -, -, then one look-back flag per chunk (zeroed once)
+    uint32_t seg_lb_cap = 0;        // chunks of kSegLbMinRows segments the look-back buffers hold
+    mutable uint32_t seg_epoch = 0; // fused level-2 launches so far (the flags' epoch)
     uint32_t* bstart;       // [4097] bucket starts (two-level path; k_seg_plan handles up to 4096)
     uint32_t* sstart;       // [4098] first segment of each bucket; [4097] = a bucket has > 64 segments (skew flag)
     uint32_t* gap_q;        // [kGapQueueWords] LSD offsets: long-gap queue (zeroed once; k_offsets_long empties it)
@@ -262,8 +270,8 @@ struct Scratch {
     unsigned long long* hot_bmax = nullptr;  // [offset-scan chunks] per-chunk max of (count << 32 | key)
     unsigned long long* pick_word = nullptr; // the fused level-2 pick's max of (count << 32 | key), zero between batches
     uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
-    uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key, [1] the last level-2 plan's skew
-                                       // flag (k_seg_count_scan) — the launcher's hints
+    uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key (the launcher's hot-key hint), [1]
+                                       // unused since round 5 (was the level-2 skew hint)
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
     uint32_t* fan_blk = nullptr;   // [fan_blk_cap] fan-out: the publisher of every 256th emitted message (k_scan_down WIDEN)

@@ -656,11 +656,10 @@ def test_stage4_rank_modes_vs_oracle(torch, n_act):
 
 @pytest.mark.parametrize("n_act", [5000, 1_000_000])
 def test_stage4_skew_hint_vs_oracle(torch, n_act):
-    """Level 2's launch form follows the last plan's skew flag (a mapped host word, k_seg_count_scan): after a plan
-    without a skewed bucket no segment scan (and, below the hot-key path's batch size, no offsets scan) is launched, so
-    a skewed batch arriving then is counted by one workgroup per bucket and must still be exact; the next batch takes the
-    chunked form again.  Every batch of the sequence is bit-exact vs the oracle's stable bucketing
-    (ActivationData.cs:483-514)."""
+    """Unskewed and skewed level-2 plans alternating through the route path (synchronous calls): the fused kernel takes
+    the per-bucket form or, on the device's skew flag, the chunked look-back form in the same launch (round 5; until round
+    4 a host hint from the previous plan chose the launches).  Every batch of the sequence is bit-exact vs the oracle's
+    stable bucketing (ActivationData.cs:483-514)."""
     cl = W.default_cluster()
     n_grains = 50_000
     keys, uni, owner, reg = W.grain_population(cl, n_grains)
@@ -682,6 +681,64 @@ def test_stage4_skew_hint_vs_oracle(torch, n_act):
         order, off = o.bucket(a, n_act)
         np.testing.assert_array_equal(res.offsets, off)
         np.testing.assert_array_equal(res.order, order)
+    eng.close()
+
+
+@pytest.mark.parametrize("n_act", [3_000, 1_000_000, 2_000_000])
+def test_stage4_skewed_plans_async_vs_oracle(torch, n_act):
+    """stage 4 alone (orl_bucket_device) over a sequence enqueued on ONE stream with no host sync in between,
+    alternating small unskewed batches with large skewed ones — several hot activations (buckets of hundreds of segments
+    that continue across many look-back chunks), one activation only, a Zipf stream, the unresolved bucket — so no launch
+    decision can rely on an earlier batch's result.  n_act 3000: one bucket (no MSD pass; skewed iff the batch has > 64
+    segments); 1M: 10 + 10-bit plan; 2M: 11 + 10.  Outputs of every batch bit-exact vs the oracle's stable bucketing
+    (ActivationData.EnqueueMessage FIFO, ActivationData.cs:483-514)."""
+    t = torch
+    rng = np.random.default_rng(n_act + 5)
+    o = cpu_ref.Oracle(8)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=3_000_000, device=0)
+    W.setup_engine(eng, W.default_cluster())
+
+    def uniform(n):
+        return rng.integers(0, n_act, n, dtype=np.int64).astype(np.uint32)
+
+    def hot_mix(n, shares):
+        a = uniform(n)
+        u = rng.random(n)
+        lo = 0.0
+        for k, sh in shares:
+            a[(u >= lo) & (u < lo + sh)] = k
+            lo += sh
+        return a
+
+    def zipf(n):
+        r = np.minimum(rng.zipf(1.1, n), n_act) - 1
+        return ((r.astype(np.uint64) * np.uint64(2654435761)) % np.uint64(n_act)).astype(np.uint32)
+
+    keys = [int(x) for x in rng.integers(0, n_act, 6)]
+    batches = [uniform(200_000),
+               hot_mix(2_500_000, [(keys[0], 0.30), (keys[1], 0.15), (keys[2], 0.10), (keys[3], 0.05), (keys[4], 0.03)]),
+               uniform(150_001),
+               np.full(1_100_000, keys[5], np.uint32),                      # one activation: one bucket of ~270 segments
+               uniform(300_000),
+               zipf(2_000_000),
+               hot_mix(700_000, [(L.NO_ACT, 0.5), (keys[0], 0.2)]),        # the unresolved bucket skewed, below 2^20
+               uniform(64),
+               hot_mix(1_300_000, [(keys[1], 0.6)])]
+    s = t.cuda.Stream()
+    outs = []
+    with t.cuda.stream(s):
+        for a in batches:
+            d_a = t.from_numpy(a.view(np.int32)).to("cuda", non_blocking=False)
+            order = t.empty(len(a), dtype=t.int32, device="cuda")
+            off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
+            eng.bucket_device(d_a, len(a), order, off, stream=s.cuda_stream)
+            outs.append((d_a, order, off))
+    s.synchronize()
+    for a, (_, order, off) in zip(batches, outs):
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), ef)
+        np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), eo)
+    assert eng.query(L.Q_PART_ERROR) == 0  # no look-back gave up
     eng.close()
 
 
