@@ -471,6 +471,7 @@ int orl_partition_by_owner_padded_device(orl_ctx* ctx, const orl_msg_hdr* d_in, 
  * the look-back state is reused launch after launch (tile tickets and epochs are mirrored on the host).  A look-back
  * failure of the 32-byte form, which has no status word, is reported by orl_ctx_query(ORL_Q_PART_ERROR). */
 #define ORL_PART_LOOKBACK_FAILED 0x4u
+#define ORL_PART_CACHED 0x8u  /* (node hop 1) the sender's directory cache addressed some message of the chunk */
 int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                                  const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
                                  orl_wire_msg* d_out, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_status,
@@ -492,6 +493,24 @@ int orl_partition_narrow_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n,
 /* orl_route_batch_device over received 8-byte records, decoded with this context's wire types. */
 int orl_route_narrow_device(orl_ctx* ctx, const orl_wire8* d_in, size_t n, uint32_t opts, uint32_t* d_route,
                             uint32_t* d_act, uint32_t* d_order, uint32_t* d_bucket_offsets, void* stream);
+/* The node's hop-1 partition with the sender's directory cache (round 5): as orl_partition_narrow/compact_device (fmt =
+ * the record width, 8 / 16 / 32), except that a message whose directory owner is on another rank and whose grain the
+ * context's cache holds on a valid silo (orl_cache_add_or_update_device; LocalLookup's non-owner branch,
+ * LocalGrainDirectory.cs:690-717) is addressed here — its record goes to the rank of the cached silo (rank_of_silo), with
+ * that silo as the record's target silo — and d_act_out (device u32, the same padded regions as d_out: stride per rank)
+ * gets its cached activation handle; every other record gets ORL_NO_ACT.  *d_status also gets ORL_PART_CACHED when a
+ * message was addressed.  Without a populated cache it is the plain partition (d_act_out all ORL_NO_ACT).  Replaces
+ * the non-owner silo's cache lookup + Dispatcher.AddressMessage + the send to TargetSilo (Dispatcher.cs:555-579,
+ * OutboundMessageQueue.cs:113-145). */
+int orl_partition_cached_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, uint32_t fmt,
+                                uint32_t* d_act_out, uint64_t* d_counts, uint32_t* d_status, void* stream);
+/* Stages 1-3 of received hop-1 records (fmt 8 / 16 / 32) with their act lane: a record whose lane entry is not ORL_NO_ACT
+ * was addressed by its sender's cache and gets HIT | ORL_RF_CACHED with its target silo as host and that handle, without
+ * a directory probe (the receiving silo's Dispatcher takes an addressed message as is); the others are routed as
+ * orl_route_*_device do.  No stage 4 (ORL_OPT_NO_BUCKETS implied; orl_bucket_device follows over the hosted set). */
+int orl_route_received_device(orl_ctx* ctx, const void* d_in, uint32_t fmt, size_t n, uint32_t opts, const uint32_t* d_in_act,
+                              uint32_t* d_route, uint32_t* d_act, void* stream);
 
 /* Stage 4 alone: group already-routed messages by activation handle, FIFO inside each bucket (ActivationData.EnqueueMessage,
  * ActivationData.cs:483-514) — the receiving silo's side when the routing ran elsewhere (node hop 2).  Same outputs as
@@ -628,7 +647,8 @@ int orl_node_get_stats(const orl_node* node, orl_node_stats* out);
  * run the exchange over a transport of their own (orl_partition_*_padded/compact/narrow_device, the route entry points,
  * orl_bucket_device + these two), and for the multi-process CPU tests.  ORL_NODE_HEAD_WORDS u64 per rank are
  * all-gathered before each exchange.  Hop 1 (one per chunk): [0, nranks) records for each destination rank, [8] the
- * partition status word (bit 0 = a message lacks the 16-B form, bit 1 = lacks the 8-B form, ORL_PART_LOOKBACK_FAILED),
+ * partition status word (bit 0 = a message lacks the 16-B form, bit 1 = lacks the 8-B form, ORL_PART_LOOKBACK_FAILED,
+ * ORL_PART_CACHED),
  * [9] the record width the rank wrote (bits 56-63: 8 / 16 / 32) | its wire-type digest (bits 0-55, ORL_Q_WIRE_DIGEST),
  * the rest zero.  Hop 2: [0, nranks) routed messages whose activation each rank hosts (ORL_ROUTE_HOST's rank; no host:
  * the owner), the rest zero.  heads = nranks x ORL_NODE_HEAD_WORDS words in rank order. */
@@ -639,6 +659,10 @@ typedef struct orl_node_chunk_plan {
     uint64_t send[ORL_NODE_MAX_RANKS];   /* records to each rank */
     uint64_t recv[ORL_NODE_MAX_RANKS];   /* records from each rank, received back to back in rank order */
     uint64_t n_recv;
+    uint32_t act_lane;                   /* some rank's directory cache addressed a record (ORL_PART_CACHED): every rank
+                                            sends a u32 activation handle per record beside the records (ORL_NO_ACT: not
+                                            addressed), and the receivers route addressed records without a probe */
+    uint32_t reserved;
 } orl_node_chunk_plan;
 /* written = the width this rank partitioned the chunk in; owned_total[nranks] = every rank's receive total over the
  * batch's earlier chunks (zero before chunk 0; updated).  ORL_E_CAPACITY when a rank would own more than max_recv and

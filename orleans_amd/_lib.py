@@ -61,6 +61,7 @@ MERGE_INSERTED, MERGE_KEPT, MERGE_REPLACED, MERGE_SAME, MERGE_DUPLICATE, MERGE_U
 Q_PROBE_FORM, Q_FULL_UPLOADS, Q_SLOT_PATCHES, Q_DEVICE, Q_N_ACT, Q_MAX_BATCH, Q_RANK_MODE = 1, 2, 3, 4, 5, 6, 7
 Q_WIRE_DIGEST = 8
 Q_PART_ERROR = 9
+PART_CACHED = 0x8
 Q_HOT_KEY = 10
 Q_HOT_BATCHES = 11
 MAX_WIRE_TYPES = 16
@@ -111,7 +112,8 @@ class orl_node_stats(C.Structure):
 
 class orl_node_chunk_plan(C.Structure):
     _fields_ = [("width", C.c_uint32), ("rewrite", C.c_uint32), ("send", C.c_uint64 * NODE_MAX_RANKS),
-                ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_recv", C.c_uint64)]
+                ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_recv", C.c_uint64), ("act_lane", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 class orl_node_hop2_plan(C.Structure):
@@ -160,6 +162,9 @@ _SIGS = {
     "orl_partition_narrow_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_size_t,
                                               _P, _P, _P, _P, _P]),
     "orl_route_narrow_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, _P, _P, _P]),
+    "orl_partition_cached_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, C.c_uint32, C.c_uint32, C.c_size_t, _P,
+                                              C.c_uint32, _P, _P, _P, _P]),
+    "orl_route_received_device": (C.c_int, [_P, _P, C.c_uint32, C.c_size_t, C.c_uint32, _P, _P, _P, _P]),
     "orl_dir_insert_single_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "orl_dir_remove_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_dir_compact": (C.c_int, [_P]),

@@ -1066,7 +1066,7 @@ int orl_hash_batch(orl_ctx* c, const orl_grain_key* keys, size_t n, uint32_t* ou
 
 namespace {
 int route_impl(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
-               uint32_t* d_order, uint32_t* d_off, void* stream) {
+               uint32_t* d_order, uint32_t* d_off, void* stream, const uint32_t* d_in_act = nullptr) {
     if (!c) return ORL_E_INVALID;
     if (fmt != 8 && fmt != 16 && fmt != 32) return fail(c, ORL_E_INVALID, "record width %d (8, 16 or 32)", fmt);
     if (n && (!d_in || !d_route || !d_act)) return fail(c, ORL_E_INVALID, "null device buffer");
@@ -1083,12 +1083,23 @@ int route_impl(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, u
     if (ev) ORL_HIP(c, hipEventRecord(ev[0], st));
     if (fmt == 8 && c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
     int e = launch_route_bucket(c->d_params, dir_view(c), d_in, fmt, n, opts, c->cfg.n_act, d_route, d_act, d_order,
-                                d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
+                                d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr, d_in_act);
     if (e) return hipfail(c, (hipError_t)e, "route launch");
     if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
     return ORL_OK;
 }
 }  // namespace
+
+}  // extern "C"
+namespace orl {
+int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                       const uint32_t* d_in_act, void* stream) {
+    return route_impl(c, d_in, fmt, n, opts | ORL_OPT_NO_BUCKETS, d_route, d_act, nullptr, nullptr, stream, d_in_act);
+}
+
+bool ctx_cache_on(orl_ctx* c) { return c && c->d_cache && c->hp.cache_on; }
+}  // namespace orl
+extern "C" {
 
 int orl_route_batch_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                            uint32_t* d_order, uint32_t* d_off, void* stream) {
@@ -1317,7 +1328,7 @@ namespace orl {
 // The node's hop-1 partition: any record width, with the status word (look-back failures included) for every width.
 int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
                          uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
-                         uint32_t* d_status, void* stream) {
+                         uint32_t* d_status, void* stream, uint32_t* d_act_out) {
     if (!c || !rank_of_silo || !d_status) return ORL_E_INVALID;
     if (fmt != 8 && fmt != 16 && fmt != 32) return fail(c, ORL_E_INVALID, "record width %d", fmt);
     if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
@@ -1325,8 +1336,10 @@ int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int r = partition_prologue(c, d_in, n, rank_of_silo, nranks, my_rank, d_out, d_counts, st);
     if (r) return r;
+    const bool cached = d_act_out && ctx_cache_on(c);
     int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, fmt, nullptr,
-                                    d_counts, d_status, c->s, st);
+                                    d_counts, d_status, c->s, st, cached ? c->d_cache : nullptr,
+                                    cached ? c->cache_slots - 1 : 0, cached ? d_act_out : nullptr);
     if (e) return hipfail(c, (hipError_t)e, "node partition launch");
     return ORL_OK;
 }
@@ -1362,6 +1375,25 @@ int orl_partition_narrow_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, u
                                     d_counts, d_status, c->s, st);
     if (e) return hipfail(c, (hipError_t)e, "narrow partition launch");
     return ORL_OK;
+}
+
+int orl_partition_cached_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
+                                uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, uint32_t fmt,
+                                uint32_t* d_act_out, uint64_t* d_counts, uint32_t* d_status, void* stream) {
+    if (!c || !rank_of_silo) return ORL_E_INVALID;
+    if (n && !d_act_out) return fail(c, ORL_E_INVALID, "null act lane");
+    if (!ctx_cache_on(c) && n) {  // no cache: every record unaddressed
+        hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+        for (uint32_t r = 0; r < nranks && r < 8; ++r)
+            ORL_HIP(c, hipMemsetAsync(d_act_out + (size_t)r * stride, 0xFF, n * 4, st));
+    }
+    return ctx_partition_padded(c, d_in, n, opts, rank_of_silo, nranks, my_rank, stride, d_out, (int)fmt, d_counts, d_status,
+                                stream, d_act_out);
+}
+
+int orl_route_received_device(orl_ctx* c, const void* d_in, uint32_t fmt, size_t n, uint32_t opts, const uint32_t* d_in_act,
+                              uint32_t* d_route, uint32_t* d_act, void* stream) {
+    return ctx_route_received(c, d_in, (int)fmt, n, opts, d_route, d_act, d_in_act, stream);
 }
 
 int orl_wire_types_set(orl_ctx* c, uint32_t n, const uint64_t* tcd) {

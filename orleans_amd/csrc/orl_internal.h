@@ -301,7 +301,7 @@ int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* 
 int launch_route_bucket(const RouteParams* d_params, const DirView& dv,
                         const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route,
                         uint32_t* d_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s, void* stream,
-                        void* ev_route_begin, void* ev_route_end);
+                        void* ev_route_begin, void* ev_route_end, const uint32_t* d_in_act = nullptr);
 int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, const orl_msg_hdr* d_direct, size_t n_direct,
                                const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,
                                const uint32_t* d_pubs, const uint8_t* d_pub_silo, size_t n_pub, uint64_t follower_tcd,
@@ -358,7 +358,8 @@ size_t stamp_scan_temp_bytes(size_t n);
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
-                            Scratch& s, void* stream);
+                            Scratch& s, void* stream, const DirSlot* d_cache = nullptr, uint64_t cmask = 0,
+                            uint32_t* d_act_out = nullptr);
 // Stage 4 alone over already-routed messages (activation handles): histogram + bucket_after_route.
 int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
                        void* stream);
@@ -380,9 +381,18 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
 const uint64_t* ctx_wire_tcd(const orl_ctx* c);
 // The node's hop-1 partition (orl_api.cpp): records of `fmt` bytes (8 / 16 / 32) into padded per-rank regions, per-rank
 // counts into d_counts, and the status word (no 16-B form | no 8-B form | ORL_PART_LOOKBACK_FAILED) for every width.
+// d_act_out (optional): the context's directory cache, when populated, addresses messages with a remote owner at the
+// sender (their records go to the cached activation's rank; d_act_out, an act lane in the same padded regions, gets
+// their cached handles, ORL_NO_ACT for every other record; the status word gets ORL_PART_CACHED).
 int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
                          uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
-                         uint32_t* d_status, void* stream);
+                         uint32_t* d_status, void* stream, uint32_t* d_act_out = nullptr);
+// Whether the context's directory cache is configured and holds entries (the partition's cached destinations).
+bool ctx_cache_on(orl_ctx* c);
+// Stages 1-3 of received exchange records (fmt 8 / 16 / 32, no stage 4) with an optional act lane d_in_act: records the
+// sender addressed from its directory cache (act != ORL_NO_ACT) get HIT | CACHED without a probe.
+int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
+                       const uint32_t* d_in_act, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

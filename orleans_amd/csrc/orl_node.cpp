@@ -133,6 +133,8 @@ struct orl_node {
     uint64_t* h_heads = nullptr;                  // pinned copy
     uint64_t* h_form = nullptr;                   // pinned [2]: head word 9 of each send slot (form | digest)
     uint8_t* d_recv = nullptr;                    // owned records, chunk after chunk (max_recv x 32 B)
+    uint32_t* d_send_act[2] = {nullptr, nullptr}; // sender-cache act lane per send slot: nranks x chunk_cap (first cached batch)
+    uint32_t* d_recv_act = nullptr;               // received act lane, max_recv (first chunk that carries one)
     uint32_t *d_route = nullptr, *d_act = nullptr, *d_order = nullptr, *d_off = nullptr;
     uint64_t* d_hcount = nullptr;                 // [8] hop-2 counts by host rank
     // hop 2 (allocated on first use)
@@ -370,6 +372,7 @@ void free_node(orl_node* nd) {
     f(nd->d_ros); f(nd->d_send[0]); f(nd->d_send[1]); f(nd->d_head); f(nd->d_heads); f(nd->d_recv); f(nd->d_route); f(nd->d_act);
     f(nd->d_order); f(nd->d_off); f(nd->d_hcount); f(nd->d_fsend); f(nd->d_fsend_route); f(nd->d_fsend_act); f(nd->d_frecv);
     f(nd->d_frecv_route); f(nd->d_frecv_act); f(nd->d_forder); f(nd->d_foff); f(nd->d_fstate); f(nd->d_fcounts); f(nd->d_fan);
+    f(nd->d_send_act[0]); f(nd->d_send_act[1]); f(nd->d_recv_act);
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     if (nd->h_form) (void)hipHostFree(nd->h_form);
     if (nd->h_stall) (void)hipHostFree(nd->h_stall);
@@ -466,6 +469,8 @@ int orl_node_plan_chunk(const uint64_t* H, uint32_t nr, uint32_t me, uint32_t wr
     }
     out->width = (wide || no16) ? 32u : (all8 && !no8) ? 8u : 16u;
     out->rewrite = out->width != written;
+    for (uint32_t r = 0; r < nr; ++r)  // some sender addressed records from its directory cache: their handles travel too
+        out->act_lane |= ((uint32_t)H[r * W + 8] & ORL_PART_CACHED) ? 1u : 0u;
     for (uint32_t r = 0; r < nr; ++r) {
         out->send[r] = H[me * W + r];
         out->recv[r] = H[r * W + me];
@@ -698,6 +703,17 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     NODE_CTX(nd, orl_ctx_query(nd->ctx, ORL_Q_WIRE_DIGEST, &digest));
     const bool wide_only = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
     const uint32_t first_form = wide_only ? 32u : (digest ? 8u : 16u);
+    // The sender's directory cache (round 5): with the context's cache populated, hop 1 sends a message whose owner is
+    // remote and whose grain the cache holds straight to the rank of the cached activation, addressed (HIT | CACHED), with
+    // its handle in an act lane beside the records — LocalLookup's non-owner branch (LocalGrainDirectory.cs:690-717) before
+    // the FullLookup this exchange replaces (:719-765).  The lane travels with a chunk only when some rank cached a message
+    // of it (ORL_PART_CACHED in the all-gathered status words: every rank agrees).
+    const bool cached = ctx_cache_on(nd->ctx);
+    if (cached && !nd->d_send_act[0]) {
+        NODE_HIP(nd, hipDeviceSynchronize());
+        for (int sl = 0; sl < 2; ++sl)
+            NODE_HIP(nd, hipMalloc((void**)&nd->d_send_act[sl], (size_t)nr * nd->chunk_cap * 4));
+    }
     // Partition of chunk c into send slot c & 1 (after the slot's previous exchange): per-rank counts + wire status
     // in the slot's head words.  Chunk c + 1 is partitioned before the host waits for chunk c's counts, so the
     // partition stream does not idle through the all-gather round trip.
@@ -720,7 +736,7 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             nd->form_valid[slot] = true;
         }
         NODE_CTX(nd, ctx_partition_padded(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me, nd->chunk_cap, send,
-                                          (int)form, head, status, nd->sp));
+                                          (int)form, head, status, nd->sp, cached ? nd->d_send_act[slot] : nullptr));
         NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
         return ORL_OK;
     };
@@ -773,21 +789,30 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         // the padding fits max_recv x 32 B: a chunk of 8- or 16-B records never fills its 32-B share
         owned_bytes = (owned_bytes + 31) & ~uint64_t(31);
         uint8_t* recv = nd->d_recv + owned_bytes;
-        if (int r = exchange(nd, {Lane{send, nd->chunk_cap * width, recv, width}}, plan.send, plan.recv, nd->ev_part[slot]))
-            return r;
+        std::vector<Lane> lanes = {Lane{send, nd->chunk_cap * width, recv, width}};
+        if (plan.act_lane) {
+            if (!nd->d_recv_act) NODE_HIP(nd, hipMalloc((void**)&nd->d_recv_act, nd->cfg.max_recv * 4));
+            if (!nd->d_send_act[slot]) {  // a rank without a cache sends ORL_NO_ACT for every record
+                NODE_HIP(nd, hipDeviceSynchronize());
+                for (int sl = 0; sl < 2; ++sl)
+                    NODE_HIP(nd, hipMalloc((void**)&nd->d_send_act[sl], (size_t)nr * nd->chunk_cap * 4));
+            }
+            if (!cached)  // this rank wrote no act lane: ORL_NO_ACT over what it sends
+                for (uint32_t r = 0; r < nr; ++r)
+                    if (plan.send[r])
+                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_act[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 4, nd->sp));
+            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+            lanes.push_back(Lane{reinterpret_cast<uint8_t*>(nd->d_send_act[slot]), nd->chunk_cap * 4,
+                                 reinterpret_cast<uint8_t*>(nd->d_recv_act + owned), 4});
+        }
+        if (int r = exchange(nd, lanes, plan.send, plan.recv, nd->ev_part[slot])) return r;
         NODE_HIP(nd, hipEventRecord(nd->ev_slot[slot], nd->sx));
         nd->segs.push_back(orl_node::Seg{recv, got, width});
         if (got) {  // stages 1-3 of the received chunk, overlapping the next chunk's exchange
             NODE_HIP(nd, hipStreamWaitEvent(nd->sr, nd->ev_slot[slot], 0));
-            if (width == 32)
-                NODE_CTX(nd, orl_route_batch_device(nd->ctx, reinterpret_cast<const orl_msg_hdr*>(recv), got, ropts,
-                                                    nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
-            else if (width == 16)
-                NODE_CTX(nd, orl_route_compact_device(nd->ctx, reinterpret_cast<const orl_wire_msg*>(recv), got, ropts,
-                                                      nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
-            else
-                NODE_CTX(nd, orl_route_narrow_device(nd->ctx, reinterpret_cast<const orl_wire8*>(recv), got, ropts,
-                                                     nd->d_route + owned, nd->d_act + owned, nullptr, nullptr, nd->sr));
+            // (records a sender addressed from its cache: HIT | CACHED from the act lane, no probe)
+            NODE_CTX(nd, ctx_route_received(nd->ctx, recv, (int)width, got, ropts, nd->d_route + owned, nd->d_act + owned,
+                                            plan.act_lane ? nd->d_recv_act + owned : nullptr, nd->sr));
         }
         owned += got;
         owned_bytes += got * width;

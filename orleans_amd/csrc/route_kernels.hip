@@ -278,6 +278,48 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
     return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, vc);
 }
 
+// A hop-1 record the SENDING rank addressed from its directory cache (the node exchange's act lane holds the cached
+// activation handle, the record's target silo the cached silo; ORL_NO_ACT = not cached): the route word the sender's
+// LocalLookup cache branch decided (LocalGrainDirectory.cs:690-717 → Dispatcher.AddressMessage, Dispatcher.cs:555-579),
+// HIT | CACHED with the cached silo as host, rebuilt from the record without a directory probe at the receiver.  r is
+// route_head's word; a cached record replaces it with a final word (no probe follows).
+__device__ __forceinline__ uint32_t sender_cached(const RouteParams& P, const Msg& m, uint32_t ca, uint32_t h, uint32_t owner,
+                                                  uint32_t rf, uint32_t r, uint32_t& act) {
+    if (ca == ORL_NO_ACT) return r;
+    return route_tail(P, m, h, owner, rf, true, ca, m.meta >> 24, act, true);
+}
+
+// The hop-1 destination rank of a message with the sender's directory cache on (the node exchange, round 5): stages 1-2
+// as dest_rank; when the owner's partition is remote (LocalLookup's non-owner branch, LocalGrainDirectory.cs:690-717) the
+// cache is probed, and a hit on a valid silo (GetLocalCacheData's IsValidSilo filter, :711-717) sends the message
+// straight to the rank hosting the cached activation (cact = its handle, chost = its silo), as a reference silo sends an
+// addressed message to TargetSilo (Dispatcher.cs:555-579, OutboundMessageQueue.cs:113-145).  Otherwise the owner's rank
+// (the FullLookup path, :719-765), or this rank for messages that need no directory.
+__device__ __forceinline__ uint32_t dest_rank_cached(const RouteParams& P, const uint8_t* __restrict__ rank_of_silo,
+                                                     const DirSlot* __restrict__ cache, uint64_t cmask, const Msg& m,
+                                                     bool excl_opt, uint32_t my_rank, uint32_t& cact, uint32_t& chost) {
+    uint32_t h, owner, rf;
+    cact = ORL_NO_ACT;
+    chost = 0xFFu;
+    const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
+    if (r == kNeedProbeCache) {
+        const u32x4* c4 = reinterpret_cast<const u32x4*>(cache);
+        uint64_t slot = dir_slot(h, cmask);
+        uint32_t fact = 0, fsilo = 0;
+        int st = probe_slot(c4[2 * slot], c4[2 * slot + 1], m, fact, fsilo);
+        for (uint64_t step = 0; st == 2 && step < cmask; ++step) {
+            slot = (slot + 1) & cmask;
+            st = probe_slot(c4[2 * slot], c4[2 * slot + 1], m, fact, fsilo);
+        }
+        if (st == 0 && mask_bit(P.functional, fsilo)) {
+            cact = fact;
+            chost = fsilo;
+            return rank_of_silo[fsilo];
+        }
+    }
+    return owner == 0xFFu ? my_rank : rank_of_silo[owner];
+}
+
 // route_msg over the compact probe table for local owners (remote owners with the cache on: route_msg).
 // (the fan-out kernel reads the 16-B form; see launch_fanout_route_bucket)
 __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
@@ -619,7 +661,9 @@ __device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __rest
     return load_hdr(static_cast<const orl_msg_hdr*>(in), e);
 }
 
-template <int HB, int FMT, int PW>
+// CIN: the records come with the node exchange's act lane `in_act` (sender_cached); a template flag, since even a uniform
+// null test of the pointer cost config 2's k_route 35 us (1.277 -> 1.312 ms).
+template <int HB, int FMT, int PW, bool CIN = false>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
@@ -628,7 +672,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                                                          uint32_t excl, uint32_t* __restrict__ route,
                                                          uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt,
                                                          uint32_t bins, uint32_t shift, uint32_t items,
-                                                         const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows) {
+                                                         const uint32_t* __restrict__ hot_words, uint32_t* __restrict__ hot_rows,
+                                                         const uint32_t* __restrict__ in_act) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
@@ -652,8 +697,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         if (PW == 8) {  // same walk over the 8-B table (host-built only: no flag)
             bool can = false;
             uint2 q;
+            uint32_t cact = ORL_NO_ACT;
             if (e < n) {
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
+                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
                 if (r == kNeedProbe) {
                     can = probe8_key(sm.P, m);
                     slot = dir_slot(h, dmask);
@@ -670,7 +717,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 st = probe_slot8(q, kb, fact, fsilo);
             }
             if (e < n) {
-                uint32_t act = ORL_NO_ACT, rr = r;
+                uint32_t act = cact, rr = r;
                 if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
@@ -687,8 +734,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             // Local owner: chain walk over the 16-B probe table.  A remote owner with the cache on walks the
             // 32-B cache table (route_msg).  Same decisions as the 32-B path (the probe table mirrors `dir`).
             uint32_t mk = kNoType;
+            uint32_t cact = ORL_NO_ACT;
             if (e < n) {
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
+                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
                 if (r == kNeedProbe) {
                     mk = probe_type(sm.P, m);
                     slot = dir_slot(h, dmask);
@@ -704,7 +753,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                 st = probe_slot16(sa, m.n1, mk, fact, fsilo);
             }
             if (e < n) {
-                uint32_t act = ORL_NO_ACT, rr = r;
+                uint32_t act = cact, rr = r;
                 if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                 else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
                 store_drop(route + e, rr);
@@ -717,8 +766,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             }
             continue;
         }
+        uint32_t cact = ORL_NO_ACT;
         if (e < n) {
             r = route_head(sm.P, m, excl != 0, h, own, rf);
+            if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
             if (r >= kNeedProbeCache) {
                 if (r == kNeedProbeCache) {  // remote owner, directory cache on
                     dir4 = reinterpret_cast<const u32x4*>(cache);
@@ -739,7 +790,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             st = probe_slot(sa, sb, m, fact, fsilo);
         }
         if (e < n) {
-            uint32_t act = ORL_NO_ACT, rr = r;
+            uint32_t act = cact, rr = r;
             if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
             store_drop(route + e, rr);
             store_drop(act_out + e, act);
@@ -3007,14 +3058,18 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
 // FMT: the record written — 32 = orl_msg_hdr, 16 = orl_wire_msg (*wire_status |= 1 if a message has no 16-B form),
 // 8 = orl_wire8 (|= 1 as for 16, |= 2 if a message has no 8-B form).  wire_status (optional for FMT 32) also gets
 // ORL_PART_LOOKBACK_FAILED when a tile's look-back gave up (the record positions are then not valid).
-template <int FMT>
+// CACHE (the node exchange with the sender's directory cache on, round 5): destinations by dest_rank_cached; a cached
+// message's record carries the cached silo as its target silo and act_out (an act lane in the same padded regions) its
+// cached handle (ORL_NO_ACT for every other record); *wire_status |= ORL_PART_CACHED when the tile cached any.
+template <int FMT, bool CACHE>
 __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
                                                            void* __restrict__ out, uint32_t* __restrict__ src_index,
                                                            uint32_t* __restrict__ state, uint32_t ntiles,
                                                            uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status,
-                                                           uint32_t tbase, uint32_t epoch) {
+                                                           uint32_t tbase, uint32_t epoch, const DirSlot* __restrict__ cache,
+                                                           uint64_t cmask, uint32_t* __restrict__ act_out) {
     __shared__ PartLbSmem sm;
     const uint32_t rflags = rank_flags();
     stage_params(&sm.P, gp);
@@ -3028,7 +3083,8 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
     u32x4 h0[kPartItems], h1[kPartItems];
     uint32_t dig[kPartItems], rank[kPartItems];
     uint2 nrec[kPartItems];  // FMT 8: the records, encoded before the ranking so the 32-B headers leave the registers
-    uint32_t bad = 0;
+    uint32_t cact[CACHE ? kPartItems : 1];  // CACHE: the cached handle of each message (ORL_NO_ACT: not cached)
+    uint32_t bad = 0, ncached = 0;
     // FMT 8 loads and encodes the tile's headers in kPartGroups groups (a scheduling barrier keeps a group's loads from
     // being hoisted above the previous group's encoding), so only one group's 32-B headers are live at a time: fewer
     // VGPRs, more tiles resident per CU to cover the look-back's device round trips.  Wider records keep the headers.
@@ -3046,6 +3102,7 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
         for (uint32_t jj = 0; jj < GI; ++jj) {
             const uint32_t j = gq * GI + jj;
             dig[j] = 0;
+            if (CACHE) cact[j] = ORL_NO_ACT;
             if (wbase + j * 64u + lane < n) {
                 Msg m;
                 m.tcd = (uint64_t)h0[j].x | ((uint64_t)h0[j].y << 32);
@@ -3053,7 +3110,16 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
                 m.n1 = (uint64_t)h1[j].x | ((uint64_t)h1[j].y << 32);
                 m.meta = h1[j].z;
                 m.aux = h1[j].w;
-                dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+                if (CACHE) {
+                    uint32_t chost;
+                    dig[j] = dest_rank_cached(sm.P, sm.rank_of_silo, cache, cmask, m, excl != 0, my_rank, cact[j], chost);
+                    if (cact[j] != ORL_NO_ACT) {  // addressed: TargetSilo = the cached silo (Message.SetTargetPlacement)
+                        h1[j].z = (h1[j].z & 0x00FFFFFFu) | (chost << 24);
+                        ++ncached;
+                    }
+                } else {
+                    dig[j] = dest_rank(sm.P, sm.rank_of_silo, m, excl != 0, my_rank);
+                }
                 if (FMT == 8) {
                     u32x4 wr;
                     bad |= (encode_wire(h0[j], h1[j], wr) ? 0u : 1u) | (encode_narrow(sm.P, h0[j], h1[j], nrec[j]) ? 0u : 2u);
@@ -3063,6 +3129,7 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
         if (G > 1 && gq + 1 < G) __builtin_amdgcn_sched_barrier(0);
     }
     if (FMT == 8 && bad) atomicOr(wire_status, bad);
+    if (CACHE && __ballot(ncached != 0u) && lane == 0) atomicOr(wire_status, ORL_PART_CACHED);
     rank_steps<3, false, kPartItems, kPartRm>(&sm.lb.cnt[w][0], dig, n > wbase ? n - wbase : 0u, rank, rflags);
     __syncthreads();
     lookback_ranks(sm.lb, state, nranks, ntiles, counts, nullptr, epoch, wire_status);
@@ -3085,6 +3152,7 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
                 dp[1] = h1[j];
             }
             if (src_index) src_index[g] = e;
+            if (CACHE) act_out[g] = cact[j];
         }
     }
 }
@@ -4300,7 +4368,8 @@ int launch_probe_build(const DirSlot* d_dir, uint64_t slots, const RouteParams* 
 
 int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const void* d_in, int fmt,
                         size_t n, uint32_t opts, uint32_t n_act, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
-                        uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end) {
+                        uint32_t* d_offsets, const Scratch& s, void* stream, void* ev_begin, void* ev_end,
+                        const uint32_t* d_in_act) {
     hipStream_t st = (hipStream_t)stream;
     const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
@@ -4320,21 +4389,25 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     uint32_t* hr = hot ? s.hot_rows : nullptr;
     uint16_t* th = hist ? s.tile_cnt : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
-#define ORL_ROUTE(H, W, Q) hipLaunchKernelGGL((k_route<H, W, Q>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir,   \
-                                              dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                                     \
-                                              (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr)
+    if (d_in_act && hist) return (int)hipErrorInvalidValue;  // the act lane is the node's (no stage 4 in the same call)
+#define ORL_ROUTE_C(H, W, Q, C) hipLaunchKernelGGL((k_route<H, W, Q, C>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
+                                                   dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                         \
+                                                   (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr, d_in_act)
+#define ORL_ROUTE(H, W, Q) do { if (H == 0 && d_in_act) ORL_ROUTE_C(0, W, Q, true); else ORL_ROUTE_C(H, W, Q, false); } while (0)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
-#define ORL_ROUTE8(H, W) hipLaunchKernelGGL((k_route<H, W, 8>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
-                                            dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
-                                            shift, items, hw, hr)
+#define ORL_ROUTE8C(H, W, C) hipLaunchKernelGGL((k_route<H, W, 8, C>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
+                                                dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
+                                                shift, items, hw, hr, d_in_act)
+#define ORL_ROUTE8(H, W) do { if (H == 0 && d_in_act) ORL_ROUTE8C(0, W, true); else ORL_ROUTE8C(H, W, false); } while (0)
         if (hist) {
             if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
         } else {
             if (fmt == 16) ORL_ROUTE8(0, 16); else if (fmt == 8) ORL_ROUTE8(0, 8); else ORL_ROUTE8(0, 32);
         }
 #undef ORL_ROUTE8
+#undef ORL_ROUTE8C
     } else if (dv.probe) {
         if (hist) ORL_ROUTE_W(kMaxDigitBits, 16); else ORL_ROUTE_W(0, 16);
     } else {
@@ -4342,6 +4415,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     }
 #undef ORL_ROUTE_W
 #undef ORL_ROUTE
+#undef ORL_ROUTE_C
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();
     if (e) return e;
@@ -4658,7 +4732,7 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
-                            Scratch& s, void* stream) {
+                            Scratch& s, void* stream, const DirSlot* d_cache, uint64_t cmask, uint32_t* d_act_out) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipSuccess;
     if (fmt != 8 && fmt != 16 && fmt != 32) return (int)hipErrorInvalidValue;
@@ -4676,12 +4750,19 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
         s.lb_epoch = 1;
     }
     const uint32_t tbase = s.lb_ticket, epoch = s.lb_epoch;
-#define ORL_PLB(F) hipLaunchKernelGGL(k_part_lb<F>, dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in,     \
-                                      (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles, d_counts, \
-                                      d_wire_status, tbase, epoch)
-    if (fmt == 16) ORL_PLB(16);
-    else if (fmt == 8) ORL_PLB(8);
-    else ORL_PLB(32);
+    const bool cached = d_cache && d_act_out && d_wire_status;
+#define ORL_PLB(F, C) hipLaunchKernelGGL((k_part_lb<F, C>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, \
+                                         (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles,        \
+                                         d_counts, d_wire_status, tbase, epoch, d_cache, cmask, d_act_out)
+    if (cached) {
+        if (fmt == 16) ORL_PLB(16, true);
+        else if (fmt == 8) ORL_PLB(8, true);
+        else ORL_PLB(32, true);
+    } else {
+        if (fmt == 16) ORL_PLB(16, false);
+        else if (fmt == 8) ORL_PLB(8, false);
+        else ORL_PLB(32, false);
+    }
 #undef ORL_PLB
     e = hipGetLastError();
     if (e == hipSuccess) {

@@ -398,6 +398,22 @@ class GrainDirectoryEngine:
                                                        int(my_rank), int(stride), ptr(d_out), ptr(d_src_index),
                                                        ptr(d_counts), ptr(d_status), ptr(stream)))
 
+    def partition_cached_device(self, d_msgs, n: int, rank_of_silo: Sequence[int], nranks: int, my_rank: int,
+                                stride: int, d_out, fmt: int, d_act_out, d_counts, d_status, stream=None, opts: int = 0) -> None:
+        """The node's hop-1 partition with this context's directory cache (orl_partition_cached_device): messages with a
+        remote owner and a cached grain go to the cached activation's rank, addressed, with the handle in d_act_out."""
+        ros = np.zeros(256, np.uint8)
+        ros[:len(rank_of_silo)] = np.asarray(rank_of_silo, dtype=np.uint8)
+        self._ck(self._lib.orl_partition_cached_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(ros), int(nranks),
+                                                       int(my_rank), int(stride), ptr(d_out), int(fmt), ptr(d_act_out),
+                                                       ptr(d_counts), ptr(d_status), ptr(stream)))
+
+    def route_received_device(self, d_recs, fmt: int, n: int, d_in_act, d_route, d_act, stream=None, opts: int = 0) -> None:
+        """Stages 1-3 of received hop-1 records with their act lane (orl_route_received_device): records addressed by the
+        sender's cache become HIT | CACHED without a probe."""
+        self._ck(self._lib.orl_route_received_device(self._ctx, ptr(d_recs), int(fmt), int(n), int(opts), ptr(d_in_act),
+                                                     ptr(d_route), ptr(d_act), ptr(stream)))
+
     def address_narrow_device(self, d_recs, n: int, d_route, d_act, d_order=None, d_offsets=None, stream=None,
                               opts: int = 0) -> None:
         """address_messages_device over 8-B exchange records (orl_wire8, this context's wire types)."""

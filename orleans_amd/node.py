@@ -31,6 +31,7 @@ class ChunkPlan:
     send: List[int]     # records to each rank
     recv: List[int]     # records from each rank (back to back, rank order)
     n_recv: int
+    act_lane: bool = False  # a sender's directory cache addressed records: a u32 handle per record travels beside them
 
 
 @dataclass
@@ -54,7 +55,7 @@ def plan_chunk(heads: np.ndarray, me: int, written: int, max_recv: int, owned_to
     rc = L.load().orl_node_plan_chunk(L.ptr(h), nr, int(me), int(written), int(max_recv), L.ptr(owned_total), C.byref(out))
     if rc != L.OK:
         raise L.OrleansRouteError(rc, "orl_node_plan_chunk")
-    return ChunkPlan(out.width, bool(out.rewrite), list(out.send)[:nr], list(out.recv)[:nr], out.n_recv)
+    return ChunkPlan(out.width, bool(out.rewrite), list(out.send)[:nr], list(out.recv)[:nr], out.n_recv, bool(out.act_lane))
 
 
 def plan_hop2(heads: np.ndarray, me: int, n_owned: int, width_mask: int, max_recv: int) -> Hop2Plan:

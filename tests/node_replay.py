@@ -77,21 +77,61 @@ def host_rank(route: np.ndarray, ros: np.ndarray, me: int) -> np.ndarray:
     return np.where(h == 0xFF, me, ros[np.minimum(h, 7).astype(np.int64)])
 
 
-def expected(oracles, ros, batches, chunks, n_act):
-    """The oracle's replay of one batch per rank -> ([per rank (route, act, order, offsets, hosted headers)], forward)."""
+def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None):
+    """The oracle's replay of one batch per rank -> ([per rank (route, act, order, offsets, hosted headers)], forward).
+
+    caches[s] (optional): rank s's directory cache {(tcd, n0, n1): (act, silo)}.  A message whose owner is on another rank
+    and whose grain rank s caches on a functional silo is addressed at the sender (LocalLookup's cache branch,
+    LocalGrainDirectory.cs:690-717; pyref.apply_directory_cache: HIT | CACHED, TargetSilo = the cached silo) and sent to
+    the rank hosting that silo instead of the owner's; the others follow the oracle partition by owner rank."""
+    from oracle import pyref as P
     nr = len(batches)
+    functional = functional if functional is not None else [1] * 8
     owned = [[] for _ in range(nr)]
+    pre = [[] for _ in range(nr)]  # per owned record: (route, act) the sender's cache decided, or None
     for c in range(chunks):
         for s in range(nr):
             lo, hi = chunk_bounds(len(batches[s]), chunks, c)
-            ch = batches[s][lo:hi]
+            ch = batches[s][lo:hi].copy()
             src, cnt = oracles[0].partition(ch, ros, nr, s)
+            dest = np.zeros(len(ch), np.int64)
             o0 = 0
             for d in range(nr):
-                owned[d].append(ch[src[o0:o0 + int(cnt[d])]])
+                dest[src[o0:o0 + int(cnt[d])]] = d
                 o0 += int(cnt[d])
+            croute = np.full(len(ch), -1, np.int64)
+            cact = np.zeros(len(ch), np.uint32)
+            if caches is not None and caches[s] and len(ch):
+                r0, a0 = oracles[s].route(ch)  # rank s's view: REMOTE_OWNER for grains owned elsewhere
+                kt = list(zip(ch["tcd"].tolist(), ch["n0"].tolist(), ch["n1"].tolist()))
+                r1, a1 = P.apply_directory_cache(r0.tolist(), a0.tolist(), ch["sending_silo"].tolist(), kt, caches[s],
+                                                 functional)
+                r1 = np.array(r1, np.uint32)
+                hit = (r1 >> 24) & 0x08 != 0
+                hit &= ((r0 >> 16) & 0xFF) == L.ST_REMOTE_OWNER
+                hs = ((r1 >> 8) & 0xFF).astype(np.int64)
+                dest[hit] = ros[hs[hit]]
+                croute[hit] = r1[hit]
+                cact[hit] = np.array(a1, np.uint32)[hit]
+                ch["target_silo"][hit] = hs[hit].astype(np.uint8)  # the addressed record's TargetSilo
+            order = np.argsort(dest, kind="stable")
+            for d in range(nr):
+                sel = order[dest[order] == d]
+                owned[d].append(ch[sel])
+                pre[d].append((croute[sel], cact[sel]))
     owned = [np.concatenate(x) if x else np.zeros(0, L.MSG_DTYPE) for x in owned]
-    routed = [oracles[d].route(owned[d]) for d in range(nr)]
+    routed = []
+    for d in range(nr):
+        r, a = oracles[d].route(owned[d])
+        if pre[d]:
+            cr = np.concatenate([x[0] for x in pre[d]])
+            ca = np.concatenate([x[1] for x in pre[d]])
+            m = cr >= 0
+            r = r.copy()
+            a = a.copy()
+            r[m] = cr[m].astype(np.uint32)
+            a[m] = ca[m]
+        routed.append((r, a))
     hostr = [host_rank(routed[d][0], ros, d) for d in range(nr)]
     forward = any((hostr[d] != d).any() for d in range(nr))
     out = []

@@ -126,6 +126,81 @@ def test_node_local_transport_vs_oracle(torch, nranks, chunks, host_mix, wire):
     world.close()
 
 
+def _fill_caches(t, world, frac, stale_frac, seed, skip_rank=None):
+    """Each rank's directory cache (orl_cache_add_or_update_device): `frac` of the registered grains whose directory entry
+    another rank holds, with their true activation (the earlier lookups' results, LocalGrainDirectory.cs:761-762), plus
+    `stale_frac` as many entries pointing at another activation / silo (stale entries: the sender follows its cache, as the
+    reference's does).  Returns the per-rank caches as {(tcd, n0, n1): (act, silo)} for node_replay.expected."""
+    p = world.p
+    rng = np.random.default_rng(seed)
+    caches = []
+    for r in range(world.nr):
+        if r == skip_rank:
+            caches.append({})
+            continue
+        remote = np.nonzero(p.reg & (p.ros[p.owner] != r))[0]
+        pick = rng.choice(remote, int(len(remote) * frac), replace=False)
+        acts = p.act[pick].copy()
+        silos = p.host[pick].copy()
+        stale = rng.choice(remote, int(len(remote) * stale_frac), replace=False)
+        acts = np.concatenate([acts, rng.integers(0, world.n_act, len(stale)).astype(np.uint32)])
+        silos = np.concatenate([silos, rng.integers(0, 8, len(stale)).astype(np.uint8)])
+        pick = np.concatenate([pick, stale])  # a grain in both: the batch's last writer (the stale entry) wins
+        e = world.engs[r]
+        e.cache_config(max(len(pick), 16))
+        dev = lambda a: t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()  # noqa: E731
+        e.cache_add_or_update_device(dev(p.keys[pick]), dev(acts), dev(silos), len(pick),
+                                     stream=t.cuda.current_stream().cuda_stream)
+        c = {}
+        for g, a, sl in zip(pick.tolist(), acts.tolist(), silos.tolist()):
+            c[(int(p.keys["tcd"][g]), int(p.keys["n0"][g]), int(p.keys["n1"][g]))] = (int(a), int(sl))
+        caches.append(c)
+    t.cuda.synchronize()
+    return caches
+
+
+@pytest.mark.parametrize("nranks,chunks,host_mix,wire,skip", [(2, 2, 0.0, "both", None), (3, 3, 0.3, "both", None),
+                                                              (4, 4, 0.3, None, None), (4, 2, 0.3, "both", 1),
+                                                              (8, 4, 0.0, "both", None), (8, 3, 0.3, "grain_only", 5)])
+def test_node_sender_cache_vs_oracle(torch, nranks, chunks, host_mix, wire, skip):
+    """the sender's directory cache in the node exchange.  A message whose owner is on another rank and
+    whose grain the sending rank's cache holds (on a functional silo) is addressed at the sender — HIT | CACHED, TargetSilo
+    = the cached silo (LocalLookup's non-owner branch, LocalGrainDirectory.cs:690-717; Dispatcher.AddressMessage,
+    Dispatcher.cs:555-579) — and travels in hop 1 straight to the rank hosting the cached activation with its handle in the
+    act lane; the receiver routes it without a probe.  Caches hold true entries for half the remote grains and stale ones for
+    a few; one rank may have none (it sends ORL_NO_ACT in the lane).  Every rank's hosted output of two batches (8-, 16-
+    and 32-B chunks, with and without hop 2) == the oracle's replay with the same caches."""
+    t = torch
+    ros = None if nranks != 3 else [s % 3 for s in range(8)]
+    world = World(nranks, host_mix=host_mix, ros=ros)
+    world.set_wire_types(wire)
+    caches = _fill_caches(t, world, 0.5, 0.05, seed=nranks * 7 + chunks, skip_rank=skip)
+    gid = b"node-cache-%d-%d-%d-%s" % (nranks, chunks, int(host_mix * 10), str(skip).encode())
+    nodes = [GrainNode(world.engs[r], nranks, r, world.ros, max_batch=200_000, max_recv=400_000,
+                       transport=L.TRANSPORT_LOCAL, group_id=gid, chunks=chunks) for r in range(nranks)]
+    streams = [t.cuda.Stream() for _ in range(nranks)]
+    for b in range(2):
+        batches = [world.messages(r, 120_000 - 5000 * r - 1000 * b, seed=300 * b + r,
+                                  wide_at=(50_000 if (b == 1 and r == nranks - 1) else None)) for r in range(nranks)]
+        got = _run(t, world, nodes, batches, streams)
+        exp, forward = R.expected(world.oracles, world.ros, batches, chunks, world.n_act, caches=caches)
+        n_cached = 0
+        for r in range(nranks):
+            res, (route, act, order, off, hdrs) = got[r]
+            er, ea, eo, ef, eh = exp[r]
+            assert res.hop2 == forward
+            np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} batch {b} headers")
+            np.testing.assert_array_equal(route, er, err_msg=f"rank {r} batch {b} route")
+            np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} batch {b} act")
+            np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} batch {b} order")
+            np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} batch {b} offsets")
+            n_cached += int(((route >> 24) & L.RF_CACHED != 0).sum())
+        assert n_cached > 0.2 * sum(len(x) for x in batches), n_cached  # the caches addressed a real share
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("host_mix", [0.0, 0.3])
 def test_node_config3_8ranks_vs_oracle(torch, host_mix):
