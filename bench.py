@@ -80,6 +80,47 @@ def owner_rank_counts(torch, cl, d_msgs, n, ros, world, device=0, piece=1 << 22)
     return total
 
 
+class WarmCaches:
+    """The bench's warm sender directory caches (--sender-cache N): rank s caches the N hottest grains of the Zipf stream
+    (rank order = the workload's permutation) that are registered and owned by another rank, with the handle their owner's
+    catalog registered (dense per owner rank) and the owner silo (activations live on their owners).  thresh[s] = the
+    Zipf position of rank s's last cached grain, so the self-check can tell which hosted messages a sender addressed."""
+
+    def __init__(self, zperm, reg, owner, ros, world, n):
+        self.n = int(n)
+        orank = ros[owner]
+        self.pos = np.empty(len(zperm), np.int64)
+        self.pos[zperm] = np.arange(len(zperm))
+        self.orank = orank
+        self.handle = np.zeros(len(owner), np.uint32)
+        for r in range(world):
+            idx = np.nonzero(reg & (orank == r))[0]
+            self.handle[idx] = np.arange(len(idx), dtype=np.uint32)
+        self.grains, self.thresh = [], []
+        for s in range(world):
+            z = zperm[:min(len(zperm), 2 * self.n)]
+            z = z[reg[z] & (orank[z] != s)]
+            while len(z) < self.n and len(z) < int((reg & (orank != s)).sum()):  # (tiny populations only)
+                z = zperm[reg[zperm] & (orank[zperm] != s)]
+            g = z[:self.n]
+            self.grains.append(g)
+            self.thresh.append(int(self.pos[g[-1]]) if len(g) else -1)
+
+    def fill(self, torch, eng, keys, owner, s, stream):
+        g = self.grains[s]
+        eng.cache_config(max(self.n, 16))
+        if len(g):
+            eng.cache_add_or_update_device(torch.from_numpy(np.ascontiguousarray(keys[g]).view(np.uint8)).cuda(),
+                                           torch.from_numpy(self.handle[g].view(np.int32)).cuda(),
+                                           torch.from_numpy(owner[g].astype(np.uint8)).cuda(), len(g), stream=stream)
+        torch.cuda.synchronize()
+
+    def addressed(self, grains, senders, me):
+        """Whether the sender rank of each hosted message addressed it from its cache (its owner is `me`)."""
+        t = np.asarray(self.thresh, np.int64)[senders]
+        return (senders != me) & (self.pos[grains] <= t)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +149,11 @@ def main():
     ap.add_argument("--unregistered", type=float, default=0.0,
                     help="configs 2/3: fraction of the grains never registered (SURVEY §8(d) config 2's 10%% variant: "
                          "their messages miss the directory and are placed PreferLocal)")
+    ap.add_argument("--sender-cache", type=int, default=0,
+                    help="N > 1 (and --local-ranks), config 3: every rank's directory cache holds this many entries, warm: "
+                         "the hottest grains of the Zipf stream whose directory entry another rank holds (the reference's "
+                         "default cache capacity is 1M, GlobalConfiguration.cs:413,417); hop 1 then addresses those messages "
+                         "at the sender (LocalGrainDirectory.cs:690-717)")
     ap.add_argument("--wire16", action="store_true",
                     help="N > 1: exchange 16-B records (no wire types) instead of the 8-B form")
     ap.add_argument("--cpu-wall", type=float, default=1.5, help="target wall seconds of the CPU baseline sample")
@@ -211,7 +257,8 @@ def read_traffic(path, msgs_per_launch, world, config):
 
 
 # ---- the node's correctness evidence (checker: after the timed steps, outside timing) ------------------------
-def node_self_check(torch, eng, res, rank, cl, keys, owner, reg, local_mask, n_act, ros, expect_owned, sample, stream=None):
+def node_self_check(torch, eng, res, rank, cl, keys, owner, reg, local_mask, n_act, ros, expect_owned, sample, stream=None,
+                    caches=None):
     """One rank's hosted output of the last timed batch: the size-independent properties of every hosted message on the
     device (orleans_amd/selfcheck.py: owner / host / status / handle per message, a permutation grouped by activation, FIFO
     inside every bucket, offsets = the count prefix), the owned count against the workload's own per-destination count,
@@ -252,6 +299,10 @@ def node_self_check(torch, eng, res, rank, cl, keys, owner, reg, local_mask, n_a
         sel = np.nonzero(h >= 0)[0]
         o.register(keys[sel], h[sel].astype(np.uint32), owner[sel])
         r_ref, a_ref = o.route(hdr)
+        if caches is not None:  # messages the sender addressed from its warm cache: HIT | CACHED (same host and handle)
+            sent = np.asarray(ros, np.int64)[hdr["sending_silo"].astype(np.int64)]
+            cached = caches.addressed(hdr["n1"].astype(np.int64), sent, rank)
+            r_ref = np.where(cached, r_ref | np.uint32(L.RF_CACHED << 24), r_ref).astype(np.uint32)
         r_got = d["route"][:k].cpu().numpy().astype(np.uint32)
         a_got = d["act"][:k].cpu().numpy().astype(np.uint32)
         if not np.array_equal(r_got, r_ref):
@@ -308,10 +359,14 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
         eng.set_wire_types([W.grain_tcd(cl)])
     n_reg = W.register_population(eng, keys, owner, reg, local_mask, dense_local=world > 1)
     del uni
+    caches = None
+    if world > 1 and args.sender_cache and zipf:  # warm sender directory caches (the reference's default path, f4)
+        caches = WarmCaches(ztab[1].cpu().numpy(), reg, owner, ros, world, args.sender_cache)
+        caches.fill(torch, eng, keys, owner, rank, torch.cuda.current_stream().cuda_stream)
     if world == 1:
         del keys
     log(f"rank {rank}/{world}: silos {[int(s) for s in mine]}, {n_reg} grains registered, {n_msgs} messages, "
-        f"receive capacity {cap}")
+        f"receive capacity {cap}" + (f", sender cache {args.sender_cache} entries" if caches else ""))
     stream = torch.cuda.current_stream().cuda_stream
     stats = {}
     if args.host_io:
@@ -385,7 +440,7 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     if node is not None:  # correctness evidence of the multi-GPU run: every rank checks what it hosted (outside timing)
         t_chk = time.perf_counter()
         errs = node_self_check(torch, eng, stats["last"], rank, cl, keys, owner, reg, local_mask, n_act, ros, expect_owned,
-                               args.check_sample, stream=stream)
+                               args.check_sample, stream=stream, caches=caches)
         tot = torch.tensor([stats["last"].n_hosted], dtype=torch.int64, device="cuda")
         dist.all_reduce(tot)
         if int(tot.item()) != n_total:
@@ -407,6 +462,9 @@ def run_single_target(args, torch, dist, rank, world, local_rank):
     if world > 1:
         name += (", + owner partition, RCCL counts all-gather + grouped send/recv, routing at the owner, hop 2, "
                  f"stage 4 at the host (orl_node, {args.chunks} chunks)")
+        if caches:
+            name += (f", warm sender directory caches of {args.sender_cache} entries per rank (the hottest remote grains; "
+                     "cached messages addressed at the sender)")
     out = {
         "metric": "routed grain messages/sec (node)",
         "value": value,
@@ -481,6 +539,7 @@ def run_rehearsal(args, torch):
     cap = max(n_msgs, int(per_dest.max().item()))
     cap += cap // 64 + 4096
     engs, nodes, streams, masks, n_acts = [], [], [], [], []
+    caches = WarmCaches(ztab[1].cpu().numpy(), reg, owner, ros, R, args.sender_cache) if (args.sender_cache and zipf) else None
     gid = b"bench-rehearsal"
     expect_owned = [int(x) for x in per_dest.cpu().numpy()]
     for r in range(R):
@@ -495,6 +554,8 @@ def run_rehearsal(args, torch):
         if not args.wire16:
             e.set_wire_types([W.grain_tcd(cl)])
         W.register_population(e, keys, owner, reg, mask, dense_local=True)
+        if caches is not None:
+            caches.fill(torch, e, keys, owner, r, None)
         engs.append(e)
         nodes.append(GrainNode(e, R, r, ros, max_batch=n_msgs, max_recv=cap, transport=L.TRANSPORT_LOCAL, group_id=gid,
                                chunks=args.chunks))
@@ -532,7 +593,7 @@ def run_rehearsal(args, torch):
     bad = []
     for r in range(R):
         errs = node_self_check(torch, engs[r], stats[r]["last"], r, cl, keys, owner, reg, masks[r], n_acts[r], ros,
-                               expect_owned[r], args.check_sample)
+                               expect_owned[r], args.check_sample, caches=caches)
         if errs:
             log(f"rank {r}: segments (count, width) {[(c, w) for _, c, w in stats[r]['last'].segments]}")
         bad += [f"rank {r}: {e}" for e in errs]
@@ -551,7 +612,10 @@ def run_rehearsal(args, torch):
             "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "none",
             "vs_baseline": None, "dtype": "u32/u64 integer", "data": f"synthetic (config {args.config})",
             "config": {"workload": f"config{args.config} split over {R} ranks ({n_msgs} messages each), orl_node LOCAL "
-                                   f"transport, {args.chunks} chunks", "receive_capacity": cap},
+                                   f"transport, {args.chunks} chunks" + (f", warm sender directory caches of "
+                                                                         f"{args.sender_cache} entries per rank"
+                                                                         if caches else ""),
+                       "receive_capacity": cap},
             "owned_per_rank": owned, "max_over_mean_owned": max(owned) / (sum(owned) / R),
             "sent_remote_per_rank": [st["remote"] / args.steps for st in stats],
             "exchange": {"ncclCommCount": stats[0]["comm_count"], "mode": stats[0]["exchange_mode"],

@@ -345,13 +345,48 @@ int orl_ring_owner_batch_device(orl_ctx* ctx, uint32_t kind, const uint32_t* d_k
 int orl_stream_queue_batch_device(orl_ctx* ctx, uint32_t kind, const uint8_t* d_guids, size_t n, uint32_t n_queues,
                                   uint32_t me, uint32_t opts, uint32_t* d_queue, uint8_t* d_silo, void* stream);
 
+/* ---- KeyExt (string-key) grains in the directory (round 5) --------------------------------------------
+ * GrainDirectoryPartition holds any GrainId (GrainDirectoryPartition.cs:270-287,326-344); a KeyExt grain's identity is
+ * its UniqueKey including the string extension, and its uniform hash is Jenkins over Write(UniqueKey) (UniqueKey.cs:288-
+ * 294: N0, N1, TypeCodeData, int32 length, UTF-8).  The context keeps KeyExt grains in a table of their own: the 24-B key,
+ * the hash and the extension bytes (a blob the library owns), first writer wins like the main partition.  A string is
+ * passed as orl_ext_ref into a caller's UTF-8 blob (host or device as the call says). */
+typedef struct orl_ext_ref {
+    uint32_t off;  /* first byte in the blob */
+    uint32_t len;  /* bytes (UTF-8, as BinaryTokenStreamWriter.Write(string) writes them) */
+} orl_ext_ref;
+/* RegisterSingleActivation of KeyExt grains (category ORL_CAT_KEYEXT_GRAIN; the same statuses as orl_dir_insert_single:
+ * owner = the ring owner of the KeyExt hash, excludeThisSiloIfStopping; a key of another category gives
+ * ORL_INS_UNSUPPORTED).  Host arrays; `blob` holds the extensions. */
+int orl_dir_insert_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                          const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* winner_act,
+                          uint8_t* winner_silo, uint8_t* status);
+int orl_dir_remove_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
+                          uint8_t* removed);
+/* LookUpGrain of KeyExt grains on the host copy (no IsValidSilo filter; ORL_NO_ACT / ORL_NULL_SILO when absent). */
+int orl_dir_lookup_keyext_host(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                               size_t n, uint32_t* act, uint8_t* silo);
+int orl_dir_keyext_count(const orl_ctx* ctx, uint64_t* n);
+/* orl_route_batch_device with the batch's KeyExt strings: d_ext[i] locates message i's extension in d_blob (device,
+ * blob_bytes long; read only for KeyExt messages).  A KeyExt message whose header carries ORL_HDR_HASH_VALID uses that
+ * hash, otherwise the kernel computes it from the bytes.  Its owner's KeyExt table is probed when the owner is local:
+ * HIT (IsValidSilo-filtered), or a miss placed like any grain (PlacementDirectorsManager); a remote owner gives
+ * ORL_ST_REMOTE_OWNER (the FullLookup path).  A reference outside the blob leaves ORL_ST_KEYEXT_UNRESOLVED.  Other
+ * messages route exactly as in orl_route_batch_device; stage 4 follows as there. */
+int orl_route_keyext_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                            const uint8_t* d_blob, uint64_t blob_bytes, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                            uint32_t* d_bucket_offsets, void* stream);
+
 /* ---- directory cache -----------------------------------------------------------
  * AdaptiveGrainDirectoryCache (src/OrleansRuntime/GrainDirectory/AdaptiveGrainDirectoryCache.cs) as a device
  * table consulted by the route kernels for grains whose directory owner is remote: LocalGrainDirectory.LocalLookup's
  * cache branch (LocalGrainDirectory.cs:691-702, GetLocalCacheData :711-717: entries on invalid silos are
  * filtered).  A hit is ORL_ST_HIT with ORL_RF_CACHED (host = the cached activation's silo); a miss stays
- * ORL_ST_REMOTE_OWNER (the FullLookup path).  Cached activations use the caller's activation-handle space
- * [0, n_act), so stage 4 groups messages to a remote activation like a local one (its outbound batch, FIFO).
+ * ORL_ST_REMOTE_OWNER (the FullLookup path).  Cached activations on this context's silos use its activation-handle
+ * space [0, n_act) (entries outside it are dropped), so stage 4 groups messages to them like any other; an activation
+ * on a silo the context does not host keeps the handle its host's catalog gave it (any value but ORL_NO_ACT: the node
+ * exchange delivers such messages to the host rank, whose stage 4 buckets them; in a single context they share the
+ * unresolved bucket when the handle is >= n_act).
  * AddOrUpdate: the batch's last writer of a key wins.  Remove = CACHE_INVALIDATION_HEADER handling
  * (InsideGrainClient.cs:298-308).  Expiry / size policy (the maintainer) stays with the host: remove or clear. */
 #define ORL_RF_CACHED 0x08u

@@ -392,6 +392,20 @@ def register_single_activation(ring: "Ring", part: "Partition", view: "SiloView"
     return part.add_single_activation(key, act, silo, view)
 
 
+def register_keyext(ring: "Ring", part: "Partition", view: "SiloView", key: Key, act: int, silo: int) -> Tuple[int, int, int]:
+    """RegisterSingleActivationAsync for a KeyExt grain (the engine's KeyExt table, round 5): the same steps as
+    register_single_activation with the owner of the KeyExt uniform hash (UniqueKey.cs:288-294); GrainDirectoryPartition
+    keys it by the whole UniqueKey, extension included (Partition._k).  Non-KeyExt keys: INS_UNSUPPORTED."""
+    if key.category != CAT_KEYEXT_GRAIN or key.key_ext is None:
+        return INS_UNSUPPORTED, NO_ACT, NULL_SILO
+    owner, code = calculate_target_silo(ring, key, uniform_hash(key), silo, view, True)
+    if code != OWN_OK:
+        return INS_OWNER_NULL, NO_ACT, NULL_SILO
+    if not view.is_local(owner):
+        return INS_REMOTE_OWNER, NO_ACT, NULL_SILO
+    return part.add_single_activation(key, act, silo, view)
+
+
 # ---------------------------------------------------------------------------------------
 # Full per-message routing decision (Dispatcher.AddressMessage + placement)
 # ---------------------------------------------------------------------------------------
@@ -444,7 +458,7 @@ def placement_silo(policy: int, me: int, hash32: int, view: SiloView) -> int:
 
 
 def route_one(m: Msg, ring: Ring, part: Partition, view: SiloView, exclude_if_stopping: bool = False,
-              policy: int = POLICY_PREFER_LOCAL) -> Tuple[int, int]:
+              policy: int = POLICY_PREFER_LOCAL, keyext_directory: bool = False) -> Tuple[int, int]:
     """One message: returns (route word, activation handle).
 
     Dispatcher.AddressMessage (Dispatcher.cs:555-579): complete TargetAddress -> untouched;
@@ -469,7 +483,7 @@ def route_one(m: Msg, ring: Ring, part: Partition, view: SiloView, exclude_if_st
         return pack_route(NULL_SILO, NULL_SILO, ST_OWNER_NULL, 0), NO_ACT
     if key.category == CAT_SYSTEM_TARGET:                                # InsideGrainClient.cs:174-181
         return pack_route(owner, me, ST_SYSTEM_TARGET, FL_LOOPBACK), NO_ACT
-    if key.category == CAT_KEYEXT_GRAIN:      # ValidateKeyExt (UniqueKey.cs:328+) forbids a null KeyExt
+    if key.category == CAT_KEYEXT_GRAIN and not keyext_directory:  # the plain route entry points leave them to the host
         return pack_route(owner, NULL_SILO, ST_KEYEXT_UNRESOLVED, fl), NO_ACT
     if not view.is_local(owner):              # LocalLookup non-owner branch -> cache / remote FullLookup (:711-754)
         return pack_route(owner, NULL_SILO, ST_REMOTE_OWNER, fl), NO_ACT
@@ -486,10 +500,10 @@ def route_one(m: Msg, ring: Ring, part: Partition, view: SiloView, exclude_if_st
 
 
 def route_batch(msgs: Sequence[Msg], ring: Ring, part: Partition, view: SiloView,
-                exclude_if_stopping: bool = False, policy: int = POLICY_PREFER_LOCAL):
+                exclude_if_stopping: bool = False, policy: int = POLICY_PREFER_LOCAL, keyext_directory: bool = False):
     routes, acts = [], []
     for m in msgs:
-        r, a = route_one(m, ring, part, view, exclude_if_stopping, policy)
+        r, a = route_one(m, ring, part, view, exclude_if_stopping, policy, keyext_directory)
         routes.append(r)
         acts.append(a)
     return routes, acts

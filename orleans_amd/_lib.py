@@ -71,6 +71,7 @@ INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, 
 
 # orl_grain_key / orl_msg_hdr as numpy structured dtypes (byte-identical to the C structs)
 KEY_DTYPE = np.dtype([("tcd", "<u8"), ("n0", "<u8"), ("n1", "<u8")])
+EXT_REF_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])  # orl_ext_ref: a KeyExt string in a UTF-8 blob
 MSG_DTYPE = np.dtype([("tcd", "<u8"), ("n0", "<u8"), ("n1", "<u8"), ("sending_silo", "u1"), ("category", "u1"),
                       ("flags", "u1"), ("target_silo", "u1"), ("aux", "<u4")])
 assert KEY_DTYPE.itemsize == 24 and MSG_DTYPE.itemsize == 32
@@ -139,6 +140,11 @@ _SIGS = {
     "orl_keyext_uniform_hash": (C.c_uint32, [_P, C.c_char_p, C.c_size_t]),
     "orl_dir_insert_single": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P]),
     "orl_dir_remove": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "orl_dir_insert_keyext": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_size_t, _P, _P, _P]),
+    "orl_dir_remove_keyext": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),
+    "orl_dir_lookup_keyext_host": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P]),
+    "orl_dir_keyext_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "orl_route_keyext_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64, _P, _P, _P, _P, _P]),
     "orl_dir_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_dir_lookup_host": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "orl_hash_batch": (C.c_int, [_P, _P, C.c_size_t, _P]),

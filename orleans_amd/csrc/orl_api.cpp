@@ -226,6 +226,14 @@ struct orl_ctx {
     uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
     uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
     uint8_t* d_dflag = nullptr;      // per-message flag of a device cache batch
+    // KeyExt grains (round 5): host table + extension blob, uploaded whole when changed
+    std::vector<ExtSlot> ext_table;
+    std::vector<uint8_t> ext_blob;
+    uint64_t ext_count = 0, ext_tombs = 0;
+    bool ext_dirty = false;
+    ExtSlot* d_ext_table = nullptr;
+    uint8_t* d_ext_blob = nullptr;
+    size_t d_ext_table_cap = 0, d_ext_blob_cap = 0;
     // directory cache (AdaptiveGrainDirectoryCache, f4): device table of remote-owned grains
     DirSlot* d_cache = nullptr;
     uint32_t* d_cclaim = nullptr;
@@ -701,7 +709,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt);
+    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
@@ -963,6 +971,191 @@ uint32_t orl_keyext_uniform_hash(const orl_grain_key* k, const char* ext, size_t
     return jenkins_bytes(b.data(), b.size());
 }
 
+}  // extern "C"
+namespace {
+// ---- KeyExt grains (round 5): the host table, first writer wins, tombstones, rebuilt (and the blob compacted) when full
+uint32_t keyext_hash(const orl_grain_key& k, const uint8_t* ext, uint32_t len) {
+    return orl_keyext_uniform_hash(&k, reinterpret_cast<const char*>(ext), len);
+}
+
+bool ext_equal(const orl_ctx* c, const ExtSlot& e, const orl_grain_key& k, uint32_t h, const uint8_t* ext, uint32_t len) {
+    return e.state == SLOT_FULL && e.hash == h && e.tcd == k.type_code_data && e.n0 == k.n0 && e.n1 == k.n1 && e.len == len &&
+           (len == 0 || std::memcmp(c->ext_blob.data() + e.off, ext, len) == 0);
+}
+
+// Slot of the key (or -1); *free_slot = the first tombstone / empty slot of its chain.
+int64_t ext_find(const orl_ctx* c, const orl_grain_key& k, uint32_t h, const uint8_t* ext, uint32_t len, int64_t* free_slot) {
+    if (free_slot) *free_slot = -1;
+    if (c->ext_table.empty()) return -1;
+    const uint64_t mask = c->ext_table.size() - 1;
+    uint64_t i = dir_slot(h, mask);
+    for (uint64_t step = 0; step <= mask; ++step, i = (i + 1) & mask) {
+        const ExtSlot& e = c->ext_table[i];
+        if (e.state == SLOT_EMPTY) {
+            if (free_slot && *free_slot < 0) *free_slot = (int64_t)i;
+            return -1;
+        }
+        if (e.state == SLOT_TOMB) {
+            if (free_slot && *free_slot < 0) *free_slot = (int64_t)i;
+            continue;
+        }
+        if (ext_equal(c, e, k, h, ext, len)) return (int64_t)i;
+    }
+    return -1;
+}
+
+// Rebuild with room for `need` entries at load <= 1/2, without tombstones, the blob compacted.
+void ext_rebuild(orl_ctx* c, uint64_t need) {
+    uint64_t size = 1024;
+    while (size < 2 * need) size <<= 1;
+    std::vector<ExtSlot> old;
+    old.swap(c->ext_table);
+    std::vector<uint8_t> oblob;
+    oblob.swap(c->ext_blob);
+    c->ext_table.assign(size, ExtSlot{});
+    for (auto& e : c->ext_table) e.state = SLOT_EMPTY;
+    for (const ExtSlot& e : old) {
+        if (e.state != SLOT_FULL) continue;
+        ExtSlot n = e;
+        n.off = (uint32_t)c->ext_blob.size();
+        c->ext_blob.insert(c->ext_blob.end(), oblob.begin() + e.off, oblob.begin() + e.off + e.len);
+        uint64_t i = dir_slot(e.hash, size - 1);
+        while (c->ext_table[i].state != SLOT_EMPTY) i = (i + 1) & (size - 1);
+        c->ext_table[i] = n;
+    }
+    c->ext_tombs = 0;
+    c->ext_dirty = true;
+}
+
+// The ring owner of a KeyExt hash (CalculateTargetSilo :466-494), as host_owner computes it for the u64 path.
+uint32_t host_owner_hash(const orl_ctx* c, int32_t h, uint32_t me, bool excl) {
+    const bool running = me < c->n_silos && c->running[me];
+    const int n = (int)c->ring.size();
+    if (n == 0) return (excl && !running) ? ORL_NULL_SILO : me;
+    const bool ex = excl && !running;
+    int found = -1;
+    for (int i = 0; i < n; ++i)
+        if (c->ring[i].first <= h && !(c->ring[i].second == me && ex)) found = i;
+    if (found < 0) {
+        found = n - 1;
+        if (c->ring[found].second == me && ex) {
+            if (n > 1) found = n - 2; else return ORL_NULL_SILO;
+        }
+    }
+    return c->ring[found].second;
+}
+
+int upload_keyext(orl_ctx* c) {
+    if (!c->ext_dirty) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());  // batches in flight may read the old table (snapshot semantics, as the partition)
+    const size_t tb = c->ext_table.size() * sizeof(ExtSlot), bb = std::max<size_t>(c->ext_blob.size(), 4);
+    if (tb > c->d_ext_table_cap) {
+        (void)hipFree(c->d_ext_table);
+        c->d_ext_table = nullptr;
+        ORL_HIP(c, hipMalloc((void**)&c->d_ext_table, tb));
+        c->d_ext_table_cap = tb;
+    }
+    if (bb > c->d_ext_blob_cap) {
+        (void)hipFree(c->d_ext_blob);
+        c->d_ext_blob = nullptr;
+        ORL_HIP(c, hipMalloc((void**)&c->d_ext_blob, bb + bb / 2));
+        c->d_ext_blob_cap = bb + bb / 2;
+    }
+    if (tb) ORL_HIP(c, hipMemcpy(c->d_ext_table, c->ext_table.data(), tb, hipMemcpyHostToDevice));
+    if (!c->ext_blob.empty()) ORL_HIP(c, hipMemcpy(c->d_ext_blob, c->ext_blob.data(), c->ext_blob.size(), hipMemcpyHostToDevice));
+    c->ext_dirty = false;
+    return ORL_OK;
+}
+}  // namespace
+extern "C" {
+
+int orl_dir_insert_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                          const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* wact, uint8_t* wsilo, uint8_t* status) {
+    if (!c || (n && (!keys || !ext || !blob || !acts || !silos))) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t st;
+        uint32_t a = ORL_NO_ACT;
+        uint8_t s = ORL_NULL_SILO;
+        const orl_grain_key& k = keys[i];
+        if (acts[i] >= c->cfg.n_act) return fail(c, ORL_E_INVALID, "act %u >= n_act %u at %zu", acts[i], c->cfg.n_act, i);
+        if (!silo_ok(c, silos[i])) return fail(c, ORL_E_INVALID, "silo %u out of range at %zu", silos[i], i);
+        if ((uint32_t)(k.type_code_data >> 56) != ORL_CAT_KEYEXT_GRAIN) {
+            st = ORL_INS_UNSUPPORTED;
+        } else {
+            const uint8_t* x = blob + ext[i].off;
+            const uint32_t len = ext[i].len;
+            const uint32_t h = keyext_hash(k, x, len);
+            const uint32_t owner = host_owner_hash(c, (int32_t)h, silos[i], true);
+            if (owner == ORL_NULL_SILO) st = ORL_INS_OWNER_NULL;
+            else if (!c->local[owner]) st = ORL_INS_REMOTE_OWNER;
+            else if (!c->functional[silos[i]]) st = ORL_INS_INVALID_SILO;  // AddSingleActivation :277-279
+            else {
+                if ((c->ext_count + c->ext_tombs + 1) * 2 > c->ext_table.size()) ext_rebuild(c, c->ext_count + 1);
+                int64_t fr = -1;
+                const int64_t at = ext_find(c, k, h, x, len, &fr);
+                if (at >= 0) {  // GrainInfo.AddSingleActivation: an instance exists → return it (:103-107)
+                    st = ORL_INS_EXISTING;
+                    a = c->ext_table[at].act;
+                    s = c->ext_table[at].silo;
+                } else {
+                    ExtSlot& e = c->ext_table[fr];
+                    if (e.state == SLOT_TOMB) --c->ext_tombs;
+                    e.tcd = k.type_code_data; e.n0 = k.n0; e.n1 = k.n1;
+                    e.hash = h; e.act = acts[i]; e.silo = silos[i]; e.state = SLOT_FULL;
+                    e.off = (uint32_t)c->ext_blob.size();
+                    e.len = len;
+                    c->ext_blob.insert(c->ext_blob.end(), x, x + len);
+                    ++c->ext_count;
+                    c->ext_dirty = true;
+                    st = ORL_INS_INSERTED;
+                    a = acts[i];
+                    s = silos[i];
+                }
+            }
+        }
+        if (status) status[i] = st;
+        if (wact) wact[i] = a;
+        if (wsilo) wsilo[i] = s;
+    }
+    return ORL_OK;
+}
+
+int orl_dir_remove_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
+                          uint8_t* removed) {
+    if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t* x = blob + ext[i].off;
+        const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
+        if (at >= 0) {
+            c->ext_table[at].state = SLOT_TOMB;
+            --c->ext_count;
+            ++c->ext_tombs;
+            c->ext_dirty = true;
+        }
+        if (removed) removed[i] = at >= 0 ? 1 : 0;
+    }
+    return ORL_OK;
+}
+
+int orl_dir_lookup_keyext_host(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
+                               uint32_t* act, uint8_t* silo) {
+    if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t* x = blob + ext[i].off;
+        const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
+        if (act) act[i] = at >= 0 ? c->ext_table[at].act : ORL_NO_ACT;
+        if (silo) silo[i] = at >= 0 ? c->ext_table[at].silo : (uint8_t)ORL_NULL_SILO;
+    }
+    return ORL_OK;
+}
+
+int orl_dir_keyext_count(const orl_ctx* c, uint64_t* n) {
+    if (!c || !n) return ORL_E_INVALID;
+    *n = c->ext_count;
+    return ORL_OK;
+}
+
 int orl_dir_insert_single(orl_ctx* c, const orl_grain_key* keys, const uint32_t* acts, const uint8_t* silos, size_t n,
                           uint32_t* wact, uint8_t* wsilo, uint8_t* status) {
     if (!c || (n && (!keys || !acts || !silos))) return ORL_E_INVALID;
@@ -1114,6 +1307,30 @@ int orl_route_compact_device(orl_ctx* c, const orl_wire_msg* d_in, size_t n, uin
 int orl_route_narrow_device(orl_ctx* c, const orl_wire8* d_in, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                             uint32_t* d_order, uint32_t* d_off, void* stream) {
     return route_impl(c, d_in, 8, n, opts, d_route, d_act, d_order, d_off, stream);
+}
+
+// Stages 1-3 (k_route leaves KeyExt messages ORL_ST_KEYEXT_UNRESOLVED with their owner), the KeyExt lookups
+// (k_keyext_route), then stage 4 over the final handles (orl_bucket_device's path: its own histogram pass).
+int orl_route_keyext_device(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                            const uint8_t* d_blob, uint64_t blob_bytes, uint32_t* d_route, uint32_t* d_act, uint32_t* d_order,
+                            uint32_t* d_off, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (n && (!d_ext || !d_blob)) return fail(c, ORL_E_INVALID, "null KeyExt references or blob");
+    const bool buckets = !(opts & ORL_OPT_NO_BUCKETS);
+    if (buckets && (!d_off || (n && !d_order))) return fail(c, ORL_E_INVALID, "null order/offsets buffer");
+    if (int r = upload_keyext(c)) return r;
+    if (int r = route_impl(c, d_in, 32, n, opts | ORL_OPT_NO_BUCKETS, d_route, d_act, nullptr, nullptr, stream)) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (n) {
+        const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+        int e = launch_keyext_route(c->d_params, d_in, n, d_ext, d_blob, blob_bytes, c->d_ext_table,
+                                    c->ext_table.empty() ? 0 : c->ext_table.size() - 1, c->d_ext_blob, excl, d_route, d_act, st);
+        if (e) return hipfail(c, (hipError_t)e, "KeyExt route launch");
+    }
+    if (!buckets) return ORL_OK;
+    int e = launch_bucket_acts(d_act, n, c->cfg.n_act, d_order, d_off, c->s, st);
+    if (e) return hipfail(c, (hipError_t)e, "bucket launch");
+    return ORL_OK;
 }
 
 // Host-array form (the P/Invoke call): the batch is cut into chunks; chunk k's upload (copy stream), its stages 1-3
@@ -1685,7 +1902,7 @@ int orl_cache_add_or_update_device(orl_ctx* c, const orl_grain_key* d_keys, cons
     if ((r = sync_device_state(c))) return r;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int e = launch_cache_update(c->d_cache, c->cache_slots - 1, c->d_cclaim, c->d_cstate, d_keys, d_acts, d_silos, n, c->cfg.n_act,
-                                c->n_silos, c->d_dslot, c->d_dflag, reinterpret_cast<uint32_t*>(c->d_cstate + 2), st);
+                                c->n_silos, c->d_dslot, c->d_dflag, reinterpret_cast<uint32_t*>(c->d_cstate + 2), st, c->d_params);
     if (e) return hipfail(c, (hipError_t)e, "cache update launch");
     c->cache_ub += n;
     return ORL_OK;

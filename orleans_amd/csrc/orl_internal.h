@@ -234,6 +234,16 @@ struct DirView {
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
 // All return hipError_t as int; they only enqueue on `stream`.
+// KeyExt (string-key) directory slot, 48 B (round 5): the UniqueKey's 24 B, its KeyExt uniform hash, the activation
+// handle, where the KeyExt bytes lie in the context's KeyExt blob, the silo and the slot state (SLOT_*).  Open addressing
+// from dir_slot(hash) like the main partition.
+struct ExtSlot {
+    uint64_t tcd, n0, n1;
+    uint32_t hash, act, off, len;
+    uint8_t silo, state, pad[6];
+};
+static_assert(sizeof(ExtSlot) == 48, "KeyExt slot layout");
+
 // Fused level 2 on skewed plans: segments per look-back chunk (k_seg_count_scan's kLbRows, ORL_SEG_LB_ROWS for lab builds)
 // is at least this; the look-back buffers are sized for it.
 constexpr uint32_t kSegLbMinRows = 8;
@@ -321,7 +331,7 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
                       void* stream);
 int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                         const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
-                        uint8_t* d_flag, uint32_t* d_err, void* stream);
+                        uint8_t* d_flag, uint32_t* d_err, void* stream, const RouteParams* d_params);
 int launch_dir_merge(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                      const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos,
                      const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint32_t* d_slot, uint8_t* d_status,
@@ -393,6 +403,11 @@ bool ctx_cache_on(orl_ctx* c);
 // sender addressed from its directory cache (act != ORL_NO_ACT) get HIT | CACHED without a probe.
 int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,
                        const uint32_t* d_in_act, void* stream);
+// KeyExt grains of a routed batch (orl_route_keyext_device): each message k_route left ORL_ST_KEYEXT_UNRESOLVED gets
+// its owner's lookup in the KeyExt table when the owner is local (HIT, or placement on a miss) or ORL_ST_REMOTE_OWNER.
+int launch_keyext_route(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, const orl_ext_ref* d_ext,
+                        const uint8_t* d_blob, uint64_t blob_bytes, const ExtSlot* d_table, uint64_t mask,
+                        const uint8_t* d_tblob, uint32_t excl, uint32_t* d_route, uint32_t* d_act, void* stream);
 int launch_partition_by_owner(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                               const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, orl_msg_hdr* d_out,
                               uint32_t* d_src_index, uint64_t* d_counts, const Scratch& s, void* stream);

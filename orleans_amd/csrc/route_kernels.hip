@@ -1958,7 +1958,9 @@ __device__ __forceinline__ void bucket_finish(const uint32_t* tot, uint32_t b, u
 constexpr uint32_t kLbRows = ORL_SEG_LB_ROWS;
 static_assert(kLbRows >= kSegLbMinRows, "the look-back buffers are sized for chunks of >= kSegLbMinRows segments");
 constexpr uint32_t kLbAgg = 1u, kLbInc = 2u;
-constexpr uint32_t kLbBatch = 8;  // look-back rows whose loads are in flight together
+// look-back rows whose loads are in flight together: 32 registers' worth (8 rows of 1024 digits, 4 of 2048)
+template <int LB>
+constexpr uint32_t lb_batch() { return (1u << LB) >= 2048u ? 4u : 8u; }
 
 template <int LB>
 __device__ __forceinline__ void row_publish(uint32_t* __restrict__ dst, const uint32_t* src, const uint32_t* add) {
@@ -2000,6 +2002,7 @@ __device__ __forceinline__ void chunk_lookback(uint32_t t, const uint32_t* __res
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // the consumed rows, kLbBatch at a time with every load in flight before the adds (a row per round trip otherwise)
         const uint32_t mm = (uint32_t)min<int64_t>((int64_t)m, k + 1);
+        constexpr uint32_t kLbBatch = lb_batch<LB>();
         for (uint32_t i0 = 0; i0 < mm; i0 += kLbBatch) {
             uint32_t v[kLbBatch][Q];
 #pragma unroll
@@ -3158,6 +3161,107 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// KeyExt (string-key) grains (round 5; GrainDirectoryPartition holds any GrainId, GrainDirectoryPartition.cs:270-287,
+// 326-344).  After k_route (which leaves a KeyExt message ORL_ST_KEYEXT_UNRESOLVED), one thread per message re-decides
+// every KeyExt message without a complete address: its uniform hash (the header's precomputed one with
+// ORL_HDR_HASH_VALID, else Jenkins over Write(UniqueKey) = N0, N1, TypeCodeData, int32 length, the UTF-8 bytes;
+// UniqueKey.cs:288-294, JenkinsHash.cs:68-115), its ring owner, and — owner local — a probe of the KeyExt table comparing
+// the hash, the 24-B key, the length and the bytes; HIT or placement (route_tail), or ORL_ST_REMOTE_OWNER.  Rare in a
+// batch, so a plain per-thread walk.
+
+// Jenkins lookup2 over the virtual byte string {N0, N1, TCD (LE8 each), len (LE4), s[0, len)}.
+__device__ uint32_t keyext_hash_dev(uint64_t n0, uint64_t n1, uint64_t tcd, const uint8_t* __restrict__ s, uint32_t len) {
+    auto at = [&](uint32_t k) -> uint32_t {
+        if (k < 8) return (uint32_t)(n0 >> (8 * k)) & 0xFFu;
+        if (k < 16) return (uint32_t)(n1 >> (8 * (k - 8))) & 0xFFu;
+        if (k < 24) return (uint32_t)(tcd >> (8 * (k - 16))) & 0xFFu;
+        if (k < 28) return (len >> (8 * (k - 24))) & 0xFFu;
+        return s[k - 28];
+    };
+    auto rd = [&](uint32_t k) { return at(k) | at(k + 1) << 8 | at(k + 2) << 16 | at(k + 3) << 24; };
+    const uint32_t total = 28u + len;
+    uint32_t a = 0x9e3779b9u, b = 0x9e3779b9u, c = 0, i = 0;
+    for (; i + 12 <= total; i += 12) {
+        a += rd(i);
+        b += rd(i + 4);
+        c += rd(i + 8);
+        ORL_MIX(a, b, c);
+    }
+    c += total;
+    for (uint32_t k = 0; i + k < total; ++k) {
+        const uint32_t v = at(i + k);
+        if (k < 4) a += v << (8 * k);
+        else if (k < 8) b += v << (8 * (k - 4));
+        else c += v << (8 * (k - 7));
+    }
+    ORL_MIX(a, b, c);
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_keyext_route(const RouteParams* __restrict__ gp, const orl_msg_hdr* __restrict__ in,
+                                                      uint32_t n, const orl_ext_ref* __restrict__ ext,
+                                                      const uint8_t* __restrict__ blob, uint64_t blob_bytes,
+                                                      const ExtSlot* __restrict__ table, uint64_t mask,
+                                                      const uint8_t* __restrict__ tblob, uint32_t excl,
+                                                      uint32_t* __restrict__ route, uint32_t* __restrict__ act_out) {
+    __shared__ RouteParams P;
+    stage_params(&P, gp);
+    __syncthreads();
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= n) return;
+    const Msg m = load_hdr(in, e);
+    const uint32_t hflags = (m.meta >> 16) & 0xFFu;
+    if ((uint32_t)(m.tcd >> 56) != ORL_CAT_KEYEXT_GRAIN || (hflags & ORL_HDR_ADDRESS_COMPLETE)) return;
+    const orl_ext_ref x = ext[e];
+    if ((uint64_t)x.off + x.len > blob_bytes) return;  // stays ORL_ST_KEYEXT_UNRESOLVED
+    const uint8_t* xs = blob + x.off;
+    const uint32_t h = (hflags & ORL_HDR_HASH_VALID) ? m.aux : keyext_hash_dev(m.n0, m.n1, m.tcd, xs, x.len);
+    const uint32_t me = m.meta & 0xFFu;
+    uint32_t owner;
+    if (P.ring_n == 0) {  // CalculateTargetSilo :471-475
+        if (excl && !mask_bit(P.running, me)) {
+            route[e] = pack_route(0xFFu, 0xFFu, ORL_ST_OWNER_NULL, 0);
+            act_out[e] = ORL_NO_ACT;
+            return;
+        }
+        owner = me;
+    } else {
+        owner = ring_owner(P, (int32_t)h, me, excl && !mask_bit(P.running, me));
+        if (owner == 0xFFu) {
+            route[e] = pack_route(0xFFu, 0xFFu, ORL_ST_OWNER_NULL, 0);
+            act_out[e] = ORL_NO_ACT;
+            return;
+        }
+    }
+    if (!mask_bit(P.local, owner)) {  // LocalLookup's non-owner branch: the FullLookup path (the cache holds no KeyExt)
+        route[e] = pack_route(owner, 0xFFu, ORL_ST_REMOTE_OWNER, 0);
+        act_out[e] = ORL_NO_ACT;
+        return;
+    }
+    bool found = false;
+    uint32_t fact = 0, fsilo = 0;
+    if (table) {
+        uint64_t slot = dir_slot(h, mask);
+        for (uint64_t step = 0; step <= mask; ++step, slot = (slot + 1) & mask) {
+            const ExtSlot& t = table[slot];
+            if (t.state == SLOT_EMPTY) break;
+            if (t.state != SLOT_FULL || t.hash != h || t.tcd != m.tcd || t.n0 != m.n0 || t.n1 != m.n1 || t.len != x.len) continue;
+            bool same = true;
+            for (uint32_t k = 0; k < x.len && same; ++k) same = tblob[t.off + k] == xs[k];
+            if (same) {
+                found = true;
+                fact = t.act;
+                fsilo = t.silo;
+                break;
+            }
+        }
+    }
+    uint32_t act = ORL_NO_ACT;
+    route[e] = route_tail(P, m, h, owner, 0u, found, fact, fsilo, act, false);
+    act_out[e] = act;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Node exchange, hop 2 (Dispatcher.TransportMessage → OutboundMessageQueue.SendMessage,
 // OutboundMessageQueue.cs:113-145): after the directory owner routed a message, it travels on to the rank hosting its
 // activation (the route word's host silo); messages without a host (host 0xFF) stay.
@@ -3491,14 +3595,19 @@ __global__ __launch_bounds__(256) void k_dir_ins_commit(DirSlot* __restrict__ di
 // Directory cache AddOrUpdate (AdaptiveGrainDirectoryCache.AddOrUpdate; f4): the batch's LAST writer of a key
 // sets its entry (insert or update).  Claim tag = ~index, so atomicMin keeps the largest index.  Entries with an
 // activation handle >= n_act or a silo outside the table are skipped.
+// An entry is kept when its silo is known and its handle is in this context's space [0, n_act) — or, for a silo this
+// context does not host (`local`, a node's other ranks), any handle but ORL_NO_ACT: the host rank's catalog numbers it
+// (round 5: the node exchange delivers cached messages to that rank, whose stage 4 buckets them).
 __global__ __launch_bounds__(256) void k_cache_probe(DirSlot* __restrict__ cache, uint64_t mask, uint32_t* __restrict__ claim,
                                                      const orl_grain_key* __restrict__ keys, const uint32_t* __restrict__ acts,
                                                      const uint8_t* __restrict__ silos, uint32_t n, uint32_t n_act,
-                                                     uint32_t n_silos, uint32_t* __restrict__ slot_out, uint32_t* __restrict__ err) {
+                                                     uint32_t n_silos, const uint32_t* __restrict__ local,
+                                                     uint32_t* __restrict__ slot_out, uint32_t* __restrict__ err) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     uint32_t out = kSlotNone;
-    if (acts[i] < n_act && silos[i] < n_silos) {
+    const uint32_t sl = silos[i];
+    if (sl < n_silos && (acts[i] < n_act || (acts[i] != ORL_NO_ACT && !mask_bit(local, sl)))) {
         uint64_t slot = 0;
         bool was_tomb = false;
         if (find_or_claim<true>(cache, mask, claim, keys[i], ~i, slot, was_tomb) >= 0)
@@ -4583,12 +4692,12 @@ int launch_dir_merge(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint6
 
 int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                         const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
-                        uint8_t* d_flag, uint32_t* d_err, void* stream) {
+                        uint8_t* d_flag, uint32_t* d_err, void* stream, const RouteParams* d_params) {
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) return 0;
     const dim3 g(ceil_div(n, 256)), b(256);
     hipLaunchKernelGGL(k_cache_probe, g, b, 0, st, d_cache, mask, d_claim, d_keys, d_acts, d_silos, (uint32_t)n, n_act, n_silos,
-                       d_slot, d_err);
+                       d_params->local, d_slot, d_err);
     hipLaunchKernelGGL(k_cache_resolve, g, b, 0, st, d_claim, (uint32_t)n, d_slot, d_flag);
     hipLaunchKernelGGL(k_cache_commit, g, b, 0, st, d_cache, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_flag, d_cnt);
     return (int)hipGetLastError();
@@ -4660,6 +4769,15 @@ int launch_client_buckets(const orl_msg_hdr* d_msgs, size_t n, uint32_t n_bucket
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_client_buckets, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_msgs, (uint32_t)n, n_buckets,
                        d_bucket);
+    return (int)hipGetLastError();
+}
+
+int launch_keyext_route(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, const orl_ext_ref* d_ext,
+                        const uint8_t* d_blob, uint64_t blob_bytes, const ExtSlot* d_table, uint64_t mask,
+                        const uint8_t* d_tblob, uint32_t excl, uint32_t* d_route, uint32_t* d_act, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_keyext_route, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_params, d_in, (uint32_t)n,
+                       d_ext, d_blob, blob_bytes, d_table, mask, d_tblob, excl, d_route, d_act);
     return (int)hipGetLastError();
 }
 

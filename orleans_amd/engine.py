@@ -221,6 +221,57 @@ class GrainDirectoryEngine:
                                                  ptr(st)))
         return st, wa, ws
 
+    # -- KeyExt (string-key) grains: their own device table (orl_dir_*_keyext)
+    @staticmethod
+    def ext_blob(strings):
+        """(orl_ext_ref array, UTF-8 blob) for a sequence of str / bytes."""
+        bs = [x.encode("utf-8") if isinstance(x, str) else bytes(x) for x in strings]
+        ref = np.zeros(len(bs), L.EXT_REF_DTYPE)
+        off = 0
+        for i, b in enumerate(bs):
+            ref[i] = (off, len(b))
+            off += len(b)
+        blob = np.frombuffer(b"".join(bs) or b"\0", np.uint8).copy()
+        return ref, blob
+
+    def register_keyext(self, keys: np.ndarray, strings, acts: np.ndarray, silos: np.ndarray):
+        """RegisterSingleActivation of KeyExt grains (orl_dir_insert_keyext): (status, winner act, winner silo)."""
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        ref, blob = self.ext_blob(strings)
+        acts = np.ascontiguousarray(acts, dtype=np.uint32)
+        silos = np.ascontiguousarray(silos, dtype=np.uint8)
+        n = len(keys)
+        st, wa, ws = np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint8)
+        self._ck(self._lib.orl_dir_insert_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), ptr(acts), ptr(silos), n, ptr(wa),
+                                                 ptr(ws), ptr(st)))
+        return st, wa, ws
+
+    def unregister_keyext(self, keys: np.ndarray, strings) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        ref, blob = self.ext_blob(strings)
+        out = np.zeros(len(keys), np.uint8)
+        self._ck(self._lib.orl_dir_remove_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), len(keys), ptr(out)))
+        return out
+
+    def lookup_keyext_host(self, keys: np.ndarray, strings):
+        keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
+        ref, blob = self.ext_blob(strings)
+        a, s = np.zeros(len(keys), np.uint32), np.zeros(len(keys), np.uint8)
+        self._ck(self._lib.orl_dir_lookup_keyext_host(self._ctx, ptr(keys), ptr(ref), ptr(blob), len(keys), ptr(a), ptr(s)))
+        return a, s
+
+    def keyext_count(self) -> int:
+        n = C.c_uint64()
+        self._ck(self._lib.orl_dir_keyext_count(self._ctx, C.byref(n)))
+        return n.value
+
+    def address_keyext_device(self, d_msgs, n: int, d_ext, d_blob, blob_bytes: int, d_route, d_act, d_order=None,
+                              d_offsets=None, stream=None, opts: int = 0) -> None:
+        """orl_route_keyext_device: the batch routed with its KeyExt strings (d_ext: orl_ext_ref per message into d_blob)."""
+        self._ck(self._lib.orl_route_keyext_device(self._ctx, ptr(d_msgs), int(n), int(opts), ptr(d_ext), ptr(d_blob),
+                                                   int(blob_bytes), ptr(d_route), ptr(d_act), ptr(d_order), ptr(d_offsets),
+                                                   ptr(stream)))
+
     def unregister(self, keys: np.ndarray) -> np.ndarray:
         keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
         out = np.zeros(len(keys), np.uint8)
