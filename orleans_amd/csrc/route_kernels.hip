@@ -854,15 +854,17 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
-template <int SRC>
+// CH: elements per block (kScanChunk; the fan-out prologue takes 1024 up to 1M publishers, so a config-5 tick's 64k
+// publishers keep 64 workgroups busy instead of 16: its dependent CSR loads were latency-bound on 16 CUs, round 5).
+template <int SRC, uint32_t CH = kScanChunk>
 __global__ __launch_bounds__(256) void k_scan_reduce(uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums,
                                                      const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
                                                      uint64_t* __restrict__ pstart, unsigned long long* __restrict__ bmax = nullptr,
                                                      uint32_t nkeys = 0) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ unsigned long long wmax[kWaves];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
-    constexpr uint32_t J = kScanChunk / 256;
+    const uint64_t base = (uint64_t)blockIdx.x * CH;
+    constexpr uint32_t J = CH / 256;
     uint32_t s = 0;
     if (SRC != 1) {
         unsigned long long best = 0;
@@ -947,6 +949,35 @@ __device__ __forceinline__ void load16(const uint32_t* __restrict__ a, uint64_t 
     }
 }
 
+template <int E>
+__device__ __forceinline__ void load_e(const uint32_t* __restrict__ a, uint64_t base, uint64_t m, uint32_t fill, uint32_t (&v)[E]) {
+    static_assert(E % 4 == 0, "whole 16-B vectors");
+    if (base + E <= m && (reinterpret_cast<uintptr_t>(a) & 15u) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(a + base);
+#pragma unroll
+        for (int q = 0; q < E / 4; ++q) {
+            const uint4 x = p[q];
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i) v[i] = base + i < m ? a[base + i] : fill;
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void store_e(uint32_t* __restrict__ a, uint64_t base, uint64_t m, const uint32_t (&v)[E]) {
+    if (base + E <= m && (reinterpret_cast<uintptr_t>(a) & 15u) == 0) {
+        uint4* p = reinterpret_cast<uint4*>(a + base);
+#pragma unroll
+        for (int q = 0; q < E / 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (base + i < m) a[base + i] = v[i];
+    }
+}
+
 __device__ __forceinline__ void store16(uint32_t* __restrict__ a, uint64_t base, uint64_t m, const uint32_t (&v)[16]) {
     if (base + 16 <= m && (reinterpret_cast<uintptr_t>(a) & 15u) == 0) {
         uint4* p = reinterpret_cast<uint4*>(a + base);
@@ -970,7 +1001,7 @@ constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4
 // fblk[k] = the p with poff[p] <= k * kFanBlk < poff[p + 1], and fblk[ceil(total / kFanBlk)] = n_pub - 1 (written by
 // the last element, m - 1 = n_pub): a fan-out tile reads its publisher range with two independent loads.
 constexpr uint32_t kFanBlkShift = 8, kFanBlk = 1u << kFanBlkShift;
-template <bool DIRECT, bool WIDEN, bool PICK = false>
+template <bool DIRECT, bool WIDEN, bool PICK = false, uint32_t CH = kScanChunk>
 __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums,
                                                    uint64_t* __restrict__ out64, uint64_t add64,
                                                    const unsigned long long* __restrict__ bmax = nullptr, uint32_t n = 0,
@@ -993,12 +1024,13 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
             if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16u;
-    uint32_t v[16];
-    load16(a, base, m, 0u, v);
+    constexpr int E = (int)(CH / 256);  // elements per thread
+    const uint64_t base = (uint64_t)blockIdx.x * CH + (uint64_t)threadIdx.x * E;
+    uint32_t v[E];
+    load_e<E>(a, base, m, 0u, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s += v[i];
+    for (int i = 0; i < E; ++i) s += v[i];
     uint32_t pre;
     if (DIRECT) {
         uint32_t q = 0;
@@ -1009,9 +1041,9 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
     }
     uint32_t total;
     uint32_t run = block_excl_scan(s, wsum, total) + pre;
-    uint32_t o[16];
+    uint32_t o[E];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < E; ++i) {
         o[i] = run;
         if (WIDEN && base + i < m) {
             out64[base + i] = add64 + run;
@@ -1026,7 +1058,7 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
         }
         run += v[i];
     }
-    store16(a, base, m, o);
+    store_e<E>(a, base, m, o);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1114,8 +1146,11 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint16_t* __restrict__ C,
     const uint32_t t0 = blockIdx.x * kScanRows;
     const uint32_t t1 = min(t0 + kScanRows, ntiles);
     uint32_t acc = 0;
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) acc += C[(size_t)t * bins + d];
+    uint32_t v[kScanRows];  // the chunk's rows, every load in flight together
+#pragma unroll
+    for (uint32_t k = 0; k < kScanRows; ++k) v[k] = t0 + k < t1 ? C[(size_t)(t0 + k) * bins + d] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanRows; ++k) acc += v[k];
     S[(size_t)blockIdx.x * bins + d] = acc;
 }
 
@@ -1210,15 +1245,15 @@ __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ 
     uint32_t run = red + ex + S[(size_t)blockIdx.x * bins + d];
     const uint32_t t0 = blockIdx.x * kScanRows;
     const uint32_t t1 = min(t0 + kScanRows, ntiles);
-    // 8 rows per step: all 8 loads in flight before the stores (a load-store-load chain per row measured 10.7 us over
-    // config 5's 2304 rows)
-    for (uint32_t t = t0; t < t1; t += 8) {
-        uint32_t v[8];
+    // the chunk's 64 rows: every load in flight before the stores (8 at a time, a load round trip per 8 rows, measured
+    // 10.8 us over config 5's 2304 rows; one load-store-load chain per row 10.7 us before that)
+    {
+        uint32_t v[kScanRows];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) v[k] = t + k < t1 ? C[(size_t)(t + k) * bins + d] : 0u;
+        for (uint32_t k = 0; k < kScanRows; ++k) v[k] = t0 + k < t1 ? C[(size_t)(t0 + k) * bins + d] : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            if (t + k < t1 && (t + k) % row_step == 0) M[(size_t)(t + k) * bins + d] = run;
+        for (uint32_t k = 0; k < kScanRows; ++k) {
+            if (t0 + k < t1 && (t0 + k) % row_step == 0) M[(size_t)(t0 + k) * bins + d] = run;
             run += v[k];
         }
     }
@@ -4010,6 +4045,7 @@ inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1)
 // ~9 us for the 2 launches — each chunk's ticket, granule and look-back atomics are device-coherent round trips — and
 // no faster at config 2's 16M offsets.)
 constexpr uint32_t kScanDirectChunks = 1024;
+constexpr uint32_t kScanSmallChunk = 1024;  // the fan-out prologue's chunk up to kScanDirectChunks chunks
 
 int scan_inplace(uint32_t* a, uint64_t m, const Scratch& s, hipStream_t st) {
     const uint32_t nb = ceil_div(m, kScanChunk);
@@ -4547,13 +4583,20 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     uint32_t* poff32 = s.idx_a;
     uint64_t* pstart = reinterpret_cast<uint64_t*>(s.pairs_b);  // free until a later LSD pass (after the route kernel)
     const uint32_t m = (uint32_t)n_pub + 1;
-    const uint32_t nbs = ceil_div(m, kScanChunk);
-    hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
     const uint32_t fcap = s.fan_blk ? (uint32_t)std::min<uint64_t>((max_out + kFanBlk - 1) / kFanBlk + 1, s.fan_blk_cap) : 0u;
-    if (nbs <= kScanDirectChunks) {
+    const bool small = m <= kScanSmallChunk * kScanDirectChunks;  // 1024-element chunks: 4x the workgroups (k_scan_reduce)
+    const uint32_t nbs = ceil_div(m, small ? kScanSmallChunk : kScanChunk);
+    if (small) {
+        hipLaunchKernelGGL((k_scan_reduce<1, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
+                           d_csr_off, d_pubs, pstart, nullptr, 0u);
+        hipLaunchKernelGGL((k_scan_down<true, true, false, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m,
+                           s.scan_sums, d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
+    } else if (nbs <= kScanDirectChunks) {
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
         hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
                            d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else {
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
         hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
                            d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
@@ -4614,13 +4657,20 @@ int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, c
     uint32_t* poff32 = s.idx_a;
     uint64_t* pstart = reinterpret_cast<uint64_t*>(s.pairs_b);
     const uint32_t m = (uint32_t)n_pub + 1;
-    const uint32_t nbs = ceil_div(m, kScanChunk);
-    hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
     const uint32_t fcap = s.fan_blk ? (uint32_t)std::min<uint64_t>((cap + kFanBlk - 1) / kFanBlk + 1, s.fan_blk_cap) : 0u;
-    if (nbs <= kScanDirectChunks) {
+    const bool small = m <= kScanSmallChunk * kScanDirectChunks;
+    const uint32_t nbs = ceil_div(m, small ? kScanSmallChunk : kScanChunk);
+    if (small) {
+        hipLaunchKernelGGL((k_scan_reduce<1, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
+                           d_csr_off, d_pubs, pstart, nullptr, 0u);
+        hipLaunchKernelGGL((k_scan_down<true, true, false, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m,
+                           s.scan_sums, d_pub_offsets, 0ull, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
+    } else if (nbs <= kScanDirectChunks) {
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
         hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
                            0ull, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else {
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
         hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_pub_offsets,
                            0ull, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
