@@ -2205,7 +2205,7 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
         case ORL_Q_HOT_BATCHES:
             *v = c->s.hot_batches;
             return ORL_OK;
-case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
+        case ORL_Q_HOT_KEY: {  // stage 4's hot key for the next batch (synchronises the device)
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             ORL_HIP(c, hipSetDevice(c->cfg.device));
             ORL_HIP(c, hipDeviceSynchronize());

@@ -860,9 +860,12 @@ template <int SRC, uint32_t CH = kScanChunk>
 __global__ __launch_bounds__(256) void k_scan_reduce(uint32_t* __restrict__ a, uint64_t m, uint32_t* __restrict__ sums,
                                                      const uint64_t* __restrict__ csr_off, const uint32_t* __restrict__ pubs,
                                                      uint64_t* __restrict__ pstart, unsigned long long* __restrict__ bmax = nullptr,
-                                                     uint32_t nkeys = 0) {
+                                                     uint32_t nkeys = 0, uint32_t* __restrict__ zero_p = nullptr,
+                                                     uint32_t zero_n = 0) {
     __shared__ uint32_t wsum[kWaves];
     __shared__ unsigned long long wmax[kWaves];
+    // zero_p: the fan-out route's column sums, accumulated by its tiles' atomics (a small batch's self-scanned columns)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < zero_n; i += gridDim.x * 256u) zero_p[i] = 0;
     const uint64_t base = (uint64_t)blockIdx.x * CH;
     constexpr uint32_t J = CH / 256;
     uint32_t s = 0;
@@ -1127,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 // Column scan of the [ntiles][bins] count matrix, in chunks of kScanRows tiles.
 //   k_col_sum:   S[c][d] = sum of rows of chunk c                       (grid: chunks x ceil(bins/256))
 //   k_col_scan:  S[c][d] → exclusive prefix over chunks; T[d] = column total (grid: ceil(bins/16))
-//   k_col_apply: M[t][d] = base(d) + S[c][d] + rows of chunk c before t (grid: chunks x ceil(bins/256))
+//   k_col_apply: M[t][d] = base(d) + S[c][d] + rows of chunk c before t (grid: chunks x ceil(bins/64))
 constexpr uint32_t kScanRows = 64;
 
 // hot_rows (stage 4's hot-key path): the hot key's per-row counts, one more column kept apart: the last grid row of each
@@ -1211,13 +1214,23 @@ __device__ void seg_plan_body(const uint32_t* __restrict__ col_tot, uint32_t nbk
 // only those are written.
 // plan_bstart (the two-level stage 4 with an MSD pass): one more grid column does k_seg_plan's work over the column
 // totals T — the segment plan is ready before the MSD pass, one launch fewer (round 4).
+// A small fan-out batch (at most kSelfScanChunks chunks of 64 rows, no hot column) has its chunk sums S accumulated by the
+// fan-out kernel's atomics instead of k_col_sum (ORL_COL_SELF=0: k_col_sum; measured -1 us at config 5).
+constexpr uint32_t kSelfScanChunks = 64;
+constexpr uint32_t kApplyCols = 64;                        // columns per k_col_apply block, one per lane
+constexpr uint32_t kApplyGroups = 256 / kApplyCols;        // row groups per chunk, one per wave
+constexpr uint32_t kApplyRows = kScanRows / kApplyGroups;  // rows per thread
+
+// grid: chunks (+1 plan column) x ceil(bins / 64) (+1 hot row).  Each wave owns 16 of the chunk's 64 rows for the block's
+// 64 columns: its rows' sums meet in LDS for the row groups' bases (round 5: 4x the workgroups and a quarter of the
+// dependent loads per thread of the 256-column form, config 5 11.6 -> see DESIGN §5).
 __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ C, uint32_t* __restrict__ M, uint32_t ntiles, uint32_t bins,
                                                    const uint32_t* __restrict__ S, const uint32_t* __restrict__ T,
                                                    uint32_t row_step, uint32_t* __restrict__ hot_rows, uint32_t plan_n,
                                                    uint32_t plan_seg, uint32_t* __restrict__ plan_bstart,
                                                    uint32_t* __restrict__ plan_sstart) {
-    __shared__ uint32_t wsum[kWaves];
     __shared__ uint32_t red;
+    __shared__ uint32_t gsum[kApplyGroups][kApplyCols];
     __shared__ uint32_t pw[3][16];
     if (plan_bstart && blockIdx.x == gridDim.x - 1) {
         if (blockIdx.y == 0) seg_plan_body<256>(T, bins, plan_n, plan_seg, plan_bstart, plan_sstart, pw);
@@ -1231,31 +1244,36 @@ __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ 
         if (t < ntiles) hot_rows[t] = ex;
         return;
     }
-    const uint32_t d0 = blockIdx.y * 256;
-    const uint32_t d = d0 + threadIdx.x;
-    // base(d) = sum of column totals before d: columns before this block's 256, then an in-block scan
+    const uint32_t col = threadIdx.x % kApplyCols, grp = threadIdx.x / kApplyCols;
+    const uint32_t d0 = blockIdx.y * kApplyCols;
+    const uint32_t d = d0 + col;
+    const bool live = d < bins;
+    // base(d) = sum of column totals before d: columns before this block's 64 (block sum), then a wave scan over them
     uint32_t before = 0;
     for (uint32_t i = threadIdx.x; i < d0; i += 256) before += T[i];
     if (threadIdx.x == 0) red = 0;
+    const uint32_t t0 = blockIdx.x * kScanRows + grp * kApplyRows;
+    const uint32_t t1 = min(t0 + kApplyRows, ntiles);
+    uint32_t v[kApplyRows];  // the group's 16 rows, every load in flight together
+#pragma unroll
+    for (uint32_t k = 0; k < kApplyRows; ++k) v[k] = live && t0 + k < t1 ? C[(size_t)(t0 + k) * bins + d] : 0u;
+    uint32_t rs = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kApplyRows; ++k) rs += v[k];
+    gsum[grp][col] = rs;
     __syncthreads();
     atomicAdd(&red, before);
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(d < bins ? T[d] : 0u, wsum, total);
-    if (d >= bins) return;
-    uint32_t run = red + ex + S[(size_t)blockIdx.x * bins + d];
-    const uint32_t t0 = blockIdx.x * kScanRows;
-    const uint32_t t1 = min(t0 + kScanRows, ntiles);
-    // the chunk's 64 rows: every load in flight before the stores (8 at a time, a load round trip per 8 rows, measured
-    // 10.8 us over config 5's 2304 rows; one load-store-load chain per row 10.7 us before that)
-    {
-        uint32_t v[kScanRows];
+    const uint32_t tot_d = live ? T[d] : 0u;
+    const uint32_t ex = wave_incl_scan(tot_d) - tot_d;  // every wave holds the block's 64 columns
+    uint32_t gpre = 0;
+    for (uint32_t g = 0; g < grp; ++g) gpre += gsum[g][col];
+    __syncthreads();
+    if (!live) return;
+    uint32_t run = red + ex + S[(size_t)blockIdx.x * bins + d] + gpre;
 #pragma unroll
-        for (uint32_t k = 0; k < kScanRows; ++k) v[k] = t0 + k < t1 ? C[(size_t)(t0 + k) * bins + d] : 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < kScanRows; ++k) {
-            if (t0 + k < t1 && (t0 + k) % row_step == 0) M[(size_t)(t0 + k) * bins + d] = run;
-            run += v[k];
-        }
+    for (uint32_t k = 0; k < kApplyRows; ++k) {
+        if (t0 + k < t1 && (t0 + k) % row_step == 0) M[(size_t)(t0 + k) * bins + d] = run;
+        run += v[k];
     }
 }
 
@@ -2601,7 +2619,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     const orl_grain_key* __restrict__ follower_keys, const orl_msg_hdr* __restrict__ direct, uint32_t nd, uint32_t n,
     uint32_t excl, uint32_t* __restrict__ route,
     uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift, uint32_t items,
-    const uint32_t* __restrict__ fblk) {
+    const uint32_t* __restrict__ fblk, uint32_t* __restrict__ col_atomic) {
     __shared__ FanSmem<HB> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
@@ -2752,6 +2770,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
     if (HIST) {
         __syncthreads();
         store_count_row(tile_cnt + (size_t)blockIdx.x * bins, sm.hist, bins);
+        // a small batch (col_atomic): the tile's counts also go to its 64-row chunk's column sums (S, zeroed by the degree
+        // scan), in place of k_col_sum's launch (config 5, round 5)
+        if (col_atomic)
+            for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x)
+                if (sm.hist[b]) atomicAdd(&col_atomic[(size_t)(blockIdx.x / kScanRows) * bins + b], sm.hist[b]);
     }
 }
 
@@ -4208,18 +4231,22 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
 // row_step: the reading pass uses rows t % row_step == 0 only.
 // plan_n > 0: the two-level plan's MSD columns — the apply kernel also writes the segment plan (k_seg_plan's work) for
 // plan_n messages in segments of plan_seg.
+// self_sums: the histogram pass accumulated s.col_sums' raw chunk sums itself (a small fan-out batch, nch <=
+// kSelfScanChunks, no hot column): no k_col_sum.
 void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, const Scratch& s, hipStream_t st,
-              uint32_t* hot_rows = nullptr, uint32_t plan_n = 0, uint32_t plan_seg = 0) {
+              uint32_t* hot_rows = nullptr, uint32_t plan_n = 0, uint32_t plan_seg = 0, bool self_sums = false) {
     const uint16_t* C = s.tile_cnt;
     const uint32_t nch = ceil_div(ntiles, kScanRows);
     const uint32_t cb = ceil_div(bins, 256);
     const uint32_t hy = hot_rows ? 1u : 0u;  // the hot column's extra grid row / block
-    hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, C, ntiles, bins, s.col_sums, hot_rows);
+    if (!self_sums || hot_rows || nch > kSelfScanChunks)
+        hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, C, ntiles, bins, s.col_sums, hot_rows);
     hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
                        ntiles);
     const bool plan = plan_n > 0;
-    hipLaunchKernelGGL(k_col_apply, dim3(nch + (plan ? 1u : 0u), cb + hy), dim3(256), 0, st, C, M, ntiles, bins, s.col_sums, s.col_tot,
-                       row_step, hot_rows, plan_n, plan_seg, plan ? s.bstart : nullptr, plan ? s.sstart : nullptr);
+    hipLaunchKernelGGL(k_col_apply, dim3(nch + (plan ? 1u : 0u), ceil_div(bins, kApplyCols) + hy), dim3(256), 0, st, C, M, ntiles,
+                       bins, s.col_sums, s.col_tot, row_step, hot_rows, plan_n, plan_seg, plan ? s.bstart : nullptr,
+                       plan ? s.sstart : nullptr);
 }
 
 // Digit whose tile histogram the route kernel builds (first LSD digit, or the MSD bucket digit of the
@@ -4334,6 +4361,15 @@ bool stage4_soa() {
 
 // Level 2's count and segment scan fused for plans without a skewed bucket (k_seg_count_scan); ORL_SEG_FUSED=0 keeps the
 // two-kernel form for every plan (A/B).
+// A small fan-out batch's column chunk sums accumulated by the fan-out kernel (round 5); ORL_COL_SELF=0: k_col_sum (A/B).
+bool col_self() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_COL_SELF");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool seg_fused() {
     static const bool on = [] {
         const char* e = getenv("ORL_SEG_FUSED");
@@ -4378,7 +4414,8 @@ bool hot_known(const Scratch& s) {
 // hot: the histogram pass wrote the hot key's per-row counts (s.hot_rows): this batch takes the hot-key path.  pick: the
 // batch is large enough for the path: the tail kernel picks the next batch's key (hot implies pick).
 int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t route_items, uint32_t* d_order,
-                       uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick = false) {
+                       uint32_t* d_offsets, const Scratch& s, hipStream_t st, bool hot, bool pick = false,
+                       bool self_cols = false) {
     const BucketPlan bp = make_bucket_plan(n_act);  // keys in [0, n_act]
     const uint32_t ntiles = ceil_div(n, kTile);
     const uint32_t nb = n_act + 2;
@@ -4392,7 +4429,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
         const void* kin = d_act;
         if (bp.hb > 0) {
-            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr, n, seg);  // + the segment plan
+            col_scan(s.tile_hist, nrows0, nbk, row_step0, s, st, hot ? s.hot_rows : nullptr, n, seg, self_cols);  // + the segment plan
             if (stage4_soa()) {  // the MSD pass writes level 2's input as SoA: indices, then the low digits only (u8 / u16)
                 uint32_t* idx = reinterpret_cast<uint32_t*>(s.pairs_a);
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
@@ -4420,7 +4457,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
                                (uint32_t)plan.shift[p], bins, s.tile_cnt);
-        col_scan(s.tile_hist, nrows, bins, row_step, s, st);
+        col_scan(s.tile_hist, nrows, bins, row_step, s, st, nullptr, 0, 0, p == 0 && self_cols);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
         launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
@@ -4586,17 +4623,25 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     const uint32_t fcap = s.fan_blk ? (uint32_t)std::min<uint64_t>((max_out + kFanBlk - 1) / kFanBlk + 1, s.fan_blk_cap) : 0u;
     const bool small = m <= kScanSmallChunk * kScanDirectChunks;  // 1024-element chunks: 4x the workgroups (k_scan_reduce)
     const uint32_t nbs = ceil_div(m, small ? kScanSmallChunk : kScanChunk);
+    // a small batch (at most kSelfScanChunks 64-row chunks of fan-out tiles, bounded by max_out): the fan-out kernel adds
+    // its tiles' counts into s.col_sums, which the degree scan zeroes first (no k_col_sum launch)
+    const RouteHist rh = route_hist(n_act);
+    const uint64_t nch_max = ceil_div(ceil_div(std::max<uint64_t>(max_out, 1), (uint64_t)kRouteThreads), (uint64_t)kScanRows);
+    const uint32_t zero_n = (buckets && rh.on && col_self()) ? (uint32_t)std::min<uint64_t>(nch_max, kSelfScanChunks) * rh.bins : 0u;
+    uint32_t* zero_p = zero_n ? s.col_sums : nullptr;
     if (small) {
         hipLaunchKernelGGL((k_scan_reduce<1, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
-                           d_csr_off, d_pubs, pstart, nullptr, 0u);
+                           d_csr_off, d_pubs, pstart, nullptr, 0u, zero_p, zero_n);
         hipLaunchKernelGGL((k_scan_down<true, true, false, kScanSmallChunk>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m,
                            s.scan_sums, d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else if (nbs <= kScanDirectChunks) {
-        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart,
+                           nullptr, 0u, zero_p, zero_n);
         hipLaunchKernelGGL((k_scan_down<true, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
                            d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
     } else {
-        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart);
+        hipLaunchKernelGGL(k_scan_reduce<1>, dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums, d_csr_off, d_pubs, pstart,
+                           nullptr, 0u, zero_p, zero_n);
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, s.scan_sums, nbs);
         hipLaunchKernelGGL((k_scan_down<false, true>), dim3(nbs), dim3(256), 0, st, poff32, (uint64_t)m, s.scan_sums,
                            d_pub_offsets, (uint64_t)n_direct, nullptr, 0u, nullptr, nullptr, s.fan_blk, fcap);
@@ -4622,9 +4667,10 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     // the scan's publisher-block map, when its capacity covered the batch (else the kernel's wave searches)
     const uint32_t* fblk = (fcap && (total + kFanBlk - 1) / kFanBlk < fcap) ? s.fan_blk : nullptr;
     const uint32_t nwg = ceil_div(total, kRouteThreads * items);
-    const RouteHist rh = route_hist(n_act);
     if (ev_route_begin) (void)hipEventRecord((hipEvent_t)ev_route_begin, st);
     const bool hist = buckets && rh.on;
+    const bool self_cols = hist && zero_n && (uint64_t)ceil_div(nwg, kScanRows) * rh.bins <= zero_n;
+    uint32_t* col_atomic = self_cols ? s.col_sums : nullptr;
 
 // the fan-out kernel's probe table: the 8-B form when the context has one (round 4), else the 16-B form (ORL_FAN_PROBE16=1
 // forces the 16-B form: A/B); U messages per thread and step (s.fan_u: ORL_FAN_U at context creation, A/B)
@@ -4638,7 +4684,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
                                                        dv.mask, dv.cache, dv.cmask, PROBE, PBAD, pstart, d_csr_tgt, d_pub_silo, poff32, (uint32_t)n_pub,            \
                                                        follower_tcd, d_follower_keys, d_direct, (uint32_t)n_direct, (uint32_t)total,    \
                                                        excl, d_route, d_act, TH, BINS, \
-                                                       SHIFT, items, fblk)
+                                                       SHIFT, items, fblk, col_atomic)
     if (hist) ORL_FAN(kMaxDigitBits, s.tile_cnt, rh.bins, rh.shift);
     else ORL_FAN(0, nullptr, 1u, 0u);
 #undef ORL_FAN
@@ -4646,7 +4692,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     if (ev_route_end) (void)hipEventRecord((hipEvent_t)ev_route_end, st);
     int e = (int)hipGetLastError();
     if (e || !buckets) return e;
-    return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st, false);
+    return bucket_after_route(d_act, (uint32_t)total, n_act, items, d_order, d_offsets, s, st, false, false, self_cols);
 }
 
 int launch_fanout_expand(const uint64_t* d_csr_off, const uint32_t* d_csr_tgt, const orl_grain_key* d_follower_keys,

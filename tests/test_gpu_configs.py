@@ -368,7 +368,7 @@ def test_config3_8ranks_bench_size_rehearsal(torch):
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     args = argparse.Namespace(local_ranks=8, config=3, grains=None, msgs=None, chunks=4, steps=1, warmup=1, wire16=False,
-                              unregistered=0.0, check_sample=1 << 20)
+                              unregistered=0.0, check_sample=1 << 20, sender_cache=0)
     res = bench.run_rehearsal(args, torch)
     print({k: res[k] for k in ("ms_per_step", "owned_per_rank", "max_over_mean_owned", "exchange")}, flush=True)
     assert res["check"] == "ok", res["check"]
