@@ -1447,25 +1447,29 @@ def run_presence(args, torch):
             exp["tcd"], exp["n0"], exp["n1"] = k["tcd"], k["n0"], k["n1"]
             return np.concatenate([m0, exp])
         cpu = cpu_step_baseline(o, make_msgs, n_keys, args.cpu_wall, f"{n_hb} game messages + {n_fan} player messages")
-    value = per_step * steps / thr_graph
+    # the step's three launch forms all do the whole step's work; the value is the fastest (named in config.timed_form).
+    # A one-step graph replay pays the HIP runtime's per-graph-launch gap (~5-8 us); 8 steps per graph amortise it
+    forms = {"eager": thr_eager * 1e3 / steps, "graph": thr_graph * 1e3 / steps,
+             f"graph_{n_sets}_steps_per_launch": thr_graph_all * 1e3 / (reps * n_sets)}
+    best = min(forms, key=forms.get)
+    value = per_step / (forms[best] * 1e-3)
     log(f"config 5: eager {thr_eager * 1e3 / steps:.3f} ms/step (p50 {np.percentile(lat_eager, 50):.3f}, "
         f"p99 {np.percentile(lat_eager, 99):.3f} ms); graph {thr_graph * 1e3 / steps:.3f} ms/step "
         f"(p50 {np.percentile(lat_graph, 50):.3f}, p99 {np.percentile(lat_graph, 99):.3f} ms); "
         f"{n_sets} steps per graph {thr_graph_all * 1e3 / (reps * n_sets):.3f} ms/step")
     return {"metric": "routed grain messages/sec (node)", "value": value, "unit": "messages/s", "n_gpus": 1,
-            "steps": steps, "warmup": args.warmup, "ms_per_step": thr_graph * 1e3 / steps, "higher_is_better": True,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": forms[best], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64 integer",
             "data": "synthetic (seeded Guids; config 5 of SURVEY §8(d))",
             "config": {"workload": f"config5: {n_games} Guid-keyed games x {per_game} players, {n_hb} heartbeats per "
-                                   f"step = {n_hb} game + {n_fan} player messages, stages 1-5, hipGraph replay",
-                       "messages_per_step": per_step, "mode": args.c5_mode,
+                                   f"step = {n_hb} game + {n_fan} player messages, stages 1-5",
+                       "timed_form": best, "messages_per_step": per_step, "mode": args.c5_mode,
                        "routing_contexts": 1 if mixed else args.c5_contexts},
             "latency_ms": {"eager_p50": float(np.percentile(lat_eager, 50)),
                            "eager_p99": float(np.percentile(lat_eager, 99)),
                            "graph_p50": float(np.percentile(lat_graph, 50)),
                            "graph_p99": float(np.percentile(lat_graph, 99))},
-            "throughput_msgs_per_s": {"eager": per_step * steps / thr_eager, "graph": value,
-                                      f"graph_{n_sets}_steps_per_launch": per_step * reps * n_sets / thr_graph_all},
+            "throughput_msgs_per_s": {k: per_step / (v * 1e-3) for k, v in forms.items()},
             "roofline": roof, "cpu_baseline": cpu}
 
 
