@@ -1299,7 +1299,8 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
 enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4 };  // LSD_PAIR: an LSD pass's pairs
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_PAIR_SMALL = 5 };
+// LSD_PAIR: an LSD pass's pairs; PAIR_SMALL: the MSD pass's pairs from 2048-element tiles (kMsdItemsSmall, small batches)
 
 // Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
 // zero-degree publishers share an offset with the next one and are skipped).  Whole wave, same v in every lane: each
@@ -4112,6 +4113,14 @@ int scan_offsets_pick(uint32_t* a, uint64_t m, uint32_t nkeys, uint32_t n, const
 // Elements per thread of the two-level path's MSD pass (tile 8192) and of the route kernels feeding it.
 // (32 = 8192-element tiles measured slower: route 1297 -> 1321 us, MSD pass 221 -> 256 us; profiles/r02_stage4_ab.txt)
 constexpr uint32_t kMsdItems = 16;
+// A small batch (<= kMsdSmallMax messages, route tiles of <= 8 items) takes the MSD pass in 2048-element tiles: twice the
+// workgroups (config 5: 144 tiles of 4096 fill only 144 of the 256 CUs)
+constexpr uint32_t kMsdItemsSmall = 8;
+constexpr uint32_t kMsdSmallMax = 8u << 20;
+uint32_t msd_items(uint32_t n, uint32_t route_items) {
+    static const bool off = [] { const char* e = getenv("ORL_MSD_SMALL"); return e && e[0] == '0'; }();  // A/B
+    return (!off && n <= kMsdSmallMax && route_items <= kMsdItemsSmall) ? kMsdItemsSmall : kMsdItems;
+}
 static_assert(kRouteThreads * kMsdItems <= 65535u, "a route tile's digit counts must fit the u16 count rows (store_count_row)");
 
 // ---- stage 4's hot-key path: the three small steps around the two-level sort (see kNoHotKey) -------------------------
@@ -4200,6 +4209,7 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
         switch (out) {
             case OUT_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kMsdItems); break;
+            case OUT_PAIR_SMALL: ORL_RP(IN_ACT, OUT_PAIR, kMsdItemsSmall); break;
             case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8, kMsdItems); break;
             case OUT_SOA16: ORL_RP(IN_ACT, OUT_SOA16, kMsdItems); break;
             case OUT_LSD_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kItems); break;
@@ -4422,8 +4432,9 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     // pass 0's histogram rows were written by the route kernel, one per route tile of 256 * route_items
     const uint32_t nrows0 = ceil_div(n, kRouteThreads * route_items);
     if (bp.two_level) {
-        const uint32_t row_step0 = kMsdItems / route_items;
-        const uint32_t ntiles = ceil_div(n, kRouteThreads * kMsdItems);
+        const uint32_t mitems = stage4_soa() ? kMsdItems : msd_items(n, route_items);
+        const uint32_t row_step0 = mitems / route_items;
+        const uint32_t ntiles = ceil_div(n, kRouteThreads * mitems);
         const uint32_t nbk = 1u << bp.hb;
         const uint32_t seg = seg_elems(n);
         const uint32_t grid = (uint32_t)max_segments(n, bp.hb);
@@ -4435,7 +4446,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
                 launch_pass(host_rm(s.device), bp.hb, IN_ACT, bp.lb <= 8 ? OUT_SOA8 : OUT_SOA16, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, nullptr, idx, idx + n, st);
             } else {
-                launch_pass(host_rm(s.device), bp.hb, IN_ACT, OUT_PAIR, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
+                launch_pass(host_rm(s.device), bp.hb, IN_ACT, mitems == kMsdItems ? OUT_PAIR : OUT_PAIR_SMALL, d_act, n, n_act, (uint32_t)bp.lb, s.tile_hist,
                             row_step0, ntiles, s.pairs_a, nullptr, nullptr, st, hot ? hot_cur(s) : nullptr, hot ? s.hot_rows : nullptr,
                             hot ? s.sorted_keys : nullptr);
             }
