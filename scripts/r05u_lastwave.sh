@@ -1,0 +1,15 @@
+# k_route's histogram row stored by the last wave out (default) vs a barrier (lab build -DORL_ROUTE_LASTWAVE=0)
+set -o pipefail
+O=gpurun_out/r05u; mkdir -p $O
+for rep in 1 2; do
+for v in main barrier; do
+  if [ $v = main ]; then unset LAB_LIB; else export LAB_LIB=lab/liborleans_route_$v.so; fi
+  timeout -k 10 300 python3 scripts/ab_lib.py --no-cpu --steps 10 > $O/c3_$v.txt 2>&1 || exit 1
+  echo "$v c3: $(grep -h 'rank 0:' $O/c3_$v.txt)"
+  timeout -k 10 200 python3 scripts/ab_lib.py --config 2 --no-cpu > $O/c2_$v.txt 2>&1 || exit 1
+  echo "$v c2: $(grep -h 'rank 0:' $O/c2_$v.txt)"
+done
+done
+unset LAB_LIB
+timeout -k 10 300 python3 scripts/rank_cost_lab.py > $O/rank_main.txt 2>&1 || exit 1
+grep -h 'hottest\|median\|hop 1' $O/rank_main.txt | sed 's/receives.*//'
