@@ -1071,6 +1071,32 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 // Pass 0's histogram is built by k_route itself; later passes read the previous pass's {key, index} pairs.
 // ACTS: the input is activation handles (clamped to the unresolved bucket n_act) instead of {key, index} pairs: the
 // first digit's histogram for stage 4 over messages routed earlier (orl_bucket_device, the host side of hop 2).
+// Stage 4's streamed inputs (each element read once per pass) are loaded non-temporally, so the passes' GBs do not evict
+// the partition's probe lines from L2 / the Infinity Cache before the next batch's route kernel (round 5).  ORL_STAGE4_NT=0
+// at build time: ordinary loads (A/B).
+#ifndef ORL_STAGE4_NT
+#define ORL_STAGE4_NT 1
+#endif
+__device__ __forceinline__ uint32_t ld_s4(const uint32_t* p) {
+    if (ORL_STAGE4_NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+__device__ __forceinline__ uint2 ld_s4(const uint2* p) {
+    using v2 = unsigned int __attribute__((ext_vector_type(2)));
+    if (ORL_STAGE4_NT) {
+        const v2 v = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
+        return make_uint2(v.x, v.y);
+    }
+    return *p;
+}
+__device__ __forceinline__ uint4 ld_s4(const uint4* p) {
+    if (ORL_STAGE4_NT) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
+
 template <bool ACTS>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     uint32_t bins, uint16_t* __restrict__ tile_cnt,
@@ -1089,7 +1115,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
             const uint32_t e = base + j * 256 + threadIdx.x;
-            k[j] = bucket_key(static_cast<const uint32_t*>(in)[e < n ? e : n - 1], n_act);
+            k[j] = bucket_key(ld_s4(static_cast<const uint32_t*>(in) + (e < n ? e : n - 1)), n_act);
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
@@ -1106,7 +1132,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
             const uint32_t e = base + j * 256 + threadIdx.x;
-            k[j] = static_cast<const uint2*>(in)[e < n ? e : n - 1].x;
+            k[j] = ld_s4(static_cast<const uint2*>(in) + (e < n ? e : n - 1)).x;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
@@ -1425,10 +1451,10 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         const uint32_t e = wbase + j * 64u + lane;
         const uint32_t ec = e < n ? e : n - 1;
         if (IN == IN_ACT) {
-            key[j] = bucket_key(static_cast<const uint32_t*>(in)[ec], n_act);
+            key[j] = bucket_key(ld_s4(static_cast<const uint32_t*>(in) + ec), n_act);
             idx[j] = e;
         } else {
-            const uint2 v = static_cast<const uint2*>(in)[ec];
+            const uint2 v = ld_s4(static_cast<const uint2*>(in) + ec);
             key[j] = v.x;
             idx[j] = v.y;
         }
@@ -1667,7 +1693,7 @@ __global__ __launch_bounds__(256) void k_offsets_gaps(const uint32_t* __restrict
         const uint4* p = reinterpret_cast<const uint4*>(sorted + i0);
 #pragma unroll
         for (uint32_t j = 0; j < kGapPer / 4; ++j) {
-            const uint4 v = p[j];
+            const uint4 v = ld_s4(p + j);
             k[4 * j] = v.x; k[4 * j + 1] = v.y; k[4 * j + 2] = v.z; k[4 * j + 3] = v.w;
         }
     } else {
@@ -1846,7 +1872,7 @@ template <int IN>
 __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n_total, uint32_t e, uint32_t n_act, uint32_t& key,
                                          uint32_t& idx) {
     if (IN == IN_ACT) {
-        key = bucket_key(static_cast<const uint32_t*>(in)[e], n_act);
+        key = bucket_key(ld_s4(static_cast<const uint32_t*>(in) + e), n_act);
         idx = e;
     } else if (IN == IN_SOA8 || IN == IN_SOA16) {
         const uint32_t* ix = static_cast<const uint32_t*>(in);
@@ -1854,7 +1880,7 @@ __device__ __forceinline__ void seg_load(const void* __restrict__ in, uint32_t n
                             : (uint32_t) reinterpret_cast<const uint16_t*>(ix + n_total)[e];
         idx = ix[e];
     } else {
-        const uint2 v = static_cast<const uint2*>(in)[e];
+        const uint2 v = ld_s4(static_cast<const uint2*>(in) + e);
         key = v.x;
         idx = v.y;
     }
