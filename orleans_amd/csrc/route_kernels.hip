@@ -2595,7 +2595,10 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 #ifndef ORL_FAN_LDS
 #define ORL_FAN_LDS 1024
 #endif
-constexpr uint32_t kFanLds = ORL_FAN_LDS;  // publishers staged per tile; beyond that fall back to global search
+constexpr uint32_t kFanLds = ORL_FAN_LDS;
+#ifndef ORL_FAN_NT
+#define ORL_FAN_NT 1  // the CSR targets loaded non-temporally (0: ordinary loads, A/B)
+#endif  // publishers staged per tile; beyond that fall back to global search
 
 template <int HB>
 struct FanSmem {
@@ -2707,7 +2710,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                     ci = pstart[pq] + (f - poff32[pq]);
                 }
                 pub[q] = pq;
-                tgt[q] = csr_tgt[ci];
+                tgt[q] = ORL_FAN_NT ? __builtin_nontemporal_load(csr_tgt + ci) : csr_tgt[ci];  // a stream per publisher
             }
         }
         Msg m[U];
@@ -4173,7 +4176,7 @@ __global__ __launch_bounds__(256) void k_hot_tail(const uint32_t* __restrict__ h
     for (; i + (kTailUnroll - 1) * stride < cnt; i += kTailUnroll * stride) {
         uint32_t v[kTailUnroll];
 #pragma unroll
-        for (uint32_t u = 0; u < kTailUnroll; ++u) v[u] = hot_idx[i + u * stride];
+        for (uint32_t u = 0; u < kTailUnroll; ++u) v[u] = ld_s4(hot_idx + i + u * stride);
 #pragma unroll
         for (uint32_t u = 0; u < kTailUnroll; ++u) order[off + i + u * stride] = v[u];
     }
