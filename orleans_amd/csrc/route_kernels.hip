@@ -2595,10 +2595,7 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 #ifndef ORL_FAN_LDS
 #define ORL_FAN_LDS 1024
 #endif
-constexpr uint32_t kFanLds = ORL_FAN_LDS;
-#ifndef ORL_FAN_NT
-#define ORL_FAN_NT 1  // the CSR targets loaded non-temporally (0: ordinary loads, A/B)
-#endif  // publishers staged per tile; beyond that fall back to global search
+constexpr uint32_t kFanLds = ORL_FAN_LDS;  // publishers staged per tile; beyond that fall back to global search
 
 template <int HB>
 struct FanSmem {
@@ -2710,7 +2707,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                     ci = pstart[pq] + (f - poff32[pq]);
                 }
                 pub[q] = pq;
-                tgt[q] = ORL_FAN_NT ? __builtin_nontemporal_load(csr_tgt + ci) : csr_tgt[ci];  // a stream per publisher
+                tgt[q] = csr_tgt[ci];
             }
         }
         Msg m[U];
