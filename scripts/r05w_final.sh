@@ -1,5 +1,5 @@
 # round-5 end-of-session evidence: smoke, the default bench line (config 3, 256M, with its CPU baseline), its kernel
-# trace, and the other configs' lines
+# trace, the other configs' lines, the per-rank cost at 8 ranks and the 8-rank rehearsal
 set -o pipefail
 O=gpurun_out/r05w; mkdir -p $O
 export TMPDIR=/tmp
@@ -13,7 +13,13 @@ for c in 2 4 5 1; do
   timeout -k 10 300 python3 bench.py --config $c > $O/config${c}_bench.txt 2>&1 || exit 1
   grep -h "^{" $O/config${c}_bench.txt > $O/config${c}_bench.json
 done
-head -12 $O/config3_kernel_stats.txt
+timeout -k 10 300 python3 scripts/rank_cost_lab.py > $O/rank_cost_8ranks.txt 2>&1 || exit 1
+timeout -k 10 600 python3 bench.py --local-ranks 8 --no-cpu > $O/rehearsal.txt 2>&1 || exit 1
+grep -h "^{" $O/rehearsal.txt > $O/node_rehearsal_8ranks_config3.json
+head -8 $O/config3_kernel_stats.txt
 for c in 3 2 4 5 1; do python3 -c "
 import json; d=json.load(open('$O/config${c}_bench.json')); r=d.get('roofline') or {}; cb=d.get('cpu_baseline') or {}
 print('config $c', round(d['ms_per_step'],4), 'ms', '%.3g'%d['value'], d['unit'], 'frac', r.get('frac'), 'cpu', cb.get('value'))"; done
+grep -h "hottest\|median\|hop 1" $O/rank_cost_8ranks.txt | sed 's/receives.*//'
+python3 -c "
+import json; d=json.load(open('$O/node_rehearsal_8ranks_config3.json')); print('rehearsal', d['ms_per_step'], d.get('check'))"
