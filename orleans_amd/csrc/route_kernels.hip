@@ -615,11 +615,17 @@ __global__ __launch_bounds__(256) void k_hash(const orl_grain_key* __restrict__ 
 // slower: profiles/r01_route_variants.txt.)  The probe chain is continued by a flag loop in the same
 // basic block as the first probe (an early-return helper loop for the chain cost 13 %: 1.76 vs 1.56 ms).
 // HB: capacity of the fused digit histogram in bits (0: none; 11 or 12 so the LDS is sized for the digit).
-// k_route's outputs: write-through stores that drop the line from the XCD's L2 (sc1; MI355X_MICROARCH.md, the stores
-// row), so the 512 MB of route/act words a config-2 batch writes do not displace probe-table lines; the stores are
-// whole 256-B wave runs.  Route kernel 1.294 -> 1.283 ms at config 2 (two A/B repeats, same box).
+// k_route's outputs: non-temporal stores (whole 256-B wave runs), so the route/act words a batch writes (512 MB at
+// config 2, 2 GB at config 3) do not displace probe-table lines.  Round 2's write-through agent-scope stores (sc1) gave
+// 1.294 -> 1.283 ms at config 2; the non-temporal form (round 5) 1.280 -> 1.277 ms there and 4.33 -> 4.15 ms at
+// config 3, whose Zipf-hot table lines are what L2 keeps (profiles/r05ntst_route_store_ab.txt).  ORL_ROUTE_STORE_SC1=1
+// at build time: the sc1 form (A/B).
 __device__ __forceinline__ void store_drop(uint32_t* p, uint32_t v) {
+#ifdef ORL_ROUTE_STORE_SC1
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
 }
 
 template <int HB>
@@ -2789,7 +2795,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
                 }
                 rr = route_tail(sm.P, m[q], h[q], own[q], rf[q], st == 0, fact, fsilo, act, false);
             }
-            route[e[q]] = rr;
+            route[e[q]] = rr;  // (non-temporal stores here: no change at configs 4 / 5, round 5)
             act_out[e[q]] = act;
             if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
         }
