@@ -1010,6 +1010,7 @@ constexpr uint32_t kHotMinBatch = 1u << 20, kHotShare = 32, kHotMinCount = 2 * 4
 // fblk[k] = the p with poff[p] <= k * kFanBlk < poff[p + 1], and fblk[ceil(total / kFanBlk)] = n_pub - 1 (written by
 // the last element, m - 1 = n_pub): a fan-out tile reads its publisher range with two independent loads.
 constexpr uint32_t kFanBlkShift = 8, kFanBlk = 1u << kFanBlkShift;
+constexpr uint32_t kFblkSerial = 8;  // blocks a publisher's own thread writes; more go to the whole wave
 template <bool DIRECT, bool WIDEN, bool PICK = false, uint32_t CH = kScanChunk>
 __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uint64_t m, const uint32_t* __restrict__ sums,
                                                    uint64_t* __restrict__ out64, uint64_t add64,
@@ -1054,15 +1055,26 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t* __restrict__ a, uin
 #pragma unroll
     for (int i = 0; i < E; ++i) {
         o[i] = run;
-        if (WIDEN && base + i < m) {
-            out64[base + i] = add64 + run;
-            if (fblk) {  // the fan-out blocks this publisher's messages start
-                const uint32_t k0 = (run + kFanBlk - 1u) >> kFanBlkShift;  // (a total past fblk_cap fails the launch after
-                if (base + i + 1 < m) {                                    //  the scan: its map is never read)
-                    for (uint32_t k = k0; (k << kFanBlkShift) < run + v[i] && k < fblk_cap; ++k) fblk[k] = (uint32_t)(base + i);
-                } else if (m > 1 && k0 < fblk_cap) {
-                    fblk[k0] = (uint32_t)(m - 2);
-                }
+        const bool live = base + i < m;
+        if (WIDEN && live) out64[base + i] = add64 + run;
+        if (WIDEN && fblk) {  // the fan-out blocks this publisher's messages start: [k0, k1)
+            const uint32_t k0 = (run + kFanBlk - 1u) >> kFanBlkShift;  // (a total past fblk_cap fails the launch after the
+            uint32_t k1 = k0;                                           //  scan: its map is never read)
+            if (live && base + i + 1 < m)
+                k1 = (uint32_t)std::min<uint64_t>(((uint64_t)run + v[i] + kFanBlk - 1u) >> kFanBlkShift, fblk_cap);
+            else if (live && m > 1 && k0 < fblk_cap)
+                fblk[k0] = (uint32_t)(m - 2);
+            const uint32_t cnt = k1 > k0 ? k1 - k0 : 0u;
+            if (cnt <= kFblkSerial)
+                for (uint32_t k = k0; k < k1; ++k) fblk[k] = (uint32_t)(base + i);
+            // a high-degree publisher's blocks: written by the whole wave, 64 at a time
+            uint64_t big = __ballot(cnt > kFblkSerial);
+            while (big) {
+                const int src = __builtin_ctzll(big);
+                big &= big - 1;
+                const uint32_t b0 = __shfl(k0, src, 64), b1 = __shfl(k1, src, 64);
+                const uint32_t p = __shfl((uint32_t)(base + i), src, 64);
+                for (uint32_t k = b0 + (threadIdx.x & 63u); k < b1; k += 64u) fblk[k] = p;
             }
         }
         run += v[i];
