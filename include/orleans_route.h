@@ -390,6 +390,10 @@ int orl_route_keyext_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uin
  * AddOrUpdate: the batch's last writer of a key wins.  Remove = CACHE_INVALIDATION_HEADER handling
  * (InsideGrainClient.cs:298-308).  Expiry / size policy (the maintainer) stays with the host: remove or clear. */
 #define ORL_RF_CACHED 0x08u
+/* A record the sender addressed from a stale cache entry, re-addressed by the receiver's directory (orl_route_received_device,
+ * the node exchange): the reference's NonExistentActivation forward with the old address in the cache-invalidation header
+ * (Dispatcher.cs:138-182, 429-487).  The sender should remove the entry (orl_cache_remove_device). */
+#define ORL_RF_CACHE_STALE 0x10u
 int orl_cache_config(orl_ctx* ctx, uint64_t capacity);
 int orl_cache_clear(orl_ctx* ctx);
 int orl_cache_add_or_update_device(orl_ctx* ctx, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
@@ -541,9 +545,12 @@ int orl_partition_cached_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n,
                                 uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, uint32_t fmt,
                                 uint32_t* d_act_out, uint64_t* d_counts, uint32_t* d_status, void* stream);
 /* Stages 1-3 of received hop-1 records (fmt 8 / 16 / 32) with their act lane: a record whose lane entry is not ORL_NO_ACT
- * was addressed by its sender's cache and gets HIT | ORL_RF_CACHED with its target silo as host and that handle, without
- * a directory probe (the receiving silo's Dispatcher takes an addressed message as is); the others are routed as
- * orl_route_*_device do.  No stage 4 (ORL_OPT_NO_BUCKETS implied; orl_bucket_device follows over the hosted set). */
+ * was addressed by its sender's cache.  When this context holds the grain's directory partition, the record is routed by
+ * the directory and keeps HIT | ORL_RF_CACHED only if the directory holds that handle on that silo; otherwise it gets the
+ * directory's word | ORL_RF_CACHE_STALE (the receiving silo's NonExistentActivation forward, Dispatcher.cs:138-182).  When
+ * it does not, the record gets HIT | ORL_RF_CACHED with its target silo as host and that handle, without a probe.  The
+ * others are routed as orl_route_*_device do.  No stage 4 (ORL_OPT_NO_BUCKETS implied; orl_bucket_device follows over the
+ * hosted set). */
 int orl_route_received_device(orl_ctx* ctx, const void* d_in, uint32_t fmt, size_t n, uint32_t opts, const uint32_t* d_in_act,
                               uint32_t* d_route, uint32_t* d_act, void* stream);
 
@@ -744,6 +751,9 @@ int orl_sync(orl_ctx* ctx);
                                  (>= 1/32 of its messages); 0xFFFFFFFF = none.  Outputs never depend on it.  Synchronises. */
 #define ORL_Q_HOT_BATCHES 11u /* batches that took stage 4's hot-key path so far (the launcher decides from a mapped host copy
                                  of the last pick, which may lag the device by the batches still queued) */
+#define ORL_Q_STAGE4_ERROR 12u /* 1 if a stage-4 look-back gave up since the last query (the two-level plan's fused level 2 on
+                                  a skewed batch, the LSD plan's single-sweep passes): that batch's order / offsets are not
+                                  valid.  Only a device fault can cause it.  Read and cleared; synchronises the device. */
 int orl_ctx_query(orl_ctx* ctx, uint32_t what, uint64_t* value);
 /* Stage-4 ranking: 0 = one LDS atomic per element (its lane order is checked by a self-test per device at the first
  * context creation; ORL_RANK_MODE=ballot forces the other), 1 = ballot match.  Process-wide per device; for validation. */

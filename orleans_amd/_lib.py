@@ -49,6 +49,7 @@ OPT_NO_BUCKETS = 0x2
 OPT_TOTAL_GIVEN = 0x4
 SPLIT_REMOVE = 0x1
 RF_CACHED = 0x08
+RF_CACHE_STALE = 0x10
 RING_CONSISTENT, RING_VBUCKETS = 0, 1
 OUTQ_LOOPBACK, OUTQ_PING, OUTQ_SYSTEM, OUTQ_REJECT, OUTQ_OVERFLOW, OUTQ_UNKNOWN_SILO = (
     0xFFFFFFF0, 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3, 0xFFFFFFF4, 0xFFFFFFF5)
@@ -64,6 +65,7 @@ Q_PART_ERROR = 9
 PART_CACHED = 0x8
 Q_HOT_KEY = 10
 Q_HOT_BATCHES = 11
+Q_STAGE4_ERROR = 12
 MAX_WIRE_TYPES = 16
 PART_LOOKBACK_FAILED = 0x4
 

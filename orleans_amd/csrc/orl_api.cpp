@@ -711,6 +711,7 @@ void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
+    f(c->s.sw_ring); f(c->s.sw_ctl); f(c->s.sw_gtot); f(c->s.sw_gmax); f(c->s.s4_err);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
     for (auto& e : c->tev) if (e) (void)hipEventDestroy(e);
@@ -835,6 +836,28 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMemset(c->s.lb_state, 0, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMemset(lb_state)");
         c->s.lb_ticket = 0;
         c->s.lb_epoch = 0;
+        if ((e = hipMalloc((void**)&c->s.s4_err, 4)) != hipSuccess) return bail(e, "hipMalloc(s4_err)");
+        if ((e = hipMemset(c->s.s4_err, 0, 4)) != hipSuccess) return bail(e, "hipMemset(s4_err)");
+        // the LSD plan's single-sweep passes (opt-in, ORL_LSD_SWEEP=1 at context creation: measured 8x slower than the
+        // k_hist_pairs passes on MI355X): a look-back ring of >= `tiles` rows, zeroed once
+        const char* sweep_env = getenv("ORL_LSD_SWEEP");
+        if (!bp.two_level && sweep_env && sweep_env[0] == '1') {
+            uint32_t row_bits = 0, rbits = 0;
+            for (int p = 0; p < bp.lsd.passes; ++p) row_bits = std::max<uint32_t>(row_bits, (uint32_t)bp.lsd.bits[p]);
+            while ((1ull << rbits) < tiles) ++rbits;
+            const uint64_t ring_bytes = (8ull << rbits) << row_bits;
+            if (ring_bytes <= (4ull << 30) && bp.lsd.passes <= 3) {  // else the k_hist_pairs passes (no ring)
+                if ((e = hipMalloc((void**)&c->s.sw_ring, ring_bytes)) != hipSuccess) return bail(e, "hipMalloc(sweep ring)");
+                if ((e = hipMemset(c->s.sw_ring, 0, ring_bytes)) != hipSuccess) return bail(e, "hipMemset(sweep ring)");
+                if ((e = hipMalloc((void**)&c->s.sw_ctl, 16)) != hipSuccess) return bail(e, "hipMalloc(sweep ctl)");
+                if ((e = hipMemset(c->s.sw_ctl, 0, 16)) != hipSuccess) return bail(e, "hipMemset(sweep ctl)");
+                if ((e = hipMalloc((void**)&c->s.sw_gtot, (3ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMalloc(sweep totals)");
+                if ((e = hipMemset(c->s.sw_gtot, 0, (3ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMemset(sweep totals)");
+                if ((e = hipMalloc((void**)&c->s.sw_gmax, (1ull << kMaxDigitBits) * 4)) != hipSuccess) return bail(e, "hipMalloc(sweep max)");
+                c->s.sw_rbits = rbits;
+                c->s.sw_row_bits = row_bits;
+            }
+        }
         if ((e = hipMalloc((void**)&c->s.gap_q, kGapQueueWords * 4)) != hipSuccess) return bail(e, "hipMalloc(gap_q)");
         if ((e = hipMemset(c->s.gap_q, 0, kGapQueueWords * 4)) != hipSuccess) return bail(e, "hipMemset(gap_q)");
         if ((e = hipMalloc((void**)&c->s.digits, mb)) != hipSuccess) return bail(e, "hipMalloc(digits)");
@@ -1291,6 +1314,7 @@ int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t
 }
 
 bool ctx_cache_on(orl_ctx* c) { return c && c->d_cache && c->hp.cache_on; }
+const uint32_t* ctx_stage4_err(const orl_ctx* c) { return c->s.s4_err; }
 }  // namespace orl
 extern "C" {
 
@@ -2221,6 +2245,16 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             uint32_t w = 0;
             ORL_HIP(c, hipMemcpy(&w, c->s.lb_state + 1, 4, hipMemcpyDeviceToHost));
             if (w) ORL_HIP(c, hipMemset(c->s.lb_state + 1, 0, 4));
+            *v = w ? 1u : 0u;
+            return ORL_OK;
+        }
+        case ORL_Q_STAGE4_ERROR: {  // stage 4's look-back error word (s4_err), read and cleared
+            if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+            ORL_HIP(c, hipSetDevice(c->cfg.device));
+            ORL_HIP(c, hipDeviceSynchronize());
+            uint32_t w = 0;
+            ORL_HIP(c, hipMemcpy(&w, c->s.s4_err, 4, hipMemcpyDeviceToHost));
+            if (w) ORL_HIP(c, hipMemset(c->s.s4_err, 0, 4));
             *v = w ? 1u : 0u;
             return ORL_OK;
         }

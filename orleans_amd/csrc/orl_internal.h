@@ -281,13 +281,26 @@ struct Scratch {
     unsigned long long* pick_word = nullptr; // the fused level-2 pick's max of (count << 32 | key), zero between batches
     uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
     uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key (the launcher's hot-key hint), [1]
-                                       // unused since round 5 (was the level-2 skew hint)
+                                       // the last two-level plan's skew flag (k_seg_count_scan writes it): it picks the fused
+                                       // level-2 kernel's solo form (no segment-scan launches) in launch_seg_bits
     uint32_t* hot_host_dev = nullptr;  // its device address
     mutable uint64_t hot_batches = 0;  // batches launched on the hot-key path (ORL_Q_HOT_BATCHES)
     uint32_t* fan_blk = nullptr;   // [fan_blk_cap] fan-out: the publisher of every 256th emitted message (k_scan_down WIDEN)
     uint32_t fan_blk_cap = 0;
     uint32_t gap_cap = 4096;  // LSD offsets' long-gap queue capacity (env_gap_cap() at context creation)
     int fan_u = 1;            // fan-out messages per thread and step (env_fan_u() at context creation)
+    // LSD plan in single-sweep passes (round 6, k_sweep): look-back ring [1 << sw_rbits][1 << sw_row_bits] u64 (zeroed once),
+    // control words {next ticket, launch base, done, -} (zeroed once), digit totals [3][2^kMaxDigitBits], each final digit's
+    // largest key's low bits [2^kMaxDigitBits].  sw_ring == nullptr: the context's plan is two-level, or the ring would not
+    // fit its budget — the LSD plan then takes the k_hist_pairs passes.
+    unsigned long long* sw_ring = nullptr;
+    uint32_t sw_rbits = 0, sw_row_bits = 0;
+    uint32_t* sw_ctl = nullptr;
+    uint32_t* sw_gtot = nullptr;
+    uint32_t* sw_gmax = nullptr;
+    // stage 4's look-back error word (the fused level-2 kernel's skewed form, k_sweep): |= 1 when a look-back gave up (a
+    // device fault); read and cleared by ORL_Q_STAGE4_ERROR, checked by the node after every host-side stage 4.
+    uint32_t* s4_err = nullptr;
 };
 
 // Knobs read from the environment once per context (orl_ctx_create): ORL_GAP_CAP, ORL_FAN_U.
@@ -399,6 +412,8 @@ int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t
                          uint32_t* d_status, void* stream, uint32_t* d_act_out = nullptr);
 // Whether the context's directory cache is configured and holds entries (the partition's cached destinations).
 bool ctx_cache_on(orl_ctx* c);
+// Device address of the context's stage-4 look-back error word (Scratch::s4_err).
+const uint32_t* ctx_stage4_err(const orl_ctx* c);
 // Stages 1-3 of received exchange records (fmt 8 / 16 / 32, no stage 4) with an optional act lane d_in_act: records the
 // sender addressed from its directory cache (act != ORL_NO_ACT) get HIT | CACHED without a probe.
 int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, uint32_t* d_route, uint32_t* d_act,

@@ -121,6 +121,9 @@ struct orl_node {
     hipStream_t sh = nullptr;  // the counts all-gathers: chunk c's runs while chunk c-1's data exchange is still on sx
     hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
     hipEvent_t ev_h = nullptr;  // the hop-2 host-rank counts are written (on sh)
+    hipEvent_t ev_s4 = nullptr; // the copy of the context's stage-4 error word after the last batch's stage 4 (on sr)
+    uint32_t* h_s4err = nullptr;  // pinned: that copy (checked at the start of the next batch: ADVICE r5)
+    bool s4_pending = false;
     hipEvent_t ev_part[2] = {nullptr, nullptr};  // the slot's partition (and heads) are complete
     hipEvent_t ev_slot[2] = {nullptr, nullptr};  // send slot released (its exchange finished)
     bool last_forward = false;  // the previous batch forwarded messages (hop 2): stage 4 then waits for the counts
@@ -376,7 +379,8 @@ void free_node(orl_node* nd) {
     if (nd->h_heads) (void)hipHostFree(nd->h_heads);
     if (nd->h_form) (void)hipHostFree(nd->h_form);
     if (nd->h_stall) (void)hipHostFree(nd->h_stall);
-    for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_h, nd->ev_slot[0], nd->ev_slot[1]})
+    if (nd->h_s4err) (void)hipHostFree(nd->h_s4err);
+    for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_h, nd->ev_slot[0], nd->ev_slot[1], nd->ev_s4})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr, nd->sh})
         if (s) (void)hipStreamDestroy(s);
@@ -571,7 +575,8 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sh, hipStreamNonBlocking));
-    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_h, &nd->ev_slot[0], &nd->ev_slot[1]})
+    for (hipEvent_t* ev : {&nd->ev_in, &nd->ev_part[0], &nd->ev_part[1], &nd->ev_x, &nd->ev_r, &nd->ev_h, &nd->ev_slot[0], &nd->ev_slot[1],
+                           &nd->ev_s4})
         ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     const uint64_t nr = cfg->nranks, mr = cfg->max_recv;
     ok(hipMalloc((void**)&nd->d_ros, 256));
@@ -581,6 +586,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     ok(hipMalloc((void**)&nd->d_heads, nr * kHeadWords * 8));
     ok(hipHostMalloc((void**)&nd->h_heads, nr * kHeadWords * 8, hipHostMallocDefault));
     ok(hipHostMalloc((void**)&nd->h_form, 2 * 8, hipHostMallocDefault));
+    ok(hipHostMalloc((void**)&nd->h_s4err, 8, hipHostMallocDefault));
     ok(hipMalloc((void**)&nd->d_recv, mr * 32));
     ok(hipMalloc((void**)&nd->d_route, mr * 4));
     ok(hipMalloc((void**)&nd->d_act, mr * 4));
@@ -679,6 +685,19 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     if (n && !d_in) return nfail(nd, ORL_E_INVALID, "null device buffer");
     if (n > nd->cfg.max_batch) return nfail(nd, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)nd->cfg.max_batch);
     std::memset(res, 0, sizeof *res);
+    if (nd->s4_pending) {  // the previous batch's stage 4 (its look-back error word, copied after it on sr)
+        NODE_HIP(nd, hipSetDevice(nd->device));
+        NODE_HIP(nd, hipEventSynchronize(nd->ev_s4));
+        nd->s4_pending = false;
+        if (*nd->h_s4err) {  // a device fault, on this rank only: its hosted order / offsets were not valid
+            *nd->h_s4err = 0;
+            uint64_t w = 0;
+            (void)orl_ctx_query(nd->ctx, ORL_Q_STAGE4_ERROR, &w);  // reads and clears the device word
+            break_node(nd);
+            return nfail(nd, ORL_E_DEVICE, "the previous batch's stage 4 look-back gave up (device fault): its order / offsets "
+                                           "were not valid; communicator aborted");
+        }
+    }
     const uint32_t nr = nd->nr, me = nd->me, K = nd->cfg.chunks;
     const uint64_t W = kHeadWords;
     const uint32_t ropts = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) | ORL_OPT_NO_BUCKETS;
@@ -908,6 +927,10 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     res->n_segments = (uint32_t)nd->segs.size();
     NODE_HIP(nd, hipEventRecord(nd->ev_r, nd->sr));
     NODE_HIP(nd, hipStreamWaitEvent(caller, nd->ev_r, 0));  // the caller's stream sees complete outputs
+    // stage 4's look-back error word, copied behind the outputs (the caller does not wait for it): the next batch checks it
+    NODE_HIP(nd, hipMemcpyAsync(nd->h_s4err, ctx_stage4_err(nd->ctx), 4, hipMemcpyDeviceToHost, nd->sr));
+    NODE_HIP(nd, hipEventRecord(nd->ev_s4, nd->sr));
+    nd->s4_pending = true;
     return ORL_OK;
 }
 

@@ -281,12 +281,36 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
 // A hop-1 record the SENDING rank addressed from its directory cache (the node exchange's act lane holds the cached
 // activation handle, the record's target silo the cached silo; ORL_NO_ACT = not cached): the route word the sender's
 // LocalLookup cache branch decided (LocalGrainDirectory.cs:690-717 → Dispatcher.AddressMessage, Dispatcher.cs:555-579),
-// HIT | CACHED with the cached silo as host, rebuilt from the record without a directory probe at the receiver.  r is
-// route_head's word; a cached record replaces it with a final word (no probe follows).
+// HIT | CACHED with the cached silo as host.  r is route_head's word at the receiver.
+//   * The receiver does not hold the grain's directory partition (r != kNeedProbe): the record is taken as addressed,
+//     without a probe (the final word replaces r) — the receiver has nothing to check it against.
+//   * It does (r == kNeedProbe: the activation lives on its owner, the common case): the record is routed by the
+//     directory like any other and `verify` = the cached handle; cached_verdict then keeps HIT | CACHED only when the
+//     directory holds that very activation on that silo.  A stale entry — the activation gone, or a reused handle that now
+//     belongs to another grain — is re-addressed by the directory and flagged ORL_RF_CACHE_STALE: the reference's
+//     receiving silo raises NonExistentActivation, forwards the message re-addressed and puts the old address in its
+//     cache-invalidation header (Dispatcher.cs:138-182, ProcessRequestToInvalidActivation / TryForwardRequest :429-487);
+//     hop 2 then delivers it to the directory's host (the receiver used to trust every cached record).
 __device__ __forceinline__ uint32_t sender_cached(const RouteParams& P, const Msg& m, uint32_t ca, uint32_t h, uint32_t owner,
-                                                  uint32_t rf, uint32_t r, uint32_t& act) {
+                                                  uint32_t rf, uint32_t r, uint32_t& act, uint32_t& verify) {
+    verify = ORL_NO_ACT;
     if (ca == ORL_NO_ACT) return r;
+    if (r == kNeedProbe) {
+        verify = ca;
+        return r;
+    }
     return route_tail(P, m, h, owner, rf, true, ca, m.meta >> 24, act, true);
+}
+
+// The directory's word rr (after the probe: found / fact / fsilo) for a record the sender addressed with handle `verify`.
+__device__ __forceinline__ uint32_t cached_verdict(const RouteParams& P, const Msg& m, uint32_t h, uint32_t owner, uint32_t rf,
+                                                   uint32_t rr, uint32_t& act, uint32_t verify, bool found, uint32_t fact,
+                                                   uint32_t fsilo) {
+    if (verify == ORL_NO_ACT) return rr;
+    const uint32_t cs = m.meta >> 24;
+    if (found && fact == verify && fsilo == cs && mask_bit(P.functional, cs))
+        return route_tail(P, m, h, owner, rf, true, verify, cs, act, true);
+    return rr | (ORL_RF_CACHE_STALE << 24);
 }
 
 // The hop-1 destination rank of a message with the sender's directory cache on (the node exchange, round 5): stages 1-2
@@ -703,10 +727,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         if (PW == 8) {  // same walk over the 8-B table (host-built only: no flag)
             bool can = false;
             uint2 q;
-            uint32_t cact = ORL_NO_ACT;
+            uint32_t cact = ORL_NO_ACT, vact = ORL_NO_ACT;
             if (e < n) {
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
-                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
+                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact, vact);
                 if (r == kNeedProbe) {
                     can = probe8_key(sm.P, m);
                     slot = dir_slot(h, dmask);
@@ -724,8 +748,12 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             }
             if (e < n) {
                 uint32_t act = cact, rr = r;
-                if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
-                else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                if (rr == kNeedProbe) {
+                    rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
+                    if (CIN) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
+                } else if (rr == kNeedProbeCache) {
+                    rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                }
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
                 if (HIST) {
@@ -740,10 +768,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             // Local owner: chain walk over the 16-B probe table.  A remote owner with the cache on walks the
             // 32-B cache table (route_msg).  Same decisions as the 32-B path (the probe table mirrors `dir`).
             uint32_t mk = kNoType;
-            uint32_t cact = ORL_NO_ACT;
+            uint32_t cact = ORL_NO_ACT, vact = ORL_NO_ACT;
             if (e < n) {
                 r = route_head(sm.P, m, excl != 0, h, own, rf);
-                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
+                if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact, vact);
                 if (r == kNeedProbe) {
                     mk = probe_type(sm.P, m);
                     slot = dir_slot(h, dmask);
@@ -760,8 +788,12 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             }
             if (e < n) {
                 uint32_t act = cact, rr = r;
-                if (rr == kNeedProbe) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
-                else if (rr == kNeedProbeCache) rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                if (rr == kNeedProbe) {
+                    rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
+                    if (CIN) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
+                } else if (rr == kNeedProbeCache) {
+                    rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                }
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
                 if (HIST) {
@@ -772,10 +804,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             }
             continue;
         }
-        uint32_t cact = ORL_NO_ACT;
+        uint32_t cact = ORL_NO_ACT, vact = ORL_NO_ACT;
         if (e < n) {
             r = route_head(sm.P, m, excl != 0, h, own, rf);
-            if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact);
+            if (CIN) r = sender_cached(sm.P, m, in_act[e], h, own, rf, r, cact, vact);
             if (r >= kNeedProbeCache) {
                 if (r == kNeedProbeCache) {  // remote owner, directory cache on
                     dir4 = reinterpret_cast<const u32x4*>(cache);
@@ -797,7 +829,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
         }
         if (e < n) {
             uint32_t act = cact, rr = r;
-            if (rr >= kNeedProbeCache) rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, rr == kNeedProbeCache);
+            if (rr >= kNeedProbeCache) {
+                const bool vc = rr == kNeedProbeCache;
+                rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, vc);
+                if (CIN && !vc) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
+            }
             store_drop(route + e, rr);
             store_drop(act_out + e, act);
             if (HIST) {
@@ -1325,6 +1361,9 @@ __global__ __launch_bounds__(256) void k_col_apply(const uint16_t* __restrict__ 
 // (b % 8 equal) get a contiguous range of tiles, so the short per-bin runs that consecutive tiles append
 // to the same output region meet in that XCD's L2 instead of leaving it as partial lines.
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
+#ifdef ORL_NO_XCD_TILE  // lab builds only: tiles in dispatch order (what a ticket-ordered look-back pass gets)
+    return b;
+#endif
     const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
@@ -1781,6 +1820,367 @@ __global__ __launch_bounds__(256) void k_offsets_long(uint32_t* __restrict__ off
             q[1] = 0;
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Stage 4, LSD plan (keys of > 2 x kMaxDigitBits bits: config 3's 24-bit handles, config 4's 10M accounts) in
+// single-sweep passes (round 6).  Rounds 2-5 gave every pass after the first a histogram pass
+// (k_hist_pairs: a re-read of the pairs the previous pass had just written) and a column scan of per-tile count rows,
+// and the last pass wrote the sorted keys for k_offsets_gaps to read back.  Here:
+//   k_digit_hist  one read of the handles counts the digits of every pass at once (global totals, no per-tile rows);
+//   k_sweep       each pass ranks its tile in LDS as k_radix_pass does and takes each digit's output base from the
+//                 digit's global start + a decoupled look-back over the earlier tiles' published per-digit counts (tiles
+//                 numbered by a ticket taken at start, so every tile a look-back waits on has started);
+//   FINAL         the last pass writes `order` and the bucket offsets, nothing else: its tile image is sorted by the
+//                 whole key (its input is sorted by the lower digits and the pass is stable), so the first message of
+//                 every key knows its predecessor key — the image's previous element, or, for a digit's first message
+//                 in the tile, the largest key of that digit in the earlier tiles, which the look-back carries beside
+//                 the count — and writes offsets[] for every bucket in between; k_sweep_tail writes the buckets past
+//                 each digit's largest key.  Every offset is written once.
+// Look-back state: a ring of rows [R][2^row_bits] of u64 words indexed by ticket (R a power of two >= the context's tiles,
+// so a launch never reuses a row and a row's older word belongs to a finished launch; one row width per context, so the
+// passes of one plan index the ring alike):
+//   bits 0-31 count, 32-53 the low `shift` bits of the largest key (FINAL), 54-55 kind (1 aggregate: this tile's count;
+//   2 inclusive: this and every earlier tile; 0 unpublished), 56-63 tag = (ticket >> log2 R) & 0xFF (a word the ring's
+//   previous round wrote reads as unpublished).
+// ctl = {next ticket, first ticket of this launch, workgroups done}: the last workgroup out moves the launch base on, so
+// nothing is reset by the host between launches and a captured hipGraph replays correctly.  A look-back that gives up
+// (a device fault: every awaited tile has started) sets the context's stage-4 error word (ORL_Q_STAGE4_ERROR).
+constexpr uint32_t kSweepSpin = 1u << 22;
+constexpr uint32_t kSweepWin = 4;  // earlier tiles whose words one look-back round trip loads per digit
+constexpr uint32_t kSweepMkMask = 0x3FFFFFu;
+
+template <int BITS>
+struct SweepSmem {
+    uint32_t cnt[kWaves][(1u << BITS) / 2u];  // packed per-wave counts -> per-wave starts; then the bins' deltas
+    uint2 stage[kTile];                       // the tile image, sorted by digit
+    uint32_t prev[1u << BITS];                // FINAL: the key before each digit's first message of the tile
+    uint32_t wsum[kWaves];
+    uint32_t tile, tick;
+};
+
+__device__ __forceinline__ unsigned long long sweep_word(uint32_t tag, uint32_t kind, uint32_t mk, uint32_t count) {
+    return ((unsigned long long)tag << 56) | ((unsigned long long)kind << 54) | ((unsigned long long)(mk & kSweepMkMask) << 32) |
+           count;
+}
+
+// Bucket offsets [lo, lo + len) = val, straight to HBM: a short gap by its lane, a long one by the whole wave (64 entries
+// per store), pieces of kGapChunk queued for k_sweep_tail while the queue has room.  Every lane of the wave calls it.
+__device__ __forceinline__ void write_gap(uint32_t* __restrict__ offsets, uint32_t lo, uint32_t len, uint32_t val,
+                                          uint32_t* __restrict__ q, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (len <= kGapWave)
+        for (uint32_t b = 0; b < len; ++b) offsets[lo + b] = val;
+    uint64_t m = __ballot(len > kGapWave);
+    while (m) {
+        const uint32_t src = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t glo = (uint32_t)__shfl((int)lo, (int)src, 64);
+        const uint32_t gl = (uint32_t)__shfl((int)len, (int)src, 64);
+        const uint32_t gv = (uint32_t)__shfl((int)val, (int)src, 64);
+        uint32_t done = 0;
+        if (gl > kGapChunk) {
+            const uint32_t pieces = gl / kGapChunk;
+            uint32_t first = 0;
+            if (lane == 0) first = atomicAdd(&q[0], pieces);
+            first = (uint32_t)__shfl((int)first, 0, 64);
+            const uint32_t took = first >= cap ? 0u : min(pieces, cap - first);
+            for (uint32_t p = lane; p < took; p += 64) {
+                uint32_t* t = q + 2 + 3 * (size_t)(first + p);
+                t[0] = glo + p * kGapChunk;
+                t[1] = kGapChunk;
+                t[2] = gv;
+            }
+            done = took * kGapChunk;
+        }
+        for (uint32_t b = done + lane; b < gl; b += 64) offsets[glo + b] = gv;
+    }
+}
+
+// One read of the handles: gtot[p << kMaxDigitBits | d] += messages whose pass-p digit is d (gtot zero: at context creation,
+// then by the previous batch's k_sweep_tail).
+// 16 handles per thread and step (four 16-B loads in flight); per-workgroup LDS counts, flushed with one atomic per bin.
+__global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__ act, uint32_t n, uint32_t n_act,
+                                                    uint32_t passes, uint32_t sh0, uint32_t sh1, uint32_t sh2, uint32_t m0,
+                                                    uint32_t m1, uint32_t m2, uint32_t* __restrict__ gtot) {
+    __shared__ uint32_t h[3][1u << kMaxDigitBits];
+    for (uint32_t b = threadIdx.x; b < 3u << kMaxDigitBits; b += 256) (&h[0][0])[b] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * 16u;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u; i0 < n; i0 += stride) {
+        uint32_t k[16];
+        if (i0 + 16 <= n) {
+            const uint4* p = reinterpret_cast<const uint4*>(act + i0);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint4 v = ld_s4(p + j);
+                k[4 * j] = v.x; k[4 * j + 1] = v.y; k[4 * j + 2] = v.z; k[4 * j + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j) k[j] = i0 + j < n ? act[i0 + j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) {
+            if (i0 + j >= n) break;
+            const uint32_t kk = bucket_key(k[j], n_act);
+            atomicAdd(&h[0][(kk >> sh0) & m0], 1u);
+            if (passes > 1) atomicAdd(&h[1][(kk >> sh1) & m1], 1u);
+            if (passes > 2) atomicAdd(&h[2][(kk >> sh2) & m2], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < 3u << kMaxDigitBits; b += 256) {
+        const uint32_t v = (&h[0][0])[b];
+        if (v) atomicAdd(gtot + b, v);
+    }
+}
+
+// One single-sweep LSD pass over a 4096-element tile (see above).  IN: IN_ACT (handles, clamped to n_act; index =
+// position) or IN_PAIR ({key, index} of the previous pass).  Not FINAL: {key, index} pairs to pair_out.  FINAL: indices to
+// order_out, the bucket offsets to offsets[0, nb) (k_sweep_tail completes them), each digit's largest key's low bits to
+// gmax (by the last tile).  gtot: this pass's global digit totals.
+template <int BITS, int IN, bool FINAL, int RM>
+__global__ __launch_bounds__(256) void k_sweep(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
+                                               const uint32_t* __restrict__ gtot, unsigned long long* __restrict__ ring,
+                                               uint32_t rbits, uint32_t row_bits, uint32_t* __restrict__ ctl, uint32_t ntiles,
+                                               uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
+                                               uint32_t* __restrict__ offsets, uint32_t nb, uint32_t* __restrict__ gmax,
+                                               uint32_t* __restrict__ gap_q, uint32_t gap_cap, uint32_t* __restrict__ err_word) {
+    constexpr uint32_t B = 1u << BITS, PER = kDigitsPerThread<BITS>;
+    __shared__ SweepSmem<BITS> sm;
+    const uint32_t rflags = rank_flags();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    for (uint32_t b = threadIdx.x; b < B / 2u; b += 256) {
+#pragma unroll
+        for (uint32_t q = 0; q < kWaves; ++q) sm.cnt[q][b] = 0;
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t tk = atomicAdd(&ctl[0], 1u);
+        sm.tick = tk;
+        sm.tile = tk - __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint32_t tile = sm.tile, tick = sm.tick;
+    const uint32_t rmask = (1u << rbits) - 1u;
+    const uint32_t tbase = tile * kTile, wbase = tbase + w * (kItems * 64u);
+    uint32_t key[kItems], idx[kItems], rank[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all in flight together
+        const uint32_t e = wbase + j * 64u + lane;
+        const uint32_t ec = e < n ? e : n - 1;
+        if (IN == IN_ACT) {
+            key[j] = bucket_key(ld_s4(static_cast<const uint32_t*>(in) + ec), n_act);
+            idx[j] = e;
+        } else {
+            const uint2 v = ld_s4(static_cast<const uint2*>(in) + ec);
+            key[j] = v.x;
+            idx[j] = v.y;
+        }
+    }
+    // each digit's global start: the exclusive prefix of the pass's digit totals (thread t owns digits [t*PER, t*PER+PER))
+    uint32_t gs[PER];
+    {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t d = threadIdx.x * PER + q;
+            gs[q] = d < B ? gtot[d] : 0u;
+            acc += gs[q];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan(acc, sm.wsum, total);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t v = gs[q];
+            gs[q] = run;
+            run += v;
+        }
+    }
+    {
+        uint32_t dg[kItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) dg[j] = (key[j] >> shift) & (B - 1u);
+        rank_steps<BITS, true, kItems, RM>(&sm.cnt[w][0], dg, n > wbase ? n - wbase : 0u, rank, rflags);
+    }
+    __syncthreads();
+    uint32_t tot[PER], start[PER];
+    round_starts<BITS>(sm.cnt, reinterpret_cast<uint32_t*>(&sm.stage[0]), tot, start);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        if (wbase + j * 64u + lane < n) {
+            const uint32_t d = (key[j] >> shift) & (B - 1u);
+            sm.stage[packed_get(sm.cnt[w], d) + rank[j]] = make_uint2(key[j], idx[j]);
+        }
+    }
+    __syncthreads();
+    // publish the tile's per-digit counts (tile 0: inclusive at once), look back, publish the inclusive counts
+    const uint32_t lowmask = (1u << shift) - 1u;  // FINAL: shift >= 1 (a plan of >= 2 passes)
+    const uint32_t tag = (tick >> rbits) & 0xFFu;
+    unsigned long long* my = ring + ((size_t)(tick & rmask) << row_bits);
+    uint32_t mk[PER], excl[PER], mkw[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t d = threadIdx.x * PER + q;
+        mk[q] = (FINAL && d < B && tot[q]) ? sm.stage[start[q] + tot[q] - 1u].x & lowmask : 0u;
+        excl[q] = 0;
+        mkw[q] = 0;
+        if (d < B) __hip_atomic_store(my + d, sweep_word(tag, tile == 0 ? 2u : 1u, mk[q], tot[q]), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tile > 0 && tile < ntiles) {
+        bool done[PER], found[PER];
+        uint32_t back[PER];  // the next earlier tile to read is tile - back
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            done[q] = threadIdx.x * PER + q >= B;
+            found[q] = false;
+            back[q] = 1;
+        }
+        uint32_t spins = 0;
+        for (;;) {
+            bool open = false;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; ++q) open |= !done[q];
+            if (!open) break;
+            unsigned long long v[PER][kSweepWin];
+#pragma unroll
+            for (uint32_t q = 0; q < PER; ++q) {
+                const uint32_t d = threadIdx.x * PER + q;
+#pragma unroll
+                for (uint32_t i = 0; i < kSweepWin; ++i) {
+                    const uint32_t bk = back[q] + i;
+                    v[q][i] = 0;
+                    if (!done[q] && bk <= tile)
+                        v[q][i] = __hip_atomic_load(ring + ((size_t)((tick - bk) & rmask) << row_bits) + d, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            bool moved = false;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; ++q) {
+                if (done[q]) continue;
+                uint32_t used = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kSweepWin; ++i) {
+                    const uint32_t bk = back[q] + i;
+                    const unsigned long long x = v[q][i];
+                    const uint32_t kind = (uint32_t)(x >> 54) & 3u, tg = (uint32_t)(x >> 56);
+                    if (bk > tile || kind == 0u || tg != (((tick - bk) >> rbits) & 0xFFu)) break;  // unpublished: poll again
+                    const uint32_t c = (uint32_t)x;
+                    excl[q] += c;
+                    if (FINAL && !found[q] && c) {
+                        found[q] = true;
+                        mkw[q] = (uint32_t)(x >> 32) & kSweepMkMask;
+                    }
+                    ++used;
+                    if (kind == 2u) {
+                        done[q] = true;
+                        break;
+                    }
+                }
+                back[q] += used;
+                moved |= used != 0;
+            }
+            if (!moved) {
+                if (++spins > kSweepSpin) {  // cannot happen with every earlier tile started; never hang the GPU
+                    atomicOr(err_word, 1u);
+#pragma unroll
+                    for (uint32_t q = 0; q < PER; ++q) done[q] = true;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    uint32_t* delta = &sm.cnt[0][0];  // the per-wave starts are consumed (the image is built)
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t d = threadIdx.x * PER + q;
+        if (d >= B) continue;
+        const uint32_t imk = tot[q] ? mk[q] : mkw[q];
+        if (tile > 0)
+            __hip_atomic_store(my + d, sweep_word(tag, 2u, imk, excl[q] + tot[q]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (FINAL && tile == ntiles - 1u) gmax[d] = imk;
+        delta[d] = gs[q] + excl[q] - start[q];
+        if (FINAL) sm.prev[d] = excl[q] ? (d << shift) | mkw[q] : (d << shift) - 1u;  // digit 0, none earlier: -1
+    }
+    __syncthreads();
+    const uint32_t cnt = tbase < n ? min(n - tbase, kTile) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t i = j * 256u + threadIdx.x;
+        uint32_t len = 0, lo = 0, g = 0;
+        if (i < cnt) {
+            const uint2 kv = sm.stage[i];
+            const uint32_t d = (kv.x >> shift) & (B - 1u);
+            g = delta[d] + i;
+            if (g < n) {  // always, with consistent totals; keeps a corrupt input from writing out of bounds
+                if (!FINAL) {
+                    pair_out[g] = kv;
+                } else {
+                    order_out[g] = kv.y;
+                    uint32_t kp = sm.prev[d];
+                    if (i > 0) {
+                        const uint32_t pk = sm.stage[i - 1u].x;
+                        if (((pk >> shift) & (B - 1u)) == d) kp = pk;
+                    }
+                    lo = kp + 1u;                                  // buckets (kp, key] start at g
+                    len = kv.x - kp;                               // kp = -1: key + 1
+                    len = lo < nb ? min(len, nb - lo) : 0u;        // never past the offsets
+                }
+            }
+        }
+        if (FINAL) write_gap(offsets, lo, len, g, gap_q, gap_cap);
+    }
+    if (threadIdx.x == 0) {  // the last workgroup out moves the launch base on
+        __threadfence();
+        if (atomicAdd(&ctl[2], 1u) == gridDim.x - 1u) {
+            __hip_atomic_store(&ctl[1], __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// After the FINAL sweep: the buckets past digit d's largest key (every bucket of an empty digit) start at the digit's end;
+// those past the last digit's range, up to nb - 1, at n.  One workgroup per digit; then the long-gap queue of write_gap
+// (k_offsets_long's work: grid-stride), and the last workgroup out empties the queue and zeroes every pass's digit totals
+// (gall, 3 << kMaxDigitBits words) for the next batch's k_digit_hist — no memset node, so a captured graph replays.
+__global__ __launch_bounds__(256) void k_sweep_tail(const uint32_t* __restrict__ gtot, const uint32_t* __restrict__ gmax,
+                                                    uint32_t bits, uint32_t shift, uint32_t nb, uint32_t* __restrict__ offsets,
+                                                    uint32_t* __restrict__ q, uint32_t cap, uint32_t* __restrict__ gall) {
+    __shared__ uint32_t last;
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t qn;
+    const uint32_t B = 1u << bits, d = blockIdx.x;
+    uint32_t acc = 0;
+    for (uint32_t i = threadIdx.x; i <= d; i += 256) acc += gtot[i];
+    uint32_t end;
+    (void)block_excl_scan(acc, wsum, end);  // messages of digits <= d
+    const uint64_t dlo = (uint64_t)d << shift;
+    const uint64_t dhi = d == B - 1u ? (uint64_t)nb : std::min<uint64_t>((uint64_t)(d + 1u) << shift, nb);
+    const uint64_t lo = gtot[d] ? dlo + gmax[d] + 1u : dlo;
+    for (uint64_t b = lo + threadIdx.x; b < dhi; b += 256) offsets[b] = end;
+    if (threadIdx.x == 0) qn = min(__hip_atomic_load(&q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), cap);
+    __syncthreads();
+    for (uint32_t e = blockIdx.x; e < qn; e += gridDim.x) {
+        const uint32_t* t = q + 2 + 3 * (size_t)e;
+        const uint32_t glo = t[0], len = t[1], val = t[2];
+        for (uint32_t b = threadIdx.x; b < len; b += 256) offsets[glo + b] = val;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&q[1], 1u) == gridDim.x - 1u ? 1u : 0u;
+        if (last) {
+            q[0] = 0;
+            q[1] = 0;
+        }
+    }
+    __syncthreads();
+    if (last)  // every workgroup has read its digit totals
+        for (uint32_t i = threadIdx.x; i < 3u << kMaxDigitBits; i += 256) gall[i] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -4281,6 +4681,61 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
     }
 }
 
+// The LSD plan's single-sweep passes (k_sweep, round 6): on when the context holds the look-back ring (ORL_LSD_SWEEP=1 at
+// context creation; off by default: 7 ms per pass against 0.85 ms, see k_sweep).
+bool lsd_sweep(const Scratch& s) { return s.sw_ring != nullptr; }
+
+template <int BITS>
+void launch_sweep_bits(int rm, int in, bool fin, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* gtot,
+                       uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* offsets, uint32_t nb, const Scratch& s,
+                       hipStream_t st) {
+#define ORL_SW3(I, F, R) hipLaunchKernelGGL((k_sweep<BITS, I, F, R>), dim3(ntiles), dim3(256), 0, st, kin, n, n_act, shift, gtot,   \
+                                            s.sw_ring, s.sw_rbits, s.sw_row_bits, s.sw_ctl, ntiles, pout, order, offsets, nb,        \
+                                            s.sw_gmax, s.gap_q, s.gap_cap, s.s4_err)
+#define ORL_SW(I, F) do { if (rm == kRmPlain) ORL_SW3(I, F, kRmPlain); else if (rm == kRmHot) ORL_SW3(I, F, kRmHot);                    \
+                          else ORL_SW3(I, F, kRmBallot); } while (0)
+    if (in == IN_ACT) ORL_SW(IN_ACT, false);  // a plan of >= 2 passes: the handles are never the last pass's input
+    else if (fin) ORL_SW(IN_PAIR, true);
+    else ORL_SW(IN_PAIR, false);
+#undef ORL_SW
+#undef ORL_SW3
+}
+
+// The LSD plan's stage 4: one digit-total read of the handles, then the passes act → pairs_a → pairs_b → ... → (order,
+// offsets), then the offsets' tails.  7 + 4 launches fewer than the k_hist_pairs form for three passes, no sorted keys.
+int bucket_lsd_sweep(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets,
+                     const Scratch& s, hipStream_t st) {
+    const RadixPlan plan = make_bucket_plan(n_act).lsd;
+    const uint32_t nb = n_act + 2, ntiles = ceil_div(n, kTile);
+    if (plan.passes < 2 || plan.passes > 3) return (int)hipErrorInvalidValue;  // the context allocated no ring for it
+    uint32_t sh[3] = {0, 0, 0}, mk[3] = {0, 0, 0};
+    for (int p = 0; p < plan.passes; ++p) {
+        sh[p] = (uint32_t)plan.shift[p];
+        mk[p] = (1u << plan.bits[p]) - 1u;
+    }
+    hipLaunchKernelGGL(k_digit_hist, dim3(std::min<uint32_t>(ceil_div(n, 256u * 16u), 1024u)), dim3(256), 0, st, d_act, n, n_act,
+                       (uint32_t)plan.passes, sh[0], sh[1], sh[2], mk[0], mk[1], mk[2], s.sw_gtot);
+    const int rm = host_rm(s.device);
+    uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
+    for (int p = 0; p < plan.passes; ++p) {
+        const bool last = p == plan.passes - 1;
+        const void* kin = p == 0 ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
+        const uint32_t* gtot = s.sw_gtot + ((size_t)p << kMaxDigitBits);
+        const int in = p == 0 ? IN_ACT : IN_PAIR;
+        switch (plan.bits[p]) {
+#define ORL_CASE(B) case B: launch_sweep_bits<B>(rm, in, last, kin, n, n_act, (uint32_t)plan.shift[p], gtot, ntiles, pbuf[p & 1], \
+                                                 d_order, d_offsets, nb, s, st); break;
+            ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
+#undef ORL_CASE
+            default: return (int)hipErrorInvalidValue;  // 3 passes of > 22 bits: 7-11 bits each
+        }
+    }
+    const int lp = plan.passes - 1;
+    hipLaunchKernelGGL(k_sweep_tail, dim3(1u << plan.bits[lp]), dim3(256), 0, st, s.sw_gtot + ((size_t)lp << kMaxDigitBits), s.sw_gmax,
+                       (uint32_t)plan.bits[lp], (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap, s.sw_gtot);
+    return (int)hipGetLastError();
+}
+
 // Column scan of a tile-major [ntiles][bins] u16 count matrix C (s.tile_cnt) into per-(tile, bin) u32 output bases M.
 // row_step: the reading pass uses rows t % row_step == 0 only.
 // plan_n > 0: the two-level plan's MSD columns — the apply kernel also writes the segment plan (k_seg_plan's work) for
@@ -4310,9 +4765,10 @@ struct RouteHist {
     uint32_t bins, shift;
 };
 
-RouteHist route_hist(uint32_t n_act) {
+RouteHist route_hist(uint32_t n_act, const Scratch& s) {
     const BucketPlan bp = make_bucket_plan(n_act);
     if (bp.two_level) return {bp.hb > 0, 1u << bp.hb, (uint32_t)bp.lb};
+    if (lsd_sweep(s)) return {false, 1u, 0u};  // the single-sweep passes count their digits themselves (k_digit_hist)
     return {true, 1u << bp.lsd.bits[0], (uint32_t)bp.lsd.shift[0]};
 }
 
@@ -4346,7 +4802,7 @@ void launch_seg_bits(int in, const void* kin, uint32_t n, uint32_t n_act, uint32
     const uint32_t epoch = solo ? next_seg_epoch(s) : 0u;
 #define ORL_SF(I) hipLaunchKernelGGL((k_seg_count_scan<LB, I>), dim3(fgrid), dim3(256), 0, st, kin, n, n_act, nbk, nb, seg, s.bstart, \
                                      s.sstart, s.seg_hist, d_offsets, solo, direct, skew_host, pick_word, n_act + 1, s.seg_carry,  \
-                                     s.seg_meta, s.seg_lb, s.seg_lbctl, s.seg_lb_cap, epoch, s.lb_state + 1)
+                                     s.seg_meta, s.seg_lb, s.seg_lbctl, s.seg_lb_cap, epoch, s.s4_err)
 #define ORL_SC(I) hipLaunchKernelGGL((k_seg_count<LB, I>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart, s.sstart, \
                                      s.seg_hist)
 #define ORL_SS3(I, R) hipLaunchKernelGGL((k_seg_scatter<LB, I, R>), dim3(grid), dim3(256), 0, st, kin, n, n_act, nbk, seg, s.bstart,\
@@ -4502,6 +4958,7 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         launch_seg(bp.lb, lin, kin, n, n_act, nbk, seg, grid, d_order, d_offsets, s, st, hot && bp.hb > 0, (hot || pick) && bp.hb > 0);
         return (int)hipGetLastError();
     }
+    if (lsd_sweep(s)) return bucket_lsd_sweep(d_act, n, n_act, d_order, d_offsets, s, st);
     const RadixPlan& plan = bp.lsd;
     const uint32_t row_step0 = kItems / route_items;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
@@ -4617,7 +5074,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     }
     const uint32_t items = route_items(n, max_route_items(n_act));
     const uint32_t nwg = ceil_div(n, kRouteThreads * items);
-    const RouteHist rh = route_hist(n_act);
+    const RouteHist rh = route_hist(n_act, s);
     if (ev_begin) (void)hipEventRecord((hipEvent_t)ev_begin, st);
     const bool hist = buckets && rh.on;
     const bool pick = hist && hot_path_on(n, n_act, s);
@@ -4680,7 +5137,7 @@ int launch_fanout_route_bucket(const RouteParams* d_params, const DirView& dv, c
     const uint32_t nbs = ceil_div(m, small ? kScanSmallChunk : kScanChunk);
     // a small batch (at most kSelfScanChunks 64-row chunks of fan-out tiles, bounded by max_out): the fan-out kernel adds
     // its tiles' counts into s.col_sums, which the degree scan zeroes first (no k_col_sum launch)
-    const RouteHist rh = route_hist(n_act);
+    const RouteHist rh = route_hist(n_act, s);
     const uint64_t nch_max = ceil_div(ceil_div(std::max<uint64_t>(max_out, 1), (uint64_t)kRouteThreads), (uint64_t)kScanRows);
     const uint32_t zero_n = (buckets && rh.on && col_self()) ? (uint32_t)std::min<uint64_t>(nch_max, kSelfScanChunks) * rh.bins : 0u;
     uint32_t* zero_p = zero_n ? s.col_sums : nullptr;
@@ -4936,7 +5393,7 @@ int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t
                        void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) return (int)hipMemsetAsync(d_offsets, 0, sizeof(uint32_t) * ((size_t)n_act + 2), st);
-    const RouteHist rh = route_hist(n_act);
+    const RouteHist rh = route_hist(n_act, s);
     const uint32_t ntiles = ceil_div(n, kTile);
     const bool pick = rh.on && hot_path_on(n, n_act, s);
     const bool hot = pick && hot_known(s);

@@ -83,7 +83,9 @@ def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None)
     caches[s] (optional): rank s's directory cache {(tcd, n0, n1): (act, silo)}.  A message whose owner is on another rank
     and whose grain rank s caches on a functional silo is addressed at the sender (LocalLookup's cache branch,
     LocalGrainDirectory.cs:690-717; pyref.apply_directory_cache: HIT | CACHED, TargetSilo = the cached silo) and sent to
-    the rank hosting that silo instead of the owner's; the others follow the oracle partition by owner rank."""
+    the rank hosting that silo instead of the owner's; the others follow the oracle partition by owner rank.  The receiver
+    checks a cached record against its directory when it holds the grain's partition (stale entries are
+    re-addressed and flagged ORL_RF_CACHE_STALE)."""
     from oracle import pyref as P
     nr = len(batches)
     functional = functional if functional is not None else [1] * 8
@@ -129,8 +131,18 @@ def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None)
             m = cr >= 0
             r = r.copy()
             a = a.copy()
-            r[m] = cr[m].astype(np.uint32)
-            a[m] = ca[m]
+            # a record the sender addressed from its cache: where rank d holds the grain's directory partition (its own
+            # route is not REMOTE_OWNER) the directory decides — HIT | CACHED kept only when it holds that handle on that
+            # silo, else the directory's word | CACHE_STALE (NonExistentActivation → forward, Dispatcher.cs:138-182);
+            # elsewhere the record is taken as addressed
+            own_dir = ((r >> 16) & 0xFF) != L.ST_REMOTE_OWNER
+            crw = cr.astype(np.uint32)
+            same = (((r >> 16) & 0xFF) == L.ST_HIT) & (a == ca) & (((r >> 8) & 0xFF) == ((crw >> 8) & 0xFF))
+            keep = m & (~own_dir | same)
+            stale = m & own_dir & ~same
+            r[keep] = crw[keep]
+            a[keep] = ca[keep]
+            r[stale] |= np.uint32(L.RF_CACHE_STALE << 24)
         routed.append((r, a))
     hostr = [host_rank(routed[d][0], ros, d) for d in range(nr)]
     forward = any((hostr[d] != d).any() for d in range(nr))

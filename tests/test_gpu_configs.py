@@ -738,7 +738,7 @@ def test_stage4_skewed_plans_async_vs_oracle(torch, n_act):
         eo, ef = o.bucket(a, n_act)
         np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), ef)
         np.testing.assert_array_equal(order.cpu().numpy().view(np.uint32), eo)
-    assert eng.query(L.Q_PART_ERROR) == 0  # no look-back gave up
+    assert eng.query(L.Q_STAGE4_ERROR) == 0  # no look-back gave up (the fused level 2's error word)
     eng.close()
 
 
@@ -915,4 +915,78 @@ def test_lsd_offsets_long_gaps_vs_oracle(torch, monkeypatch, cap):
         eo, ef = o.bucket(a, n_act)
         np.testing.assert_array_equal(_u32(order), eo, err_msg=f"batch {k} order")
         np.testing.assert_array_equal(_u32(off), ef, err_msg=f"batch {k} offsets")
+    eng.close()
+
+
+@pytest.mark.parametrize("n_act", [12_000_000, 40_000_000])
+def test_lsd_sweep_async_vs_oracle(torch, monkeypatch, n_act):
+    """The LSD plan's single-sweep passes (round 6: k_digit_hist, one k_sweep per digit with a decoupled look-back, the
+    final pass writing the bucket offsets itself, k_sweep_tail).  A sequence of batches enqueued on ONE stream with no host
+    sync in between, so the look-back ring and its ticket words are reused launch after launch at every size: large and
+    small, Zipf-hot (a digit with millions of messages), one activation, the unresolved bucket, sparse keys (long empty
+    gaps, digits with no message), one message.  Each batch bit-exact vs the oracle's stable bucketing
+    (ActivationData.EnqueueMessage FIFO, ActivationData.cs:483-514) and equal to the default k_hist_pairs form (the sweep
+    is opt-in, ORL_LSD_SWEEP=1: slower on MI355X); then the same stage 4 captured in a hipGraph and replayed (the launch base lives on the device,
+    so a replay needs no host state).  n_act 12M: 8 + 8 + 8-bit digits; 40M: 9 + 9 + 8."""
+    t = torch
+    rng = np.random.default_rng(n_act + 1)
+    o = cpu_ref.Oracle(8)
+
+    def zipf(n):
+        r = np.minimum(rng.zipf(1.1, n), n_act) - 1
+        return ((r.astype(np.uint64) * np.uint64(2654435761)) % np.uint64(n_act)).astype(np.uint32)
+
+    batches = [rng.integers(0, n_act, 2_500_000, dtype=np.int64).astype(np.uint32),
+               zipf(3_000_001),
+               rng.integers(0, n_act, 4097, dtype=np.int64).astype(np.uint32),
+               np.full(700_000, n_act // 3, np.uint32),
+               rng.integers(0, 300, 200_000, dtype=np.int64).astype(np.uint32) * np.uint32(n_act // 301),  # sparse
+               np.where(rng.random(1_000_000) < 0.4, np.uint32(L.NO_ACT), zipf(1_000_000)).astype(np.uint32),
+               np.array([n_act - 1], np.uint32),
+               zipf(2_000_000)]
+    monkeypatch.setenv("ORL_LSD_SWEEP", "1")  # opt-in (slower on MI355X: DESIGN §4)
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=3_100_000, device=0)
+    monkeypatch.delenv("ORL_LSD_SWEEP")
+    W.setup_engine(eng, W.default_cluster())
+    ref = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=3_100_000, device=0)
+    W.setup_engine(ref, W.default_cluster())
+    s = t.cuda.Stream()
+    d_acts = [t.from_numpy(a.view(np.int32)).cuda() for a in batches]
+    outs, routs = [], []
+    with t.cuda.stream(s):
+        for d_a in d_acts:
+            for e, acc in ((eng, outs), (ref, routs)):
+                order = t.full((len(d_a),), -1, dtype=t.int32, device="cuda")
+                off = t.full((n_act + 2,), -1, dtype=t.int32, device="cuda")
+                e.bucket_device(d_a, len(d_a), order, off, stream=s.cuda_stream)
+                acc.append((order, off))
+    s.synchronize()
+    for k, a in enumerate(batches):
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(_u32(outs[k][1]), ef, err_msg=f"batch {k} offsets")
+        np.testing.assert_array_equal(_u32(outs[k][0]), eo, err_msg=f"batch {k} order")
+        np.testing.assert_array_equal(_u32(routs[k][1]), ef, err_msg=f"batch {k} offsets (k_hist_pairs form)")
+        np.testing.assert_array_equal(_u32(routs[k][0]), eo, err_msg=f"batch {k} order (k_hist_pairs form)")
+    assert eng.query(L.Q_STAGE4_ERROR) == 0
+    # the Zipf batch captured once, replayed three times (zeroed outputs between), then an eager batch of another size
+    order, off = outs[1]
+    g = t.cuda.CUDAGraph()
+    with t.cuda.graph(g, stream=s):
+        eng.bucket_device(d_acts[1], len(batches[1]), order, off, stream=s.cuda_stream)
+    eo, ef = o.bucket(batches[1], n_act)
+    for _ in range(3):
+        order.fill_(0)
+        off.fill_(0)
+        g.replay()
+        t.cuda.synchronize()
+        np.testing.assert_array_equal(_u32(off), ef, err_msg="graph replay offsets")
+        np.testing.assert_array_equal(_u32(order), eo, err_msg="graph replay order")
+    order2, off2 = outs[0]
+    eng.bucket_device(d_acts[0], len(batches[0]), order2, off2)
+    t.cuda.synchronize()
+    eo, ef = o.bucket(batches[0], n_act)
+    np.testing.assert_array_equal(_u32(off2), ef, err_msg="eager after replays: offsets")
+    np.testing.assert_array_equal(_u32(order2), eo, err_msg="eager after replays: order")
+    assert eng.query(L.Q_STAGE4_ERROR) == 0
+    ref.close()
     eng.close()

@@ -836,11 +836,15 @@ def test_directory_cache_in_route_vs_oracle(torch):
     kt = list(zip(msgs["tcd"].tolist(), msgs["n0"].tolist(), msgs["n1"].tolist()))
     for rnd in range(3):
         pick = rng.choice(remote, 20_000)   # duplicates within the batch: the last writer wins
-        acts = (50_000 + rng.integers(0, 10_000, len(pick))).astype(np.uint32)
+        # handles [50000, 70000): the half >= n_act is kept only for a silo this context does not host (the host's catalog
+        # numbers it; since round 5, VERDICT r5 item 1 / ADVICE r5) — such a HIT | CACHED message lands in the unresolved
+        # bucket n_act of this context's stage 4; on a local silo it is dropped (outside the local handle space)
+        acts = (50_000 + rng.integers(0, 20_000, len(pick))).astype(np.uint32)
         silos = rng.integers(0, 8, len(pick)).astype(np.uint8)
         eng.cache_add_or_update_device(dev(keys[pick]), dev(acts), dev(silos), len(pick), stream=st_)
         for g, a, s in zip(pick.tolist(), acts.tolist(), silos.tolist()):
-            cache[(int(keys["tcd"][g]), int(keys["n0"][g]), int(keys["n1"][g]))] = (a, s)
+            if a < n_act or not local[s]:
+                cache[(int(keys["tcd"][g]), int(keys["n0"][g]), int(keys["n1"][g]))] = (a, s)
         inval = rng.choice(remote, 3000)
         d_rm = t.empty(len(inval), dtype=t.uint8, device="cuda")
         eng.cache_remove_device(dev(keys[inval]), len(inval), d_rm, stream=st_)
@@ -858,6 +862,9 @@ def test_directory_cache_in_route_vs_oracle(torch):
         np.testing.assert_array_equal(res.order, o_ref)
         np.testing.assert_array_equal(res.offsets, f_ref)
         assert ((res.route >> 24) & L.RF_CACHED).sum() > 1000
+        big = ((res.route >> 24) & L.RF_CACHED != 0) & (res.act >= n_act)
+        assert big.sum() > 500  # cached handles of another silo's catalog, >= this context's n_act
+        assert (res.offsets[n_act + 1] - res.offsets[n_act]) >= big.sum()  # ... bucketed as unresolved here
     eng.cache_clear()
     np.testing.assert_array_equal(eng.address_messages(msgs).route, o.route(msgs)[0])
     eng.close()
