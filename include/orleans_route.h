@@ -357,15 +357,16 @@ typedef struct orl_ext_ref {
 } orl_ext_ref;
 /* RegisterSingleActivation of KeyExt grains (category ORL_CAT_KEYEXT_GRAIN; the same statuses as orl_dir_insert_single:
  * owner = the ring owner of the KeyExt hash, excludeThisSiloIfStopping; a key of another category gives
- * ORL_INS_UNSUPPORTED).  Host arrays; `blob` holds the extensions. */
+ * ORL_INS_UNSUPPORTED).  Host arrays; `blob` (blob_bytes long) holds the extensions: a reference outside it fails the call
+ * with ORL_E_INVALID before anything is inserted; ORL_E_CAPACITY when the library's extension store would pass 4 GiB. */
 int orl_dir_insert_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
-                          const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* winner_act,
+                          uint64_t blob_bytes, const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* winner_act,
                           uint8_t* winner_silo, uint8_t* status);
-int orl_dir_remove_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
-                          uint8_t* removed);
+int orl_dir_remove_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                          uint64_t blob_bytes, size_t n, uint8_t* removed);
 /* LookUpGrain of KeyExt grains on the host copy (no IsValidSilo filter; ORL_NO_ACT / ORL_NULL_SILO when absent). */
 int orl_dir_lookup_keyext_host(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
-                               size_t n, uint32_t* act, uint8_t* silo);
+                               uint64_t blob_bytes, size_t n, uint32_t* act, uint8_t* silo);
 int orl_dir_keyext_count(const orl_ctx* ctx, uint64_t* n);
 /* orl_route_batch_device with the batch's KeyExt strings: d_ext[i] locates message i's extension in d_blob (device,
  * blob_bytes long; read only for KeyExt messages).  A KeyExt message whose header carries ORL_HDR_HASH_VALID uses that
@@ -511,6 +512,8 @@ int orl_partition_by_owner_padded_device(orl_ctx* ctx, const orl_msg_hdr* d_in, 
  * failure of the 32-byte form, which has no status word, is reported by orl_ctx_query(ORL_Q_PART_ERROR). */
 #define ORL_PART_LOOKBACK_FAILED 0x4u
 #define ORL_PART_CACHED 0x8u  /* (node hop 1) the sender's directory cache addressed some message of the chunk */
+#define ORL_PART_KEYEXT 0x10u    /* (node hop 1, orl_node_route_batch_keyext_device) a KeyExt string travels with the chunk */
+#define ORL_PART_EXT_FULL 0x20u  /* (node hop 1) a destination's KeyExt string region overflowed: ORL_E_CAPACITY on every rank */
 int orl_partition_compact_device(orl_ctx* ctx, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                                  const uint8_t* rank_of_silo, uint32_t nranks, uint32_t my_rank, size_t stride,
                                  orl_wire_msg* d_out, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_status,
@@ -657,6 +660,16 @@ int orl_node_set_timeout(orl_node* node, uint32_t ms);
  * every rank return ORL_E_DEVICE for that chunk. */
 int orl_node_route_batch_device(orl_node* node, const orl_msg_hdr* d_in, size_t n, uint32_t opts, orl_node_result* out,
                                 void* stream);
+/* The same with the batch's KeyExt strings (round 6): d_ext[i] locates message i's extension in d_blob (device, blob_bytes
+ * long; read for KeyExt messages only), as orl_route_keyext_device takes them.  A KeyExt message without ORL_HDR_HASH_VALID
+ * gets its uniform hash from the bytes at the sender (its owner is that hash's ring owner, UniqueKey.cs:288-294); the batch
+ * is exchanged as 32-B records with each KeyExt message's string beside it, and the owner resolves it in its KeyExt table
+ * (HIT / placement / IsValidSilo as orl_route_keyext_device: LocalGrainDirectory.cs:719-765 with the whole GrainId).  Every
+ * rank calls one of the two entry points per batch; a rank without strings takes part in the string lanes of the
+ * chunks another rank's strings travel in.  A KeyExt string region of a sender (max(blob_bytes, 4096) bytes per
+ * destination per chunk) that overflows fails the chunk on every rank with ORL_E_CAPACITY. */
+int orl_node_route_batch_keyext_device(orl_node* node, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                                       const uint8_t* d_blob, uint64_t blob_bytes, orl_node_result* out, void* stream);
 /* A multicast batch across the node (config 4 sharded by publisher): every rank expands its own publishes
  * (orl_fanout_expand_device into a node buffer of max_batch records) and routes the emitted messages as
  * orl_node_route_batch_device does.  *total: in = the exact emitted count with ORL_OPT_TOTAL_GIVEN, out = the count. */
@@ -704,7 +717,10 @@ typedef struct orl_node_chunk_plan {
     uint32_t act_lane;                   /* some rank's directory cache addressed a record (ORL_PART_CACHED): every rank
                                             sends a u32 activation handle per record beside the records (ORL_NO_ACT: not
                                             addressed), and the receivers route addressed records without a probe */
-    uint32_t reserved;
+    uint32_t ext_lane;                   /* some rank sent KeyExt strings (ORL_PART_KEYEXT; 32-B records): every rank sends an
+                                            orl_ext_ref per record ({~0, ~0}: none) and its strings, head words [10, 14) =
+                                            the string bytes to each rank (u32 each, rank r in word 10 + r / 2, bits
+                                            32 * (r & 1)); ORL_PART_EXT_FULL on any rank gives ORL_E_CAPACITY */
 } orl_node_chunk_plan;
 /* written = the width this rank partitioned the chunk in; owned_total[nranks] = every rank's receive total over the
  * batch's earlier chunks (zero before chunk 0; updated).  ORL_E_CAPACITY when a rank would own more than max_recv and

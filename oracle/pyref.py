@@ -722,3 +722,76 @@ def apply_directory_cache(route: Sequence[int], act: Sequence[int], sending_silo
         r_out[i] = pack_route(r & 0xFF, silo, ST_HIT, fl)
         a_out[i] = a
     return r_out, a_out
+
+
+class LRUCache:
+    """AdaptiveGrainDirectoryCache over LRU<GrainId, entry> (AdaptiveGrainDirectoryCache.cs:97-133, src/Orleans/Utils/LRU.cs),
+    restated sequentially as the reference runs it (maxAge = TimeSpan.MaxValue: nothing expires):
+      add       LRU.Add (:104-108): AdjustSize, then AddOrUpdate with the next generation;
+      adjust    LRU.AdjustSize (:188-205): while Count >= MaximumSize, generationToFree += 1 and the entry whose generation
+                equals it (if any) is removed;
+      try_get   LRU.TryGetValue (:147-174): a hit takes the next generation;
+      remove    LRU.RemoveKey (:118-125)."""
+
+    def __init__(self, max_size: int):
+        self.max = max_size
+        self.next_gen = 0
+        self.gen_free = 0
+        self.d: Dict[Tuple[int, int, int], list] = {}   # key -> [(act, silo), generation]
+        self.by_gen: Dict[int, Tuple[int, int, int]] = {}
+
+    def _stamp(self, key):
+        self.next_gen += 1
+        old = self.d[key][1]
+        self.by_gen.pop(old, None)
+        self.d[key][1] = self.next_gen
+        self.by_gen[self.next_gen] = key
+
+    def add(self, key, value):
+        while len(self.d) >= self.max:  # AdjustSize
+            self.gen_free += 1
+            victim = self.by_gen.pop(self.gen_free, None)
+            if victim is not None:
+                del self.d[victim]
+        if key in self.d:
+            self.d[key][0] = value
+        else:
+            self.d[key] = [value, 0]
+        self._stamp(key)
+
+    def try_get(self, key):
+        if key not in self.d:
+            return None
+        self._stamp(key)
+        return self.d[key][0]
+
+    def remove(self, key) -> bool:
+        e = self.d.pop(key, None)
+        if e is None:
+            return False
+        self.by_gen.pop(e[1], None)
+        return True
+
+    def items(self):
+        return {k: v[0] for k, v in self.d.items()}
+
+
+def apply_directory_cache_lru(route: Sequence[int], act: Sequence[int], sending_silos: Sequence[int],
+                              keys: Sequence[Tuple[int, int, int]], cache: LRUCache, functional: Sequence[int]):
+    """apply_directory_cache with the LRU's side effect: every message of the batch whose owner is remote looks the cache
+    up in batch order (LocalGrainDirectory.LocalLookup's cache branch, LocalGrainDirectory.cs:691-702 — TryGetValue stamps
+    a found entry before GetLocalCacheData's IsValidSilo filter, :711-717)."""
+    r_out, a_out = list(route), list(act)
+    for i, (r, k) in enumerate(zip(route, keys)):
+        if (r >> 16) & 0xFF != ST_REMOTE_OWNER:
+            continue
+        v = cache.try_get(k)
+        if v is None:
+            continue
+        a, silo = v
+        if not functional[silo]:
+            continue
+        fl = ((r >> 24) & 0xFF) | 0x08 | (FL_LOOPBACK if silo == sending_silos[i] else 0)
+        r_out[i] = pack_route(r & 0xFF, silo, ST_HIT, fl)
+        a_out[i] = a
+    return r_out, a_out

@@ -68,6 +68,8 @@ Q_HOT_BATCHES = 11
 Q_STAGE4_ERROR = 12
 MAX_WIRE_TYPES = 16
 PART_LOOKBACK_FAILED = 0x4
+PART_KEYEXT = 0x10
+PART_EXT_FULL = 0x20
 
 INS_INSERTED, INS_EXISTING, INS_INVALID_SILO, INS_REMOTE_OWNER, INS_OWNER_NULL, INS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 
@@ -116,7 +118,7 @@ class orl_node_stats(C.Structure):
 class orl_node_chunk_plan(C.Structure):
     _fields_ = [("width", C.c_uint32), ("rewrite", C.c_uint32), ("send", C.c_uint64 * NODE_MAX_RANKS),
                 ("recv", C.c_uint64 * NODE_MAX_RANKS), ("n_recv", C.c_uint64), ("act_lane", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("ext_lane", C.c_uint32)]
 
 
 class orl_node_hop2_plan(C.Structure):
@@ -142,9 +144,9 @@ _SIGS = {
     "orl_keyext_uniform_hash": (C.c_uint32, [_P, C.c_char_p, C.c_size_t]),
     "orl_dir_insert_single": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P, _P]),
     "orl_dir_remove": (C.c_int, [_P, _P, C.c_size_t, _P]),
-    "orl_dir_insert_keyext": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_size_t, _P, _P, _P]),
-    "orl_dir_remove_keyext": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),
-    "orl_dir_lookup_keyext_host": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P, _P]),
+    "orl_dir_insert_keyext": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, _P, _P, _P]),
+    "orl_dir_remove_keyext": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_size_t, _P]),
+    "orl_dir_lookup_keyext_host": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_size_t, _P, _P]),
     "orl_dir_keyext_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_route_keyext_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64, _P, _P, _P, _P, _P]),
     "orl_dir_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
@@ -223,6 +225,8 @@ _SIGS = {
     "orl_node_plan_hop2": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64,
                                      C.POINTER(orl_node_hop2_plan)]),
     "orl_node_route_batch_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.POINTER(orl_node_result), _P]),
+    "orl_node_route_batch_keyext_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64,
+                                                     C.POINTER(orl_node_result), _P]),
     "orl_node_segment": (C.c_int, [_P, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "orl_node_get_stats": (C.c_int, [_P, C.POINTER(orl_node_stats)]),
     "orl_node_fanout_batch_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, C.c_uint32, _P,

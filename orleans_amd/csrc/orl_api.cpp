@@ -14,6 +14,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "orl_internal.h"
@@ -239,6 +240,8 @@ struct orl_ctx {
     uint32_t* d_cclaim = nullptr;
     uint64_t* d_cstate = nullptr;    // {entries, tombstones, error flag}
     uint64_t cache_slots = 0, cache_ub = 0, cache_tombs_ub = 0;
+    uint64_t cache_cap = 0;       // LRU.MaximumSize (orl_cache_config's capacity)
+    uint64_t cache_gen_free = 0;  // LRU.generationToFree: the generation of the last entry evicted
     RouteParams hp{};
     RouteParams* d_params = nullptr;
     bool params_dirty = true;
@@ -615,7 +618,7 @@ int sync_device_state(orl_ctx* c) {
 DirView dir_view(const orl_ctx* c) {
     return DirView{c->d_table, c->mask, c->d_cache, c->cache_slots ? c->cache_slots - 1 : 0,
                    (c->probe_valid || c->probe_dev) ? c->d_probe : nullptr, c->probe_dev ? c->d_probe_bad : nullptr,
-                   c->probe8_valid ? c->d_probe8 : nullptr};
+                   c->probe8_valid ? c->d_probe8 : nullptr, c->d_cache != nullptr && c->hp.cache_on != 0};
 }
 
 // After a device mutation of the partition: the probe table no longer mirrors it.  When it held a type list,
@@ -1068,6 +1071,15 @@ uint32_t host_owner_hash(const orl_ctx* c, int32_t h, uint32_t me, bool excl) {
     return c->ring[found].second;
 }
 
+// Every reference of a host KeyExt call inside the caller's blob (the entry points used to read past it).
+int check_ext_refs(orl_ctx* c, const orl_ext_ref* ext, size_t n, uint64_t blob_bytes) {
+    for (size_t i = 0; i < n; ++i)
+        if ((uint64_t)ext[i].off + ext[i].len > blob_bytes)
+            return fail(c, ORL_E_INVALID, "KeyExt reference %zu (%u + %u bytes) outside the %llu-byte blob", i, ext[i].off,
+                        ext[i].len, (unsigned long long)blob_bytes);
+    return ORL_OK;
+}
+
 int upload_keyext(orl_ctx* c) {
     if (!c->ext_dirty) return ORL_OK;
     ORL_HIP(c, hipSetDevice(c->cfg.device));
@@ -1094,8 +1106,10 @@ int upload_keyext(orl_ctx* c) {
 extern "C" {
 
 int orl_dir_insert_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
-                          const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* wact, uint8_t* wsilo, uint8_t* status) {
+                          uint64_t blob_bytes, const uint32_t* acts, const uint8_t* silos, size_t n, uint32_t* wact,
+                          uint8_t* wsilo, uint8_t* status) {
     if (!c || (n && (!keys || !ext || !blob || !acts || !silos))) return ORL_E_INVALID;
+    if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
     for (size_t i = 0; i < n; ++i) {
         uint8_t st;
         uint32_t a = ORL_NO_ACT;
@@ -1122,6 +1136,8 @@ int orl_dir_insert_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_r
                     a = c->ext_table[at].act;
                     s = c->ext_table[at].silo;
                 } else {
+                    if (c->ext_blob.size() + len > UINT32_MAX)  // ExtSlot.off is 32-bit: the store never wraps
+                        return fail(c, ORL_E_CAPACITY, "KeyExt extension store full (4 GiB) at %zu", i);
                     ExtSlot& e = c->ext_table[fr];
                     if (e.state == SLOT_TOMB) --c->ext_tombs;
                     e.tcd = k.type_code_data; e.n0 = k.n0; e.n1 = k.n1;
@@ -1144,9 +1160,10 @@ int orl_dir_insert_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_r
     return ORL_OK;
 }
 
-int orl_dir_remove_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
-                          uint8_t* removed) {
+int orl_dir_remove_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                          uint64_t blob_bytes, size_t n, uint8_t* removed) {
     if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
+    if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
     for (size_t i = 0; i < n; ++i) {
         const uint8_t* x = blob + ext[i].off;
         const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
@@ -1161,9 +1178,10 @@ int orl_dir_remove_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_r
     return ORL_OK;
 }
 
-int orl_dir_lookup_keyext_host(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob, size_t n,
-                               uint32_t* act, uint8_t* silo) {
+int orl_dir_lookup_keyext_host(orl_ctx* c, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
+                               uint64_t blob_bytes, size_t n, uint32_t* act, uint8_t* silo) {
     if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
+    if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
     for (size_t i = 0; i < n; ++i) {
         const uint8_t* x = blob + ext[i].off;
         const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
@@ -1300,6 +1318,7 @@ int route_impl(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t opts, u
     if (fmt == 8 && c->hp.n_wire_types == 0) return fail(c, ORL_E_STATE, "8-byte records need the wire types (orl_wire_types_set)");
     int e = launch_route_bucket(c->d_params, dir_view(c), d_in, fmt, n, opts, c->cfg.n_act, d_route, d_act, d_order,
                                 d_off, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr, d_in_act);
+    if (!e && ctx_cache_on(c)) e = launch_cache_gen_advance(c->d_cache, c->cache_slots - 1, n, st);  // the lookups' LRU stamps
     if (e) return hipfail(c, (hipError_t)e, "route launch");
     if (ev) ORL_HIP(c, hipEventRecord(ev[3], st));
     return ORL_OK;
@@ -1314,6 +1333,19 @@ int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t
 }
 
 bool ctx_cache_on(orl_ctx* c) { return c && c->d_cache && c->hp.cache_on; }
+
+int ctx_keyext_prepare(orl_ctx* c) { return upload_keyext(c); }
+
+int ctx_route_keyext_received(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                              const uint8_t* d_blob, uint64_t blob_bytes, uint32_t* d_route, uint32_t* d_act, void* stream) {
+    if (n == 0) return ORL_OK;
+    const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
+    int e = launch_keyext_route(c->d_params, d_in, n, d_ext, d_blob, blob_bytes, c->d_ext_table,
+                                c->ext_table.empty() ? 0 : c->ext_table.size() - 1, c->d_ext_blob, excl, d_route, d_act,
+                                stream ? stream : c->stream);
+    if (e) return hipfail(c, (hipError_t)e, "KeyExt route launch (node)");
+    return ORL_OK;
+}
 const uint32_t* ctx_stage4_err(const orl_ctx* c) { return c->s.s4_err; }
 }  // namespace orl
 extern "C" {
@@ -1453,6 +1485,7 @@ int fanout_impl(orl_ctx* c, const orl_msg_hdr* d_direct, size_t n_direct, const 
                                        follower_tcd, opts, c->cfg.n_act, d_pub_offsets, d_route, d_act, d_order, d_off, n_out,
                                        c->s.max_batch, c->s, st, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr);
     if (e == -1) return fail(c, ORL_E_CAPACITY, "fan-out emits %llu > max_batch", (unsigned long long)*n_out);
+    if (!e && ctx_cache_on(c)) e = launch_cache_gen_advance(c->d_cache, c->cache_slots - 1, c->s.max_batch, st);  // LRU stamps
     if (e) return hipfail(c, (hipError_t)e, "fanout launch");
     if (ev) {
         if (*n_out == 0) {  // no route kernel ran: mark it empty
@@ -1569,7 +1602,7 @@ namespace orl {
 // The node's hop-1 partition: any record width, with the status word (look-back failures included) for every width.
 int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
                          uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
-                         uint32_t* d_status, void* stream, uint32_t* d_act_out) {
+                         uint32_t* d_status, void* stream, uint32_t* d_act_out, const KxLanes* kxl) {
     if (!c || !rank_of_silo || !d_status) return ORL_E_INVALID;
     if (fmt != 8 && fmt != 16 && fmt != 32) return fail(c, ORL_E_INVALID, "record width %d", fmt);
     if (stride < n) return fail(c, ORL_E_INVALID, "stride %zu < batch %zu", stride, n);
@@ -1580,7 +1613,8 @@ int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t
     const bool cached = d_act_out && ctx_cache_on(c);
     int e = launch_partition_padded(c->d_params, d_in, n, opts, c->d_rank_of_silo, nranks, my_rank, stride, d_out, fmt, nullptr,
                                     d_counts, d_status, c->s, st, cached ? c->d_cache : nullptr,
-                                    cached ? c->cache_slots - 1 : 0, cached ? d_act_out : nullptr);
+                                    cached ? c->cache_slots - 1 : 0, cached ? d_act_out : nullptr, kxl);
+    if (!e && cached) e = launch_cache_gen_advance(c->d_cache, c->cache_slots - 1, n, st);  // the sender's lookups' LRU stamps
     if (e) return hipfail(c, (hipError_t)e, "node partition launch");
     return ORL_OK;
 }
@@ -1879,19 +1913,23 @@ int orl_cache_config(orl_ctx* c, uint64_t capacity) {
     (void)hipFree(c->d_cache); (void)hipFree(c->d_cclaim); (void)hipFree(c->d_cstate);
     c->d_cache = nullptr; c->d_cclaim = nullptr; c->d_cstate = nullptr;
     const uint64_t slots = next_pow2(2 * capacity);
-    ORL_HIP(c, hipMalloc((void**)&c->d_cache, slots * sizeof(DirSlot)));
+    // the table, then one u64 LRU generation per slot and the generation base (route_kernels.hip cache_gens)
+    const size_t bytes = slots * sizeof(DirSlot) + (slots + 1) * 8;
+    ORL_HIP(c, hipMalloc((void**)&c->d_cache, bytes));
     ORL_HIP(c, hipMalloc((void**)&c->d_cclaim, slots * 4));
     ORL_HIP(c, hipMalloc((void**)&c->d_cstate, 32));
-    ORL_HIP(c, hipMemset(c->d_cache, 0, slots * sizeof(DirSlot)));
+    ORL_HIP(c, hipMemset(c->d_cache, 0, bytes));
     ORL_HIP(c, hipMemset(c->d_cclaim, 0xFF, slots * 4));
     ORL_HIP(c, hipMemset(c->d_cstate, 0, 32));
     c->cache_slots = slots;
+    c->cache_cap = capacity;
+    c->cache_gen_free = 0;
     c->cache_ub = c->cache_tombs_ub = 0;
     set_cache_on(c, false);
     return ORL_OK;
 }
 
-int orl_cache_clear(orl_ctx* c) {
+int orl_cache_clear(orl_ctx* c) {  // LRU.Clear: the entries go, the generation counters run on
     if (!c) return ORL_E_INVALID;
     if (!c->cache_slots) return ORL_OK;
     ORL_HIP(c, hipDeviceSynchronize());
@@ -1902,28 +1940,111 @@ int orl_cache_clear(orl_ctx* c) {
     return ORL_OK;
 }
 
+namespace {
+// AddOrUpdate of a batch that can overflow the capacity: the reference's sequential LRU on the host, exactly
+// (AdaptiveGrainDirectoryCache.AddOrUpdate → LRU.Add: AdjustSize — while Count >= MaximumSize free the entry of the next
+// generation, LRU.cs:188-205 — then AddOrUpdate with the next generation, :104-108), over the device table read back, then
+// the table rebuilt and uploaded (no tombstones).  Entries the device path would not keep (an invalid silo, a handle
+// outside this context's space on a local silo: k_cache_probe) are skipped as there.  Generations stay the device's
+// sparse stamps (only their order matters); G advances by n as on the fast path.
+int cache_add_host_lru(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos, size_t n) {
+    const uint64_t slots = c->cache_slots, mask = slots - 1;
+    ORL_HIP(c, hipDeviceSynchronize());
+    std::vector<DirSlot> tab(slots);
+    std::vector<uint64_t> gen(slots + 1);
+    ORL_HIP(c, hipMemcpy(tab.data(), c->d_cache, slots * sizeof(DirSlot), hipMemcpyDeviceToHost));
+    ORL_HIP(c, hipMemcpy(gen.data(), reinterpret_cast<uint8_t*>(c->d_cache) + slots * sizeof(DirSlot), (slots + 1) * 8,
+                         hipMemcpyDeviceToHost));
+    std::vector<orl_grain_key> keys(n);
+    std::vector<uint32_t> acts(n);
+    std::vector<uint8_t> silos(n);
+    if (n) {
+        ORL_HIP(c, hipMemcpy(keys.data(), d_keys, n * sizeof(orl_grain_key), hipMemcpyDeviceToHost));
+        ORL_HIP(c, hipMemcpy(acts.data(), d_acts, n * 4, hipMemcpyDeviceToHost));
+        ORL_HIP(c, hipMemcpy(silos.data(), d_silos, n, hipMemcpyDeviceToHost));
+    }
+    struct Ent {
+        orl_grain_key k;
+        uint32_t act;
+        uint8_t silo;
+        uint64_t gen;
+    };
+    auto kk = [](const orl_grain_key& k) { return std::make_tuple(k.type_code_data, k.n0, k.n1); };
+    std::map<std::tuple<uint64_t, uint64_t, uint64_t>, Ent> ents;  // the cache
+    std::map<uint64_t, std::tuple<uint64_t, uint64_t, uint64_t>> by_gen;  // LRU order
+    for (uint64_t i = 0; i < slots; ++i)
+        if (tab[i].state == SLOT_FULL) {
+            const orl_grain_key k{tab[i].tcd, tab[i].n0, tab[i].n1};
+            ents[kk(k)] = Ent{k, tab[i].act, tab[i].silo, gen[i]};
+            by_gen[gen[i]] = kk(k);
+        }
+    const uint64_t G = gen[slots];
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t sl = silos[i];
+        if (!(sl < c->n_silos && (acts[i] < c->cfg.n_act || (acts[i] != ORL_NO_ACT && !c->local[sl])))) continue;
+        while (ents.size() >= c->cache_cap && !by_gen.empty()) {  // AdjustSize
+            auto v = by_gen.begin();
+            c->cache_gen_free = v->first;
+            ents.erase(v->second);
+            by_gen.erase(v);
+        }
+        const auto key = kk(keys[i]);
+        const uint64_t g = G + i + 1;
+        auto it = ents.find(key);
+        if (it != ents.end()) {
+            by_gen.erase(it->second.gen);
+            it->second = Ent{keys[i], acts[i], (uint8_t)sl, g};
+        } else {
+            ents[key] = Ent{keys[i], acts[i], (uint8_t)sl, g};
+        }
+        by_gen[g] = key;
+    }
+    std::fill(tab.begin(), tab.end(), DirSlot{});
+    std::fill(gen.begin(), gen.end() - 1, 0ull);
+    gen[slots] = G + n;
+    for (const auto& kv : ents) {
+        const Ent& e = kv.second;
+        uint64_t i = dir_slot(jenkins3(e.k.type_code_data, e.k.n0, e.k.n1), mask);
+        while (tab[i].state != SLOT_EMPTY) i = (i + 1) & mask;
+        tab[i].tcd = e.k.type_code_data; tab[i].n0 = e.k.n0; tab[i].n1 = e.k.n1;
+        tab[i].act = e.act; tab[i].silo = e.silo; tab[i].state = SLOT_FULL;
+        gen[i] = e.gen;
+    }
+    ORL_HIP(c, hipMemcpy(c->d_cache, tab.data(), slots * sizeof(DirSlot), hipMemcpyHostToDevice));
+    ORL_HIP(c, hipMemcpy(reinterpret_cast<uint8_t*>(c->d_cache) + slots * sizeof(DirSlot), gen.data(), (slots + 1) * 8,
+                         hipMemcpyHostToDevice));
+    const uint64_t stw[3] = {ents.size(), 0, 0};
+    ORL_HIP(c, hipMemcpy(c->d_cstate, stw, sizeof stw, hipMemcpyHostToDevice));
+    c->cache_ub = ents.size();
+    c->cache_tombs_ub = 0;
+    return ORL_OK;
+}
+}  // namespace
+
+// LRU.Add per entry in batch order.  No entry can be evicted while the cache holds <= capacity - n entries before the batch
+// (every add then finds Count < MaximumSize): the device path (the batch's last writer of a key wins, its generation
+// stamped).  Otherwise the exact sequential LRU on the host (cache_add_host_lru).
 int orl_cache_add_or_update_device(orl_ctx* c, const orl_grain_key* d_keys, const uint32_t* d_acts, const uint8_t* d_silos,
                                    size_t n, void* stream) {
     if (!c) return ORL_E_INVALID;
     if (!c->cache_slots) return fail(c, ORL_E_STATE, "directory cache not configured (orl_cache_config)");
     if (n && (!d_keys || !d_acts || !d_silos)) return fail(c, ORL_E_INVALID, "null device buffer");
     if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
-    auto fits = [&](uint64_t cnt, uint64_t tombs) {
-        return (cnt + n) * 2 <= c->cache_slots && (cnt + tombs + n) * 8 <= c->cache_slots * 7;
+    auto fits = [&](uint64_t cnt, uint64_t tombs) {  // no eviction possible, and the table's load stays <= 7/8
+        return cnt + n <= c->cache_cap && (cnt + tombs + n) * 8 <= c->cache_slots * 7;
     };
-    if (!fits(c->cache_ub, c->cache_tombs_ub)) {  // exact counters (a sync), then the cache is full: the host evicts
-        ORL_HIP(c, hipDeviceSynchronize());
-        uint64_t st[3];
-        ORL_HIP(c, hipMemcpy(st, c->d_cstate, sizeof st, hipMemcpyDeviceToHost));
-        c->cache_ub = st[0];
-        c->cache_tombs_ub = st[1];
-        if (!fits(c->cache_ub, c->cache_tombs_ub))
-            return fail(c, ORL_E_CAPACITY, "directory cache full (%llu entries; remove or clear)", (unsigned long long)st[0]);
-    }
     int r = sync_device_state(c);
     if (r) return r;
     set_cache_on(c, true);
     if ((r = sync_device_state(c))) return r;
+    if (!fits(c->cache_ub, c->cache_tombs_ub)) {  // exact counters (a sync)
+        ORL_HIP(c, hipDeviceSynchronize());
+        uint64_t stw[3];
+        ORL_HIP(c, hipMemcpy(stw, c->d_cstate, sizeof stw, hipMemcpyDeviceToHost));
+        c->cache_ub = stw[0];
+        c->cache_tombs_ub = stw[1];
+        if (!fits(c->cache_ub, c->cache_tombs_ub)) return cache_add_host_lru(c, d_keys, d_acts, d_silos, n);
+    }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int e = launch_cache_update(c->d_cache, c->cache_slots - 1, c->d_cclaim, c->d_cstate, d_keys, d_acts, d_silos, n, c->cfg.n_act,
                                 c->n_silos, c->d_dslot, c->d_dflag, reinterpret_cast<uint32_t*>(c->d_cstate + 2), st, c->d_params);

@@ -230,6 +230,7 @@ struct DirView {
     const ProbeSlot* probe = nullptr;
     const uint32_t* probe_bad = nullptr;  // device-built probe table: nonzero = a key did not fit, probe `dir`
     const void* probe8 = nullptr;         // 8-B form of `probe` ({u32 key, u32 value} pairs) when the keys fit it
+    bool lru = false;                     // the cache is populated: lookups stamp its LRU generations (k_route<..., LRU>)
 };
 
 // ---- kernel launchers (route_kernels.hip) ---------------------------------------------------------
@@ -345,6 +346,8 @@ int launch_dir_insert(const RouteParams* d_params, DirSlot* d_dir, uint64_t dir_
 int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                         const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos, uint32_t* d_slot,
                         uint8_t* d_flag, uint32_t* d_err, void* stream, const RouteParams* d_params);
+// The directory cache's LRU generation base (after the cache table and its per-slot generations): += n, on `stream`.
+int launch_cache_gen_advance(const DirSlot* d_cache, uint64_t mask, uint64_t n, void* stream);
 int launch_dir_merge(DirSlot* d_dir, uint64_t dir_mask, uint32_t* d_claim, uint64_t* d_cnt, const orl_grain_key* d_keys,
                      const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act, uint32_t n_silos,
                      const orl_grain_key* d_act_keys, uint32_t n_act_keys, uint32_t* d_slot, uint8_t* d_status,
@@ -378,11 +381,25 @@ int launch_stamp_frames(const uint8_t* d_bytes, uint64_t nbytes, const uint64_t*
                         const uint32_t* d_silo_words, uint64_t* d_sizes, void* d_temp, size_t temp_bytes, uint8_t* d_out,
                         uint64_t out_cap, uint64_t* d_out_offsets, uint64_t* d_out_total, uint8_t* d_status, void* stream);
 size_t stamp_scan_temp_bytes(size_t n);
+// A node batch's KeyExt strings for the hop-1 partition (k_part_lb KX): the caller's references and blob, and the lanes
+// they are written to (ext_out: one orl_ext_ref per record in the padded regions; blob_out: blob_cap bytes per destination,
+// appended at cur[destination], u32 each).
+struct KxLanes {
+    const orl_ext_ref* ext;
+    const uint8_t* blob;
+    uint64_t blob_bytes;
+    orl_ext_ref* ext_out;
+    uint8_t* blob_out;
+    uint64_t blob_cap;
+    uint32_t* cur;
+};
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
                             Scratch& s, void* stream, const DirSlot* d_cache = nullptr, uint64_t cmask = 0,
-                            uint32_t* d_act_out = nullptr);
+                            uint32_t* d_act_out = nullptr, const KxLanes* kxl = nullptr);
+// The received ext-ref lane of a chunk: source s's references (cnt[s] records, in rank order) += base[s].
+int launch_ext_rebase(orl_ext_ref* d_refs, uint64_t n, uint32_t nranks, const uint64_t* cnt, const uint64_t* base, void* stream);
 // Stage 4 alone over already-routed messages (activation handles): histogram + bucket_after_route.
 int launch_bucket_acts(const uint32_t* d_act, size_t n, uint32_t n_act, uint32_t* d_order, uint32_t* d_offsets, const Scratch& s,
                        void* stream);
@@ -409,7 +426,12 @@ const uint64_t* ctx_wire_tcd(const orl_ctx* c);
 // their cached handles, ORL_NO_ACT for every other record; the status word gets ORL_PART_CACHED).
 int ctx_partition_padded(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const uint8_t* rank_of_silo,
                          uint32_t nranks, uint32_t my_rank, size_t stride, void* d_out, int fmt, uint64_t* d_counts,
-                         uint32_t* d_status, void* stream, uint32_t* d_act_out = nullptr);
+                         uint32_t* d_status, void* stream, uint32_t* d_act_out = nullptr, const KxLanes* kxl = nullptr);
+// The KeyExt lookups of received 32-B records (k_keyext_route over messages the route kernel left ORL_ST_KEYEXT_UNRESOLVED)
+// with their ext-ref lane into d_blob; ctx_keyext_prepare uploads a changed KeyExt table first (call it before a batch).
+int ctx_route_keyext_received(orl_ctx* c, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                              const uint8_t* d_blob, uint64_t blob_bytes, uint32_t* d_route, uint32_t* d_act, void* stream);
+int ctx_keyext_prepare(orl_ctx* c);
 // Whether the context's directory cache is configured and holds entries (the partition's cached destinations).
 bool ctx_cache_on(orl_ctx* c);
 // Device address of the context's stage-4 look-back error word (Scratch::s4_err).

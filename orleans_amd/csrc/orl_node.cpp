@@ -155,6 +155,16 @@ struct orl_node {
     };
     std::vector<Seg> segs;
     orl_msg_hdr* d_fan = nullptr;                 // expanded multicast records (orl_node_fanout_batch_device), max_batch
+    // KeyExt strings of the current batch (orl_node_route_batch_keyext_device; null otherwise) and their hop-1 lanes
+    const orl_ext_ref* kx_ext = nullptr;
+    const uint8_t* kx_blob = nullptr;
+    uint64_t kx_bytes = 0;
+    orl_ext_ref* d_send_ext[2] = {nullptr, nullptr};  // nranks x chunk_cap references per slot
+    uint8_t* d_send_blob[2] = {nullptr, nullptr};     // nranks x send_blob_cap bytes per slot
+    uint64_t send_blob_cap = 0;
+    orl_ext_ref* d_recv_ext = nullptr;                // max_recv references (the owned set's)
+    uint8_t* d_recv_blob[2] = {nullptr, nullptr};     // a chunk's received strings, per slot
+    uint64_t recv_blob_cap = 0;
     orl_node_stats stats{};                       // the last batch's bytes and host waits (orl_node_get_stats)
 };
 
@@ -380,6 +390,12 @@ void free_node(orl_node* nd) {
     if (nd->h_form) (void)hipHostFree(nd->h_form);
     if (nd->h_stall) (void)hipHostFree(nd->h_stall);
     if (nd->h_s4err) (void)hipHostFree(nd->h_s4err);
+    for (int sl = 0; sl < 2; ++sl) {
+        (void)hipFree(nd->d_send_ext[sl]);
+        (void)hipFree(nd->d_send_blob[sl]);
+        (void)hipFree(nd->d_recv_blob[sl]);
+    }
+    (void)hipFree(nd->d_recv_ext);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_h, nd->ev_slot[0], nd->ev_slot[1], nd->ev_s4})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {nd->sp, nd->sx, nd->sr, nd->sh})
@@ -473,8 +489,12 @@ int orl_node_plan_chunk(const uint64_t* H, uint32_t nr, uint32_t me, uint32_t wr
     }
     out->width = (wide || no16) ? 32u : (all8 && !no8) ? 8u : 16u;
     out->rewrite = out->width != written;
-    for (uint32_t r = 0; r < nr; ++r)  // some sender addressed records from its directory cache: their handles travel too
+    bool ext_full = false;
+    for (uint32_t r = 0; r < nr; ++r) {  // some sender addressed records from its directory cache: their handles travel too
         out->act_lane |= ((uint32_t)H[r * W + 8] & ORL_PART_CACHED) ? 1u : 0u;
+        out->ext_lane |= ((uint32_t)H[r * W + 8] & ORL_PART_KEYEXT) ? 1u : 0u;  // ... KeyExt strings: their lanes travel
+        ext_full |= ((uint32_t)H[r * W + 8] & ORL_PART_EXT_FULL) != 0;
+    }
     for (uint32_t r = 0; r < nr; ++r) {
         out->send[r] = H[me * W + r];
         out->recv[r] = H[r * W + me];
@@ -487,6 +507,7 @@ int orl_node_plan_chunk(const uint64_t* H, uint32_t nr, uint32_t me, uint32_t wr
         owned_total[d] += in;
         if (owned_total[d] > max_recv) rc = ORL_E_CAPACITY;
     }
+    if (ext_full) rc = ORL_E_CAPACITY;  // a sender's string region overflowed (every rank sees its status word)
     return rc;
 }
 
@@ -721,7 +742,26 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     uint64_t digest = 0;
     NODE_CTX(nd, orl_ctx_query(nd->ctx, ORL_Q_WIRE_DIGEST, &digest));
     const bool wide_only = (nd->cfg.flags & ORL_NODE_WIDE_ONLY) != 0;
-    const uint32_t first_form = wide_only ? 32u : (digest ? 8u : 16u);
+    // KeyExt strings (round 6): a batch that carries them (orl_node_route_batch_keyext_device) is
+    // exchanged as 32-B records with an ext-ref lane and a string lane beside them; the owner resolves the KeyExt messages
+    // in its KeyExt table (a changed table is uploaded here, before anything of the batch runs, on every rank: another
+    // rank's strings may arrive even when this rank sends none)
+    const bool kx = nd->kx_ext != nullptr;
+    NODE_CTX(nd, ctx_keyext_prepare(nd->ctx));
+    const uint32_t first_form = (wide_only || kx) ? 32u : (digest ? 8u : 16u);
+    if (kx) {
+        const uint64_t cap = std::max<uint64_t>((nd->kx_bytes + 255) & ~uint64_t(255), 4096);
+        if (!nd->d_send_ext[0] || cap > nd->send_blob_cap) {
+            NODE_HIP(nd, hipDeviceSynchronize());
+            for (int sl = 0; sl < 2; ++sl) {
+                if (!nd->d_send_ext[sl]) NODE_HIP(nd, hipMalloc((void**)&nd->d_send_ext[sl], (size_t)nr * nd->chunk_cap * 8));
+                (void)hipFree(nd->d_send_blob[sl]);
+                nd->d_send_blob[sl] = nullptr;
+                NODE_HIP(nd, hipMalloc((void**)&nd->d_send_blob[sl], (size_t)nr * cap));
+            }
+            nd->send_blob_cap = cap;
+        }
+    }
     // The sender's directory cache (round 5): with the context's cache populated, hop 1 sends a message whose owner is
     // remote and whose grain the cache holds straight to the rank of the cached activation, addressed (HIT | CACHED), with
     // its handle in an act lane beside the records — LocalLookup's non-owner branch (LocalGrainDirectory.cs:690-717) before
@@ -754,8 +794,15 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             nd->form_word[slot] = fw;
             nd->form_valid[slot] = true;
         }
+        KxLanes kxl{};
+        if (kx && form == 32) {  // head words [10, 14): the string bytes to each destination (u32 each), the append cursors
+            NODE_HIP(nd, hipMemsetAsync(head + 10, 0, 4 * 8, nd->sp));
+            kxl = KxLanes{nd->kx_ext + start, nd->kx_blob, nd->kx_bytes, nd->d_send_ext[slot], nd->d_send_blob[slot],
+                          nd->send_blob_cap, reinterpret_cast<uint32_t*>(head + 10)};
+        }
         NODE_CTX(nd, ctx_partition_padded(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me, nd->chunk_cap, send,
-                                          (int)form, head, status, nd->sp, cached ? nd->d_send_act[slot] : nullptr));
+                                          (int)form, head, status, nd->sp, cached ? nd->d_send_act[slot] : nullptr,
+                                          kxl.ext ? &kxl : nullptr));
         NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
         return ORL_OK;
     };
@@ -824,7 +871,44 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             lanes.push_back(Lane{reinterpret_cast<uint8_t*>(nd->d_send_act[slot]), nd->chunk_cap * 4,
                                  reinterpret_cast<uint8_t*>(nd->d_recv_act + owned), 4});
         }
+        uint64_t bsend[ORL_NODE_MAX_RANKS] = {0}, brecv[ORL_NODE_MAX_RANKS] = {0}, bbase[ORL_NODE_MAX_RANKS] = {0}, btot = 0;
+        if (plan.ext_lane) {  // some rank's chunk carries KeyExt strings: every rank sends the ext-ref lane (+ its strings)
+            if (width != 32) return nfail(nd, ORL_E_STATE, "chunk %u: KeyExt strings with %u-byte records", c, width);
+            for (uint32_t r = 0; r < nr; ++r) {
+                bsend[r] = (H[me * W + 10 + r / 2] >> (32 * (r & 1))) & 0xFFFFFFFFull;
+                brecv[r] = (H[r * W + 10 + me / 2] >> (32 * (me & 1))) & 0xFFFFFFFFull;
+                bbase[r] = btot;
+                btot += brecv[r];
+            }
+            if (!nd->d_recv_ext || !nd->d_send_ext[slot] || btot > nd->recv_blob_cap) {
+                NODE_HIP(nd, hipDeviceSynchronize());
+                if (!nd->d_recv_ext) NODE_HIP(nd, hipMalloc((void**)&nd->d_recv_ext, nd->cfg.max_recv * 8));
+                for (int sl = 0; sl < 2; ++sl)
+                    if (!nd->d_send_ext[sl]) NODE_HIP(nd, hipMalloc((void**)&nd->d_send_ext[sl], (size_t)nr * nd->chunk_cap * 8));
+                if (btot > nd->recv_blob_cap) {
+                    const uint64_t cap = std::max<uint64_t>(btot + btot / 2, 4096);
+                    for (int sl = 0; sl < 2; ++sl) {
+                        (void)hipFree(nd->d_recv_blob[sl]);
+                        nd->d_recv_blob[sl] = nullptr;
+                        NODE_HIP(nd, hipMalloc((void**)&nd->d_recv_blob[sl], cap));
+                    }
+                    nd->recv_blob_cap = cap;
+                }
+            }
+            if (!kx)  // this rank wrote no ext lane: {~0, ~0} (no string) over what it sends
+                for (uint32_t r = 0; r < nr; ++r)
+                    if (plan.send[r])
+                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_ext[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 8, nd->sp));
+            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+            lanes.push_back(Lane{reinterpret_cast<uint8_t*>(nd->d_send_ext[slot]), nd->chunk_cap * 8,
+                                 reinterpret_cast<uint8_t*>(nd->d_recv_ext + owned), 8});
+        }
         if (int r = exchange(nd, lanes, plan.send, plan.recv, nd->ev_part[slot])) return r;
+        if (plan.ext_lane) {  // the strings: per-rank byte counts of their own (the head words [10, 14))
+            const std::vector<Lane> blane = {Lane{kx ? nd->d_send_blob[slot] : nd->d_recv_blob[slot], kx ? nd->send_blob_cap : 0,
+                                                  nd->d_recv_blob[slot], 1}};
+            if (int r = exchange(nd, blane, bsend, brecv, nd->ev_part[slot])) return r;
+        }
         NODE_HIP(nd, hipEventRecord(nd->ev_slot[slot], nd->sx));
         nd->segs.push_back(orl_node::Seg{recv, got, width});
         if (got) {  // stages 1-3 of the received chunk, overlapping the next chunk's exchange
@@ -832,6 +916,13 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             // (records a sender addressed from its cache: HIT | CACHED from the act lane, no probe)
             NODE_CTX(nd, ctx_route_received(nd->ctx, recv, (int)width, got, ropts, nd->d_route + owned, nd->d_act + owned,
                                             plan.act_lane ? nd->d_recv_act + owned : nullptr, nd->sr));
+            if (plan.ext_lane) {  // the KeyExt messages the route left unresolved: the owner's KeyExt table, with the strings
+                int e = launch_ext_rebase(nd->d_recv_ext + owned, got, nr, plan.recv, bbase, nd->sr);
+                if (e) return nfail(nd, ORL_E_DEVICE, "ext rebase launch: %s", hipGetErrorString((hipError_t)e));
+                NODE_CTX(nd, ctx_route_keyext_received(nd->ctx, reinterpret_cast<const orl_msg_hdr*>(recv), got, ropts,
+                                                       nd->d_recv_ext + owned, nd->d_recv_blob[slot], btot, nd->d_route + owned,
+                                                       nd->d_act + owned, nd->sr));
+            }
         }
         owned += got;
         owned_bytes += got * width;
@@ -932,6 +1023,21 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     NODE_HIP(nd, hipEventRecord(nd->ev_s4, nd->sr));
     nd->s4_pending = true;
     return ORL_OK;
+}
+
+int orl_node_route_batch_keyext_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n, uint32_t opts, const orl_ext_ref* d_ext,
+                                       const uint8_t* d_blob, uint64_t blob_bytes, orl_node_result* res, void* stream) {
+    if (!nd || !res) return ORL_E_INVALID;
+    if (n && (!d_ext || !d_blob)) return nfail(nd, ORL_E_INVALID, "null KeyExt references or blob");
+    if (blob_bytes > 0xFFFFFFFFull) return nfail(nd, ORL_E_INVALID, "KeyExt blob of %llu bytes (<= 4 GiB)", (unsigned long long)blob_bytes);
+    nd->kx_ext = n ? d_ext : nullptr;
+    nd->kx_blob = d_blob;
+    nd->kx_bytes = blob_bytes;
+    const int r = orl_node_route_batch_device(nd, d_in, n, opts, res, stream);
+    nd->kx_ext = nullptr;
+    nd->kx_blob = nullptr;
+    nd->kx_bytes = 0;
+    return r;
 }
 
 }  // extern "C"

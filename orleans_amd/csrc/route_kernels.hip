@@ -256,11 +256,29 @@ __device__ __forceinline__ uint32_t route_tail(const RouteParams& P, const Msg& 
     return pack_route(owner, host, ORL_ST_NEW_PLACEMENT, rf);
 }
 
+// The directory cache's LRU generations (round 6): the cache table of cmask + 1 slots is followed by one
+// u64 generation per slot and the generation base G (gen[cmask + 1]).  AdaptiveGrainDirectoryCache.LookUp →
+// LRU.TryGetValue gives a found entry the next generation (LRU.cs:147-174); here a batch's lookups stamp G + their message
+// index + 1 (atomicMax: an entry's last lookup in batch order wins, the order the reference's sequential lookups give) and
+// the launcher advances G by the batch size afterwards (k_gen_advance), so stamps grow across batches as generations do.
+// Only the order matters to the eviction (LRU.AdjustSize frees the smallest generation, LRU.cs:188-205).
+__device__ __forceinline__ unsigned long long* cache_gens(const DirSlot* cache, uint64_t cmask) {
+    return reinterpret_cast<unsigned long long*>(const_cast<DirSlot*>(cache + cmask + 1));
+}
+__device__ __forceinline__ void cache_touch(const DirSlot* cache, uint64_t cmask, uint64_t slot, uint32_t e) {
+    unsigned long long* gen = cache_gens(cache, cmask);
+    const unsigned long long g = __hip_atomic_load(gen + cmask + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + e + 1ull;
+    atomicMax(gen + slot, g);
+}
+
 // Stages 1-3 for one message.  The linear-probe chain is continued by a flag loop (measured 13 % faster in
-// k_route than an early-return helper loop).
+// k_route than an early-return helper loop).  e: the message's index in its batch (the cache's LRU stamp).
+// LRU: stamp the cache's generations (a launch with the cache populated; the plain route kernels are built without it: the
+// stamp's atomics cost k_route 4 SGPRs, one workgroup per CU at config 3, +10 %).
+template <bool LRU = true>
 __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlot* __restrict__ dir, uint64_t dmask,
                                               const DirSlot* __restrict__ cache, uint64_t cmask, const Msg& m, bool excl_opt,
-                                              uint32_t& act) {
+                                              uint32_t& act, uint32_t e) {
     uint32_t h, owner, rf;
     act = ORL_NO_ACT;
     const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
@@ -275,6 +293,7 @@ __device__ __forceinline__ uint32_t route_msg(const RouteParams& P, const DirSlo
         slot = (slot + 1) & mask;
         st = probe_slot(dir4[2 * slot], dir4[2 * slot + 1], m, fact, fsilo);
     }
+    if (LRU && vc && st == 0) cache_touch(cache, cmask, slot, e);  // LookUp found it (IsValidSilo filters after)
     return route_tail(P, m, h, owner, rf, st == 0, fact, fsilo, act, vc);
 }
 
@@ -321,7 +340,8 @@ __device__ __forceinline__ uint32_t cached_verdict(const RouteParams& P, const M
 // (the FullLookup path, :719-765), or this rank for messages that need no directory.
 __device__ __forceinline__ uint32_t dest_rank_cached(const RouteParams& P, const uint8_t* __restrict__ rank_of_silo,
                                                      const DirSlot* __restrict__ cache, uint64_t cmask, const Msg& m,
-                                                     bool excl_opt, uint32_t my_rank, uint32_t& cact, uint32_t& chost) {
+                                                     bool excl_opt, uint32_t my_rank, uint32_t& cact, uint32_t& chost,
+                                                     uint32_t e) {
     uint32_t h, owner, rf;
     cact = ORL_NO_ACT;
     chost = 0xFFu;
@@ -335,6 +355,7 @@ __device__ __forceinline__ uint32_t dest_rank_cached(const RouteParams& P, const
             slot = (slot + 1) & cmask;
             st = probe_slot(c4[2 * slot], c4[2 * slot + 1], m, fact, fsilo);
         }
+        if (st == 0) cache_touch(cache, cmask, slot, e);
         if (st == 0 && mask_bit(P.functional, fsilo)) {
             cact = fact;
             chost = fsilo;
@@ -353,7 +374,7 @@ __device__ __forceinline__ uint32_t route_msg16(const RouteParams& P, const DirS
     act = ORL_NO_ACT;
     const uint32_t r = route_head(P, m, excl_opt, h, owner, rf);
     if (r < kNeedProbeCache) return r;
-    if (r == kNeedProbeCache) return route_msg(P, dir, dmask, cache, cmask, m, excl_opt, act);
+    if (r == kNeedProbeCache) return route_msg(P, dir, dmask, cache, cmask, m, excl_opt, act, 0u);
     uint32_t fact = 0, fsilo = 0;
     int st = 1;
     const uint32_t mk = probe_type(P, m);
@@ -693,7 +714,7 @@ __device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __rest
 
 // CIN: the records come with the node exchange's act lane `in_act` (sender_cached); a template flag, since even a uniform
 // null test of the pointer cost config 2's k_route 35 us (1.277 -> 1.312 ms).
-template <int HB, int FMT, int PW, bool CIN = false>
+template <int HB, int FMT, int PW, bool CIN = false, bool LRU = false>
 __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
@@ -752,7 +773,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                     rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                     if (CIN) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
                 } else if (rr == kNeedProbeCache) {
-                    rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                    rr = route_msg<LRU>(sm.P, dir, dmask, cache, cmask, m, excl != 0, act, e);
                 }
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
@@ -792,7 +813,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
                     rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, false);
                     if (CIN) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
                 } else if (rr == kNeedProbeCache) {
-                    rr = route_msg(sm.P, dir, dmask, cache, cmask, m, excl != 0, act);
+                    rr = route_msg<LRU>(sm.P, dir, dmask, cache, cmask, m, excl != 0, act, e);
                 }
                 store_drop(route + e, rr);
                 store_drop(act_out + e, act);
@@ -827,6 +848,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __re
             sb = dir4[2 * slot + 1];
             st = probe_slot(sa, sb, m, fact, fsilo);
         }
+        if (LRU && r == kNeedProbeCache && st == 0) cache_touch(cache, cmask, slot, e);
         if (e < n) {
             uint32_t act = cact, rr = r;
             if (rr >= kNeedProbeCache) {
@@ -1382,7 +1404,9 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
 enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_PAIR_SMALL = 5 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_PAIR_SMALL = 5, OUT_FINAL_GAPS = 6 };
+// FINAL_GAPS (the LSD plan's last pass, round 6): `order` plus the bucket offsets instead of the sorted keys — see
+// k_bound_last.
 // LSD_PAIR: an LSD pass's pairs; PAIR_SMALL: the MSD pass's pairs from 2048-element tiles (kMsdItemsSmall, small batches)
 
 // Publisher of fan-out message v: the last p in [0, n_pub) with poff[p] <= v (upper_bound(poff[0..n_pub], v) - 1;
@@ -1476,6 +1500,44 @@ struct PassSmem : PassSmemCore<BITS, ITEMS> {
     uint8_t pad[BITS == 10 && kCore < kScatterLdsFloor ? kScatterLdsFloor - kCore : 4];  // 10 bits: <= 3 per CU
 };
 
+// OUT_FINAL_GAPS's FL row entry of a digit with no message in the tile: first > last (a real entry has first <= last).
+constexpr uint32_t kFlEmpty = 0x0000FFFFu;
+// LSD offsets' gaps (k_offsets_gaps, the final passes): see k_offsets_gaps.
+constexpr uint32_t kGapWave = 16, kGapChunk = 32768, kGapCap = 4096, kGapLds = 4096, kGapPer = 8, kGapBlock = 256 * kGapPer;
+
+// Bucket offsets [lo, lo + len) = val, straight to HBM: a short gap by its lane, a long one by the whole wave (64 entries
+// per store), pieces of kGapChunk queued for k_sweep_tail while the queue has room.  Every lane of the wave calls it.
+__device__ __forceinline__ void write_gap(uint32_t* __restrict__ offsets, uint32_t lo, uint32_t len, uint32_t val,
+                                          uint32_t* __restrict__ q, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (len <= kGapWave)
+        for (uint32_t b = 0; b < len; ++b) offsets[lo + b] = val;
+    uint64_t m = __ballot(len > kGapWave);
+    while (m) {
+        const uint32_t src = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t glo = (uint32_t)__shfl((int)lo, (int)src, 64);
+        const uint32_t gl = (uint32_t)__shfl((int)len, (int)src, 64);
+        const uint32_t gv = (uint32_t)__shfl((int)val, (int)src, 64);
+        uint32_t done = 0;
+        if (gl > kGapChunk) {
+            const uint32_t pieces = gl / kGapChunk;
+            uint32_t first = 0;
+            if (lane == 0) first = atomicAdd(&q[0], pieces);
+            first = (uint32_t)__shfl((int)first, 0, 64);
+            const uint32_t took = first >= cap ? 0u : min(pieces, cap - first);
+            for (uint32_t p = lane; p < took; p += 64) {
+                uint32_t* t = q + 2 + 3 * (size_t)(first + p);
+                t[0] = glo + p * kGapChunk;
+                t[1] = kGapChunk;
+                t[2] = gv;
+            }
+            done = took * kGapChunk;
+        }
+        for (uint32_t b = done + lane; b < gl; b += 64) offsets[glo + b] = gv;
+    }
+}
+
 // ITEMS: elements per thread; the tile is 256 * ITEMS (the MSD pass of the two-level path takes kMsdItems: half the
 // digit-histogram rows of 4096-element tiles and twice the run length per digit in its scattered writes).
 // hot_rows (IN_ACT + OUT_PAIR only; col_scan'ed per-row hot counts): the hot key's elements are not ranked; their indices
@@ -1486,7 +1548,9 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
                                                     const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out, const uint32_t* __restrict__ hot_words,
-                                                    const uint32_t* __restrict__ hot_rows, uint32_t* __restrict__ hot_idx) {
+                                                    const uint32_t* __restrict__ hot_rows, uint32_t* __restrict__ hot_idx,
+                                                    uint32_t* __restrict__ offsets, uint32_t nb, uint32_t* __restrict__ gap_q,
+                                                    uint32_t gap_cap) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
@@ -1572,6 +1636,16 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
         }
     }
     __syncthreads();
+    if (OUT == OUT_FINAL_GAPS) {  // the tile's first and last key of every digit (low 16 bits each): one row of key_out
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t d = threadIdx.x * PER + q;
+            if (d < B)
+                key_out[(size_t)tile * B + d] = tot[q] ? (sm.stage[start[q]].x & 0xFFFFu) |
+                                                             ((sm.stage[start[q] + tot[q] - 1u].x & 0xFFFFu) << 16)
+                                                       : kFlEmpty;
+        }
+    }
     uint32_t* delta = &sm.cnt[0][0];  // the starts are consumed: the bins' deltas take their place
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q)
@@ -1581,6 +1655,26 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t i = j * 256u + threadIdx.x;
+        if (OUT == OUT_FINAL_GAPS) {  // order + the buckets between this key and the image's previous one (same digit)
+            uint32_t lo = 0, len = 0, g = 0;
+            if (i < cnt) {
+                const uint2 kv = sm.stage[i];
+                const uint32_t d = (kv.x >> shift) & (B - 1u);
+                g = delta[d] + i;
+                if (g < n) {
+                    order_out[g] = kv.y;
+                    if (i > 0) {
+                        const uint32_t pk = sm.stage[i - 1u].x;
+                        if (((pk >> shift) & (B - 1u)) == d && pk < kv.x) {  // a digit's first key in the tile: k_bound_apply
+                            lo = pk + 1u;
+                            len = lo < nb ? min(kv.x - pk, nb - lo) : 0u;
+                        }
+                    }
+                }
+            }
+            write_gap(offsets, lo, len, g, gap_q, gap_cap);
+            continue;
+        }
         if (i < cnt) {
             const uint2 kv = sm.stage[i];
             const uint32_t k = kv.x;
@@ -1731,7 +1825,6 @@ __global__ __launch_bounds__(256) void k_sufmin_down(uint32_t* __restrict__ a, u
 // kGapChunk buckets queued in kGapChunk pieces for k_offsets_long (a workgroup per piece).  Queue: q[0] = count, q[1] =
 // finished workgroups of k_offsets_long (which zeroes both at its end), then {lo, len, value} triples; a full queue
 // leaves the gap to the wave.
-constexpr uint32_t kGapWave = 16, kGapChunk = 32768, kGapCap = 4096, kGapLds = 4096, kGapPer = 8, kGapBlock = 256 * kGapPer;
 static_assert(kGapQueueWords == 2 + 3 * (size_t)kGapCap, "gap queue size");
 
 __global__ __launch_bounds__(256) void k_offsets_gaps(const uint32_t* __restrict__ sorted, uint32_t n, uint32_t nb,
@@ -1862,39 +1955,6 @@ struct SweepSmem {
 __device__ __forceinline__ unsigned long long sweep_word(uint32_t tag, uint32_t kind, uint32_t mk, uint32_t count) {
     return ((unsigned long long)tag << 56) | ((unsigned long long)kind << 54) | ((unsigned long long)(mk & kSweepMkMask) << 32) |
            count;
-}
-
-// Bucket offsets [lo, lo + len) = val, straight to HBM: a short gap by its lane, a long one by the whole wave (64 entries
-// per store), pieces of kGapChunk queued for k_sweep_tail while the queue has room.  Every lane of the wave calls it.
-__device__ __forceinline__ void write_gap(uint32_t* __restrict__ offsets, uint32_t lo, uint32_t len, uint32_t val,
-                                          uint32_t* __restrict__ q, uint32_t cap) {
-    const uint32_t lane = threadIdx.x & 63u;
-    if (len <= kGapWave)
-        for (uint32_t b = 0; b < len; ++b) offsets[lo + b] = val;
-    uint64_t m = __ballot(len > kGapWave);
-    while (m) {
-        const uint32_t src = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t glo = (uint32_t)__shfl((int)lo, (int)src, 64);
-        const uint32_t gl = (uint32_t)__shfl((int)len, (int)src, 64);
-        const uint32_t gv = (uint32_t)__shfl((int)val, (int)src, 64);
-        uint32_t done = 0;
-        if (gl > kGapChunk) {
-            const uint32_t pieces = gl / kGapChunk;
-            uint32_t first = 0;
-            if (lane == 0) first = atomicAdd(&q[0], pieces);
-            first = (uint32_t)__shfl((int)first, 0, 64);
-            const uint32_t took = first >= cap ? 0u : min(pieces, cap - first);
-            for (uint32_t p = lane; p < took; p += 64) {
-                uint32_t* t = q + 2 + 3 * (size_t)(first + p);
-                t[0] = glo + p * kGapChunk;
-                t[1] = kGapChunk;
-                t[2] = gv;
-            }
-            done = took * kGapChunk;
-        }
-        for (uint32_t b = done + lane; b < gl; b += 64) offsets[glo + b] = gv;
-    }
 }
 
 // One read of the handles: gtot[p << kMaxDigitBits | d] += messages whose pass-p digit is d (gtot zero: at context creation,
@@ -2179,8 +2239,118 @@ __global__ __launch_bounds__(256) void k_sweep_tail(const uint32_t* __restrict__
         }
     }
     __syncthreads();
-    if (last)  // every workgroup has read its digit totals
+    if (last && gall)  // every workgroup has read its digit totals
         for (uint32_t i = threadIdx.x; i < 3u << kMaxDigitBits; i += 256) gall[i] = 0;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// The LSD plan's bucket offsets without the sorted keys (round 6).  Its last pass (k_radix_pass
+// OUT_FINAL_GAPS) has each tile's image sorted by the whole key (the input is sorted by the lower digits, the pass is
+// stable), so it writes the buckets between consecutive keys of one digit inside the tile itself, and one row per tile of
+// FL[t][d] = each digit's first and last key's low 16 bits (the plan's last shift is <= 16 for this form).  What crosses
+// tiles — the buckets between the last key of digit d in the nearest earlier tile that has one and the first key of d in
+// tile t — is three column launches over the [tiles][2^bits] rows the pass already has (its counts C, its output bases M):
+//   k_bound_last   S[c][d] = the last key of d in chunk c of kScanRows tiles (kFlNone: no message of d there);
+//   k_bound_scan   P[c][d] = the last key of d in the chunks before c; gmax[d] = the last key of d overall;
+//   k_bound_apply  every tile with messages of d: offsets[(d << shift) + prev + 1, (d << shift) + first] = M[t][d];
+// then k_sweep_tail: the buckets past each digit's last key.  2 GB less traffic per 256M messages than writing the sorted
+// keys and reading them back (k_offsets_gaps), and every offset is still written exactly once.
+constexpr uint32_t kFlNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool fl_has(uint32_t fl) { return (fl & 0xFFFFu) <= (fl >> 16); }
+
+// One wave per digit at a time, one lane per tile of the chunk (the wave's 64 loads share 64 rows' lines with the next
+// digits'), 8 digits' loads in flight per lane.
+__global__ __launch_bounds__(256) void k_bound_last(const uint32_t* __restrict__ FL, uint32_t ntiles, uint32_t bins,
+                                                    uint32_t* __restrict__ S) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * kScanRows + lane;
+    for (uint32_t d0 = w * 8u; d0 < bins; d0 += kWaves * 8u) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v[k] = (t < ntiles && d0 + k < bins) ? FL[(size_t)t * bins + d0 + k] : kFlEmpty;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint64_t m = __ballot(fl_has(v[k]));
+            const uint32_t hl = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+            const uint32_t l = (uint32_t)__shfl((int)(v[k] >> 16), (int)hl, 64);
+            if (lane == 0 && d0 + k < bins) S[(size_t)blockIdx.x * bins + d0 + k] = m ? l : kFlNone;
+        }
+    }
+}
+
+// 16 columns per block, 16 threads per column each owning a contiguous run of chunks (k_col_scan's shape).
+__global__ __launch_bounds__(256) void k_bound_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
+                                                    uint32_t* __restrict__ gmax) {
+    __shared__ uint32_t part[16][17];
+    const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
+    const uint32_t d = blockIdx.x * 16 + col;
+    const uint32_t per = (nchunks + 15) / 16;
+    const uint32_t c0 = grp * per, c1 = min(c0 + per, nchunks);
+    uint32_t last = kFlNone;
+    if (d < bins)
+        for (uint32_t c = c0; c < c1; ++c) {
+            const uint32_t v = S[(size_t)c * bins + d];
+            if (v != kFlNone) last = v;
+        }
+    part[grp][col] = last;
+    __syncthreads();
+    uint32_t run = kFlNone, all = kFlNone;
+    for (uint32_t g = 0; g < 16; ++g) {
+        const uint32_t v = part[g][col];
+        if (v != kFlNone) {
+            if (g < grp) run = v;
+            all = v;
+        }
+    }
+    if (d < bins) {
+        for (uint32_t c = c0; c < c1; ++c) {
+            const uint32_t v = S[(size_t)c * bins + d];
+            S[(size_t)c * bins + d] = run;
+            if (v != kFlNone) run = v;
+        }
+        if (grp == 0) gmax[d] = all == kFlNone ? 0u : all;
+    }
+}
+
+// Same mapping as k_bound_last: lane = tile of the chunk, so the gaps of consecutive tiles of one digit — consecutive
+// bucket ranges — leave in one store instruction.  A lane's previous key: the last key of the nearest lower lane with
+// messages of the digit (ballot + shuffle), else the chunks before (P).  Every lane takes part in write_gap.
+__global__ __launch_bounds__(256) void k_bound_apply(const uint32_t* __restrict__ FL, const uint32_t* __restrict__ M,
+                                                     const uint32_t* __restrict__ P, uint32_t ntiles, uint32_t bins,
+                                                     uint32_t shift, uint32_t nb, uint32_t* __restrict__ offsets,
+                                                     uint32_t* __restrict__ q, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * kScanRows + lane;
+    const uint64_t below = lanes_below();
+    for (uint32_t d0 = w * 4u; d0 < bins; d0 += kWaves * 4u) {
+        uint32_t v[4], m4[4], p4[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const bool on = t < ntiles && d0 + k < bins;
+            v[k] = on ? FL[(size_t)t * bins + d0 + k] : kFlEmpty;
+            m4[k] = on ? M[(size_t)t * bins + d0 + k] : 0u;
+            p4[k] = d0 + k < bins ? P[(size_t)blockIdx.x * bins + d0 + k] : kFlNone;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const bool has = fl_has(v[k]);
+            const uint64_t lower = __ballot(has) & below;
+            const uint32_t src = lower ? 63u - (uint32_t)__builtin_clzll(lower) : lane;
+            const uint32_t pl = (uint32_t)__shfl((int)(v[k] >> 16), (int)src, 64);
+            const uint32_t prev = lower ? pl : p4[k];
+            uint32_t lo = 0, len = 0;
+            if (has) {
+                const uint32_t first = v[k] & 0xFFFFu;
+                const uint32_t from = prev == kFlNone ? 0u : prev + 1u;  // the first bucket of the digit not started yet
+                if (first >= from) {
+                    lo = ((d0 + k) << shift) + from;
+                    len = lo < nb ? min(first - from + 1u, nb - lo) : 0u;
+                }
+            }
+            write_gap(offsets, lo, len, m4[k], q, cap);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -3185,7 +3355,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
             if (r[q] == kNoAct4) continue;
             uint32_t act = ORL_NO_ACT, rr = r[q];
             if (rr == kFanSlow || rr == kNeedProbeCache) {  // the 32-B table, or a remote owner's cache
-                rr = route_msg(sm.P, dir, mask, cache, cmask, m[q], excl != 0, act);
+                rr = route_msg(sm.P, dir, mask, cache, cmask, m[q], excl != 0, act, e[q]);
             } else if (rr == kNeedProbe) {
                 uint32_t fact = 0, fsilo = 0;
                 int st = 1;
@@ -3567,7 +3737,25 @@ __device__ __forceinline__ void lookback_ranks(LbShared& lb, uint32_t* __restric
 // CACHE (the node exchange with the sender's directory cache on, round 5): destinations by dest_rank_cached; a cached
 // message's record carries the cached silo as its target silo and act_out (an act lane in the same padded regions) its
 // cached handle (ORL_NO_ACT for every other record); *wire_status |= ORL_PART_CACHED when the tile cached any.
-template <int FMT, bool CACHE>
+// KX (the node exchange of a batch with KeyExt strings, round 6; 32-B records only): a KeyExt message without the
+// precomputed hash gets it from its bytes first (its owner is that hash's ring owner, UniqueKey.cs:288-294; the record
+// carries it with ORL_HDR_HASH_VALID), and the extension travels beside the record: kx.out (an ext-ref lane in the same
+// padded regions) gets {offset, length} into destination d's region of kx.blob_out (kx.blob_cap bytes per destination,
+// appended at kx.cur[d], the head's blob-byte words), every other record {~0, ~0} (never a valid reference: the receiver
+// leaves such a KeyExt message ORL_ST_KEYEXT_UNRESOLVED); *wire_status |= ORL_PART_KEYEXT when the tile sent a string,
+// ORL_PART_EXT_FULL when a destination's region overflowed.
+struct KxArgs {
+    const orl_ext_ref* in;
+    const uint8_t* blob;
+    uint64_t blob_bytes;
+    orl_ext_ref* out;
+    uint8_t* blob_out;
+    uint64_t blob_cap;
+    uint32_t* cur;
+};
+__device__ uint32_t keyext_hash_dev(uint64_t n0, uint64_t n1, uint64_t tcd, const uint8_t* __restrict__ s, uint32_t len);
+
+template <int FMT, bool CACHE, bool KX = false>
 __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
@@ -3575,7 +3763,8 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
                                                            uint32_t* __restrict__ state, uint32_t ntiles,
                                                            uint64_t* __restrict__ counts, uint32_t* __restrict__ wire_status,
                                                            uint32_t tbase, uint32_t epoch, const DirSlot* __restrict__ cache,
-                                                           uint64_t cmask, uint32_t* __restrict__ act_out) {
+                                                           uint64_t cmask, uint32_t* __restrict__ act_out, KxArgs kx) {
+    static_assert(!KX || FMT == 32, "KeyExt strings travel beside 32-B records only");
     __shared__ PartLbSmem sm;
     const uint32_t rflags = rank_flags();
     stage_params(&sm.P, gp);
@@ -3616,9 +3805,20 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
                 m.n1 = (uint64_t)h1[j].x | ((uint64_t)h1[j].y << 32);
                 m.meta = h1[j].z;
                 m.aux = h1[j].w;
+                if (KX && (uint32_t)(m.tcd >> 56) == ORL_CAT_KEYEXT_GRAIN &&
+                    !(((m.meta >> 16) & 0xFFu) & (ORL_HDR_HASH_VALID | ORL_HDR_ADDRESS_COMPLETE))) {
+                    const orl_ext_ref x = kx.in[wbase + j * 64u + lane];
+                    if ((uint64_t)x.off + x.len <= kx.blob_bytes) {  // the KeyExt hash from the bytes, carried by the record
+                        m.aux = keyext_hash_dev(m.n0, m.n1, m.tcd, kx.blob + x.off, x.len);
+                        m.meta |= ORL_HDR_HASH_VALID << 16;
+                        h1[j].z = m.meta;
+                        h1[j].w = m.aux;
+                    }
+                }
                 if (CACHE) {
                     uint32_t chost;
-                    dig[j] = dest_rank_cached(sm.P, sm.rank_of_silo, cache, cmask, m, excl != 0, my_rank, cact[j], chost);
+                    dig[j] = dest_rank_cached(sm.P, sm.rank_of_silo, cache, cmask, m, excl != 0, my_rank, cact[j], chost,
+                                              wbase + j * 64u + lane);
                     if (cact[j] != ORL_NO_ACT) {  // addressed: TargetSilo = the cached silo (Message.SetTargetPlacement)
                         h1[j].z = (h1[j].z & 0x00FFFFFFu) | (chost << 24);
                         ++ncached;
@@ -3659,7 +3859,45 @@ __global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void 
             }
             if (src_index) src_index[g] = e;
             if (CACHE) act_out[g] = cact[j];
+            if (KX) {
+                orl_ext_ref r{0xFFFFFFFFu, 0xFFFFFFFFu};
+                const uint32_t hf = (h1[j].z >> 16) & 0xFFu;
+                if ((h0[j].y >> 24) == ORL_CAT_KEYEXT_GRAIN && !(hf & ORL_HDR_ADDRESS_COMPLETE)) {
+                    const orl_ext_ref x = kx.in[e];
+                    if ((uint64_t)x.off + x.len <= kx.blob_bytes) {
+                        const uint32_t o = atomicAdd(&kx.cur[d], x.len);
+                        if ((uint64_t)o + x.len <= kx.blob_cap) {
+                            uint8_t* dst = kx.blob_out + (uint64_t)d * kx.blob_cap + o;
+                            for (uint32_t b = 0; b < x.len; ++b) dst[b] = kx.blob[x.off + b];
+                            r = orl_ext_ref{o, x.len};
+                            atomicOr(wire_status, ORL_PART_KEYEXT);
+                        } else {
+                            atomicOr(wire_status, ORL_PART_EXT_FULL);
+                        }
+                    }
+                }
+                kx.out[g] = r;
+            }
         }
+    }
+}
+
+// The ext-ref lane of a received chunk: the references of the records from source s (plan.recv[s] records, received back
+// to back in rank order) point into s's part of the received blob, which starts at base[s] (valid ones only).
+struct KxRebase {
+    uint64_t cnt[ORL_NODE_MAX_RANKS];
+    uint64_t base[ORL_NODE_MAX_RANKS];
+};
+__global__ __launch_bounds__(256) void k_ext_rebase(orl_ext_ref* __restrict__ refs, uint64_t n, uint32_t nranks, KxRebase rb) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    uint64_t lo = 0;
+    uint32_t s = 0;
+    while (s + 1 < nranks && i >= lo + rb.cnt[s]) lo += rb.cnt[s++];
+    orl_ext_ref r = refs[i];
+    if (r.off != 0xFFFFFFFFu) {
+        r.off += (uint32_t)rb.base[s];
+        refs[i] = r;
     }
 }
 
@@ -4129,13 +4367,17 @@ __global__ __launch_bounds__(256) void k_cache_resolve(const uint32_t* __restric
     win[i] = (sl != kSlotNone && claim[sl & kSlotMask] == ~i) ? 1u : 0u;
 }
 
+// The winner (the batch's last writer i of its key) also stamps the entry's LRU generation G + i + 1 (LRU.Add: a new
+// TimestampedValue takes the next generation, LRU.cs:104-108); G advances by n afterwards (k_gen_advance).
 __global__ __launch_bounds__(256) void k_cache_commit(DirSlot* __restrict__ cache, uint32_t* __restrict__ claim,
                                                       const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos, uint32_t n,
                                                       const uint32_t* __restrict__ slot_in, const uint8_t* __restrict__ win,
-                                                      uint64_t* __restrict__ cnt) {
+                                                      uint64_t* __restrict__ cnt, uint64_t mask) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n || !win[i]) return;
     const uint32_t slot = slot_in[i] & kSlotMask;
+    unsigned long long* gen = cache_gens(cache, mask);
+    gen[slot] = gen[mask + 1] + i + 1ull;
     const bool fresh = cache[slot].state == SLOT_CLAIMED;  // a new entry (else an update of a FULL one)
     uint64_t* w24 = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(cache + slot) + 24);
     *w24 = (uint64_t)acts[i] | ((uint64_t)silos[i] << 32) | ((uint64_t)SLOT_FULL << 40);
@@ -4144,6 +4386,11 @@ __global__ __launch_bounds__(256) void k_cache_commit(DirSlot* __restrict__ cach
         atomicAdd(reinterpret_cast<unsigned long long*>(cnt), 1ull);
         if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);
     }
+}
+
+// The cache's generation base after a batch that stamped generations (lookups or adds): G += the batch size.
+__global__ void k_gen_advance(unsigned long long* __restrict__ g, uint64_t n) {
+    if (threadIdx.x == 0) *g += n;
 }
 
 // Merge of a partition copy (GrainDirectoryPartition.Merge, GrainDirectoryPartition.cs:366-383, on
@@ -4644,10 +4891,12 @@ uint32_t route_items(uint64_t n, uint32_t max_items, uint32_t min_wg = 0) {
 template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
-                      const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx) {
+                      const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx, uint32_t* offsets, uint32_t nb,
+                      uint32_t* gap_q, uint32_t gap_cap) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
-                                                row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx)
+                                                row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx, offsets, nb,   \
+                                                gap_q, gap_cap)
 #define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
@@ -4661,6 +4910,8 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
         }
     } else if (out == OUT_PAIR || out == OUT_LSD_PAIR) {
         ORL_RP(IN_PAIR, OUT_PAIR, kItems);
+    } else if (out == OUT_FINAL_GAPS) {
+        ORL_RP(IN_PAIR, OUT_FINAL_GAPS, kItems);
     } else {
         ORL_RP(IN_PAIR, OUT_FINAL, kItems);
     }
@@ -4670,10 +4921,11 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
 
 void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
-                 const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr) {
+                 const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr,
+                 uint32_t* offsets = nullptr, uint32_t nb = 0, uint32_t* gap_q = nullptr, uint32_t gap_cap = 0) {
     switch (bits) {
 #define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
-                                                hot_words, hot_rows, hot_idx); break;
+                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -4888,6 +5140,16 @@ bool seg_fused() {
     return on;
 }
 
+// LSD path's bucket offsets written by the last pass and k_bound_* (round 6); ORL_LSD_FUSED_OFFSETS=0: the sorted keys +
+// k_offsets_gaps (A/B).
+bool lsd_fused_offsets() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_LSD_FUSED_OFFSETS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // LSD path's bucket offsets: ORL_OFFSETS_SUFMIN=1 keeps the round-2 five-launch form (A/B).
 bool offsets_sufmin() {
     static const bool on = [] {
@@ -4961,6 +5223,8 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     if (lsd_sweep(s)) return bucket_lsd_sweep(d_act, n, n_act, d_order, d_offsets, s, st);
     const RadixPlan& plan = bp.lsd;
     const uint32_t row_step0 = kItems / route_items;
+    // the last pass writes the bucket offsets itself (round 6) when its keys' low part fits the 16-bit halves of FL
+    const bool gaps = lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
@@ -4972,8 +5236,21 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         col_scan(s.tile_hist, nrows, bins, row_step, s, st, nullptr, 0, 0, p == 0 && self_cols);
         const bool last = p == plan.passes - 1;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
-        launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, last ? OUT_FINAL : OUT_LSD_PAIR, kin, n, n_act, (uint32_t)plan.shift[p],
-                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st);
+        const int out = !last ? OUT_LSD_PAIR : gaps ? OUT_FINAL_GAPS : OUT_FINAL;
+        launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, out, kin, n, n_act, (uint32_t)plan.shift[p],
+                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st, nullptr, nullptr, nullptr, d_offsets,
+                    nb, s.gap_q, s.gap_cap);
+    }
+    if (gaps) {  // the buckets the last pass could not see from inside a tile (k_bound_last), then the digits' tails
+        const int lp = plan.passes - 1;
+        const uint32_t bins = 1u << plan.bits[lp], nch = ceil_div(ntiles, kScanRows);
+        hipLaunchKernelGGL(k_bound_last, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
+        hipLaunchKernelGGL(k_bound_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.sorted_keys + (size_t)ntiles * bins);
+        hipLaunchKernelGGL(k_bound_apply, dim3(nch), dim3(256), 0, st, s.sorted_keys, s.tile_hist, s.col_sums, ntiles, bins,
+                           (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
+        hipLaunchKernelGGL(k_sweep_tail, dim3(bins), dim3(256), 0, st, s.col_tot, s.sorted_keys + (size_t)ntiles * bins,
+                           (uint32_t)plan.bits[lp], (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap, nullptr);
+        return (int)hipGetLastError();
     }
     if (offsets_sufmin()) {  // A/B: the five-launch form (fill, mark, suffix minima)
         hipLaunchKernelGGL(k_fill_u32, dim3(ceil_div(nb, 256)), dim3(256), 0, st, d_offsets, nb, kNoOffset);
@@ -5084,16 +5361,18 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
     uint16_t* th = hist ? s.tile_cnt : nullptr;
     const uint32_t bins = hist ? rh.bins : 1u, shift = hist ? rh.shift : 0u;
     if (d_in_act && hist) return (int)hipErrorInvalidValue;  // the act lane is the node's (no stage 4 in the same call)
-#define ORL_ROUTE_C(H, W, Q, C) hipLaunchKernelGGL((k_route<H, W, Q, C>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, \
-                                                   dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                         \
+#define ORL_ROUTE_L(H, W, Q, C, LR) hipLaunchKernelGGL((k_route<H, W, Q, C, LR>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params,\
+                                                   dv.dir, dv.mask, dv.cache, dv.cmask, dv.probe, dv.probe_bad, d_in,                 \
                                                    (uint32_t)n, excl, d_route, d_act, th, bins, shift, items, hw, hr, d_in_act)
+#define ORL_ROUTE_C(H, W, Q, C) do { if (dv.lru) ORL_ROUTE_L(H, W, Q, C, true); else ORL_ROUTE_L(H, W, Q, C, false); } while (0)
 #define ORL_ROUTE(H, W, Q) do { if (H == 0 && d_in_act) ORL_ROUTE_C(0, W, Q, true); else ORL_ROUTE_C(H, W, Q, false); } while (0)
 #define ORL_ROUTE_W(H, Q) do { if (fmt == 16) ORL_ROUTE(H, 16, Q); else if (fmt == 8) ORL_ROUTE(H, 8, Q); else ORL_ROUTE(H, 32, Q); } while (0)  // fmt checked above
     if (dv.probe8) {  // the route kernel takes the 8-B form (config 2: route 1.43 -> 1.30 ms)
         const ProbeSlot* p8 = static_cast<const ProbeSlot*>(dv.probe8);
-#define ORL_ROUTE8C(H, W, C) hipLaunchKernelGGL((k_route<H, W, 8, C>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params, dv.dir, dv.mask, \
-                                                dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route, d_act, th, bins,  \
-                                                shift, items, hw, hr, d_in_act)
+#define ORL_ROUTE8L(H, W, C, LR) hipLaunchKernelGGL((k_route<H, W, 8, C, LR>), dim3(nwg), dim3(kRouteThreads), 0, st, d_params,   \
+                                                dv.dir, dv.mask, dv.cache, dv.cmask, p8, nullptr, d_in, (uint32_t)n, excl, d_route,  \
+                                                d_act, th, bins, shift, items, hw, hr, d_in_act)
+#define ORL_ROUTE8C(H, W, C) do { if (dv.lru) ORL_ROUTE8L(H, W, C, true); else ORL_ROUTE8L(H, W, C, false); } while (0)
 #define ORL_ROUTE8(H, W) do { if (H == 0 && d_in_act) ORL_ROUTE8C(0, W, true); else ORL_ROUTE8C(H, W, false); } while (0)
         if (hist) {
             if (fmt == 16) ORL_ROUTE8(kMaxDigitBits, 16); else if (fmt == 8) ORL_ROUTE8(kMaxDigitBits, 8); else ORL_ROUTE8(kMaxDigitBits, 32);
@@ -5102,6 +5381,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
         }
 #undef ORL_ROUTE8
 #undef ORL_ROUTE8C
+#undef ORL_ROUTE8L
     } else if (dv.probe) {
         if (hist) ORL_ROUTE_W(kMaxDigitBits, 16); else ORL_ROUTE_W(0, 16);
     } else {
@@ -5110,6 +5390,7 @@ int launch_route_bucket(const RouteParams* d_params, const DirView& dv, const vo
 #undef ORL_ROUTE_W
 #undef ORL_ROUTE
 #undef ORL_ROUTE_C
+#undef ORL_ROUTE_L
     if (ev_end) (void)hipEventRecord((hipEvent_t)ev_end, st);
     int e = (int)hipGetLastError();
     if (e) return e;
@@ -5307,7 +5588,25 @@ int launch_cache_update(DirSlot* d_cache, uint64_t mask, uint32_t* d_claim, uint
     hipLaunchKernelGGL(k_cache_probe, g, b, 0, st, d_cache, mask, d_claim, d_keys, d_acts, d_silos, (uint32_t)n, n_act, n_silos,
                        d_params->local, d_slot, d_err);
     hipLaunchKernelGGL(k_cache_resolve, g, b, 0, st, d_claim, (uint32_t)n, d_slot, d_flag);
-    hipLaunchKernelGGL(k_cache_commit, g, b, 0, st, d_cache, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_flag, d_cnt);
+    hipLaunchKernelGGL(k_cache_commit, g, b, 0, st, d_cache, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_flag, d_cnt, mask);
+    return launch_cache_gen_advance(d_cache, mask, n, stream);
+}
+
+int launch_ext_rebase(orl_ext_ref* d_refs, uint64_t n, uint32_t nranks, const uint64_t* cnt, const uint64_t* base, void* stream) {
+    if (n == 0) return 0;
+    KxRebase rb{};
+    for (uint32_t r = 0; r < nranks && r < ORL_NODE_MAX_RANKS; ++r) {
+        rb.cnt[r] = cnt[r];
+        rb.base[r] = base[r];
+    }
+    hipLaunchKernelGGL(k_ext_rebase, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_refs, n, nranks, rb);
+    return (int)hipGetLastError();
+}
+
+int launch_cache_gen_advance(const DirSlot* d_cache, uint64_t mask, uint64_t n, void* stream) {
+    if (!d_cache || n == 0) return 0;
+    hipLaunchKernelGGL(k_gen_advance, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       reinterpret_cast<unsigned long long*>(const_cast<DirSlot*>(d_cache + mask + 1)) + mask + 1, n);
     return (int)hipGetLastError();
 }
 
@@ -5458,7 +5757,8 @@ int launch_part_routed(const uint8_t* d_ros, const void* d_in, int win, int wout
 int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, uint32_t opts,
                             const uint8_t* d_rank_of_silo, uint32_t nranks, uint32_t my_rank, uint64_t stride,
                             void* d_out, int fmt, uint32_t* d_src_index, uint64_t* d_counts, uint32_t* d_wire_status,
-                            Scratch& s, void* stream, const DirSlot* d_cache, uint64_t cmask, uint32_t* d_act_out) {
+                            Scratch& s, void* stream, const DirSlot* d_cache, uint64_t cmask, uint32_t* d_act_out,
+                            const KxLanes* kxl) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipSuccess;
     if (fmt != 8 && fmt != 16 && fmt != 32) return (int)hipErrorInvalidValue;
@@ -5477,10 +5777,18 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
     }
     const uint32_t tbase = s.lb_ticket, epoch = s.lb_epoch;
     const bool cached = d_cache && d_act_out && d_wire_status;
-#define ORL_PLB(F, C) hipLaunchKernelGGL((k_part_lb<F, C>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo, d_in, \
-                                         (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state, ntiles,        \
-                                         d_counts, d_wire_status, tbase, epoch, d_cache, cmask, d_act_out)
-    if (cached) {
+    const bool kxon = kxl && kxl->ext && d_wire_status;
+    if (kxon && fmt != 32) return (int)hipErrorInvalidValue;
+    KxArgs kx{};
+    if (kxon) kx = KxArgs{kxl->ext, kxl->blob, kxl->blob_bytes, kxl->ext_out, kxl->blob_out, kxl->blob_cap, kxl->cur};
+#define ORL_PLB3(F, C, X) hipLaunchKernelGGL((k_part_lb<F, C, X>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo,\
+                                             d_in, (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state,     \
+                                             ntiles, d_counts, d_wire_status, tbase, epoch, d_cache, cmask, d_act_out, kx)
+#define ORL_PLB(F, C) ORL_PLB3(F, C, false)
+    if (kxon) {
+        if (cached) ORL_PLB3(32, true, true);
+        else ORL_PLB3(32, false, true);
+    } else if (cached) {
         if (fmt == 16) ORL_PLB(16, true);
         else if (fmt == 8) ORL_PLB(8, true);
         else ORL_PLB(32, true);
@@ -5490,6 +5798,7 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
         else ORL_PLB(32, false);
     }
 #undef ORL_PLB
+#undef ORL_PLB3
     e = hipGetLastError();
     if (e == hipSuccess) {
         s.lb_ticket += ntiles;

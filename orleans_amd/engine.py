@@ -242,22 +242,24 @@ class GrainDirectoryEngine:
         silos = np.ascontiguousarray(silos, dtype=np.uint8)
         n = len(keys)
         st, wa, ws = np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint8)
-        self._ck(self._lib.orl_dir_insert_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), ptr(acts), ptr(silos), n, ptr(wa),
-                                                 ptr(ws), ptr(st)))
+        self._ck(self._lib.orl_dir_insert_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), int(ref["len"].sum()), ptr(acts),
+                                                 ptr(silos), n, ptr(wa), ptr(ws), ptr(st)))
         return st, wa, ws
 
     def unregister_keyext(self, keys: np.ndarray, strings) -> np.ndarray:
         keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
         ref, blob = self.ext_blob(strings)
         out = np.zeros(len(keys), np.uint8)
-        self._ck(self._lib.orl_dir_remove_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), len(keys), ptr(out)))
+        self._ck(self._lib.orl_dir_remove_keyext(self._ctx, ptr(keys), ptr(ref), ptr(blob), int(ref["len"].sum()), len(keys),
+                                                 ptr(out)))
         return out
 
     def lookup_keyext_host(self, keys: np.ndarray, strings):
         keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
         ref, blob = self.ext_blob(strings)
         a, s = np.zeros(len(keys), np.uint32), np.zeros(len(keys), np.uint8)
-        self._ck(self._lib.orl_dir_lookup_keyext_host(self._ctx, ptr(keys), ptr(ref), ptr(blob), len(keys), ptr(a), ptr(s)))
+        self._ck(self._lib.orl_dir_lookup_keyext_host(self._ctx, ptr(keys), ptr(ref), ptr(blob), int(ref["len"].sum()),
+                                                      len(keys), ptr(a), ptr(s)))
         return a, s
 
     def keyext_count(self) -> int:

@@ -172,6 +172,14 @@ class GrainNode:
         rc = self._lib.orl_node_route_batch_device(self._node, L.ptr(d_msgs), int(n), int(opts), C.byref(r), L.ptr(stream))
         return self._result(rc, r)
 
+    def route_batch_keyext_device(self, d_msgs, n: int, d_ext, d_blob, blob_bytes: int, stream=None, opts: int = 0) -> NodeResult:
+        """orl_node_route_batch_keyext_device: the batch with its KeyExt strings (d_ext: orl_ext_ref per message into d_blob)."""
+        C = self._C
+        r = L.orl_node_result()
+        rc = self._lib.orl_node_route_batch_keyext_device(self._node, L.ptr(d_msgs), int(n), int(opts), L.ptr(d_ext), L.ptr(d_blob),
+                                                          int(blob_bytes), C.byref(r), L.ptr(stream))
+        return self._result(rc, r)
+
     def fanout_batch_device(self, d_csr_off, d_csr_tgt, d_follower_keys, follower_tcd: int, d_pubs, d_pub_silo, n_pub: int,
                             d_pub_offsets, total=None, stream=None, opts: int = 0) -> NodeResult:
         """This rank's publishes expanded (orl_fanout_expand_device) and routed across the node

@@ -11,6 +11,12 @@
  *      c. the narrow call: the same batch as 8-byte orl_wire8 records (orl_wire_types_set with the grain class),
  *         orl_route_batch_narrow on page-locked arrays
  *   4. all three compared word for word with the oracle's route + stable bucketing of the same batch.
+ *   5. KeyExt (string-key) grains (argv[1]: the golden KeyExt cases, one "tcd n0 n1 uniform hex-utf8" per line, written by
+ *      tests/test_c_host.py from tests/golden/jenkins.json): their uniform hashes (orl_keyext_uniform_hash), registration
+ *      (orl_dir_insert_keyext + orl_dir_lookup_keyext_host), then a batch through orl_route_keyext_device on library
+ *      buffers — every registered grain HIT on its silo with its handle, the same keys with an unregistered extension
+ *      placed PreferLocal, half the messages with the precomputed hash (ORL_HDR_HASH_VALID), half hashed by the kernel;
+ *      owners from the oracle's ring, order / offsets from the oracle's stable bucketing.
  *
  * Build: gcc -std=c11 -O2 -I include tests/c_host/orl_host_demo.c -L orleans_amd -lorleans_route
  *        -L oracle -lorleans_cpu_ref -Wl,-rpath,<dirs> -o tools/orl_host_demo        (tests/test_c_host.py does this)
@@ -65,7 +71,134 @@ static int compare(const char* what, const uint32_t* got, const uint32_t* exp, s
     return 0;
 }
 
-int main(void) {
+#define MAX_KX 64
+
+/* step 5: returns nonzero on any difference (the golden cases' file is argv[1]) */
+static int keyext_step(orl_ctx* ctx, const ref_cluster* cl, const char* path) {
+    FILE* f = fopen(path, "r");
+    if (!f) {
+        fprintf(stderr, "cannot open %s\n", path);
+        return 1;
+    }
+    static orl_grain_key keys[2 * MAX_KX];
+    static uint32_t uni[MAX_KX], acts[MAX_KX];
+    static uint8_t blob[2 * MAX_KX * 512], silos[MAX_KX];
+    static orl_ext_ref ext[2 * MAX_KX];
+    size_t nk = 0, used = 0;
+    unsigned long long tcd, n0, n1;
+    unsigned u;
+    char hex[1024];
+    while (nk < MAX_KX && fscanf(f, "%llx %llx %llx %u %1023s", &tcd, &n0, &n1, &u, hex) == 5) {
+        const size_t len = strcmp(hex, "-") == 0 ? 0 : strlen(hex) / 2;
+        keys[nk].type_code_data = tcd;
+        keys[nk].n0 = n0;
+        keys[nk].n1 = n1;
+        uni[nk] = u;
+        ext[nk].off = (uint32_t)used;
+        ext[nk].len = (uint32_t)len;
+        for (size_t b = 0; b < len; ++b) {
+            unsigned v;
+            sscanf(hex + 2 * b, "%2x", &v);
+            blob[used + b] = (uint8_t)v;
+        }
+        used += len;
+        acts[nk] = 100 + (uint32_t)nk;
+        silos[nk] = (uint8_t)(nk % N_SILOS);
+        ++nk;
+    }
+    fclose(f);
+    int bad = nk == 0;
+    for (size_t i = 0; i < nk; ++i) {
+        const uint32_t h = orl_keyext_uniform_hash(&keys[i], (const char*)blob + ext[i].off, ext[i].len);
+        if (h != uni[i]) {
+            fprintf(stderr, "KeyExt uniform hash %zu: %u vs golden %u\n", i, h, uni[i]);
+            bad = 1;
+        }
+    }
+    uint8_t st[MAX_KX];
+    check(ctx, orl_dir_insert_keyext(ctx, keys, ext, blob, used, acts, silos, nk, NULL, NULL, st), "orl_dir_insert_keyext");
+    uint32_t la[MAX_KX];
+    uint8_t ls[MAX_KX];
+    check(ctx, orl_dir_lookup_keyext_host(ctx, keys, ext, blob, used, nk, la, ls), "orl_dir_lookup_keyext_host");
+    for (size_t i = 0; i < nk; ++i)
+        if (st[i] != ORL_INS_INSERTED || la[i] != acts[i] || ls[i] != silos[i]) {
+            fprintf(stderr, "KeyExt registration %zu: status %u, lookup %u / %u\n", i, st[i], la[i], ls[i]);
+            bad = 1;
+        }
+    /* the same keys with an unregistered extension (the string + "!"): another grain */
+    for (size_t i = 0; i < nk; ++i) {
+        keys[nk + i] = keys[i];
+        ext[nk + i].off = (uint32_t)used;
+        ext[nk + i].len = ext[i].len + 1;
+        memcpy(blob + used, blob + ext[i].off, ext[i].len);
+        blob[used + ext[i].len] = '!';
+        used += ext[i].len + 1;
+    }
+    const size_t m = 2 * nk;
+    static orl_msg_hdr msgs[2 * MAX_KX];
+    static uint32_t er[2 * MAX_KX], ea[2 * MAX_KX], eo[2 * MAX_KX], ef[N_GRAINS + 2];
+    static uint32_t route[2 * MAX_KX], act[2 * MAX_KX], order[2 * MAX_KX], off[N_GRAINS + 2];
+    for (size_t i = 0; i < m; ++i) {
+        memset(&msgs[i], 0, sizeof msgs[i]);
+        msgs[i].target = keys[i];
+        msgs[i].sending_silo = (uint8_t)((i * 3) % N_SILOS);
+        msgs[i].category = 2;
+        if (i % 2 == 0) {  /* the precomputed hash travels with the header; the others are hashed from the bytes */
+            msgs[i].flags = ORL_HDR_HASH_VALID;
+            msgs[i].aux = orl_keyext_uniform_hash(&keys[i], (const char*)blob + ext[i].off, ext[i].len);
+        }
+    }
+    /* expected: the owner is the ring owner of the KeyExt hash (the oracle's KEYEXT_UNRESOLVED word carries it) */
+    static orl_msg_hdr hv[2 * MAX_KX];
+    for (size_t i = 0; i < m; ++i) {
+        hv[i] = msgs[i];
+        hv[i].flags = ORL_HDR_HASH_VALID;
+        hv[i].aux = orl_keyext_uniform_hash(&keys[i], (const char*)blob + ext[i].off, ext[i].len);
+    }
+    void* dir = ref_dir_new();
+    ref_route(cl, dir, hv, m, 0, er, ea);
+    ref_dir_free(dir);
+    for (size_t i = 0; i < m; ++i) {
+        const uint32_t owner = er[i] & 0xFF, me = msgs[i].sending_silo;
+        if (((er[i] >> 16) & 0xFF) != ORL_ST_KEYEXT_UNRESOLVED) bad = 1;
+        if (i < nk) {
+            const uint32_t s = silos[i];
+            er[i] = owner | (s << 8) | (ORL_ST_HIT << 16) | ((s == me ? ORL_RF_LOOPBACK : 0u) << 24);
+            ea[i] = acts[i];
+        } else {
+            er[i] = owner | (me << 8) | (ORL_ST_NEW_PLACEMENT << 16) | ((ORL_RF_NEW_PLACEMENT | ORL_RF_LOOPBACK) << 24);
+            ea[i] = ORL_NO_ACT;
+        }
+    }
+    ref_bucket(ea, m, N_GRAINS, eo, ef);
+    void *d_in, *d_ext, *d_blob, *d_route, *d_act, *d_order, *d_off;
+    check(ctx, orl_device_alloc(ctx, m * sizeof *msgs, &d_in), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, m * sizeof *ext, &d_ext), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, used, &d_blob), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, m * 4, &d_route), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, m * 4, &d_act), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, m * 4, &d_order), "orl_device_alloc");
+    check(ctx, orl_device_alloc(ctx, (N_GRAINS + 2) * 4, &d_off), "orl_device_alloc");
+    check(ctx, orl_copy_to_device(ctx, d_in, msgs, m * sizeof *msgs, NULL), "orl_copy_to_device");
+    check(ctx, orl_copy_to_device(ctx, d_ext, ext, m * sizeof *ext, NULL), "orl_copy_to_device");
+    check(ctx, orl_copy_to_device(ctx, d_blob, blob, used, NULL), "orl_copy_to_device");
+    check(ctx, orl_route_keyext_device(ctx, (const orl_msg_hdr*)d_in, m, 0, (const orl_ext_ref*)d_ext, (const uint8_t*)d_blob,
+                                       used, (uint32_t*)d_route, (uint32_t*)d_act, (uint32_t*)d_order, (uint32_t*)d_off, NULL),
+          "orl_route_keyext_device");
+    check(ctx, orl_copy_to_host(ctx, route, d_route, m * 4, NULL), "orl_copy_to_host");
+    check(ctx, orl_copy_to_host(ctx, act, d_act, m * 4, NULL), "orl_copy_to_host");
+    check(ctx, orl_copy_to_host(ctx, order, d_order, m * 4, NULL), "orl_copy_to_host");
+    check(ctx, orl_copy_to_host(ctx, off, d_off, (N_GRAINS + 2) * 4, NULL), "orl_copy_to_host");
+    check(ctx, orl_stream_sync(ctx, NULL), "orl_stream_sync");
+    bad |= compare("route (KeyExt)", route, er, m) | compare("act (KeyExt)", act, ea, m) |
+           compare("order (KeyExt)", order, eo, m) | compare("offsets (KeyExt)", off, ef, N_GRAINS + 2);
+    void* bufs[] = {d_in, d_ext, d_blob, d_route, d_act, d_order, d_off};
+    for (size_t k = 0; k < sizeof bufs / sizeof bufs[0]; ++k) check(ctx, orl_device_free(ctx, bufs[k]), "orl_device_free");
+    if (!bad) printf("c host KeyExt ok: %zu golden KeyExt grains registered and %zu messages routed bit-exact\n", nk, m);
+    return bad;
+}
+
+int main(int argc, char** argv) {
     orl_config cfg;
     memset(&cfg, 0, sizeof cfg);
     cfg.abi_version = ORL_ABI_VERSION;
@@ -184,6 +317,7 @@ int main(void) {
     free(recs);
 
     ref_dir_free(dir);
+    if (argc > 1) bad |= keyext_step(ctx, &cl, argv[1]);
     check(ctx, orl_ctx_destroy(ctx), "orl_ctx_destroy");
     if (bad) return 1;
     printf("c host ok: %d messages through orl_route_batch (pinned host arrays), orl_route_batch_device "

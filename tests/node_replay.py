@@ -77,7 +77,7 @@ def host_rank(route: np.ndarray, ros: np.ndarray, me: int) -> np.ndarray:
     return np.where(h == 0xFF, me, ros[np.minimum(h, 7).astype(np.int64)])
 
 
-def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None):
+def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None, keyext=None):
     """The oracle's replay of one batch per rank -> ([per rank (route, act, order, offsets, hosted headers)], forward).
 
     caches[s] (optional): rank s's directory cache {(tcd, n0, n1): (act, silo)}.  A message whose owner is on another rank
@@ -85,7 +85,8 @@ def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None)
     LocalGrainDirectory.cs:690-717; pyref.apply_directory_cache: HIT | CACHED, TargetSilo = the cached silo) and sent to
     the rank hosting that silo instead of the owner's; the others follow the oracle partition by owner rank.  The receiver
     checks a cached record against its directory when it holds the grain's partition (stale entries are
-    re-addressed and flagged ORL_RF_CACHE_STALE)."""
+    re-addressed and flagged ORL_RF_CACHE_STALE).  keyext(d, headers) -> (route, act) (optional): rank d's KeyExt lookups
+    of the KeyExt messages it owns (strings beside the records: orl_node_route_batch_keyext_device)."""
     from oracle import pyref as P
     nr = len(batches)
     functional = functional if functional is not None else [1] * 8
@@ -125,6 +126,11 @@ def expected(oracles, ros, batches, chunks, n_act, caches=None, functional=None)
     routed = []
     for d in range(nr):
         r, a = oracles[d].route(owned[d])
+        if keyext is not None:  # KeyExt messages with their strings: the owner's KeyExt table (keyext(d, headers))
+            kx = ((r >> 16) & 0xFF) == L.ST_KEYEXT_UNRESOLVED
+            if kx.any():
+                r, a = r.copy(), a.copy()
+                r[kx], a[kx] = keyext(d, owned[d][kx])
         if pre[d]:
             cr = np.concatenate([x[0] for x in pre[d]])
             ca = np.concatenate([x[1] for x in pre[d]])

@@ -31,9 +31,25 @@ def test_c_host_compiles_and_links(tmp_path):
     _build(str(tmp_path))
 
 
+def _keyext_cases(path):
+    """The golden KeyExt cases (tests/golden/jenkins.json) as the C host reads them: tcd n0 n1 uniform hex-utf8."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "jenkins.json")))
+    with open(path, "w") as f:
+        for c in g["keyext"]:
+            x = c["ext"].encode("utf-8").hex() or "-"
+            f.write(f"{c['tcd']} {c['n0']} {c['n1']} {c['uniform']} {x}\n")
+    return len(g["keyext"])
+
+
 @pytest.mark.gpu
 def test_c_host_routes_bit_exact(tmp_path):
+    """Steps 1-4 and, with the golden KeyExt cases, step 5: orl_dir_insert_keyext / orl_route_keyext_device from C
+    (GrainDirectoryPartition.cs:270-287,326-344, UniqueKey.cs:288-294)."""
     exe = _build(str(tmp_path))
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    cases = str(tmp_path / "keyext_cases.txt")
+    nk = _keyext_cases(cases)
+    r = subprocess.run([exe, cases], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "c host ok" in r.stdout
+    assert f"c host KeyExt ok: {nk} golden KeyExt grains registered and {2 * nk} messages routed bit-exact" in r.stdout

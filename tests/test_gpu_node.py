@@ -34,10 +34,11 @@ class World:
     host rank (each rank's catalog numbers its own activations) — node_replay.population, one engine + one oracle per
     rank."""
 
-    def __init__(self, nranks, n_grains=40_000, seed=3, host_mix=0.3, ros=None, cl=None, max_batch=1 << 20, reg_frac=0.9):
+    def __init__(self, nranks, n_grains=40_000, seed=3, host_mix=0.3, ros=None, cl=None, max_batch=1 << 20, reg_frac=0.9,
+                 extra_act=0):
         p = R.population(nranks, n_grains, seed, host_mix, ros, cl, reg_frac)
         self.p = p
-        self.cl, self.nr, self.ros, self.n_act, self.n_grains = p.cl, nranks, p.ros, p.n_act, n_grains
+        self.cl, self.nr, self.ros, self.n_act, self.n_grains = p.cl, nranks, p.ros, p.n_act + extra_act, n_grains
         self.engs, self.oracles = [], []
         for r in range(nranks):
             local = (self.ros == r).astype(np.uint8)
@@ -519,6 +520,138 @@ def test_node_mixed_width_segments_aligned(torch, chunks):
         if hit:
             break
     assert hit, "no seed produced an odd 8-B segment before a wide one"
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
+@pytest.mark.parametrize("nranks,chunks,host_mix", [(2, 2, 0.0), (3, 3, 0.3), (4, 2, 0.3)])
+def test_node_keyext_vs_oracle(torch, nranks, chunks, host_mix):
+    """KeyExt (string-key) grains across the node (orl_node_route_batch_keyext_device).  Each rank registers
+    the KeyExt grains whose directory partition it owns (the ring owner of the KeyExt hash, UniqueKey.cs:288-294); every
+    rank's batch mixes long-key messages with KeyExt ones — registered grains, grains differing only in the string, grains
+    nobody registered — half with the precomputed hash (ORL_HDR_HASH_VALID), half hashed by the sender from the bytes.  The
+    strings travel beside the 32-B records in hop 1 and the owner resolves them in its KeyExt table (HIT on the owner,
+    placement of a miss: LocalGrainDirectory.cs:719-765 with the whole GrainId); one rank sends no strings
+    (orl_node_route_batch_device) and still takes part in the string lanes.  Every rank's hosted output == the oracle's replay
+    with pyref's KeyExt directory at each owner."""
+    from oracle import pyref as P
+    t = torch
+    ros = None if nranks != 3 else [s % 3 for s in range(8)]
+    world = World(nranks, host_mix=host_mix, ros=ros, extra_act=3000)
+    p = world.p
+    tc = world.cl.type_code
+    rng = np.random.default_rng(nranks * 10 + chunks)
+    ring = P.Ring()
+    for s in range(8):
+        ring.add_server(s, int(world.cl.hashes[s]))
+    # KeyExt grains: activation on a host silo; handles dense per host rank after the long-key ones (each rank's catalog)
+    kx = [P.key_from_long(int(i % 900), tc, ("user-%d" % i) if i % 3 else ("ключ/%d/é中" % i)) for i in range(3000)]
+    kx_host = rng.integers(0, 8, len(kx)).astype(np.uint8)
+    kx_act = np.zeros(len(kx), np.uint32)
+    nxt = [int((p.ros[p.host[p.reg]] == r).sum()) for r in range(nranks)]  # after each host rank's long-key handles
+    for i in range(len(kx)):
+        r = int(world.ros[kx_host[i]])
+        kx_act[i] = nxt[r]
+        nxt[r] += 1
+    assert max(nxt) < world.n_act
+    views, parts = [], []
+    for r in range(nranks):
+        local = [bool(world.ros[s] == r) for s in range(8)]
+        v = P.SiloView(running=[True] * 8, functional=[True] * 8, local=local)
+        part = P.Partition()
+        keys = np.array([(k.tcd, k.n0, k.n1) for k in kx], L.KEY_DTYPE)
+        st, _, _ = world.engs[r].register_keyext(keys, [k.key_ext for k in kx], kx_act, kx_host)
+        exp = [P.register_keyext(ring, part, v, k, int(a), int(s)) for k, a, s in zip(kx, kx_act, kx_host)]
+        np.testing.assert_array_equal(st, np.array([e[0] for e in exp], np.uint8))
+        assert (st == L.INS_INSERTED).sum() > 100
+        views.append(v)
+        parts.append(part)
+
+    def batch(r, n, seed):
+        """rank r's batch: long-key messages (node_replay.messages) with every 4th replaced by a KeyExt message"""
+        m = world.messages(r, n, seed)
+        strings = [""] * n
+        rr = np.random.default_rng(seed + 7)
+        senders = np.nonzero(world.ros == r)[0]
+        for i in range(0, n, 4):
+            u = rr.random()
+            k = kx[int(rr.integers(0, len(kx)))] if u < 0.8 else P.key_from_long(int(rr.integers(0, 900)), tc,
+                                                                                      "nobody-%d" % int(rr.integers(0, 10 ** 6)))
+            pre = rr.random() < 0.5
+            m[i] = (k.tcd, k.n0, k.n1, int(senders[int(rr.integers(0, len(senders)))]), 2,
+                    L.HDR_HASH_VALID if pre else 0, 0xFF, P.uniform_hash(k) if pre else 0)
+            strings[i] = k.key_ext
+        return m, strings
+
+    gid = b"node-keyext-%d-%d-%d" % (nranks, chunks, int(host_mix * 10))
+    nodes = [GrainNode(world.engs[r], nranks, r, world.ros, max_batch=100_000, max_recv=300_000,
+                       transport=L.TRANSPORT_LOCAL, group_id=gid, chunks=chunks) for r in range(nranks)]
+    streams = [t.cuda.Stream() for _ in range(nranks)]
+    plain = nranks - 1  # this rank sends no strings (its KeyExt messages stay unresolved at their owners)
+    for b in range(2):
+        made = [batch(r, 60_000 - 3000 * r - 500 * b, seed=400 * b + r) for r in range(nranks)]
+        m, st = made[plain]  # the plain rank's batch: no KeyExt messages
+        keep = np.array([not x for x in st])
+        made[plain] = (m[keep], [x for x, k in zip(st, keep) if k])
+        batches = [m for m, _ in made]
+        refs = [GrainDirectoryEngine.ext_blob(s) for _, s in made]
+        d_in = [t.from_numpy(bb.view(np.int32).reshape(-1, 8)).cuda() for bb in batches]
+        d_ref = [t.from_numpy(rf.view(np.int32)).cuda() for rf, _ in refs]
+        d_blob = [t.from_numpy(bl).cuda() for _, bl in refs]
+        t.cuda.synchronize()
+
+        def one(r):
+            if r == plain:
+                res = nodes[r].route_batch_device(d_in[r], len(batches[r]), stream=streams[r].cuda_stream)
+            else:
+                res = nodes[r].route_batch_keyext_device(d_in[r], len(batches[r]), d_ref[r], d_blob[r], len(refs[r][1]),
+                                                         stream=streams[r].cuda_stream)
+            streams[r].synchronize()
+            return res, nodes[r].fetch(res, stream=streams[r].cuda_stream)
+
+        with ThreadPoolExecutor(nranks) as ex:
+            got = list(ex.map(one, range(nranks)))
+        # the records the senders wrote: KeyExt messages carry their hash (ORL_HDR_HASH_VALID) from the sender on
+        sent = []
+        for bb, (_, strs) in zip(batches, made):
+            x = bb.copy()
+            for i, s in enumerate(strs):
+                if (int(x["tcd"][i]) >> 56) == L.CAT_KEYEXT_GRAIN and not (x["flags"][i] & L.HDR_HASH_VALID):
+                    x["aux"][i] = P.uniform_hash(P.Key(int(x["tcd"][i]), int(x["n0"][i]), int(x["n1"][i]), s))
+                    x["flags"][i] |= L.HDR_HASH_VALID
+            sent.append(x)
+        strmap = {}
+        for bb, (_, strs) in zip(sent, made):
+            for i, s in enumerate(strs):
+                if (int(bb["tcd"][i]) >> 56) == L.CAT_KEYEXT_GRAIN:
+                    strmap[(int(bb["tcd"][i]), int(bb["n0"][i]), int(bb["n1"][i]), int(bb["aux"][i]))] = s
+
+        def kx_route(d, hdrs):
+            """rank d's directory for its owned KeyExt messages: pyref's KeyExt lookup (orl_route_keyext_device)"""
+            rs, acts = [], []
+            for h in hdrs:
+                k = P.Key(int(h["tcd"]), int(h["n0"]), int(h["n1"]),
+                          strmap[(int(h["tcd"]), int(h["n0"]), int(h["n1"]), int(h["aux"]))])
+                msg = P.Msg(k, int(h["sending_silo"]), int(h["flags"]), aux=int(h["aux"]))
+                r1, a1 = P.route_one(msg, ring, parts[d], views[d], keyext_directory=True)
+                rs.append(r1)
+                acts.append(a1)
+            return np.array(rs, np.uint32), np.array(acts, np.uint32)
+
+        exp, forward = R.expected(world.oracles, world.ros, sent, chunks, world.n_act, keyext=kx_route)
+        n_hit = 0
+        for r in range(nranks):
+            res, (route, act, order, off, hdrs) = got[r]
+            er, ea, eo, ef, eh = exp[r]
+            np.testing.assert_array_equal(hdrs, eh, err_msg=f"rank {r} batch {b} headers")
+            np.testing.assert_array_equal(route, er, err_msg=f"rank {r} batch {b} route")
+            np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} batch {b} act")
+            np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} batch {b} order")
+            np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} batch {b} offsets")
+            isx = (hdrs["tcd"] >> np.uint64(56)) == L.CAT_KEYEXT_GRAIN
+            n_hit += int((((route[isx] >> 16) & 0xFF) == L.ST_HIT).sum())
+        assert n_hit > 1000  # KeyExt grains owned by another rank ended HIT on their owner
     for nd in nodes:
         nd.close()
     world.close()

@@ -870,6 +870,86 @@ def test_directory_cache_in_route_vs_oracle(torch):
     eng.close()
 
 
+def test_directory_cache_lru_eviction_vs_oracle(torch):
+    """the directory cache evicts like the reference's instead of refusing (AdaptiveGrainDirectoryCache
+    .AddOrUpdate → LRU.Add → AdjustSize frees the entry of the smallest generation while Count >= MaximumSize; every
+    LookUp hit takes the next generation: AdaptiveGrainDirectoryCache.cs:97-133, LRU.cs:104-108,147-174,188-205).  A cache of
+    3000 entries goes through add batches that fit (the device path), overflow it (the exact LRU on the host), update keys
+    — the least recently used among them — at full capacity, outgrow it within one batch, lose entries by invalidation;
+    between them route batches whose remote-owner lookups reorder the LRU.  After every step the cached count and every
+    routed word / handle / bucket equal oracle/pyref.LRUCache fed the same sequence (lookups in message order)."""
+    t = torch
+    cl = W.default_cluster()
+    local = [1, 1, 0, 0, 0, 0, 0, 0]
+    functional = [1, 1, 1, 1, 1, 1, 0, 1]
+    n_grains, n_act, cap = 50_000, 60_000, 3000
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=n_grains, max_batch=1 << 20, device=0)
+    eng.set_silos(8, functional=functional, local=local)
+    o = cpu_ref.Oracle(8, functional=functional, local=local)
+    for s in range(8):
+        eng.add_server(s, int(cl.hashes[s]))
+        o.add_server(s, int(cl.hashes[s]))
+    keys, _, owner, _ = W.grain_population(cl, n_grains)
+    mine = np.nonzero(np.isin(owner, [0, 1]))[0]
+    eng.register_single_activation(keys[mine], mine.astype(np.uint32), owner[mine])
+    o.register(keys[mine], mine.astype(np.uint32), owner[mine])
+    eng.cache_config(cap)
+    lru = P.LRUCache(cap)
+    rng = np.random.default_rng(9)
+    remote = np.nonzero(~np.isin(owner, [0, 1]))[0]
+    st_ = t.cuda.current_stream().cuda_stream
+    kt_all = [(int(a), int(b), int(c)) for a, b, c in zip(keys["tcd"], keys["n0"], keys["n1"])]
+
+    def dev(a):
+        return t.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+
+    def add(pick):
+        acts = (50_000 + rng.integers(0, 20_000, len(pick))).astype(np.uint32)
+        silos = rng.integers(0, 8, len(pick)).astype(np.uint8)
+        eng.cache_add_or_update_device(dev(keys[pick]), dev(acts), dev(silos), len(pick), stream=st_)
+        for g, a, s in zip(pick.tolist(), acts.tolist(), silos.tolist()):
+            if a < n_act or not local[s]:  # what the device keeps (k_cache_probe)
+                lru.add(kt_all[g], (a, s))
+        t.cuda.synchronize()
+        assert eng.cache_count() == len(lru.d), (eng.cache_count(), len(lru.d))
+
+    def route(seed, n=60_000):
+        msgs = W.uniform_messages(cl, n_grains, n, seed=seed)
+        kt = list(zip(msgs["tcd"].tolist(), msgs["n0"].tolist(), msgs["n1"].tolist()))
+        res = eng.address_messages(msgs)
+        r0, a0 = o.route(msgs)
+        r_ref, a_ref = P.apply_directory_cache_lru(r0.tolist(), a0.tolist(), msgs["sending_silo"].tolist(), kt, lru,
+                                                   functional)
+        np.testing.assert_array_equal(res.route, np.array(r_ref, np.uint32), err_msg=f"route words, batch {seed}")
+        np.testing.assert_array_equal(res.act, np.array(a_ref, np.uint32))
+        o_ref, f_ref = o.bucket(np.array(a_ref, np.uint32), n_act)
+        np.testing.assert_array_equal(res.order, o_ref)
+        np.testing.assert_array_equal(res.offsets, f_ref)
+        return int(((res.route >> 24) & L.RF_CACHED != 0).sum())
+
+    add(rng.choice(remote, 2500))                    # fits: the device path
+    assert route(1) > 1000
+    add(rng.choice(remote, 1500))                    # overflows: the entries no lookup touched go first
+    route(2)
+    present = np.array([g for g in remote.tolist() if kt_all[g] in lru.d], np.int64)
+    lru_first = sorted(present.tolist(), key=lambda g: lru.d[kt_all[g]][1])[:300]  # the least recently used
+    add(np.concatenate([np.array(lru_first), rng.choice(present, 500)]))          # updates at full capacity
+    route(3)
+    inval = rng.choice(remote, 400)
+    d_rm = t.empty(len(inval), dtype=t.uint8, device="cuda")
+    eng.cache_remove_device(dev(keys[inval]), len(inval), d_rm, stream=st_)
+    t.cuda.synchronize()
+    for g in inval.tolist():
+        lru.remove(kt_all[g])
+    assert eng.cache_count() == len(lru.d)
+    route(4)
+    add(rng.choice(remote, cap + 700, replace=False))  # one batch larger than the cache
+    assert route(5) > 1000
+    add(rng.choice(remote, 100))
+    route(6)
+    eng.close()
+
+
 def _decode_on_device(t, eng, buf, nbytes, offs, sender_override=L.SENDER_FROM_HEADER):
     d_buf = t.from_numpy(buf).cuda()
     d_off = t.from_numpy(offs.view(np.int64)).cuda()
