@@ -35,6 +35,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 from orleans_amd import _lib as L  # noqa: E402
+
+if os.environ.get("LAB_LIB"):  # A/B only: an experimental build of the same library (make lab NAME=... DEFS=...)
+    L.LIB_PATH = os.path.abspath(os.environ["LAB_LIB"])
 L_NODE_ID_BYTES = 128
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)

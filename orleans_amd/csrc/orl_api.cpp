@@ -713,7 +713,12 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.lb_state); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
+    for (auto& L : c->s.lb) {
+        f(L.state);
+        if (L.ev) (void)hipEventDestroy(L.ev);
+        L = Scratch::LbSet{};
+    }
     f(c->s.sw_ring); f(c->s.sw_ctl); f(c->s.sw_gtot); f(c->s.sw_gmax); f(c->s.s4_err);
     if (c->s.hot_host) (void)hipHostFree(c->s.hot_host);
     f(c->st_in); f(c->st_out); f(c->st_off);
@@ -834,11 +839,12 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
         if ((e = hipMalloc((void**)&c->s.sstart, 4098 * 4)) != hipSuccess) return bail(e, "hipMalloc(sstart)");
         if ((e = hipMalloc((void**)&c->d_dslot, mb * 4)) != hipSuccess) return bail(e, "hipMalloc(dslot)");
         if ((e = hipMalloc((void**)&c->d_dflag, mb)) != hipSuccess) return bail(e, "hipMalloc(dflag)");
-        if ((e = hipMalloc((void**)&c->s.lb_state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
-        // zeroed once: later launches tag their granules with an epoch and number tiles from a host-mirrored ticket
-        if ((e = hipMemset(c->s.lb_state, 0, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMemset(lb_state)");
-        c->s.lb_ticket = 0;
-        c->s.lb_epoch = 0;
+        for (auto& L : c->s.lb) {
+            if ((e = hipMalloc((void**)&L.state, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMalloc(lb_state)");
+            if ((e = hipMemset(L.state, 0, 16 + ((mb + 2047) / 2048) * 64)) != hipSuccess) return bail(e, "hipMemset(lb_state)");
+            if ((e = hipEventCreateWithFlags(&L.ev, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate(lb)");
+        }
+        // (zeroed once: later launches tag their granules with an epoch and number tiles from a host-mirrored ticket)
         if ((e = hipMalloc((void**)&c->s.s4_err, 4)) != hipSuccess) return bail(e, "hipMalloc(s4_err)");
         if ((e = hipMemset(c->s.s4_err, 0, 4)) != hipSuccess) return bail(e, "hipMemset(s4_err)");
         // the LSD plan's single-sweep passes (opt-in, ORL_LSD_SWEEP=1 at context creation: measured 8x slower than the
@@ -2359,14 +2365,18 @@ int orl_ctx_query(orl_ctx* c, uint32_t what, uint64_t* v) {
             *v = w;
             return ORL_OK;
         }
-        case ORL_Q_PART_ERROR: {  // the look-back state's error word (lb_state[1]), read and cleared
+        case ORL_Q_PART_ERROR: {  // the look-back state sets' error words (state[1]), read and cleared
             if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
             ORL_HIP(c, hipSetDevice(c->cfg.device));
             ORL_HIP(c, hipDeviceSynchronize());
-            uint32_t w = 0;
-            ORL_HIP(c, hipMemcpy(&w, c->s.lb_state + 1, 4, hipMemcpyDeviceToHost));
-            if (w) ORL_HIP(c, hipMemset(c->s.lb_state + 1, 0, 4));
-            *v = w ? 1u : 0u;
+            uint32_t any = 0;
+            for (auto& L : c->s.lb) {
+                uint32_t w = 0;
+                ORL_HIP(c, hipMemcpy(&w, L.state + 1, 4, hipMemcpyDeviceToHost));
+                if (w) ORL_HIP(c, hipMemset(L.state + 1, 0, 4));
+                any |= w;
+            }
+            *v = any ? 1u : 0u;
             return ORL_OK;
         }
         case ORL_Q_STAGE4_ERROR: {  // stage 4's look-back error word (s4_err), read and cleared

@@ -270,9 +270,20 @@ struct Scratch {
     uint32_t* bstart;       // [4097] bucket starts (two-level path; k_seg_plan handles up to 4096)
     uint32_t* sstart;       // [4098] first segment of each bucket; [4097] = a bucket has > 64 segments (skew flag)
     uint32_t* gap_q;        // [kGapQueueWords] LSD offsets: long-gap queue (zeroed once; k_offsets_long empties it)
-    uint32_t* lb_state;     // one-pass exchange partition: ticket, error, 8 granules per 2048-message tile (zeroed once)
-    uint32_t lb_ticket = 0; // host mirror of lb_state's ticket counter after the launches so far (tile = ticket - base)
-    uint32_t lb_epoch = 0;  // launches so far: the granules of launch k carry epoch k (earlier ones read as unpublished)
+    // one-pass exchange partition's look-back state, one set per stream that partitions (round 6: the node partitions
+    // alternate chunks on two streams, so one chunk's tail overlaps the next chunk's start); a set taken over by another
+    // stream is first waited for (its event), so launches that share a set never overlap
+    struct LbSet {
+        uint32_t* state = nullptr;  // ticket, error, 8 granules per 2048-message tile (zeroed once)
+        uint32_t ticket = 0;        // host mirror of the ticket counter after the launches so far (tile = ticket - base)
+        uint32_t epoch = 0;         // launches so far: the granules of launch k carry epoch k (earlier ones read as unpublished)
+        hipStream_t stream = nullptr;
+        hipEvent_t ev = nullptr;    // recorded after each launch on the set
+        uint64_t last = 0;          // lb_clock at the last use (least recently used set is taken over)
+    };
+    static constexpr int kLbSets = 2;
+    LbSet lb[kLbSets];
+    uint64_t lb_clock = 0;
     uint64_t max_batch;
     uint64_t max_tiles;
     int device = -1;        // the context's HIP device: picks the ranking variant of its stage-4 launches (host_rm)

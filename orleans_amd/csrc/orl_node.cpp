@@ -118,6 +118,8 @@ struct orl_node {
     ncclComm_t comm_h = nullptr;  // the counts all-gathers' communicator (ncclCommSplit of comm), on stream sh (round 4)
     std::shared_ptr<LocalGroup> group;
     hipStream_t sp = nullptr, sx = nullptr, sr = nullptr;
+    hipStream_t sp1 = nullptr;  // hop-1 partitions alternate sp (even chunks) and sp1 (odd; round 6): a chunk's kernel tail
+                                // overlaps the next chunk's start (each stream has its own look-back state in the context)
     hipStream_t sh = nullptr;  // the counts all-gathers: chunk c's runs while chunk c-1's data exchange is still on sx
     hipEvent_t ev_in = nullptr, ev_x = nullptr, ev_r = nullptr;
     hipEvent_t ev_h = nullptr;  // the hop-2 host-rank counts are written (on sh)
@@ -398,7 +400,7 @@ void free_node(orl_node* nd) {
     (void)hipFree(nd->d_recv_ext);
     for (hipEvent_t e : {nd->ev_in, nd->ev_part[0], nd->ev_part[1], nd->ev_x, nd->ev_r, nd->ev_h, nd->ev_slot[0], nd->ev_slot[1], nd->ev_s4})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : {nd->sp, nd->sx, nd->sr, nd->sh})
+    for (hipStream_t s : {nd->sp, nd->sp1, nd->sx, nd->sr, nd->sh})
         if (s) (void)hipStreamDestroy(s);
     if (nd->comm_h) (void)ncclCommDestroy(nd->comm_h);
     nd->comm_h = nullptr;
@@ -593,6 +595,7 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
     hipError_t e = hipSuccess;
     auto ok = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; return x == hipSuccess; };
     ok(hipStreamCreateWithFlags(&nd->sp, hipStreamNonBlocking));
+    ok(hipStreamCreateWithFlags(&nd->sp1, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sx, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sr, hipStreamNonBlocking));
     ok(hipStreamCreateWithFlags(&nd->sh, hipStreamNonBlocking));
@@ -726,6 +729,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
     NODE_HIP(nd, hipSetDevice(nd->device));
     NODE_HIP(nd, hipEventRecord(nd->ev_in, caller));  // the caller's batch is ready
     NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_in, 0));
+    NODE_HIP(nd, hipStreamWaitEvent(nd->sp1, nd->ev_in, 0));
+    auto pstream = [&](uint32_t slot) { return slot ? nd->sp1 : nd->sp; };  // chunk c's partition stream (slot c & 1)
     nd->segs.clear();
     const uint64_t cs = (n + K - 1) / K;
     uint64_t owned = 0;                       // messages received so far (this rank)
@@ -782,7 +787,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         uint64_t* head = nd->d_head + slot * kHeadWords;
         uint8_t* send = nd->d_send[slot];
         uint32_t* status = reinterpret_cast<uint32_t*>(head + 8);
-        NODE_HIP(nd, hipStreamWaitEvent(nd->sp, nd->ev_slot[slot], 0));  // the slot's previous exchange has finished
+        hipStream_t ps = pstream(slot);
+        NODE_HIP(nd, hipStreamWaitEvent(ps, nd->ev_slot[slot], 0));  // the slot's previous exchange has finished
         // head words: [0, nr) counts and [8] status are written by the partition call itself (the counts by its last tile,
         // or zeroed for an empty chunk); [9] (form | digest) is uploaded only when it changes, so a chunk costs the
         // partition kernel and its status reset (two head writes per chunk fewer: ~10 us of small stream ops each)
@@ -790,20 +796,20 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         if (!nd->form_valid[slot] || nd->form_word[slot] != fw) {
             // the slot's previous head copy was consumed before its all-gather returned, so the pinned word is free
             nd->h_form[slot] = fw;
-            NODE_HIP(nd, hipMemcpyAsync(head + 9, nd->h_form + slot, 8, hipMemcpyHostToDevice, nd->sp));
+            NODE_HIP(nd, hipMemcpyAsync(head + 9, nd->h_form + slot, 8, hipMemcpyHostToDevice, ps));
             nd->form_word[slot] = fw;
             nd->form_valid[slot] = true;
         }
         KxLanes kxl{};
         if (kx && form == 32) {  // head words [10, 14): the string bytes to each destination (u32 each), the append cursors
-            NODE_HIP(nd, hipMemsetAsync(head + 10, 0, 4 * 8, nd->sp));
+            NODE_HIP(nd, hipMemsetAsync(head + 10, 0, 4 * 8, ps));
             kxl = KxLanes{nd->kx_ext + start, nd->kx_blob, nd->kx_bytes, nd->d_send_ext[slot], nd->d_send_blob[slot],
                           nd->send_blob_cap, reinterpret_cast<uint32_t*>(head + 10)};
         }
         NODE_CTX(nd, ctx_partition_padded(nd->ctx, d_in + start, len, opts, nd->cfg.rank_of_silo, nr, me, nd->chunk_cap, send,
-                                          (int)form, head, status, nd->sp, cached ? nd->d_send_act[slot] : nullptr,
+                                          (int)form, head, status, ps, cached ? nd->d_send_act[slot] : nullptr,
                                           kxl.ext ? &kxl : nullptr));
-        NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+        NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], ps));
         return ORL_OK;
     };
     if (K > 0)
@@ -831,14 +837,14 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         }
         if (pr) return nfail(nd, pr, "chunk %u: node plan failed", c);
         const uint32_t width = plan.width;
-        // The rewrite runs on sp behind chunk c + 1's partition and the host waits for both (not just the
-        // rewrite): the partitions share the context's look-back state (ticket counter, epoch-tagged granules), which
-        // only stream order keeps consistent, so the rewrite cannot overtake the partition queued before it.
+        // The rewrite runs on chunk c's own partition stream, behind chunk c's first partition: the look-back state
+        // (ticket counter, epoch-tagged granules) is per stream in the context, and stream order keeps each set
+        // consistent; chunk c + 1's partition, on the other stream, has a set of its own (ADVICE r3's ordering concern).
         if (plan.rewrite) {  // some rank's records do not fit the form: every rank rewrites the chunk in `width`
             if (int r = partition(c, width)) return r;
             // the rewrite's look-back is checked on this rank only (its counts are those already all-gathered)
             uint32_t st = 0;
-            if (int r = wait_bounded(nd, nd->sp, "re-partition", (int)c, nullptr)) return r;
+            if (int r = wait_bounded(nd, pstream(slot), "re-partition", (int)c, nullptr)) return r;
             NODE_HIP(nd, hipMemcpy(&st, head + 8, 4, hipMemcpyDeviceToHost));
             if (nd->lb_fail == 2) st |= ORL_PART_LOOKBACK_FAILED;
             if (st & ORL_PART_LOOKBACK_FAILED) {  // only this rank sees it: abort, so the peers fail now, not at their deadline
@@ -866,8 +872,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             if (!cached)  // this rank wrote no act lane: ORL_NO_ACT over what it sends
                 for (uint32_t r = 0; r < nr; ++r)
                     if (plan.send[r])
-                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_act[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 4, nd->sp));
-            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_act[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 4, pstream(slot)));
+            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], pstream(slot)));
             lanes.push_back(Lane{reinterpret_cast<uint8_t*>(nd->d_send_act[slot]), nd->chunk_cap * 4,
                                  reinterpret_cast<uint8_t*>(nd->d_recv_act + owned), 4});
         }
@@ -898,8 +904,8 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
             if (!kx)  // this rank wrote no ext lane: {~0, ~0} (no string) over what it sends
                 for (uint32_t r = 0; r < nr; ++r)
                     if (plan.send[r])
-                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_ext[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 8, nd->sp));
-            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], nd->sp));
+                        NODE_HIP(nd, hipMemsetAsync(nd->d_send_ext[slot] + (size_t)r * nd->chunk_cap, 0xFF, plan.send[r] * 8, pstream(slot)));
+            NODE_HIP(nd, hipEventRecord(nd->ev_part[slot], pstream(slot)));
             lanes.push_back(Lane{reinterpret_cast<uint8_t*>(nd->d_send_ext[slot]), nd->chunk_cap * 8,
                                  reinterpret_cast<uint8_t*>(nd->d_recv_ext + owned), 8});
         }

@@ -714,8 +714,11 @@ __device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __rest
 
 // CIN: the records come with the node exchange's act lane `in_act` (sender_cached); a template flag, since even a uniform
 // null test of the pointer cost config 2's k_route 35 us (1.277 -> 1.312 ms).
+#ifndef ORL_ROUTE_ATTR  // lab builds only: register-budget attributes for the A/B (make lab DEFS=...)
+#define ORL_ROUTE_ATTR
+#endif
 template <int HB, int FMT, int PW, bool CIN = false, bool LRU = false>
-__global__ __launch_bounds__(kRouteThreads) void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
+__global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
                                                          uint64_t dmask, const DirSlot* __restrict__ cache, uint64_t cmask,
                                                          const ProbeSlot* __restrict__ probe,
                                                          const uint32_t* __restrict__ probe_bad,
@@ -1173,7 +1176,9 @@ __device__ __forceinline__ uint4 ld_s4(const uint4* p) {
     return *p;
 }
 
-template <bool ACTS>
+// DIG8: the input is the previous LSD pass's digit stream (OUT_PAIR_DIG: this pass's digit of every pair, one byte each, in
+// the pairs' order) instead of the pairs: 1 B read per element instead of 8 (round 6).
+template <bool ACTS, bool DIG8 = false>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     uint32_t bins, uint16_t* __restrict__ tile_cnt,
                                                     const uint32_t* __restrict__ hot_words = nullptr,
@@ -1200,6 +1205,37 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
                 else atomicAdd(&hist[(k[j] >> shift) & (bins - 1)], 1u);
             }
         if (hot_rows) wave_add_hot(&hot, hot_mine);
+    } else if (DIG8) {
+        // 16 consecutive elements per thread (one 16-B load): sorted by the previous digit, so equal digits come in runs,
+        // each added with one atomic (a hot key's run as well)
+        const uint8_t* dg = static_cast<const uint8_t*>(in);
+        const uint32_t e0 = base + threadIdx.x * 16u;
+        if (e0 < n) {
+            uint32_t v[4];
+            if (e0 + 16u <= n) {
+                const uint4 q = ld_s4(reinterpret_cast<const uint4*>(dg + e0));
+                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+            } else {
+                for (uint32_t i = 0; i < 4; ++i) v[i] = 0;
+                for (uint32_t i = 0; e0 + i < n; ++i) v[i >> 2] |= (uint32_t)dg[e0 + i] << (8u * (i & 3u));
+            }
+            const uint32_t m = min(16u, n - e0);
+            uint32_t cur = v[0] & 0xFFu, len = 1;
+#pragma unroll
+            for (uint32_t i = 1; i < 16; ++i) {
+                if (i < m) {
+                    const uint32_t b = (v[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+                    if (b == cur) {
+                        ++len;
+                    } else {
+                        atomicAdd(&hist[cur], len);
+                        cur = b;
+                        len = 1;
+                    }
+                }
+            }
+            atomicAdd(&hist[cur], len);
+        }
     } else {
         // pairs of an LSD pass: sorted by the previous digit, so a hot key's pairs sit in consecutive lanes.  Loads stay
         // coalesced (element j * 256 + x); each run of equal digits inside a 64-lane step adds its length with one
@@ -1404,7 +1440,10 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
 //      the key's low `shift` bits — the level-2 digit, all that level 2 reads of the key — as u8 / u16 to `keys`.
 // Tiles are taken in XCD-aware order (xcd_tile) so consecutive tiles' runs of one bin meet in one L2.
 enum : int { IN_ACT = 0, IN_PAIR = 1, IN_SOA8 = 2, IN_SOA16 = 3 };
-enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_PAIR_SMALL = 5, OUT_FINAL_GAPS = 6 };
+enum : int { OUT_PAIR = 0, OUT_FINAL = 1, OUT_SOA8 = 2, OUT_SOA16 = 3, OUT_LSD_PAIR = 4, OUT_PAIR_SMALL = 5, OUT_FINAL_GAPS = 6,
+              OUT_PAIR_DIG = 7 };
+// PAIR_DIG (an LSD pass followed by one of <= 8 bits, round 6): the pairs, plus the next pass's digit of each as one byte to
+// key_out (dsel = next shift | next bits << 8), so that pass's histogram (k_hist_pairs<false, true>) reads 1 B per element.
 // FINAL_GAPS (the LSD plan's last pass, round 6): `order` plus the bucket offsets instead of the sorted keys — see
 // k_bound_last.
 // LSD_PAIR: an LSD pass's pairs; PAIR_SMALL: the MSD pass's pairs from 2048-element tiles (kMsdItemsSmall, small batches)
@@ -1550,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
                                                     uint32_t* __restrict__ key_out, const uint32_t* __restrict__ hot_words,
                                                     const uint32_t* __restrict__ hot_rows, uint32_t* __restrict__ hot_idx,
                                                     uint32_t* __restrict__ offsets, uint32_t nb, uint32_t* __restrict__ gap_q,
-                                                    uint32_t gap_cap) {
+                                                    uint32_t gap_cap, uint32_t dsel) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
@@ -1682,6 +1721,9 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
             if (g >= n) continue;  // unreachable with consistent histograms; keeps a corrupt input from writing out of bounds
             if (OUT == OUT_PAIR) {
                 pair_out[g] = kv;
+            } else if (OUT == OUT_PAIR_DIG) {
+                pair_out[g] = kv;
+                reinterpret_cast<uint8_t*>(key_out)[g] = (uint8_t)((k >> (dsel & 31u)) & ((1u << (dsel >> 8)) - 1u));
             } else if (OUT == OUT_SOA8) {
                 order_out[g] = kv.y;
                 reinterpret_cast<uint8_t*>(key_out)[g] = (uint8_t)(k & ((1u << shift) - 1u));
@@ -4892,11 +4934,11 @@ template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                       const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx, uint32_t* offsets, uint32_t nb,
-                      uint32_t* gap_q, uint32_t gap_cap) {
+                      uint32_t* gap_q, uint32_t gap_cap, uint32_t dsel) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
                                                 row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx, offsets, nb,   \
-                                                gap_q, gap_cap)
+                                                gap_q, gap_cap, dsel)
 #define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
@@ -4906,10 +4948,13 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
             case OUT_SOA8: ORL_RP(IN_ACT, OUT_SOA8, kMsdItems); break;
             case OUT_SOA16: ORL_RP(IN_ACT, OUT_SOA16, kMsdItems); break;
             case OUT_LSD_PAIR: ORL_RP(IN_ACT, OUT_PAIR, kItems); break;
+            case OUT_PAIR_DIG: ORL_RP(IN_ACT, OUT_PAIR_DIG, kItems); break;
             default: ORL_RP(IN_ACT, OUT_FINAL, kItems); break;
         }
     } else if (out == OUT_PAIR || out == OUT_LSD_PAIR) {
         ORL_RP(IN_PAIR, OUT_PAIR, kItems);
+    } else if (out == OUT_PAIR_DIG) {
+        ORL_RP(IN_PAIR, OUT_PAIR_DIG, kItems);
     } else if (out == OUT_FINAL_GAPS) {
         ORL_RP(IN_PAIR, OUT_FINAL_GAPS, kItems);
     } else {
@@ -4922,10 +4967,11 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
 void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                  const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr,
-                 uint32_t* offsets = nullptr, uint32_t nb = 0, uint32_t* gap_q = nullptr, uint32_t gap_cap = 0) {
+                 uint32_t* offsets = nullptr, uint32_t nb = 0, uint32_t* gap_q = nullptr, uint32_t gap_cap = 0,
+                 uint32_t dsel = 0) {
     switch (bits) {
 #define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
-                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap); break;
+                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap, dsel); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -5160,6 +5206,16 @@ bool offsets_sufmin() {
 }
 
 
+// LSD passes hand the next pass its digit as a byte stream (OUT_PAIR_DIG) when it has <= 8 bits; ORL_LSD_DIGITS=0: the next
+// histogram reads the pairs (A/B).
+bool lsd_digits() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_LSD_DIGITS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair
 // layout; ORL_NO_HOT=1 turns it off (A/B).
 bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
@@ -5226,20 +5282,30 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     // the last pass writes the bucket offsets itself (round 6) when its keys' low part fits the 16-bit halves of FL
     const bool gaps = lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
+    // the digit stream (OUT_PAIR_DIG) lives in sorted_keys (>= n bytes), read by the next histogram before the last pass
+    // writes sorted_keys / the FL rows there
+    uint8_t* dig = reinterpret_cast<uint8_t*>(s.sorted_keys);
+    bool have_dig = false;
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
         const uint32_t row_step = (p == 0) ? row_step0 : 1u;
         const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
-        if (p > 0)
+        if (p > 0 && have_dig)
+            hipLaunchKernelGGL((k_hist_pairs<false, true>), dim3(ntiles), dim3(256), 0, st, dig, n, n_act, 0u, bins, s.tile_cnt,
+                               nullptr, nullptr);
+        else if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
-                               (uint32_t)plan.shift[p], bins, s.tile_cnt);
+                               (uint32_t)plan.shift[p], bins, s.tile_cnt, nullptr, nullptr);
         col_scan(s.tile_hist, nrows, bins, row_step, s, st, nullptr, 0, 0, p == 0 && self_cols);
         const bool last = p == plan.passes - 1;
+        const bool wdig = !last && lsd_digits() && plan.bits[p + 1] <= 8;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
-        const int out = !last ? OUT_LSD_PAIR : gaps ? OUT_FINAL_GAPS : OUT_FINAL;
+        const int out = !last ? (wdig ? OUT_PAIR_DIG : OUT_LSD_PAIR) : gaps ? OUT_FINAL_GAPS : OUT_FINAL;
+        const uint32_t dsel = wdig ? (uint32_t)plan.shift[p + 1] | ((uint32_t)plan.bits[p + 1] << 8) : 0u;
         launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, out, kin, n, n_act, (uint32_t)plan.shift[p],
-                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, s.sorted_keys, st, nullptr, nullptr, nullptr, d_offsets,
-                    nb, s.gap_q, s.gap_cap);
+                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, wdig ? reinterpret_cast<uint32_t*>(dig) : s.sorted_keys,
+                    st, nullptr, nullptr, nullptr, d_offsets, nb, s.gap_q, s.gap_cap, dsel);
+        have_dig = wdig;
     }
     if (gaps) {  // the buckets the last pass could not see from inside a tile (k_bound_last), then the digits' tails
         const int lp = plan.passes - 1;
@@ -5768,21 +5834,34 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
     if (e != hipSuccess || n == 0) return (int)e;
     const uint32_t excl = (opts & ORL_OPT_EXCLUDE_IF_STOPPING) ? 1u : 0u;
     const uint32_t ntiles = ceil_div(n, kPartTile);
-    // look-back state: the ticket counter and the granules are not reset per launch (ticket base + epoch tag instead);
-    // it is zeroed again only when the 30-bit epoch wraps
-    if (++s.lb_epoch >= (1u << 30)) {
-        if ((e = hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ceil_div(s.max_batch, kPartTile) * 64, st)) != hipSuccess) return (int)e;
-        s.lb_ticket = 0;
-        s.lb_epoch = 1;
+    // look-back state: this stream's set (Scratch::LbSet; the least recently used one taken over, after its last launch)
+    Scratch::LbSet* L = nullptr;
+    for (auto& x : s.lb)
+        if (x.stream == st) L = &x;
+    if (!L) {
+        L = &s.lb[0];
+        for (auto& x : s.lb)
+            if (x.last < L->last) L = &x;
+        if (L->last && (e = hipStreamWaitEvent(st, L->ev, 0)) != hipSuccess) return (int)e;
+        L->stream = st;
     }
-    const uint32_t tbase = s.lb_ticket, epoch = s.lb_epoch;
+    L->last = ++s.lb_clock;
+    // the ticket counter and the granules are not reset per launch (ticket base + epoch tag instead); the set is zeroed
+    // again only when the 30-bit epoch wraps
+    const size_t lb_bytes = 16 + (size_t)ceil_div(s.max_batch, kPartTile) * 64;
+    if (++L->epoch >= (1u << 30)) {
+        if ((e = hipMemsetAsync(L->state, 0, lb_bytes, st)) != hipSuccess) return (int)e;
+        L->ticket = 0;
+        L->epoch = 1;
+    }
+    const uint32_t tbase = L->ticket, epoch = L->epoch;
     const bool cached = d_cache && d_act_out && d_wire_status;
     const bool kxon = kxl && kxl->ext && d_wire_status;
     if (kxon && fmt != 32) return (int)hipErrorInvalidValue;
     KxArgs kx{};
     if (kxon) kx = KxArgs{kxl->ext, kxl->blob, kxl->blob_bytes, kxl->ext_out, kxl->blob_out, kxl->blob_cap, kxl->cur};
 #define ORL_PLB3(F, C, X) hipLaunchKernelGGL((k_part_lb<F, C, X>), dim3(ntiles), dim3(kRouteThreads), 0, st, d_params, d_rank_of_silo,\
-                                             d_in, (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, s.lb_state,     \
+                                             d_in, (uint32_t)n, excl, my_rank, nranks, stride, d_out, d_src_index, L->state,      \
                                              ntiles, d_counts, d_wire_status, tbase, epoch, d_cache, cmask, d_act_out, kx)
 #define ORL_PLB(F, C) ORL_PLB3(F, C, false)
     if (kxon) {
@@ -5801,13 +5880,14 @@ int launch_partition_padded(const RouteParams* d_params, const orl_msg_hdr* d_in
 #undef ORL_PLB3
     e = hipGetLastError();
     if (e == hipSuccess) {
-        s.lb_ticket += ntiles;
+        L->ticket += ntiles;
     } else {  // the launch did not happen: the device counter did not move either; start over from a zeroed state
-        (void)hipMemsetAsync(s.lb_state, 0, 16 + (size_t)ceil_div(s.max_batch, kPartTile) * 64, st);
-        s.lb_ticket = 0;
-        s.lb_epoch = 0;
+        (void)hipMemsetAsync(L->state, 0, lb_bytes, st);
+        L->ticket = 0;
+        L->epoch = 0;
     }
-    return (int)e;
+    const hipError_t er = hipEventRecord(L->ev, st);  // a later taker on another stream waits for this launch
+    return (int)(e != hipSuccess ? e : er);
 }
 
 }  // namespace orl

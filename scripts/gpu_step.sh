@@ -10,6 +10,7 @@
 #   PMC="g1;g2"                extra rocprofv3 --pmc passes (one per ';'-separated group) over PROF_ARGS (PMC_ARGS: extra
 #                              rocprofv3 options, e.g. --kernel-include-regex k_probe_slice)
 #   LAB="cmd"                  an extra command (e.g. python scripts/rank_cost_lab.py 8 4 8), 300 s limit
+#   LAB2="cmd" LAB2_ENV="N=v"  a second lab command with its environment
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/step}
@@ -31,8 +32,9 @@ if [ -n "$AB" ]; then
     IFS=',' read -ra VS <<< "$vals"
     for rep in 1 2; do
       for v in "${VS[@]}"; do
-        env $name=$v timeout -k 10 180 python bench.py $BENCH_ARGS > $OUT/ab_${name}_${v}_$rep.json 2> $OUT/ab_${name}_${v}_$rep.log
-        rc=$?; echo "$name=$v rep $rep: $(python3 -c "import json,sys; d=json.load(open('$OUT/ab_${name}_${v}_$rep.json')); print(d['ms_per_step'], 'ms', d.get('roofline',{}).get('frac'))" 2>/dev/null)"
+        f=$OUT/ab_${name}_${v//\//_}_$rep
+        env $name=$v timeout -k 10 180 python bench.py $BENCH_ARGS > $f.json 2> $f.log
+        rc=$?; echo "$name=$v rep $rep: $(python3 -c "import json,sys; d=json.load(open('$f.json')); print(d['ms_per_step'], 'ms', d.get('roofline',{}).get('frac'))" 2>/dev/null)"
         stop $rc
       done
     done
@@ -63,5 +65,9 @@ fi
 if [ -n "$LAB" ]; then
   timeout -k 10 300 $LAB > $OUT/lab.log 2>&1
   rc=$?; echo "lab exit $rc"; tail -15 $OUT/lab.log; stop $rc
+fi
+if [ -n "$LAB2" ]; then  # a second lab command (LAB2_ENV="NAME=value": its environment)
+  env ${LAB2_ENV:-_LAB2=1} timeout -k 10 300 $LAB2 > $OUT/lab2.log 2>&1
+  rc=$?; echo "lab2 exit $rc"; tail -15 $OUT/lab2.log; stop $rc
 fi
 echo "=== done"

@@ -77,6 +77,8 @@ def main(R=8, chunks=4, width=8):
     recv = [[] for _ in range(R)]
     lanes = [[] for _ in range(R)]
     part_ms = []
+    two = not os.environ.get("LAB_ONE_STREAM") and chunks > 1
+    st2 = torch.cuda.Stream()
     for s in range(R):
         m = W.device_messages(torch, cl, n_grains, n_msgs, W.SEED_C3, start=s * n_msgs,
                               sender_silos=local_silos(cl.n_silos, R, s), zipf=ztab)
@@ -91,15 +93,20 @@ def main(R=8, chunks=4, width=8):
             part.cache_add_or_update_device(kd, torch.from_numpy(hnd[g].view(np.int32)).cuda(),
                                             torch.from_numpy(owner[g].astype(np.uint8)).cuda(), len(g), stream=st)
 
-            def part_one(mm, k):
-                part.partition_cached_device(mm, k, ros, R, s, cap, d_out, width, d_lane, d_counts, d_status, stream=st)
+            def part_one(mm, k, stream=st):
+                part.partition_cached_device(mm, k, ros, R, s, cap, d_out, width, d_lane, d_counts, d_status, stream=stream)
         else:
-            def part_one(mm, k):
-                partition(mm, k, ros, R, s, cap, d_out, d_counts, d_status, stream=st)
+            def part_one(mm, k, stream=st):
+                partition(mm, k, ros, R, s, cap, d_out, d_counts, d_status, stream=stream)
 
         def hop1():
+            # as the node issues them: odd chunks on a second stream (round 6; LAB_ONE_STREAM=1: all on one stream)
+            if two:
+                st2.wait_stream(torch.cuda.current_stream())
             for c in range(chunks):
-                part_one(m[c * step:], step)
+                part_one(m[c * step:], step, stream=st2.cuda_stream if (two and c & 1) else st)
+            if two:
+                torch.cuda.current_stream().wait_stream(st2)
         part_ms.append(timed(hop1))
         part_one(m, n_msgs)
         cnt = d_counts.cpu().numpy()
