@@ -724,9 +724,13 @@ def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf, reg_frac=1.0):
 
     probe = host(min(n_all, 1 << 21))
     t_probe = timed(probe, share)
-    n_mt = int(min(n_all, max(len(probe), len(probe) * target_wall / max(t_probe, 1e-6))))
+    # three timed repetitions of a third of the wall budget each: the value is their median, with the spread beside it
+    # (one sample of a shared host's cores varied 2x between boxes)
+    n_mt = int(min(n_all, max(len(probe), len(probe) * target_wall / 3 / max(t_probe, 1e-6))))
     sample = host(n_mt)
-    runs = {"share": {"threads": share, "messages": n_mt, "seconds": timed(sample, share)}}
+    reps = sorted(timed(sample, share) for _ in range(3))
+    runs = {"share": {"threads": share, "messages": n_mt, "seconds": reps[1],
+                      "spread_msgs_per_s": [n_mt / reps[2], n_mt / reps[0]]}}
     # every listed CPU (the parallel stage 4 keeps 2^12 + 2^(bits-12) counters per thread: no memory bound)
     n_cpu_threads = ncpu
     if n_cpu_threads > share:
@@ -742,8 +746,10 @@ def cpu_baseline(cl, n_grains, d_msgs, target_wall, zipf, reg_frac=1.0):
             "threads_share": runs["share"], "threads_all": runs.get("all_cpus"), "threads_1": runs["one"],
             "cpu_model": model, "os_cpu_count": ncpu, "sched_affinity": navail,
             "box_thread_share_env": os.environ.get("OMP_NUM_THREADS"),
+            "spread": runs["share"]["spread_msgs_per_s"],
             "sample": f"first {n_mt} of the {n_all} messages of this workload"
-                      f"{' (the whole batch)' if n_mt == n_all else ''} on {share} threads (the box's CPU share) and on "
+                      f"{' (the whole batch)' if n_mt == n_all else ''}, the median of 3 timed runs on {share} threads (the "
+                      f"box's CPU share; min / max in `spread`) and on "
                       f"{runs.get('all_cpus', runs['share'])['threads']} threads, the first {n_1} on 1 thread; same "
                       f"directory, stages 1-4, oracle/cpu_ref.cpp ref_route_bucket_mt"}
 

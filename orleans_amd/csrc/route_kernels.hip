@@ -712,10 +712,36 @@ __device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __rest
     return load_hdr(static_cast<const orl_msg_hdr*>(in), e);
 }
 
+// Header prefetch (FMT 32, round 6): each wave stages its next message's 32-B header in LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPRs: k_route sits at 8 waves per SIMD) while the current message probes, and the route /
+// act stores of a message are issued one step late, right after the step's wait, so the wait never covers a store issued
+// just before it.  Per step the chain is then max(header, probe) instead of header + probe.  ORL_ROUTE_PF=0: off (A/B).
+#ifndef ORL_ROUTE_PF
+#define ORL_ROUTE_PF 1
+#endif
+__device__ __forceinline__ void pf_header(const orl_msg_hdr* __restrict__ in, uint32_t e, u32x4* region) {
+    const u32x4* g = reinterpret_cast<const u32x4*>(in + e);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)region, 16, 0, 2);         // nt
+    __builtin_amdgcn_global_load_lds(g + 1, (__attribute__((address_space(3))) void*)(region + 64), 16, 0, 2);
+}
+
 // CIN: the records come with the node exchange's act lane `in_act` (sender_cached); a template flag, since even a uniform
 // null test of the pointer cost config 2's k_route 35 us (1.277 -> 1.312 ms).
-#ifndef ORL_ROUTE_ATTR  // lab builds only: register-budget attributes for the A/B (make lab DEFS=...)
-#define ORL_ROUTE_ATTR
+// Scalar-register budget (round 6).  The hardware admits floor(800 / (SGPRs rounded up to 16, + 16)) waves per SIMD, which
+// the compiler's own occupancy figure does not count: k_route at 94 SGPRs ran 7 workgroups of 256 per CU, capped at 80
+// (the compiler keeps 78, no spills) it runs 8, and config 3's step went 7.58 -> 7.35 ms (profiles/r06h_lsd_digits_sgpr80_ab.txt).
+#define ORL_SGPR80 __attribute__((amdgpu_num_sgpr(80)))
+#ifndef ORL_ROUTE_ATTR
+#define ORL_ROUTE_ATTR ORL_SGPR80
+#endif
+// k_fanout_route: 106 SGPRs held it at 6 workgroups per CU under its 22 KB of LDS (7); capped at 96 it runs 7: config 4's
+// step 0.445 -> 0.438 ms (profiles/r06i_fanout_sgpr96_ab.txt).  k_part_lb is VGPR-bound (90: 5 per CU) and gained nothing
+// from 6 or 8 per CU (forced by launch bounds: scratch spills) or 4 header groups (82 VGPRs, still 5): r06i.
+#ifndef ORL_FAN_ATTR
+#define ORL_FAN_ATTR __attribute__((amdgpu_num_sgpr(96)))
+#endif
+#ifndef ORL_PART_ATTR
+#define ORL_PART_ATTR
 #endif
 template <int HB, int FMT, int PW, bool CIN = false, bool LRU = false>
 __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir,
@@ -730,6 +756,12 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                                                          const uint32_t* __restrict__ in_act) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
+    constexpr bool PF = FMT == 32 && ORL_ROUTE_PF;
+    __shared__ u32x4 pre[PF ? 2 * kRouteThreads : 1];  // per wave: 64 first halves, then 64 second halves (lane-linear)
+    u32x4* const pregion = pre + (PF ? (threadIdx.x >> 6) * 128u : 0u);
+    const uint32_t plane = threadIdx.x & 63u;
+    uint32_t pend_e = 0, pend_rr = 0, pend_act = 0;  // PF: the previous step's stores, issued after this step's wait
+    bool pend = false;
     stage_params(&sm.P, gp);
     if (HIST)
         for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sm.hist[b] = 0;
@@ -740,10 +772,31 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
     uint32_t hot_mine = 0;
     const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
+    if (PF) pf_header(static_cast<const orl_msg_hdr*>(in), base < n ? base : n - 1u, pregion);
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
         Msg m;
-        if (e < n) m = load_msg<FMT>(sm.P, in, e);
+        if (PF) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's header has landed
+            if (pend) {
+                store_drop(route + pend_e, pend_rr);
+                store_drop(act_out + pend_e, pend_act);
+                pend = false;
+            }
+            const u32x4 a = pregion[plane], b = pregion[64u + plane];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next header overwrites the slots
+            if (j + 1u < items) {
+                const uint32_t en = e + kRouteThreads;
+                pf_header(static_cast<const orl_msg_hdr*>(in), en < n ? en : n - 1u, pregion);
+            }
+            m.tcd = (uint64_t)a.x | ((uint64_t)a.y << 32);
+            m.n0 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+            m.n1 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+            m.meta = b.z;
+            m.aux = b.w;
+        } else if (e < n) {
+            m = load_msg<FMT>(sm.P, in, e);
+        }
         uint32_t h = 0, own = 0, rf = 0, r = 0;
         uint64_t slot = 0, mask = dmask;
         u32x4 sa, sb;
@@ -778,8 +831,12 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                 } else if (rr == kNeedProbeCache) {
                     rr = route_msg<LRU>(sm.P, dir, dmask, cache, cmask, m, excl != 0, act, e);
                 }
-                store_drop(route + e, rr);
-                store_drop(act_out + e, act);
+                if (PF) {
+                    pend_e = e, pend_rr = rr, pend_act = act, pend = true;
+                } else {
+                    store_drop(route + e, rr);
+                    store_drop(act_out + e, act);
+                }
                 if (HIST) {
                     const uint32_t k = bucket_key(act, n_act);
                     if (k == hk) ++hot_mine;
@@ -818,8 +875,12 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                 } else if (rr == kNeedProbeCache) {
                     rr = route_msg<LRU>(sm.P, dir, dmask, cache, cmask, m, excl != 0, act, e);
                 }
-                store_drop(route + e, rr);
-                store_drop(act_out + e, act);
+                if (PF) {
+                    pend_e = e, pend_rr = rr, pend_act = act, pend = true;
+                } else {
+                    store_drop(route + e, rr);
+                    store_drop(act_out + e, act);
+                }
                 if (HIST) {
                     const uint32_t k = bucket_key(act, n_act);
                     if (k == hk) ++hot_mine;
@@ -859,14 +920,22 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                 rr = route_tail(sm.P, m, h, own, rf, st == 0, fact, fsilo, act, vc);
                 if (CIN && !vc) rr = cached_verdict(sm.P, m, h, own, rf, rr, act, vact, st == 0, fact, fsilo);
             }
-            store_drop(route + e, rr);
-            store_drop(act_out + e, act);
+            if (PF) {
+                pend_e = e, pend_rr = rr, pend_act = act, pend = true;
+            } else {
+                store_drop(route + e, rr);
+                store_drop(act_out + e, act);
+            }
             if (HIST) {
                 const uint32_t k = bucket_key(act, n_act);
                 if (k == hk) ++hot_mine;
                 else atomicAdd(&sm.hist[(k >> shift) & (bins - 1)], 1u);
             }
         }
+    }
+    if (PF && pend) {
+        store_drop(route + pend_e, pend_rr);
+        store_drop(act_out + pend_e, pend_act);
     }
     if (HIST) {
         if (hot_rows) wave_add_hot(&sm.hot, hot_mine);
@@ -3268,7 +3337,7 @@ constexpr uint32_t kNoAct4 = 0xFDFDFDFDu, kFanSlow = 0xFCFCFCFCu;
 constexpr int kFanIlp = 1;  // default messages per thread and step
 
 template <int HB, int PW, int U>
-__global__ __launch_bounds__(kRouteThreads) void k_fanout_route(
+__global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
     const RouteParams* __restrict__ gp, const DirSlot* __restrict__ dir, uint64_t mask, const DirSlot* __restrict__ cache,
     uint64_t cmask, const ProbeSlot* __restrict__ probe, const uint32_t* __restrict__ probe_bad,
     const uint64_t* __restrict__ pstart, const uint32_t* __restrict__ csr_tgt,
@@ -3798,7 +3867,7 @@ struct KxArgs {
 __device__ uint32_t keyext_hash_dev(uint64_t n0, uint64_t n1, uint64_t tcd, const uint8_t* __restrict__ s, uint32_t len);
 
 template <int FMT, bool CACHE, bool KX = false>
-__global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
+__global__ __launch_bounds__(kRouteThreads, FMT == 8 ? ORL_PART_MINWG : 1) ORL_PART_ATTR void k_part_lb(const RouteParams* __restrict__ gp, const uint8_t* __restrict__ ros,
                                                            const orl_msg_hdr* __restrict__ in, uint32_t n, uint32_t excl,
                                                            uint32_t my_rank, uint32_t nranks, uint64_t stride,
                                                            void* __restrict__ out, uint32_t* __restrict__ src_index,

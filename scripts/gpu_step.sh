@@ -10,6 +10,7 @@
 #   PMC="g1;g2"                extra rocprofv3 --pmc passes (one per ';'-separated group) over PROF_ARGS (PMC_ARGS: extra
 #                              rocprofv3 options, e.g. --kernel-include-regex k_probe_slice)
 #   LAB="cmd"                  an extra command (e.g. python scripts/rank_cost_lab.py 8 4 8), 300 s limit
+#   LAB_ENVS="A=1;A=2"         run LAB once per environment (lab_<i>.log)
 #   LAB2="cmd" LAB2_ENV="N=v"  a second lab command with its environment
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -62,7 +63,15 @@ if [ -n "$PMC" ]; then
   done
   python3 scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt 2>&1; head -40 $OUT/pmc_summary.txt
 fi
-if [ -n "$LAB" ]; then
+if [ -n "$LAB" ] && [ -n "$LAB_ENVS" ]; then  # LAB once per ';'-separated environment (e.g. "LAB_LIB=a.so;LAB_LIB=b.so")
+  IFS=';' read -ra LES <<< "$LAB_ENVS"
+  i=0
+  for le in "${LES[@]}"; do
+    i=$((i+1))
+    env ${le:-_LAB=1} timeout -k 10 300 $LAB > $OUT/lab_$i.log 2>&1
+    rc=$?; echo "lab $i ($le) exit $rc"; grep -v amdgpu.ids $OUT/lab_$i.log | tail -6; stop $rc
+  done
+elif [ -n "$LAB" ]; then
   timeout -k 10 300 $LAB > $OUT/lab.log 2>&1
   rc=$?; echo "lab exit $rc"; tail -15 $OUT/lab.log; stop $rc
 fi

@@ -7,8 +7,14 @@ import sys
 src = sys.argv[1] if len(sys.argv) > 1 else "orleans_amd/csrc/route_kernels.hip"
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 import os
-r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", "-o", "/tmp/_kr.o", src,
-                    "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("DEFS", "").split(), capture_output=True, text=True)
+if src.endswith(".log"):  # the remarks of a build already made (make lab DEFS="... -Rpass-analysis=kernel-resource-usage")
+    class _R:
+        stderr = open(src).read()
+    r = _R()
+else:
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", "-o", "/tmp/_kr.o", src,
+                        "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("DEFS", "").split(), capture_output=True,
+                       text=True)
 cur = None
 rows = []
 for line in r.stderr.splitlines():

@@ -197,8 +197,8 @@ def test_node_sender_cache_vs_oracle(torch, nranks, chunks, host_mix, wire, skip
             np.testing.assert_array_equal(act, ea, err_msg=f"rank {r} batch {b} act")
             np.testing.assert_array_equal(order, eo, err_msg=f"rank {r} batch {b} order")
             np.testing.assert_array_equal(off, ef, err_msg=f"rank {r} batch {b} offsets")
-            n_cached += int(((route >> 24) & L.RF_CACHED != 0).sum())
-            n_stale += int(((route >> 24) & L.RF_CACHE_STALE != 0).sum())
+            n_cached += int((((route >> 24) & L.RF_CACHED) != 0).sum())
+            n_stale += int((((route >> 24) & L.RF_CACHE_STALE) != 0).sum())
         assert n_cached > 0.15 * sum(len(x) for x in batches), n_cached  # the caches addressed a real share
         assert n_stale > 0  # stale entries (another grain's handle, another silo) re-addressed at their owner
     for nd in nodes:

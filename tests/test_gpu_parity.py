@@ -862,7 +862,7 @@ def test_directory_cache_in_route_vs_oracle(torch):
         np.testing.assert_array_equal(res.order, o_ref)
         np.testing.assert_array_equal(res.offsets, f_ref)
         assert ((res.route >> 24) & L.RF_CACHED).sum() > 1000
-        big = ((res.route >> 24) & L.RF_CACHED != 0) & (res.act >= n_act)
+        big = (((res.route >> 24) & L.RF_CACHED) != 0) & (res.act >= n_act)
         assert big.sum() > 500  # cached handles of another silo's catalog, >= this context's n_act
         assert (res.offsets[n_act + 1] - res.offsets[n_act]) >= big.sum()  # ... bucketed as unresolved here
     eng.cache_clear()
@@ -925,7 +925,7 @@ def test_directory_cache_lru_eviction_vs_oracle(torch):
         o_ref, f_ref = o.bucket(np.array(a_ref, np.uint32), n_act)
         np.testing.assert_array_equal(res.order, o_ref)
         np.testing.assert_array_equal(res.offsets, f_ref)
-        return int(((res.route >> 24) & L.RF_CACHED != 0).sum())
+        return int((((res.route >> 24) & L.RF_CACHED) != 0).sum())
 
     add(rng.choice(remote, 2500))                    # fits: the device path
     assert route(1) > 1000
