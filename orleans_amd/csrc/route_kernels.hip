@@ -70,10 +70,7 @@ struct Msg {
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
 // Headers are streamed once: non-temporal loads keep them from evicting the directory table from L2/MALL.
-__device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint32_t e) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(in + e);
-    const u32x4 a = __builtin_nontemporal_load(p);
-    const u32x4 b = __builtin_nontemporal_load(p + 1);
+__device__ __forceinline__ Msg decode_hdr(const u32x4& a, const u32x4& b) {
     Msg m;
     m.tcd = (uint64_t)a.x | ((uint64_t)a.y << 32);
     m.n0 = (uint64_t)a.z | ((uint64_t)a.w << 32);
@@ -83,9 +80,13 @@ __device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint
     return m;
 }
 
+__device__ __forceinline__ Msg load_hdr(const orl_msg_hdr* __restrict__ in, uint32_t e) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(in + e);
+    return decode_hdr(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1));
+}
+
 // Compact 16-B exchange record (orl_wire_msg, include/orleans_route.h): {n1, type code lo, meta'}.
-__device__ __forceinline__ Msg load_wire(const orl_wire_msg* __restrict__ in, uint32_t e) {
-    const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + e));
+__device__ __forceinline__ Msg decode_wire(const u32x4& a) {
     const uint32_t meta = a.w;
     Msg m;
     m.tcd = ((uint64_t)((meta >> 16) & 0xFFu) << 56) | ((uint64_t)(int64_t)(int32_t)a.z & 0x00FFFFFFFFFFFFFFull);
@@ -94,6 +95,10 @@ __device__ __forceinline__ Msg load_wire(const orl_wire_msg* __restrict__ in, ui
     m.meta = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) | (meta & 0xFF000000u);
     m.aux = 0;
     return m;
+}
+
+__device__ __forceinline__ Msg load_wire(const orl_wire_msg* __restrict__ in, uint32_t e) {
+    return decode_wire(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + e)));
 }
 
 // Encode a header as a wire record; false when it has no compact form (N0 != 0, a type-code-data that is
@@ -114,8 +119,7 @@ __device__ __forceinline__ bool encode_wire(const u32x4& h0, const u32x4& h1, u3
 
 // Narrow 8-B exchange record (orl_wire8): {n1 low 32 bits, meta with the wire type index in bits 16-19}.  The table
 // is the context's wire types (RouteParams::wire_tcd, staged in LDS with the params).
-__device__ __forceinline__ Msg load_narrow(const RouteParams& P, const orl_wire8* __restrict__ in, uint32_t e) {
-    const uint64_t a = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(in + e));
+__device__ __forceinline__ Msg decode_narrow(const RouteParams& P, uint64_t a) {
     const uint32_t meta = (uint32_t)(a >> 32);
     Msg m;
     m.tcd = P.wire_tcd[(meta >> 16) & 0xFu];
@@ -124,6 +128,10 @@ __device__ __forceinline__ Msg load_narrow(const RouteParams& P, const orl_wire8
     m.meta = (meta & 0xFFu) | (((meta >> 8) & 0x3u) << 8) | (((meta >> 10) & 0x3Fu) << 16) | (meta & 0xFF000000u);
     m.aux = 0;
     return m;
+}
+
+__device__ __forceinline__ Msg load_narrow(const RouteParams& P, const orl_wire8* __restrict__ in, uint32_t e) {
+    return decode_narrow(P, __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(in + e)));
 }
 
 // Encode a header as an 8-B record; false when it has none (N0 != 0, N1 >= 2^32, a type not in the wire table, a
@@ -712,17 +720,37 @@ __device__ __forceinline__ Msg load_msg(const RouteParams& P, const void* __rest
     return load_hdr(static_cast<const orl_msg_hdr*>(in), e);
 }
 
-// Header prefetch (FMT 32, round 6): each wave stages its next message's 32-B header in LDS by LDS-DMA
+// Record prefetch (round 6): each wave stages its next message's record (32-B header, 16- or 8-B exchange record) in LDS by LDS-DMA
 // (global_load_lds_dwordx4, no VGPRs: k_route sits at 8 waves per SIMD) while the current message probes, and the route /
 // act stores of a message are issued one step late, right after the step's wait, so the wait never covers a store issued
 // just before it.  Per step the chain is then max(header, probe) instead of header + probe.  ORL_ROUTE_PF=0: off (A/B).
 #ifndef ORL_ROUTE_PF
 #define ORL_ROUTE_PF 1
 #endif
-__device__ __forceinline__ void pf_header(const orl_msg_hdr* __restrict__ in, uint32_t e, u32x4* region) {
-    const u32x4* g = reinterpret_cast<const u32x4*>(in + e);
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)region, 16, 0, 2);         // nt
-    __builtin_amdgcn_global_load_lds(g + 1, (__attribute__((address_space(3))) void*)(region + 64), 16, 0, 2);
+// The wave's slots: FMT 32 two 1-KB halves (16 B per lane each), FMT 16 one, FMT 8 two 256-B halves (4 B per lane: the
+// LDS-DMA widths are 1, 2, 4, 12 and 16 B).
+template <int FMT>
+__device__ __forceinline__ void pf_record(const void* __restrict__ in, uint32_t e, u32x4* region) {
+    using lds_t = __attribute__((address_space(3))) void*;
+    if (FMT == 32) {
+        const u32x4* g = reinterpret_cast<const u32x4*>(static_cast<const orl_msg_hdr*>(in) + e);
+        __builtin_amdgcn_global_load_lds(g, (lds_t)region, 16, 0, 2);  // nt
+        __builtin_amdgcn_global_load_lds(g + 1, (lds_t)(region + 64), 16, 0, 2);
+    } else if (FMT == 16) {
+        __builtin_amdgcn_global_load_lds(static_cast<const orl_wire_msg*>(in) + e, (lds_t)region, 16, 0, 2);
+    } else {
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(static_cast<const orl_wire8*>(in) + e);
+        __builtin_amdgcn_global_load_lds(g, (lds_t)region, 4, 0, 2);
+        __builtin_amdgcn_global_load_lds(g + 1, (lds_t)(reinterpret_cast<uint32_t*>(region) + 64), 4, 0, 2);
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ Msg pf_decode(const RouteParams& P, const u32x4* region, uint32_t lane) {
+    if (FMT == 32) return decode_hdr(region[lane], region[64u + lane]);
+    if (FMT == 16) return decode_wire(region[lane]);
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(region);
+    return decode_narrow(P, (uint64_t)r[lane] | ((uint64_t)r[64u + lane] << 32));
 }
 
 // CIN: the records come with the node exchange's act lane `in_act` (sender_cached); a template flag, since even a uniform
@@ -756,9 +784,12 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                                                          const uint32_t* __restrict__ in_act) {
     __shared__ RouteSmem<HB> sm;
     constexpr bool HIST = HB > 0;
-    constexpr bool PF = FMT == 32 && ORL_ROUTE_PF;
-    __shared__ u32x4 pre[PF ? 2 * kRouteThreads : 1];  // per wave: 64 first halves, then 64 second halves (lane-linear)
-    u32x4* const pregion = pre + (PF ? (threadIdx.x >> 6) * 128u : 0u);
+    // (exchange records too when ORL_ROUTE_PF=2: at a node rank's route it measured 0.586 -> 0.590 ms hot, 0.385 -> 0.396
+    // median, profiles/r06k_route_prefetch_node_ab.txt; config 2's 32-B route is unchanged by it, config 3's gains 0.15 ms)
+    constexpr bool PF = ORL_ROUTE_PF == 2 || (ORL_ROUTE_PF == 1 && FMT == 32);
+    constexpr uint32_t PFW = FMT == 32 ? 128u : FMT == 16 ? 64u : 32u;  // u32x4 per wave (pf_record)
+    __shared__ u32x4 pre[PF ? kWaves * PFW : 1];
+    u32x4* const pregion = pre + (PF ? (threadIdx.x >> 6) * PFW : 0u);
     const uint32_t plane = threadIdx.x & 63u;
     uint32_t pend_e = 0, pend_rr = 0, pend_act = 0;  // PF: the previous step's stores, issued after this step's wait
     bool pend = false;
@@ -772,7 +803,7 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
     uint32_t hot_mine = 0;
     const bool use16 = PW == 16 && (probe_bad == nullptr || *probe_bad == 0u);
     const uint32_t base = blockIdx.x * (kRouteThreads * items) + threadIdx.x;
-    if (PF) pf_header(static_cast<const orl_msg_hdr*>(in), base < n ? base : n - 1u, pregion);
+    if (PF) pf_record<FMT>(in, base < n ? base : n - 1u, pregion);
     for (uint32_t j = 0; j < items; ++j) {
         const uint32_t e = base + j * kRouteThreads;
         Msg m;
@@ -783,17 +814,12 @@ __global__ __launch_bounds__(kRouteThreads) ORL_ROUTE_ATTR void k_route(const Ro
                 store_drop(act_out + pend_e, pend_act);
                 pend = false;
             }
-            const u32x4 a = pregion[plane], b = pregion[64u + plane];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next header overwrites the slots
+            m = pf_decode<FMT>(sm.P, pregion, plane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next record overwrites the slots
             if (j + 1u < items) {
                 const uint32_t en = e + kRouteThreads;
-                pf_header(static_cast<const orl_msg_hdr*>(in), en < n ? en : n - 1u, pregion);
+                pf_record<FMT>(in, en < n ? en : n - 1u, pregion);
             }
-            m.tcd = (uint64_t)a.x | ((uint64_t)a.y << 32);
-            m.n0 = (uint64_t)a.z | ((uint64_t)a.w << 32);
-            m.n1 = (uint64_t)b.x | ((uint64_t)b.y << 32);
-            m.meta = b.z;
-            m.aux = b.w;
         } else if (e < n) {
             m = load_msg<FMT>(sm.P, in, e);
         }
