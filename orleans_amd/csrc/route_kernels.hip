@@ -5374,8 +5374,11 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     if (lsd_sweep(s)) return bucket_lsd_sweep(d_act, n, n_act, d_order, d_offsets, s, st);
     const RadixPlan& plan = bp.lsd;
     const uint32_t row_step0 = kItems / route_items;
-    // the last pass writes the bucket offsets itself (round 6) when its keys' low part fits the 16-bit halves of FL
-    const bool gaps = lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16;
+    // the last pass writes the bucket offsets itself (round 6) when its keys' low part fits the 16-bit halves of FL and the
+    // batch is dense in buckets (>= 2 messages per bucket): config 3 (16 per bucket) 7.77 -> 7.62 ms, but config 4 (0.7 per
+    // bucket: most of 10M offsets are gaps that cross tiles, k_bound_apply's share) 0.392 -> 0.436 ms, where k_offsets_gaps'
+    // LDS spans stay faster (profiles/r06m_config4_lsd_ab.txt)
+    const bool gaps = lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16 && n >= 2ull * nb;
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     // the digit stream (OUT_PAIR_DIG) lives in sorted_keys (>= n bytes), read by the next histogram before the last pass
     // writes sorted_keys / the FL rows there

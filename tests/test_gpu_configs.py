@@ -918,6 +918,44 @@ def test_lsd_offsets_long_gaps_vs_oracle(torch, monkeypatch, cap):
     eng.close()
 
 
+def test_lsd_fused_offsets_dense_vs_oracle(torch):
+    """The LSD plan's last pass writing the bucket offsets itself (round 6: OUT_FINAL_GAPS + k_bound_last / k_bound_scan /
+    k_bound_apply + k_sweep_tail), taken when a batch has >= 2 messages per bucket (config 3's shape; sparser batches keep
+    k_offsets_gaps).  n_act 8.5M (24-bit keys: 8 + 8 + 8-bit digits), batches of 18-20M messages: uniform, Zipf-hot (one key
+    with millions of messages), a few keys with millions of empty buckets between and around them, the unresolved bucket,
+    keys only in the low half, and the digit stream (OUT_PAIR_DIG) feeding each later histogram.  Order and offsets == the
+    oracle's stable bucketing (ActivationData.cs:483-514).  (The sparse form: test_lsd_offsets_long_gaps_vs_oracle.)"""
+    t = torch
+    n_act = 8_500_000
+    n = 2 * (n_act + 2) + 1000
+    rng = np.random.default_rng(17)
+    o = cpu_ref.Oracle(8)
+
+    def zipf(k):
+        r = np.minimum(rng.zipf(1.1, k), n_act) - 1
+        return ((r.astype(np.uint64) * np.uint64(2654435761)) % np.uint64(n_act)).astype(np.uint32)
+
+    batches = [rng.integers(0, n_act, n, dtype=np.int64).astype(np.uint32),
+               zipf(n),
+               rng.choice(np.array([3, 4, 4_000_000, 4_000_001, 8_400_000], np.uint32), n),
+               np.where(rng.random(n) < 0.3, np.uint32(L.NO_ACT), zipf(n)).astype(np.uint32),
+               rng.integers(0, n_act // 2, n, dtype=np.int64).astype(np.uint32)]
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=n, device=0)
+    W.setup_engine(eng, W.default_cluster())
+    off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
+    order = t.empty(n, dtype=t.int32, device="cuda")
+    for k, a in enumerate(batches):
+        d_act = t.from_numpy(a.view(np.int32)).cuda()
+        off.fill_(-1)
+        order.fill_(-1)
+        eng.bucket_device(d_act, len(a), order, off)
+        t.cuda.synchronize()
+        eo, ef = o.bucket(a, n_act)
+        np.testing.assert_array_equal(_u32(order), eo, err_msg=f"batch {k} order")
+        np.testing.assert_array_equal(_u32(off), ef, err_msg=f"batch {k} offsets")
+    eng.close()
+
+
 @pytest.mark.parametrize("n_act", [12_000_000, 40_000_000])
 def test_lsd_sweep_async_vs_oracle(torch, monkeypatch, n_act):
     """The LSD plan's single-sweep passes (round 6: k_digit_hist, one k_sweep per digit with a decoupled look-back, the
