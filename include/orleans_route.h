@@ -368,6 +368,16 @@ int orl_dir_remove_keyext(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext
 int orl_dir_lookup_keyext_host(orl_ctx* ctx, const orl_grain_key* keys, const orl_ext_ref* ext, const uint8_t* blob,
                                uint64_t blob_bytes, size_t n, uint32_t* act, uint8_t* silo);
 int orl_dir_keyext_count(const orl_ctx* ctx, uint64_t* n);
+/* orl_dir_insert_keyext on the device (round 6): the same statuses and winner rule (first writer of a key in the batch,
+ * GrainInfo.AddSingleActivation :103-107) over device arrays, asynchronously on `stream`; the strings are read from
+ * `d_blob` (blob_bytes long) and appended to the library's device store.  As orl_dir_insert_single_device: an act >=
+ * n_act, a silo outside the table or a reference outside the blob gives ORL_INS_UNSUPPORTED for that message (no host
+ * validation).  The device table is then the newer one: the host KeyExt calls (insert, remove, lookup, count) first
+ * download it (they synchronise the device).  ORL_E_CAPACITY when the store would pass 4 GiB; a device-side overrun is
+ * reported by the next host KeyExt call. */
+int orl_dir_insert_keyext_device(orl_ctx* ctx, const orl_grain_key* d_keys, const orl_ext_ref* d_ext, const uint8_t* d_blob,
+                                 uint64_t blob_bytes, const uint32_t* d_acts, const uint8_t* d_silos, size_t n,
+                                 uint32_t* d_winner_act, uint8_t* d_winner_silo, uint8_t* d_status, void* stream);
 /* orl_route_batch_device with the batch's KeyExt strings: d_ext[i] locates message i's extension in d_blob (device,
  * blob_bytes long; read only for KeyExt messages).  A KeyExt message whose header carries ORL_HDR_HASH_VALID uses that
  * hash, otherwise the kernel computes it from the bytes.  Its owner's KeyExt table is probed when the owner is local:

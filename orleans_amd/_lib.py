@@ -148,6 +148,7 @@ _SIGS = {
     "orl_dir_remove_keyext": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_size_t, _P]),
     "orl_dir_lookup_keyext_host": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_size_t, _P, _P]),
     "orl_dir_keyext_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "orl_dir_insert_keyext_device": (C.c_int, [_P, _P, _P, _P, C.c_uint64, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "orl_route_keyext_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P, C.c_uint64, _P, _P, _P, _P, _P]),
     "orl_dir_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "orl_dir_lookup_host": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),

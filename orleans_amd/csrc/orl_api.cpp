@@ -227,14 +227,22 @@ struct orl_ctx {
     uint64_t* d_dirstate = nullptr;  // {entries, tombstones, error flag}
     uint32_t* d_dslot = nullptr;     // per-message slot of a device directory batch
     uint8_t* d_dflag = nullptr;      // per-message flag of a device cache batch
-    // KeyExt grains (round 5): host table + extension blob, uploaded whole when changed
+    // KeyExt grains (round 5): host table + extension blob, uploaded whole when changed.  Round 6: registrations on the
+    // device (orl_dir_insert_keyext_device) make the device table the newer one (ext_dev_newer): the host functions first
+    // download it (ext_sync_host).  ext_dirty (host newer) and ext_dev_newer never hold together.
     std::vector<ExtSlot> ext_table;
     std::vector<uint8_t> ext_blob;
     uint64_t ext_count = 0, ext_tombs = 0;
     bool ext_dirty = false;
+    bool ext_dev_newer = false;
+    uint64_t ext_count_ub = 0, ext_tombs_ub = 0, ext_blob_ub = 0;  // upper bounds while the device is newer
+    uint64_t ext_blob_min_cap = 0;   // the device string store's capacity at the next upload (room for a device batch)
     ExtSlot* d_ext_table = nullptr;
     uint8_t* d_ext_blob = nullptr;
     size_t d_ext_table_cap = 0, d_ext_blob_cap = 0;
+    uint32_t* d_ext_claim = nullptr;  // per-slot claim words of the device registration (0xFFFFFFFF at rest)
+    size_t d_ext_claim_cap = 0;
+    uint64_t* d_ext_state = nullptr;  // {string bytes used, entries, tombstones, error}
     // directory cache (AdaptiveGrainDirectoryCache, f4): device table of remote-owned grains
     DirSlot* d_cache = nullptr;
     uint32_t* d_cclaim = nullptr;
@@ -712,7 +720,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob);
+    f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob); f(c->d_ext_claim); f(c->d_ext_state);
     f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
     for (auto& L : c->s.lb) {
         f(L.state);
@@ -1086,11 +1094,35 @@ int check_ext_refs(orl_ctx* c, const orl_ext_ref* ext, size_t n, uint64_t blob_b
     return ORL_OK;
 }
 
+// The host mirror after device registrations: the table, the used string store and the exact counters (synchronises).
+int ext_sync_host(orl_ctx* c) {
+    if (!c->ext_dev_newer) return ORL_OK;
+    ORL_HIP(c, hipSetDevice(c->cfg.device));
+    ORL_HIP(c, hipDeviceSynchronize());
+    uint64_t st[4];
+    ORL_HIP(c, hipMemcpy(st, c->d_ext_state, sizeof st, hipMemcpyDeviceToHost));
+    c->ext_blob.resize(st[0]);
+    if (st[0]) ORL_HIP(c, hipMemcpy(c->ext_blob.data(), c->d_ext_blob, st[0], hipMemcpyDeviceToHost));
+    if (!c->ext_table.empty())
+        ORL_HIP(c, hipMemcpy(c->ext_table.data(), c->d_ext_table, c->ext_table.size() * sizeof(ExtSlot), hipMemcpyDeviceToHost));
+    c->ext_count = c->ext_count_ub = st[1];
+    c->ext_tombs = c->ext_tombs_ub = st[2];
+    c->ext_blob_ub = st[0];
+    c->ext_dev_newer = false;
+    if (st[3]) {
+        ORL_HIP(c, hipMemset(c->d_ext_state + 3, 0, 8));
+        return fail(c, ORL_E_CAPACITY, "a device KeyExt registration found no free slot or no string-store room (%llu)",
+                    (unsigned long long)st[3]);
+    }
+    return ORL_OK;
+}
+
 int upload_keyext(orl_ctx* c) {
     if (!c->ext_dirty) return ORL_OK;
     ORL_HIP(c, hipSetDevice(c->cfg.device));
     ORL_HIP(c, hipDeviceSynchronize());  // batches in flight may read the old table (snapshot semantics, as the partition)
-    const size_t tb = c->ext_table.size() * sizeof(ExtSlot), bb = std::max<size_t>(c->ext_blob.size(), 4);
+    const size_t tb = c->ext_table.size() * sizeof(ExtSlot);
+    const size_t bb = std::max<size_t>(std::max<size_t>(c->ext_blob.size(), 4), c->ext_blob_min_cap);
     if (tb > c->d_ext_table_cap) {
         (void)hipFree(c->d_ext_table);
         c->d_ext_table = nullptr;
@@ -1105,6 +1137,21 @@ int upload_keyext(orl_ctx* c) {
     }
     if (tb) ORL_HIP(c, hipMemcpy(c->d_ext_table, c->ext_table.data(), tb, hipMemcpyHostToDevice));
     if (!c->ext_blob.empty()) ORL_HIP(c, hipMemcpy(c->d_ext_blob, c->ext_blob.data(), c->ext_blob.size(), hipMemcpyHostToDevice));
+    // the device registration's state: claim words at rest, the string cursor 4-B aligned, the counters
+    const size_t slots = c->ext_table.size();
+    if (slots > c->d_ext_claim_cap) {
+        (void)hipFree(c->d_ext_claim);
+        c->d_ext_claim = nullptr;
+        ORL_HIP(c, hipMalloc((void**)&c->d_ext_claim, slots * 4));
+        c->d_ext_claim_cap = slots;
+    }
+    if (slots) ORL_HIP(c, hipMemset(c->d_ext_claim, 0xFF, slots * 4));
+    if (!c->d_ext_state) ORL_HIP(c, hipMalloc((void**)&c->d_ext_state, 4 * sizeof(uint64_t)));
+    const uint64_t st[4] = {(c->ext_blob.size() + 3) & ~uint64_t(3), c->ext_count, c->ext_tombs, 0};
+    ORL_HIP(c, hipMemcpy(c->d_ext_state, st, sizeof st, hipMemcpyHostToDevice));
+    c->ext_count_ub = c->ext_count;
+    c->ext_tombs_ub = c->ext_tombs;
+    c->ext_blob_ub = st[0];
     c->ext_dirty = false;
     return ORL_OK;
 }
@@ -1116,6 +1163,7 @@ int orl_dir_insert_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_r
                           uint8_t* wsilo, uint8_t* status) {
     if (!c || (n && (!keys || !ext || !blob || !acts || !silos))) return ORL_E_INVALID;
     if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
+    if (int r = ext_sync_host(c)) return r;
     for (size_t i = 0; i < n; ++i) {
         uint8_t st;
         uint32_t a = ORL_NO_ACT;
@@ -1170,6 +1218,7 @@ int orl_dir_remove_keyext(orl_ctx* c, const orl_grain_key* keys, const orl_ext_r
                           uint64_t blob_bytes, size_t n, uint8_t* removed) {
     if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
     if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
+    if (int r = ext_sync_host(c)) return r;
     for (size_t i = 0; i < n; ++i) {
         const uint8_t* x = blob + ext[i].off;
         const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
@@ -1188,6 +1237,7 @@ int orl_dir_lookup_keyext_host(orl_ctx* c, const orl_grain_key* keys, const orl_
                                uint64_t blob_bytes, size_t n, uint32_t* act, uint8_t* silo) {
     if (!c || (n && (!keys || !ext || !blob))) return ORL_E_INVALID;
     if (int r = check_ext_refs(c, ext, n, blob_bytes)) return r;
+    if (int r = ext_sync_host(c)) return r;
     for (size_t i = 0; i < n; ++i) {
         const uint8_t* x = blob + ext[i].off;
         const int64_t at = ext_find(c, keys[i], keyext_hash(keys[i], x, ext[i].len), x, ext[i].len, nullptr);
@@ -1199,7 +1249,53 @@ int orl_dir_lookup_keyext_host(orl_ctx* c, const orl_grain_key* keys, const orl_
 
 int orl_dir_keyext_count(const orl_ctx* c, uint64_t* n) {
     if (!c || !n) return ORL_E_INVALID;
+    if (int r = ext_sync_host(const_cast<orl_ctx*>(c))) return r;  // after device registrations: the exact count
     *n = c->ext_count;
+    return ORL_OK;
+}
+
+int orl_dir_insert_keyext_device(orl_ctx* c, const orl_grain_key* d_keys, const orl_ext_ref* d_ext, const uint8_t* d_blob,
+                                 uint64_t blob_bytes, const uint32_t* d_acts, const uint8_t* d_silos, size_t n,
+                                 uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status, void* stream) {
+    if (!c) return ORL_E_INVALID;
+    if (!c->device_mode) return fail(c, ORL_E_STATE, "no device");
+    if (n && (!d_keys || !d_ext || !d_blob || !d_acts || !d_silos || !d_status)) return fail(c, ORL_E_INVALID, "null device buffer");
+    if (n > c->s.max_batch) return fail(c, ORL_E_CAPACITY, "batch %zu > max_batch %llu", n, (unsigned long long)c->s.max_batch);
+    if (c->n_silos == 0) return fail(c, ORL_E_STATE, "silo table not set");
+    if (blob_bytes > UINT32_MAX) return fail(c, ORL_E_INVALID, "KeyExt blob of %llu bytes (<= 4 GiB)", (unsigned long long)blob_bytes);
+    if (n == 0) return ORL_OK;
+    int r = sync_device_state(c);
+    if (r) return r;
+    if ((r = upload_keyext(c))) return r;  // host changes first: the device table is the authority from here
+    // every message might insert (load <= 1/2) and append its string (4-B aligned)
+    const uint64_t add = blob_bytes + 3 * (uint64_t)n;
+    auto fits = [&]() {
+        return (c->ext_count_ub + c->ext_tombs_ub + n) * 2 <= c->ext_table.size() && c->ext_blob_ub + add <= c->d_ext_blob_cap &&
+               c->ext_blob_ub + add <= UINT32_MAX;
+    };
+    if (!fits()) {
+        if ((r = ext_sync_host(c))) return r;
+        if (c->ext_blob.size() + add > UINT32_MAX)
+            return fail(c, ORL_E_CAPACITY, "KeyExt extension store full (4 GiB)");
+        if ((c->ext_count + c->ext_tombs + n) * 2 > c->ext_table.size()) ext_rebuild(c, c->ext_count + n);
+        c->ext_blob_min_cap = std::max<uint64_t>(c->ext_blob_min_cap, c->ext_blob.size() + add + 64);
+        c->ext_dirty = true;
+        if (c->ext_blob_min_cap > c->d_ext_blob_cap) {  // a new store is allocated at the upload
+            (void)hipFree(c->d_ext_blob);
+            c->d_ext_blob = nullptr;
+            c->d_ext_blob_cap = 0;
+        }
+        if ((r = upload_keyext(c))) return r;
+        if (!fits()) return fail(c, ORL_E_CAPACITY, "KeyExt table: no room for a batch of %zu", n);
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int e = launch_keyext_insert(c->d_params, c->d_ext_table, c->ext_table.size() - 1, c->d_ext_claim, c->d_ext_blob,
+                                 c->d_ext_blob_cap, d_keys, d_ext, d_blob, blob_bytes, d_acts, d_silos, n, c->cfg.n_act,
+                                 c->n_silos, c->d_dslot, d_wact, d_wsilo, d_status, c->d_ext_state, st);
+    if (e) return hipfail(c, (hipError_t)e, "KeyExt insert launch");
+    c->ext_count_ub += n;
+    c->ext_blob_ub += add;
+    c->ext_dev_newer = true;
     return ORL_OK;
 }
 

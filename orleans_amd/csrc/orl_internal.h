@@ -453,6 +453,13 @@ int ctx_route_received(orl_ctx* c, const void* d_in, int fmt, size_t n, uint32_t
                        const uint32_t* d_in_act, void* stream);
 // KeyExt grains of a routed batch (orl_route_keyext_device): each message k_route left ORL_ST_KEYEXT_UNRESOLVED gets
 // its owner's lookup in the KeyExt table when the owner is local (HIT, or placement on a miss) or ORL_ST_REMOTE_OWNER.
+// KeyExt registration on the device (k_kx_ins_probe / resolve / commit); d_state = {string bytes used, entries, tombstones,
+// error}; d_slot: n words of scratch.
+int launch_keyext_insert(const RouteParams* d_params, ExtSlot* d_table, uint64_t mask, uint32_t* d_claim, uint8_t* d_tblob,
+                         uint64_t tblob_cap, const orl_grain_key* d_keys, const orl_ext_ref* d_ext, const uint8_t* d_blob,
+                         uint64_t blob_bytes, const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act,
+                         uint32_t n_silos, uint32_t* d_slot, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status,
+                         uint64_t* d_state, void* stream);
 int launch_keyext_route(const RouteParams* d_params, const orl_msg_hdr* d_in, size_t n, const orl_ext_ref* d_ext,
                         const uint8_t* d_blob, uint64_t blob_bytes, const ExtSlot* d_table, uint64_t mask,
                         const uint8_t* d_tblob, uint32_t excl, uint32_t* d_route, uint32_t* d_act, void* stream);

@@ -4470,6 +4470,195 @@ __global__ __launch_bounds__(256) void k_dir_ins_commit(DirSlot* __restrict__ di
     if (slot_in[i] & kSlotWasTomb) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + 1), ~0ull);  // tombstones - 1
 }
 
+// ---------------------------------------------------------------------------------------------------
+// KeyExt registration on the device (round 6, VERDICT r5 item 6: GrainDirectoryPartition.AddSingleActivation over any
+// GrainId, GrainDirectoryPartition.cs:270-287, first writer wins, GrainInfo.AddSingleActivation :103-107).  The same claim
+// protocol as k_dir_ins_* over the KeyExt table: a message whose key is not on its chain CAS-claims the first reusable
+// slot (EMPTY / TOMB -> CLAIMING), writes the key, its hash, length and its string (appended to the table's string store
+// at a 4-B aligned cursor) write-through, then publishes CLAIMED; a message that finds a CLAIMED slot with an equal key
+// joins it; the smallest batch index of a slot wins (atomicMin on its claim word) and commits act / silo / FULL.
+// state[0] = bytes used in the string store, [1] = entries, [2] = tombstones, [3] = error (no slot / store full).
+__device__ __forceinline__ uint32_t* ext_word40(ExtSlot* t, uint64_t slot) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(t + slot) + 40);  // {silo, state, pad, pad}
+}
+
+// The caller's string bytes [s, s + len) as little-endian word w (bytes past len read as 0).
+__device__ __forceinline__ uint32_t ext_in_word(const uint8_t* __restrict__ s, uint32_t len, uint32_t w) {
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t k = w * 4u + b;
+        if (k < len) v |= (uint32_t)s[k] << (8u * b);
+    }
+    return v;
+}
+
+// Slot `slot` holds this key (tcd, n0, n1, hash, len and the bytes; write-through loads: the slot may be another
+// workgroup's claim of this launch).
+__device__ __forceinline__ bool ext_slot_eq(const ExtSlot* t, uint64_t slot, const uint8_t* __restrict__ tblob,
+                                            const orl_grain_key& k, uint32_t h, const uint8_t* __restrict__ s, uint32_t len) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(t + slot);
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(t + slot);
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k.type_code_data ||
+        __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k.n0 ||
+        __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k.n1 ||
+        __hip_atomic_load(w32 + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != h ||
+        __hip_atomic_load(w32 + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != len)
+        return false;
+    const uint32_t off = __hip_atomic_load(w32 + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* tw = reinterpret_cast<const uint32_t*>(tblob + off);  // claims start 4-B aligned
+    for (uint32_t q = 0; q * 4u < len; ++q) {
+        const uint32_t have = __hip_atomic_load(tw + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t keep = len - q * 4u >= 4u ? 0xFFFFFFFFu : (1u << (8u * (len - q * 4u))) - 1u;
+        if ((have & keep) != ext_in_word(s, len, q)) return false;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_kx_ins_probe(const RouteParams* __restrict__ gp, ExtSlot* __restrict__ table,
+                                                      uint64_t mask, uint32_t* __restrict__ claim, uint8_t* __restrict__ tblob,
+                                                      uint64_t tblob_cap, const orl_grain_key* __restrict__ keys,
+                                                      const orl_ext_ref* __restrict__ ext, const uint8_t* __restrict__ blob,
+                                                      uint64_t blob_bytes, const uint32_t* __restrict__ acts,
+                                                      const uint8_t* __restrict__ silos, uint32_t n, uint32_t n_act,
+                                                      uint32_t n_silos, uint32_t* __restrict__ slot_out,
+                                                      uint8_t* __restrict__ status, unsigned long long* __restrict__ state) {
+    __shared__ RouteParams P;
+    stage_params(&P, gp);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const orl_grain_key k = keys[i];
+    const orl_ext_ref x = ext[i];
+    const uint32_t silo = silos[i];
+    uint8_t st;
+    uint32_t h = 0;
+    if (acts[i] >= n_act || silo >= n_silos || (uint64_t)x.off + x.len > blob_bytes) {
+        st = ORL_INS_UNSUPPORTED;
+    } else if ((uint32_t)(k.type_code_data >> 56) != ORL_CAT_KEYEXT_GRAIN) {
+        st = ORL_INS_UNSUPPORTED;
+    } else {
+        h = keyext_hash_dev(k.n0, k.n1, k.type_code_data, blob + x.off, x.len);
+        const bool running = mask_bit(P.running, silo);  // CalculateTargetSilo(excludeThisSiloIfStopping) from `silo`
+        const uint32_t owner = P.ring_n == 0 ? (running ? silo : 0xFFu) : ring_owner(P, (int32_t)h, silo, !running);
+        if (owner == 0xFFu) st = ORL_INS_OWNER_NULL;
+        else if (!mask_bit(P.local, owner)) st = ORL_INS_REMOTE_OWNER;
+        else if (!mask_bit(P.functional, silo)) st = ORL_INS_INVALID_SILO;  // AddSingleActivation :277-279
+        else st = kInsCandidate;
+    }
+    uint32_t out_slot = kSlotNone;
+    if (st == kInsCandidate) {
+        const uint8_t* s = blob + x.off;
+        const uint64_t start = dir_slot(h, mask);
+        int outcome = -1;
+        uint64_t slot = start;
+        bool was_tomb = false;
+        for (uint32_t attempt = 0; outcome < 0 && attempt < kRetryLimit; ++attempt) {
+            uint64_t cur = start, free_slot = ~0ull;
+            uint32_t free_word = 0;
+            bool blocked = false, ended = false;
+            for (uint64_t step = 0; step <= mask && outcome < 0 && !blocked && !ended; ++step) {
+                const uint32_t v = __hip_atomic_load(ext_word40(table, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t sst = (v >> 8) & 0xFFu;
+                if (sst == SLOT_EMPTY || sst == SLOT_TOMB) {
+                    if (free_slot == ~0ull) {
+                        free_slot = cur;
+                        free_word = v;
+                    }
+                    ended = sst == SLOT_EMPTY;
+                } else if (sst == SLOT_CLAIMING) {
+                    blocked = true;
+                } else if (ext_slot_eq(table, cur, tblob, k, h, s, x.len)) {  // CLAIMED (join) or FULL (existing)
+                    slot = cur;
+                    outcome = sst == SLOT_CLAIMED ? 1 : 0;
+                    if (outcome == 1) atomicMin(&claim[cur], i);
+                }
+                cur = (cur + 1) & mask;
+            }
+            if (outcome >= 0) break;
+            if (blocked || free_slot == ~0ull) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t expect = free_word;
+            if (__hip_atomic_compare_exchange_strong(ext_word40(table, free_slot), &expect, (uint32_t)SLOT_CLAIMING << 8,
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                const uint32_t padded = (x.len + 3u) & ~3u;
+                const unsigned long long off = atomicAdd(&state[0], (unsigned long long)padded);
+                if (off + padded > tblob_cap) {  // the host sized the store for the batch: never taken
+                    atomicOr(&state[3], 2ull);
+                    __hip_atomic_store(ext_word40(table, free_slot), free_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                uint32_t* tw = reinterpret_cast<uint32_t*>(tblob + off);
+                for (uint32_t q = 0; q * 4u < x.len; ++q)
+                    __hip_atomic_store(tw + q, ext_in_word(s, x.len, q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t* kw = reinterpret_cast<uint64_t*>(table + free_slot);
+                uint32_t* k32 = reinterpret_cast<uint32_t*>(table + free_slot);
+                __hip_atomic_store(kw, k.type_code_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(kw + 1, k.n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(kw + 2, k.n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(k32 + 6, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(k32 + 8, (uint32_t)off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(k32 + 9, x.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // key and bytes write-through before the state flips
+                __hip_atomic_store(ext_word40(table, free_slot), (uint32_t)SLOT_CLAIMED << 8, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                atomicMin(&claim[free_slot], i);
+                slot = free_slot;
+                was_tomb = ((free_word >> 8) & 0xFFu) == SLOT_TOMB;
+                outcome = 1;
+            }
+        }
+        if (outcome < 0) {
+            atomicOr(&state[3], 1ull);
+            st = ORL_INS_UNSUPPORTED;
+        } else {
+            out_slot = (uint32_t)slot | (was_tomb ? kSlotWasTomb : 0u);
+            st = outcome == 0 ? (uint8_t)ORL_INS_EXISTING : kInsCandidate;
+        }
+    }
+    slot_out[i] = out_slot;
+    status[i] = st;
+}
+
+__global__ __launch_bounds__(256) void k_kx_ins_resolve(const ExtSlot* __restrict__ table, const uint32_t* __restrict__ claim,
+                                                        const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                        uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                        uint8_t* __restrict__ status, uint32_t* __restrict__ wact,
+                                                        uint8_t* __restrict__ wsilo) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t st = status[i];
+    const uint32_t slot = slot_in[i] & kSlotMask;
+    uint32_t a = ORL_NO_ACT;
+    uint8_t sl = (uint8_t)ORL_NULL_SILO;
+    if (st == kInsCandidate) {
+        const uint32_t c = claim[slot];
+        a = acts[c];
+        sl = silos[c];
+        status[i] = c == i ? (uint8_t)ORL_INS_INSERTED : (uint8_t)ORL_INS_EXISTING;
+    } else if (st == ORL_INS_EXISTING) {
+        a = table[slot].act;
+        sl = table[slot].silo;
+    }
+    if (wact) wact[i] = a;
+    if (wsilo) wsilo[i] = sl;
+}
+
+__global__ __launch_bounds__(256) void k_kx_ins_commit(ExtSlot* __restrict__ table, uint32_t* __restrict__ claim,
+                                                       const uint32_t* __restrict__ acts, const uint8_t* __restrict__ silos,
+                                                       uint32_t n, const uint32_t* __restrict__ slot_in,
+                                                       const uint8_t* __restrict__ status, unsigned long long* __restrict__ state) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || status[i] != ORL_INS_INSERTED) return;
+    const uint32_t slot = slot_in[i] & kSlotMask;
+    table[slot].act = acts[i];
+    *ext_word40(table, slot) = (uint32_t)silos[i] | ((uint32_t)SLOT_FULL << 8);
+    claim[slot] = kSlotNone;
+    atomicAdd(&state[1], 1ull);
+    if (slot_in[i] & kSlotWasTomb) atomicAdd(&state[2], ~0ull);  // tombstones - 1
+}
+
 // Directory cache AddOrUpdate (AdaptiveGrainDirectoryCache.AddOrUpdate; f4): the batch's LAST writer of a key
 // sets its entry (insert or update).  Claim tag = ~index, so atomicMin keeps the largest index.  Entries with an
 // activation handle >= n_act or a silo outside the table are skipped.
@@ -5849,6 +6038,23 @@ int launch_keyext_route(const RouteParams* d_params, const orl_msg_hdr* d_in, si
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_keyext_route, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, d_params, d_in, (uint32_t)n,
                        d_ext, d_blob, blob_bytes, d_table, mask, d_tblob, excl, d_route, d_act);
+    return (int)hipGetLastError();
+}
+
+int launch_keyext_insert(const RouteParams* d_params, ExtSlot* d_table, uint64_t mask, uint32_t* d_claim, uint8_t* d_tblob,
+                         uint64_t tblob_cap, const orl_grain_key* d_keys, const orl_ext_ref* d_ext, const uint8_t* d_blob,
+                         uint64_t blob_bytes, const uint32_t* d_acts, const uint8_t* d_silos, size_t n, uint32_t n_act,
+                         uint32_t n_silos, uint32_t* d_slot, uint32_t* d_wact, uint8_t* d_wsilo, uint8_t* d_status,
+                         uint64_t* d_state, void* stream) {
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g(ceil_div(n, 256)), b(256);
+    unsigned long long* state = reinterpret_cast<unsigned long long*>(d_state);
+    hipLaunchKernelGGL(k_kx_ins_probe, g, b, 0, st, d_params, d_table, mask, d_claim, d_tblob, tblob_cap, d_keys, d_ext, d_blob,
+                       blob_bytes, d_acts, d_silos, (uint32_t)n, n_act, n_silos, d_slot, d_status, state);
+    hipLaunchKernelGGL(k_kx_ins_resolve, g, b, 0, st, d_table, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, d_wact,
+                       d_wsilo);
+    hipLaunchKernelGGL(k_kx_ins_commit, g, b, 0, st, d_table, d_claim, d_acts, d_silos, (uint32_t)n, d_slot, d_status, state);
     return (int)hipGetLastError();
 }
 

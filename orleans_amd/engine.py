@@ -246,6 +246,14 @@ class GrainDirectoryEngine:
                                                  ptr(silos), n, ptr(wa), ptr(ws), ptr(st)))
         return st, wa, ws
 
+    def register_keyext_device(self, d_keys, d_ext, d_blob, blob_bytes: int, d_acts, d_silos, n: int, d_status,
+                               d_winner_act=None, d_winner_silo=None, stream=None):
+        """RegisterSingleActivation of KeyExt grains on the device (orl_dir_insert_keyext_device): device arrays, async on
+        `stream`; statuses / winners written to the device buffers."""
+        self._ck(self._lib.orl_dir_insert_keyext_device(self._ctx, ptr(d_keys), ptr(d_ext), ptr(d_blob), int(blob_bytes),
+                                                        ptr(d_acts), ptr(d_silos), int(n), ptr(d_winner_act),
+                                                        ptr(d_winner_silo), ptr(d_status), ptr(stream)))
+
     def unregister_keyext(self, keys: np.ndarray, strings) -> np.ndarray:
         keys = np.ascontiguousarray(keys, dtype=L.KEY_DTYPE)
         ref, blob = self.ext_blob(strings)

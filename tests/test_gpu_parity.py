@@ -1512,3 +1512,123 @@ def test_keyext_directory_vs_oracle(torch, golden_dir):
         assert bool(rm[i]) == part.remove(k)
     run(msgs, strings)
     eng.close()
+
+
+def test_keyext_device_insert_vs_oracle(torch, golden_dir):
+    """VERDICT r5 item 6 (second half): KeyExt registration by device kernels (orl_dir_insert_keyext_device: claim /
+    resolve / commit over the KeyExt table, strings appended to the device store) with the host call's semantics —
+    GrainDirectoryPartition.AddSingleActivation over any GrainId (GrainDirectoryPartition.cs:270-287), first writer of a key
+    in the batch wins (GrainInfo.AddSingleActivation :103-107), invalid silo, remote owner, a key of another category;
+    out-of-range acts give ORL_INS_UNSUPPORTED on the device.  Statuses and winners equal pyref's sequential restatement;
+    then the host calls (lookup, count, a host insert, a removal) see the device's table, a second device batch after them
+    (existing keys, new ones, a table that must grow), and the routed batch (orl_route_keyext_device) equals pyref."""
+    t = torch
+    cl = W.default_cluster()
+    local = [1, 1, 1, 1, 0, 0, 0, 0]
+    functional = [1, 1, 1, 1, 1, 1, 0, 1]
+    ring = P.Ring()
+    for s in range(8):
+        ring.add_server(s, int(cl.hashes[s]))
+    view = P.SiloView(running=[True] * 8, functional=[bool(f) for f in functional], local=[bool(x) for x in local])
+    part = P.Partition()
+    n_act = 40_000
+    eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=1 << 16, device=0)
+    eng.set_silos(8, functional=functional, local=local)
+    for s in range(8):
+        eng.add_server(s, int(cl.hashes[s]))
+    rng = np.random.default_rng(23)
+    tc = cl.type_code
+    gold = json.load(open(os.path.join(golden_dir, "jenkins.json")))["keyext"]
+    kx = [P.Key(int(g["tcd"], 16), int(g["n0"], 16), int(g["n1"], 16), g["ext"]) for g in gold]
+    for i in range(1500):
+        ext = rng.choice(["user-%d", "ключ-%d", "grain/%d/part", "é中%d\U0001F600", "%d"]) % (i // 2)
+        kx.append(P.key_from_long(int(i % 300), tc, ext))
+    kx += kx[50:120] + kx[7:9]  # re-registrations in the same batch: the first writer wins
+    kx.append(P.key_from_long(5, tc))  # a long key: ORL_INS_UNSUPPORTED
+
+    def dev_insert(keys_, acts, silos):
+        strings = [k.key_ext or "" for k in keys_]
+        keys = np.array([(k.tcd, k.n0, k.n1) for k in keys_], L.KEY_DTYPE)
+        ref, blob = GrainDirectoryEngine.ext_blob(strings)
+        n = len(keys_)
+        d = lambda a: t.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()  # noqa: E731
+        d_st, d_wa, d_ws = (t.zeros(n, dtype=t.uint8, device="cuda"), t.zeros(n, dtype=t.int32, device="cuda"),
+                            t.zeros(n, dtype=t.uint8, device="cuda"))
+        eng.register_keyext_device(d(keys), d(ref), d(blob), len(blob), d(acts.astype(np.uint32)), d(silos.astype(np.uint8)), n,
+                                   d_st, d_wa, d_ws, stream=t.cuda.current_stream().cuda_stream)
+        t.cuda.synchronize()
+        return d_st.cpu().numpy(), d_wa.cpu().numpy().view(np.uint32), d_ws.cpu().numpy()
+
+    def expected(keys_, acts, silos):
+        out = []
+        for k, a, s in zip(keys_, acts, silos):
+            if a >= n_act:
+                out.append((L.INS_UNSUPPORTED, L.NO_ACT, 0xFF))
+            elif k.key_ext is None:
+                out.append((L.INS_UNSUPPORTED, L.NO_ACT, 0xFF))
+            else:
+                out.append(P.register_keyext(ring, part, view, k, int(a), int(s)))
+        return out
+
+    def check(got, exp):
+        st, wa, ws = got
+        np.testing.assert_array_equal(st, np.array([e[0] for e in exp], np.uint8))
+        ok = st <= 1
+        np.testing.assert_array_equal(wa[ok], np.array([e[1] for e in exp], np.uint32)[ok])
+        np.testing.assert_array_equal(ws[ok], np.array([e[2] for e in exp], np.uint8)[ok])
+
+    acts = (1000 + np.arange(len(kx))).astype(np.uint32)
+    acts[3] = n_act + 7  # out of range: UNSUPPORTED on the device, nothing inserted
+    silos = rng.integers(0, 8, len(kx)).astype(np.uint8)
+    got = dev_insert(kx, acts, silos)
+    exp = expected(kx, acts, silos)
+    check(got, exp)
+    assert {0, 1, 2, 3, 5} <= set(got[0].tolist())  # inserted, existing, invalid silo, remote owner, unsupported
+    # the host calls see the device's table (they download it first)
+    assert eng.keyext_count() == len(part.data)
+    q = kx[:400]
+    a_h, s_h = eng.lookup_keyext_host(np.array([(k.tcd, k.n0, k.n1) for k in q], L.KEY_DTYPE), [k.key_ext or "" for k in q])
+    for i, k in enumerate(q):
+        r = part.data.get(P.Partition._k(k)) if k.key_ext is not None else None
+        assert (a_h[i], s_h[i]) == ((r[0], r[1]) if r else (L.NO_ACT, 0xFF)), i
+    # a host insert and a removal in between, then a second, larger device batch (the table grows on the host first)
+    hk = [P.key_from_long(900 + i, tc, "host-%d" % i) for i in range(200)]
+    st_h, _, _ = eng.register_keyext(np.array([(k.tcd, k.n0, k.n1) for k in hk], L.KEY_DTYPE), [k.key_ext for k in hk],
+                                     np.arange(200, dtype=np.uint32) + 30000, np.zeros(200, np.uint8))
+    exp_h = [P.register_keyext(ring, part, view, k, 30000 + i, 0) for i, k in enumerate(hk)]
+    np.testing.assert_array_equal(st_h, np.array([e[0] for e in exp_h], np.uint8))
+    gone = kx[10:400:4]
+    rm = eng.unregister_keyext(np.array([(k.tcd, k.n0, k.n1) for k in gone], L.KEY_DTYPE), [k.key_ext or "" for k in gone])
+    for i, k in enumerate(gone):
+        assert bool(rm[i]) == (k.key_ext is not None and part.remove(k))
+    kx2 = kx[:600] + hk[:50] + [P.key_from_long(int(i % 500), tc, "second-%d" % i) for i in range(3000)]
+    acts2 = (5000 + np.arange(len(kx2))).astype(np.uint32)
+    silos2 = rng.integers(0, 8, len(kx2)).astype(np.uint8)
+    got2 = dev_insert(kx2, acts2, silos2)
+    check(got2, expected(kx2, acts2, silos2))
+    assert eng.keyext_count() == len(part.data)
+    # routing reads the device table
+    msgs, strings = [], []
+    for i in range(20_000):
+        k = kx2[int(rng.integers(0, len(kx2)))] if rng.random() < 0.85 else P.key_from_long(int(rng.integers(0, 500)), tc, "none-%d" % i)
+        if k.key_ext is None:
+            continue
+        msgs.append(P.Msg(k, int(rng.integers(0, 4))))
+        strings.append(k.key_ext)
+    h = np.zeros(len(msgs), L.MSG_DTYPE)
+    h["tcd"] = [m.key.tcd for m in msgs]
+    h["n0"] = [m.key.n0 for m in msgs]
+    h["n1"] = [m.key.n1 for m in msgs]
+    h["sending_silo"] = [m.sending_silo for m in msgs]
+    h["category"] = 2
+    h["target_silo"] = 0xFF
+    ref, blob = GrainDirectoryEngine.ext_blob(strings)
+    n = len(msgs)
+    outs = [t.empty(n, dtype=t.int32, device="cuda") for _ in range(3)] + [t.empty(n_act + 2, dtype=t.int32, device="cuda")]
+    eng.address_keyext_device(t.from_numpy(h.view(np.int32).reshape(-1, 8)).cuda(), n, t.from_numpy(ref.view(np.int32)).cuda(),
+                              t.from_numpy(blob).cuda(), len(blob), *outs, stream=t.cuda.current_stream().cuda_stream)
+    t.cuda.synchronize()
+    er, ea = P.route_batch(msgs, ring, part, view, keyext_directory=True)
+    np.testing.assert_array_equal(outs[0].cpu().numpy().view(np.uint32), np.array(er, np.uint32))
+    np.testing.assert_array_equal(outs[1].cpu().numpy().view(np.uint32), np.array(ea, np.uint32))
+    eng.close()
