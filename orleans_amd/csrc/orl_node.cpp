@@ -111,7 +111,7 @@ struct orl_node {
     bool broken = false;      // a bounded wait expired or RCCL failed: the communicator was aborted
     int stall_chunk = -1;     // ORL_NODE_INJECT_STALL: the all-gather of this chunk waits on h_stall (fault injection)
     uint32_t* h_stall = nullptr;  // pinned, device-visible release word of the injected stall
-    int lb_fail = 0;          // ORL_NODE_INJECT_LB_FAIL: 1 = the hop-2 partition's, 2 = a re-partition's look-back "gives up"
+    int lb_fail = 0;          // ORL_NODE_INJECT_LB_FAIL: 1 = the hop-2 partition's, 2 = a re-partition's, 3 = stage 4's look-back "gives up"
     uint32_t n_act = 0, nr = 1, me = 0;
     uint64_t chunk_cap = 0;
     ncclComm_t comm = nullptr;
@@ -627,8 +627,8 @@ int orl_node_create(orl_ctx* ctx, const orl_node_config* cfg, orl_node** out) {
         const long v = atol(t);
         if (v > 0) nd->timeout_ms = (uint32_t)std::min<long>(v, 0x7FFFFFFF);
     }
-    if (const char* lf = getenv("ORL_NODE_INJECT_LB_FAIL"))  // fault injection on this rank only: "hop2" or "rewrite"
-        nd->lb_fail = std::strcmp(lf, "hop2") == 0 ? 1 : std::strcmp(lf, "rewrite") == 0 ? 2 : 0;
+    if (const char* lf = getenv("ORL_NODE_INJECT_LB_FAIL"))  // fault injection on this rank only: "hop2", "rewrite", "stage4"
+        nd->lb_fail = std::strcmp(lf, "hop2") == 0 ? 1 : std::strcmp(lf, "rewrite") == 0 ? 2 : std::strcmp(lf, "stage4") == 0 ? 3 : 0;
     if (const char* st = getenv("ORL_NODE_INJECT_STALL")) {  // fault injection: "<chunk>" (hop 1) or "hop2"
         nd->stall_chunk = std::strcmp(st, "hop2") == 0 ? -2 : atoi(st);
         if (!ok(hipHostMalloc((void**)&nd->h_stall, 64, hipHostMallocMapped | hipHostMallocCoherent))) return bail(ORL_E_NOMEM);
@@ -713,7 +713,7 @@ int orl_node_route_batch_device(orl_node* nd, const orl_msg_hdr* d_in, size_t n,
         NODE_HIP(nd, hipSetDevice(nd->device));
         NODE_HIP(nd, hipEventSynchronize(nd->ev_s4));
         nd->s4_pending = false;
-        if (*nd->h_s4err) {  // a device fault, on this rank only: its hosted order / offsets were not valid
+        if (*nd->h_s4err || nd->lb_fail == 3) {  // a device fault, on this rank only: its hosted order / offsets were not valid
             *nd->h_s4err = 0;
             uint64_t w = 0;
             (void)orl_ctx_query(nd->ctx, ORL_Q_STAGE4_ERROR, &w);  // reads and clears the device word

@@ -3317,8 +3317,11 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
+#ifndef ORL_FAN_PF  // k_fanout_route<U = 1>: the next message's CSR target prefetched by LDS-DMA (round 6, opt-in: config 4
+#define ORL_FAN_PF 0  // 0.394-0.396 ms either way, the kernel 182 us: its probe into the 256 MiB table, not the CSR load, is the
+#endif                // chain's long pole; profiles/r06p_fanout_prefetch_ab.txt)
 #ifndef ORL_FAN_LDS
-#define ORL_FAN_LDS 1024
+#define ORL_FAN_LDS (ORL_FAN_PF ? 960 : 1024)  // 960 keeps 7 workgroups per CU beside the prefetch slots
 #endif
 constexpr uint32_t kFanLds = ORL_FAN_LDS;  // publishers staged per tile; beyond that fall back to global search
 
@@ -3329,6 +3332,7 @@ struct FanSmem {
     uint32_t poff[kFanLds + 1];
     uint64_t pdelta[kFanLds];  // pstart[p] - poff[p]: message f of publisher p reads csr_tgt[pdelta + f]
     uint32_t prange[2];
+    uint32_t pre[ORL_FAN_PF ? kRouteThreads : 1];  // the CSR-target prefetch slots (lane-linear per wave)
 };
 
 // A fan-out tile's publishers [p_lo, p_hi] (a superset is fine: every f of the tile has poff[p_lo] <= f < poff[p_hi + 1]):
@@ -3403,10 +3407,65 @@ __global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
     // U messages per thread and step, in three phases so their dependent loads overlap: (A) publisher search + CSR
     // target load, (B) stages 1-2 + the first probe, (C) probe chain, stage-3 tail, outputs.  U = 1 is one message at a
     // time (the round-2 loop).
+    // PF (U = 1, round 6): the next message's publisher search runs during this one's step and its CSR target comes by
+    // LDS-DMA (4 B per lane into the wave's slots), so the chain per message is CSR target ‖ probe instead of CSR target
+    // → probe; the route / act stores of a message are issued after the next step's wait (as k_route's prefetch).
+    constexpr bool PF = ORL_FAN_PF && U == 1;
+    uint32_t* const fslot = sm.pre + (PF ? (threadIdx.x & ~63u) : 0u);
+    const uint32_t flane = threadIdx.x & 63u;
+    auto fan_ci = [&](uint32_t ee, uint64_t& ci, uint32_t& pq) -> bool {  // message ee's CSR entry and publisher
+        if (ee >= lim || ee < nd) return false;
+        const uint32_t f = ee - nd;
+        uint32_t lo, hi;
+        if (in_lds) {
+            lo = 0; hi = span + 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (sm.poff[mid] <= f) lo = mid + 1; else hi = mid;
+            }
+            pq = p_lo + lo - 1;
+            ci = sm.pdelta[lo - 1] + f;
+        } else {
+            lo = p_lo; hi = p_hi + 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (poff32[mid] <= f) lo = mid + 1; else hi = mid;
+            }
+            pq = lo - 1;
+            ci = pstart[pq] + (f - poff32[pq]);
+        }
+        return true;
+    };
+    using lds_t = __attribute__((address_space(3))) void*;
+    uint32_t pf_pub = 0, pend_e = 0, pend_rr = 0, pend_act = 0;
+    bool pend = false;
+    if (PF) {
+        uint64_t ci = 0;
+        if (!fan_ci(base + threadIdx.x, ci, pf_pub)) ci = 0;
+        __builtin_amdgcn_global_load_lds(csr_tgt + ci, (lds_t)fslot, 4, 0, 0);
+    }
     for (uint32_t j = 0; j < items; j += U) {
         uint32_t e[U], tgt[U], pub[U];
+        if (PF) {  // (A) from the prefetch: this step's target, then the next step's search and CSR load
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (pend) {
+                route[pend_e] = pend_rr;
+                act_out[pend_e] = pend_act;
+                pend = false;
+            }
+            e[0] = base + j * kRouteThreads + threadIdx.x;
+            tgt[0] = fslot[flane];
+            pub[0] = pf_pub;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next target overwrites the slot
+            if (j + 1u < items) {
+                uint64_t ci = 0;
+                if (!fan_ci(e[0] + kRouteThreads, ci, pf_pub)) ci = 0;
+                __builtin_amdgcn_global_load_lds(csr_tgt + ci, (lds_t)fslot, 4, 0, 0);
+            }
+        }
 #pragma unroll
         for (int q = 0; q < U; ++q) {  // (A)
+            if (PF) break;
             e[q] = base + (j + q) * kRouteThreads + threadIdx.x;
             tgt[q] = 0;
             pub[q] = 0;
@@ -3514,10 +3573,18 @@ __global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
                 }
                 rr = route_tail(sm.P, m[q], h[q], own[q], rf[q], st == 0, fact, fsilo, act, false);
             }
-            route[e[q]] = rr;  // (non-temporal stores here: no change at configs 4 / 5, round 5)
-            act_out[e[q]] = act;
+            if (PF) {
+                pend_e = e[q], pend_rr = rr, pend_act = act, pend = true;
+            } else {
+                route[e[q]] = rr;  // (non-temporal stores here: no change at configs 4 / 5, round 5)
+                act_out[e[q]] = act;
+            }
             if (HIST) atomicAdd(&sm.hist[(bucket_key(act, n_act) >> shift) & (bins - 1)], 1u);
         }
+    }
+    if (PF && pend) {
+        route[pend_e] = pend_rr;
+        act_out[pend_e] = pend_act;
     }
     if (HIST) {
         __syncthreads();

@@ -460,6 +460,52 @@ def test_node_rank_local_lookback_fault_fails_every_rank_fast(torch, monkeypatch
     world.close()
 
 
+def test_node_stage4_lookback_fault_fails_next_batch(torch, monkeypatch):
+    """Stage 4's own look-back error word: a give-up on ONE rank (fault injection, ORL_NODE_INJECT_LB_FAIL=stage4
+    on rank 1's node: its copied word reads as set) is not hidden — that rank's next batch returns ORL_E_DEVICE naming stage
+    4 and breaks the group, the peer fails at once with ORL_E_STATE, and both report themselves broken afterwards."""
+    import time
+    t = torch
+    world = World(2, n_grains=20_000, host_mix=0.0)
+    nodes = []
+    for r in range(2):
+        if r == 1:
+            monkeypatch.setenv("ORL_NODE_INJECT_LB_FAIL", "stage4")
+        nodes.append(GrainNode(world.engs[r], 2, r, world.ros, max_batch=100_000, max_recv=300_000,
+                               transport=L.TRANSPORT_LOCAL, group_id=b"node-s4fault", chunks=2))
+        monkeypatch.delenv("ORL_NODE_INJECT_LB_FAIL", raising=False)
+    for nd in nodes:
+        nd.set_timeout(60_000)
+    batches = [world.messages(r, 50_000, seed=60 + r) for r in range(2)]
+    d_in = [t.from_numpy(b.view(np.int32).reshape(-1, 8)).cuda() for b in batches]
+    t.cuda.synchronize()
+
+    def one(r):
+        try:
+            nodes[r].route_batch_device(d_in[r], len(batches[r]))
+            t.cuda.synchronize()
+            return 0, ""
+        except L.OrleansRouteError as e:
+            return e.code, str(e)
+
+    with ThreadPoolExecutor(2) as ex:  # the first batch completes on both ranks (the word is checked at the next one)
+        assert [c for c, _ in ex.map(one, range(2))] == [0, 0]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(2) as ex:
+        (c0, m0), (c1, m1) = list(ex.map(one, range(2)))
+    took = time.perf_counter() - t0
+    assert c1 == L.E_DEVICE and "stage 4" in m1, (c1, m1)
+    assert c0 == L.E_STATE, (c0, m0)
+    assert took < 15, took
+    for r in range(2):
+        with pytest.raises(L.OrleansRouteError) as ei:
+            nodes[r].route_batch_device(d_in[r], len(batches[r]))
+        assert ei.value.code == L.E_STATE and "broken" in str(ei.value)
+    for nd in nodes:
+        nd.close()
+    world.close()
+
+
 @pytest.mark.parametrize("chunks", [3])
 def test_node_mixed_width_segments_aligned(torch, chunks):
     """An odd number of 8-B records received in one chunk, then a 32-B chunk (a Guid-keyed target): every hosted segment
