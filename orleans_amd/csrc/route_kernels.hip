@@ -3317,22 +3317,32 @@ __global__ __launch_bounds__(256) void k_seg_scatter(const void* __restrict__ in
 // Stage 5: fan-out.  deg[p] = out-degree of publisher pubs[p]; exclusive scan; then the route kernel
 // over emitted messages, each tile locating its publishers with one binary search into the scanned
 // degrees staged in LDS.
-#ifndef ORL_FAN_PF  // k_fanout_route<U = 1>: the next message's CSR target prefetched by LDS-DMA (round 6, opt-in: config 4
-#define ORL_FAN_PF 0  // 0.394-0.396 ms either way, the kernel 182 us: its probe into the 256 MiB table, not the CSR load, is the
-#endif                // chain's long pole; profiles/r06p_fanout_prefetch_ab.txt)
+// k_fanout_route<U = 1>: the next message's CSR target prefetched by LDS-DMA (round 6).  On for the 32-B-table form
+// (PW 0: key-table followers, config 5, whose chain is CSR target -> key table -> probe): 0.0867 -> 0.0861 ms per tick
+// (profiles/r06r_config5_fanout_prefetch_ab.txt); off for the probe-table forms (config 4: 0.394-0.396 ms either way, the
+// kernel 182 us, its probe into the 256 MiB table being the chain's long pole; r06p_fanout_prefetch_ab.txt).
+// ORL_FAN_PF: 0 never, 1 PW 0 only, 2 every form.
+#ifndef ORL_FAN_PF
+#define ORL_FAN_PF 1
+#endif
 #ifndef ORL_FAN_LDS
-#define ORL_FAN_LDS (ORL_FAN_PF ? 960 : 1024)  // 960 keeps 7 workgroups per CU beside the prefetch slots
+#define ORL_FAN_LDS 1024
 #endif
 constexpr uint32_t kFanLds = ORL_FAN_LDS;  // publishers staged per tile; beyond that fall back to global search
+template <int PW, int U>
+constexpr bool fan_pf() { return U == 1 && (ORL_FAN_PF == 2 || (ORL_FAN_PF == 1 && PW == 0)); }
+// with the prefetch slots, 64 fewer staged publishers keep the workgroup's LDS under 1/7 of the CU's (7 per CU)
+template <bool PF>
+constexpr uint32_t fan_lds_pubs() { return PF ? kFanLds - 64u : kFanLds; }
 
-template <int HB>
+template <int HB, bool PF>
 struct FanSmem {
     RouteParams P;
     uint32_t hist[HB ? (1u << HB) : 1u];
-    uint32_t poff[kFanLds + 1];
-    uint64_t pdelta[kFanLds];  // pstart[p] - poff[p]: message f of publisher p reads csr_tgt[pdelta + f]
+    uint32_t poff[fan_lds_pubs<PF>() + 1];
+    uint64_t pdelta[fan_lds_pubs<PF>()];  // pstart[p] - poff[p]: message f of publisher p reads csr_tgt[pdelta + f]
     uint32_t prange[2];
-    uint32_t pre[ORL_FAN_PF ? kRouteThreads : 1];  // the CSR-target prefetch slots (lane-linear per wave)
+    uint32_t pre[PF ? kRouteThreads : 1];  // the CSR-target prefetch slots (lane-linear per wave)
 };
 
 // A fan-out tile's publishers [p_lo, p_hi] (a superset is fine: every f of the tile has poff[p_lo] <= f < poff[p_hi + 1]):
@@ -3376,7 +3386,8 @@ __global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
     uint32_t excl, uint32_t* __restrict__ route,
     uint32_t* __restrict__ act_out, uint16_t* __restrict__ tile_cnt, uint32_t bins, uint32_t shift, uint32_t items,
     const uint32_t* __restrict__ fblk, uint32_t* __restrict__ col_atomic) {
-    __shared__ FanSmem<HB> sm;
+    constexpr bool PF = fan_pf<PW, U>();
+    __shared__ FanSmem<HB, PF> sm;
     constexpr bool HIST = HB > 0;
     stage_params(&sm.P, gp);
     if (HIST)
@@ -3398,7 +3409,7 @@ __global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
     __syncthreads();
     const uint32_t p_lo = fan ? sm.prange[0] : 0u, p_hi = fan ? sm.prange[1] : 0u;
     const uint32_t span = p_hi - p_lo + 1;  // publishers touching this tile
-    const bool in_lds = span <= kFanLds;
+    const bool in_lds = span <= fan_lds_pubs<PF>();
     if (in_lds && fan) fan_stage(poff32, pstart, p_lo, span, sm.poff, sm.pdelta);
     __syncthreads();
     const uint32_t n_act = sm.P.n_act;
@@ -3410,7 +3421,6 @@ __global__ __launch_bounds__(kRouteThreads) ORL_FAN_ATTR void k_fanout_route(
     // PF (U = 1, round 6): the next message's publisher search runs during this one's step and its CSR target comes by
     // LDS-DMA (4 B per lane into the wave's slots), so the chain per message is CSR target ‖ probe instead of CSR target
     // → probe; the route / act stores of a message are issued after the next step's wait (as k_route's prefetch).
-    constexpr bool PF = ORL_FAN_PF && U == 1;
     uint32_t* const fslot = sm.pre + (PF ? (threadIdx.x & ~63u) : 0u);
     const uint32_t flane = threadIdx.x & 63u;
     auto fan_ci = [&](uint32_t ee, uint64_t& ci, uint32_t& pq) -> bool {  // message ee's CSR entry and publisher
