@@ -721,7 +721,7 @@ int ensure_staging(orl_ctx* c, size_t in_bytes, size_t out_words) {
 void free_device(orl_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_table); f(c->d_probe); f(c->d_probe8); f(c->d_probe_bad); f(c->d_params); f(c->d_rank_of_silo); f(c->d_claim); f(c->d_dirstate); f(c->d_dslot); f(c->d_vr_hash); f(c->d_vr_silo); f(c->d_silo_hash); f(c->d_silo_known); f(c->d_dflag); f(c->d_cache); f(c->d_cclaim); f(c->d_cstate); f(c->d_silo_tab); f(c->d_decode_flag); f(c->d_silo_words); f(c->d_gt); f(c->d_gt_blob); f(c->d_stamp_sizes); f(c->d_stamp_temp); f(c->d_patch_data); f(c->d_csr_off); f(c->d_csr_tgt); f(c->d_ext_table); f(c->d_ext_blob); f(c->d_ext_claim); f(c->d_ext_state);
-    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk);
+    f(c->s.pairs_a); f(c->s.pairs_b); f(c->s.idx_a); f(c->s.sorted_keys); f(c->s.tile_hist); f(c->s.tile_cnt); f(c->s.scan_sums); f(c->s.digits); f(c->s.col_sums); f(c->s.col_tot); f(c->s.seg_hist); f(c->s.seg_carry); f(c->s.seg_meta); f(c->s.seg_lb); f(c->s.seg_lbctl); f(c->s.bstart); f(c->s.sstart); f(c->s.gap_q); f(c->s.hot); f(c->s.hot_rows); f(c->s.hot_bmax); f(c->s.pick_word); f(c->s.fan_blk); f(c->s.lsd_hot);
     for (auto& L : c->s.lb) {
         f(L.state);
         if (L.ev) (void)hipEventDestroy(L.ev);
@@ -853,6 +853,8 @@ int orl_ctx_create(const orl_config* cfg, orl_ctx** out) {
             if ((e = hipEventCreateWithFlags(&L.ev, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate(lb)");
         }
         // (zeroed once: later launches tag their granules with an epoch and number tiles from a host-mirrored ticket)
+        if (const char* lh = getenv("ORL_LSD_HOT"); lh && lh[0] == '1')  // the LSD plan's hot-key path: opt-in
+            if ((e = hipMalloc((void**)&c->s.lsd_hot, 16)) != hipSuccess) return bail(e, "hipMalloc(lsd_hot)");
         if ((e = hipMalloc((void**)&c->s.s4_err, 4)) != hipSuccess) return bail(e, "hipMalloc(s4_err)");
         if ((e = hipMemset(c->s.s4_err, 0, 4)) != hipSuccess) return bail(e, "hipMemset(s4_err)");
         // the LSD plan's single-sweep passes (opt-in, ORL_LSD_SWEEP=1 at context creation: measured 8x slower than the

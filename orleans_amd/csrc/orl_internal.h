@@ -292,6 +292,7 @@ struct Scratch {
     unsigned long long* hot_bmax = nullptr;  // [offset-scan chunks] per-chunk max of (count << 32 | key)
     unsigned long long* pick_word = nullptr; // the fused level-2 pick's max of (count << 32 | key), zero between batches
     uint32_t* hot_rows = nullptr;      // [rows + chunks] the hot key's count per histogram row, then its exclusive prefix
+    uint32_t* lsd_hot = nullptr;       // [4] the LSD plan's hot-key path: {hot key, its messages hc, n - hc, -}
     uint32_t* hot_host = nullptr;      // mapped pinned host words: [0] the last pick's key (the launcher's hot-key hint), [1]
                                        // the last two-level plan's skew flag (k_seg_count_scan writes it): it picks the fused
                                        // level-2 kernel's solo form (no segment-scan launches) in launch_seg_bits

@@ -1277,7 +1277,10 @@ template <bool ACTS, bool DIG8 = false>
 __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
                                                     uint32_t bins, uint16_t* __restrict__ tile_cnt,
                                                     const uint32_t* __restrict__ hot_words = nullptr,
-                                                    uint32_t* __restrict__ hot_rows = nullptr) {
+                                                    uint32_t* __restrict__ hot_rows = nullptr,
+                                                    const uint32_t* __restrict__ n_dev = nullptr) {
+    // n_dev (the LSD plan's hot-key path): the pairs the first pass wrote, n minus the hot key's messages (device word)
+    if (n_dev) n = min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(n_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), n);
     __shared__ uint32_t hist[1u << kMaxDigitBits];
     __shared__ uint32_t hot;
     for (uint32_t b = threadIdx.x; b < bins; b += 256) hist[b] = 0;
@@ -1339,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {  // unconditional (clamped) loads: all 16 in flight at once
             const uint32_t e = base + j * 256 + threadIdx.x;
-            k[j] = ld_s4(static_cast<const uint2*>(in) + (e < n ? e : n - 1)).x;
+            k[j] = ld_s4(static_cast<const uint2*>(in) + (e < n ? e : (n ? n - 1 : 0u))).x;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
@@ -1677,18 +1680,24 @@ __device__ __forceinline__ void write_gap(uint32_t* __restrict__ offsets, uint32
 // hot_rows (IN_ACT + OUT_PAIR only; col_scan'ed per-row hot counts): the hot key's elements are not ranked; their indices
 // go to hot_idx[hot_rows[the tile's first row] + rank among the tile's hot elements] (arrival order): one run at the front
 // of hot_idx.
+// lsd_hot (the LSD plan's hot-key path, round 6; IN_PAIR passes): {hot key, its message count hc, n - hc}: the pairs are
+// the first pass's n - hc non-hot ones, and the last pass places a key above the hot one hc further (its run goes there).
 template <int BITS, int IN, int OUT, int ITEMS, int RM>
-__global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n, uint32_t n_act, uint32_t shift,
+__global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in, uint32_t n_all, uint32_t n_act, uint32_t shift,
                                                     const uint32_t* __restrict__ tile_off, uint32_t row_step, uint32_t ntiles,
                                                     uint2* __restrict__ pair_out, uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ key_out, const uint32_t* __restrict__ hot_words,
                                                     const uint32_t* __restrict__ hot_rows, uint32_t* __restrict__ hot_idx,
                                                     uint32_t* __restrict__ offsets, uint32_t nb, uint32_t* __restrict__ gap_q,
-                                                    uint32_t gap_cap, uint32_t dsel) {
+                                                    uint32_t gap_cap, uint32_t dsel, const uint32_t* __restrict__ lsd_hot) {
     constexpr uint32_t B = 1u << BITS;
     constexpr uint32_t PER = kDigitsPerThread<BITS>;
     constexpr uint32_t TILE = 256u * ITEMS;
-    constexpr bool HOTP = IN == IN_ACT && OUT == OUT_PAIR;
+    constexpr bool HOTP = IN == IN_ACT && (OUT == OUT_PAIR || OUT == OUT_PAIR_DIG);
+    const bool lh = IN != IN_ACT && lsd_hot != nullptr;
+    const uint32_t lhk = lh ? __builtin_amdgcn_readfirstlane(lsd_hot[0]) : kNoHotKey;
+    const uint32_t lhc = lh ? __builtin_amdgcn_readfirstlane(lsd_hot[1]) : 0u;
+    const uint32_t n = lh ? min(__builtin_amdgcn_readfirstlane(lsd_hot[2]), n_all) : n_all;
     __shared__ PassSmem<BITS, ITEMS> sm;
     __shared__ uint32_t hotw[kWaves];
     const uint32_t rflags = rank_flags();
@@ -1704,7 +1713,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t e = wbase + j * 64u + lane;
-        const uint32_t ec = e < n ? e : n - 1;
+        const uint32_t ec = e < n ? e : (n ? n - 1 : 0u);
         if (IN == IN_ACT) {
             key[j] = bucket_key(ld_s4(static_cast<const uint32_t*>(in) + ec), n_act);
             idx[j] = e;
@@ -1785,7 +1794,7 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
     for (uint32_t q = 0; q < PER; ++q)
         if (threadIdx.x * PER + q < B) delta[threadIdx.x * PER + q] = dl[q];
     __syncthreads();
-    const uint32_t cnt = ((n - tbase) < TILE ? (n - tbase) : TILE) - tile_hot;
+    const uint32_t cnt = (n > tbase ? min(n - tbase, TILE) : 0u) - tile_hot;
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t i = j * 256u + threadIdx.x;
@@ -1796,7 +1805,8 @@ __global__ __launch_bounds__(256) void k_radix_pass(const void* __restrict__ in,
                 const uint32_t d = (kv.x >> shift) & (B - 1u);
                 g = delta[d] + i;
                 if (g < n) {
-                    order_out[g] = kv.y;
+                    const uint32_t ga = g + (kv.x > lhk && lhk != kNoHotKey ? lhc : 0u);  // after the hot key's run
+                    if (ga < n_all) order_out[ga] = kv.y;
                     if (i > 0) {
                         const uint32_t pk = sm.stage[i - 1u].x;
                         if (((pk >> shift) & (B - 1u)) == d && pk < kv.x) {  // a digit's first key in the tile: k_bound_apply
@@ -5248,6 +5258,58 @@ __global__ __launch_bounds__(256) void k_hot_tail(const uint32_t* __restrict__ h
     for (; i < cnt; i += stride) order[off + i] = hot_idx[i];
 }
 
+// ---- the LSD plan's hot-key path (round 6): the previous batch's most frequent activation skips the later passes ---------
+// k_route counts its messages per row instead of their digit (hot_rows), the first pass writes their indices to a run in
+// arrival order (HOTP), the later passes sort the n - hc others, the last pass leaves a gap of hc after the keys below it,
+// and after the offsets: the offsets above the hot key + hc, the run copied into the gap (k_hot_tail), the next pick.
+// out = {hot key, hc, n - hc} from the first pass's hot column total (kNoHotKey / 0 / n without a hot key).
+__global__ void k_lsd_hot_prep(const uint32_t* __restrict__ hot_words, const uint32_t* __restrict__ hot_total, uint32_t n,
+                               uint32_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const uint32_t hk = hot_key_of(hot_words);
+    const uint32_t hc = hk == kNoHotKey ? 0u : min(*hot_total, n);
+    out[0] = hk;
+    out[1] = hc;
+    out[2] = n - hc;
+}
+
+// offsets[b] += hc for the buckets above the hot key (b in (hk, nb)): the offsets were those of the n - hc others.
+__global__ __launch_bounds__(256) void k_lsd_hot_fix(uint32_t* __restrict__ offsets, uint32_t nb, const uint32_t* __restrict__ lh) {
+    const uint32_t hk = __builtin_amdgcn_readfirstlane(lh[0]), hc = __builtin_amdgcn_readfirstlane(lh[1]);
+    if (hk == kNoHotKey || hc == 0) return;
+    for (uint32_t b = hk + 1u + blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) offsets[b] += hc;
+}
+
+// The next batch's hot key from the final offsets: the most frequent key of [0, nkeys) (count = offsets[b + 1] -
+// offsets[b]) folded into *pick_word as count << 32 | key; k_lsd_pick_finish applies k_scan_down's rule.
+__global__ __launch_bounds__(256) void k_lsd_pick(const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                                                  unsigned long long* __restrict__ pick_word) {
+    __shared__ unsigned long long wbest[kWaves];
+    unsigned long long best = 0;
+    for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nkeys; b += gridDim.x * 256u) {
+        const unsigned long long c = (unsigned long long)(offsets[b + 1] - offsets[b]) << 32 | b;
+        best = c > best ? c : best;
+    }
+    best = wave_max_u64(best);
+    if ((threadIdx.x & 63u) == 0) wbest[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic per workgroup (one per wave on one word: 105 us of contention per batch)
+        for (uint32_t q = 1; q < kWaves; ++q) best = wbest[q] > best ? wbest[q] : best;
+        if (best >> 32) atomicMax(pick_word, best);
+    }
+}
+
+__global__ void k_lsd_pick_finish(unsigned long long* __restrict__ pick_word, uint32_t n, uint32_t* __restrict__ next_key,
+                                  uint32_t* __restrict__ host_word) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long best = *pick_word;
+    *pick_word = 0;
+    const uint32_t c = (uint32_t)(best >> 32), k = (uint32_t)best;
+    const uint32_t key = ((uint64_t)c * kHotShare >= n && c >= kHotMinCount) ? k : kNoHotKey;
+    __hip_atomic_store(next_key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_word) __hip_atomic_store(host_word, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Messages per thread of a route launch feeding stage 4 for n_act activations: the MSD tile of the two-level path,
 // else the LSD tile.
 uint32_t max_route_items(uint32_t n_act) {
@@ -5295,11 +5357,11 @@ template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                       const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx, uint32_t* offsets, uint32_t nb,
-                      uint32_t* gap_q, uint32_t gap_cap, uint32_t dsel) {
+                      uint32_t* gap_q, uint32_t gap_cap, uint32_t dsel, const uint32_t* lsd_hot) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
                                                 row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx, offsets, nb,   \
-                                                gap_q, gap_cap, dsel)
+                                                gap_q, gap_cap, dsel, lsd_hot)
 #define ORL_RP(I, O, IT) do { const int rm_ = rm; if (rm_ == kRmPlain) ORL_RP3(I, O, IT, kRmPlain);                      \
                               else if (rm_ == kRmHot) ORL_RP3(I, O, IT, kRmHot); else ORL_RP3(I, O, IT, kRmBallot); } while (0)
     if (in == IN_ACT) {  // the MSD pass of the two-level path (kMsdItems) or the first LSD pass (kItems)
@@ -5329,10 +5391,10 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                  const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr,
                  uint32_t* offsets = nullptr, uint32_t nb = 0, uint32_t* gap_q = nullptr, uint32_t gap_cap = 0,
-                 uint32_t dsel = 0) {
+                 uint32_t dsel = 0, const uint32_t* lsd_hot = nullptr) {
     switch (bits) {
 #define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
-                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap, dsel); break;
+                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap, dsel, lsd_hot); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -5579,6 +5641,14 @@ bool lsd_digits() {
 
 // The hot-key path (kNoHotKey) runs on batches of >= kHotMinBatch messages of the two-level plan with an MSD pass and pair
 // layout; ORL_NO_HOT=1 turns it off (A/B).
+// The LSD plan's last pass writes the bucket offsets itself (OUT_FINAL_GAPS) when its keys' low part fits the 16-bit halves
+// of FL and the batch is dense in buckets (>= 2 messages per bucket): config 3 (16 per bucket) 7.77 -> 7.62 ms, but config 4
+// (0.7 per bucket: most of 10M offsets are gaps that cross tiles, k_bound_apply's share) 0.392 -> 0.436 ms, where
+// k_offsets_gaps' LDS spans stay faster (profiles/r06m_config4_lsd_ab.txt).
+bool lsd_gaps(const RadixPlan& plan, uint64_t n, uint32_t n_act) {
+    return lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16 && n >= 2ull * (n_act + 2ull);
+}
+
 bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
     static const bool off = [] {
         const char* e = getenv("ORL_NO_HOT");
@@ -5586,7 +5656,11 @@ bool hot_path_on(uint64_t n, uint32_t n_act, const Scratch& s) {
     }();
     if (off || !s.hot || n < kHotMinBatch || stage4_soa()) return false;
     const BucketPlan bp = make_bucket_plan(n_act);
-    return bp.two_level && bp.hb > 0;
+    if (bp.two_level) return bp.hb > 0;
+    // the LSD plan's hot-key path: opt-in (ORL_LSD_HOT=1 at context creation allocates s.lsd_hot), measured slower at
+    // config 3 (7.22 -> 7.28 ms, profiles/r06t_lsd_hot_ab.txt): the hot key's elements are the cheapest ones of an LSD
+    // pass (long one-digit runs, coalesced stores), so skipping them saves less than the run, the fix-up and the pick cost
+    return s.lsd_hot && !lsd_sweep(s) && lsd_gaps(bp.lsd, n, n_act);
 }
 
 // Whether the last pick (the tail kernel of an earlier batch, mirrored to mapped host memory) found a hot key: a batch
@@ -5640,11 +5714,11 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     if (lsd_sweep(s)) return bucket_lsd_sweep(d_act, n, n_act, d_order, d_offsets, s, st);
     const RadixPlan& plan = bp.lsd;
     const uint32_t row_step0 = kItems / route_items;
-    // the last pass writes the bucket offsets itself (round 6) when its keys' low part fits the 16-bit halves of FL and the
-    // batch is dense in buckets (>= 2 messages per bucket): config 3 (16 per bucket) 7.77 -> 7.62 ms, but config 4 (0.7 per
-    // bucket: most of 10M offsets are gaps that cross tiles, k_bound_apply's share) 0.392 -> 0.436 ms, where k_offsets_gaps'
-    // LDS spans stay faster (profiles/r06m_config4_lsd_ab.txt)
-    const bool gaps = lsd_fused_offsets() && !offsets_sufmin() && plan.shift[plan.passes - 1] <= 16 && n >= 2ull * nb;
+    const bool gaps = lsd_gaps(plan, n, n_act);
+    // the hot-key path (hot_path_on: only with the fused offsets); pick: the next batch's key from this batch's offsets
+    const bool lhot = hot && gaps && s.lsd_hot;
+    const bool lpick = pick && gaps && s.lsd_hot;
+    const uint32_t* hw = hot_cur(s);
     uint2* pbuf[2] = {s.pairs_a, s.pairs_b};
     // the digit stream (OUT_PAIR_DIG) lives in sorted_keys (>= n bytes), read by the next histogram before the last pass
     // writes sorted_keys / the FL rows there
@@ -5654,21 +5728,26 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t bins = 1u << plan.bits[p];
         const uint32_t row_step = (p == 0) ? row_step0 : 1u;
         const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
+        const uint32_t* n_dev = (p > 0 && lhot) ? s.lsd_hot + 2 : nullptr;
         if (p > 0 && have_dig)
             hipLaunchKernelGGL((k_hist_pairs<false, true>), dim3(ntiles), dim3(256), 0, st, dig, n, n_act, 0u, bins, s.tile_cnt,
-                               nullptr, nullptr);
+                               nullptr, nullptr, n_dev);
         else if (p > 0)
             hipLaunchKernelGGL(k_hist_pairs<false>, dim3(ntiles), dim3(256), 0, st, pbuf[(p - 1) & 1], n, n_act,
-                               (uint32_t)plan.shift[p], bins, s.tile_cnt, nullptr, nullptr);
-        col_scan(s.tile_hist, nrows, bins, row_step, s, st, nullptr, 0, 0, p == 0 && self_cols);
+                               (uint32_t)plan.shift[p], bins, s.tile_cnt, nullptr, nullptr, n_dev);
+        col_scan(s.tile_hist, nrows, bins, row_step, s, st, (p == 0 && lhot) ? s.hot_rows : nullptr, 0, 0, p == 0 && self_cols);
+        if (p == 0 && lhot)  // {hot key, hc, n - hc} before the later passes' column scans reuse col_tot
+            hipLaunchKernelGGL(k_lsd_hot_prep, dim3(1), dim3(64), 0, st, hw, s.col_tot + bins, n, s.lsd_hot);
         const bool last = p == plan.passes - 1;
         const bool wdig = !last && lsd_digits() && plan.bits[p + 1] <= 8;
         const void* kin = (p == 0) ? static_cast<const void*>(d_act) : static_cast<const void*>(pbuf[(p - 1) & 1]);
         const int out = !last ? (wdig ? OUT_PAIR_DIG : OUT_LSD_PAIR) : gaps ? OUT_FINAL_GAPS : OUT_FINAL;
         const uint32_t dsel = wdig ? (uint32_t)plan.shift[p + 1] | ((uint32_t)plan.bits[p + 1] << 8) : 0u;
+        const bool hp = p == 0 && lhot;  // the first pass writes the hot key's indices to its run (idx_a: free in stage 4)
         launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, out, kin, n, n_act, (uint32_t)plan.shift[p],
                     s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, wdig ? reinterpret_cast<uint32_t*>(dig) : s.sorted_keys,
-                    st, nullptr, nullptr, nullptr, d_offsets, nb, s.gap_q, s.gap_cap, dsel);
+                    st, hp ? hw : nullptr, hp ? s.hot_rows : nullptr, hp ? s.idx_a : nullptr, d_offsets, nb, s.gap_q, s.gap_cap,
+                    dsel, (p > 0 && lhot) ? s.lsd_hot : nullptr);
         have_dig = wdig;
     }
     if (gaps) {  // the buckets the last pass could not see from inside a tile (k_bound_last), then the digits' tails
@@ -5680,6 +5759,19 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
                            (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
         hipLaunchKernelGGL(k_sweep_tail, dim3(bins), dim3(256), 0, st, s.col_tot, s.sorted_keys + (size_t)ntiles * bins,
                            (uint32_t)plan.bits[lp], (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap, nullptr);
+        if (lhot) {  // the offsets above the hot key + hc, then its run into the gap the last pass left
+            hipLaunchKernelGGL(k_lsd_hot_fix, dim3(std::min<uint32_t>(ceil_div(nb, 256u * 16u), 2048u)), dim3(256), 0, st, d_offsets,
+                               nb, s.lsd_hot);
+            hipLaunchKernelGGL(k_hot_tail, dim3(std::min<uint32_t>(ceil_div(n / 4u, 256u * kTailUnroll), 2048u)), dim3(256), 0,
+                               st, hw, s.lsd_hot + 1, n, n_act + 1, s.idx_a, d_offsets, d_order);
+        }
+        if (lpick) {  // the next batch's hot key (flips the slots: hw stays this batch's)
+            hipLaunchKernelGGL(k_lsd_pick, dim3(std::min<uint32_t>(ceil_div(n_act + 1u, 256u * 16u), 512u)), dim3(256), 0, st,
+                               d_offsets, n_act + 1u, s.pick_word);
+            hipLaunchKernelGGL(k_lsd_pick_finish, dim3(1), dim3(64), 0, st, s.pick_word, n, s.hot + ((s.hot_parity + 1u) & 1u),
+                               s.hot_host_dev);
+            s.hot_parity ^= 1u;
+        }
         return (int)hipGetLastError();
     }
     if (offsets_sufmin()) {  // A/B: the five-launch form (fill, mark, suffix minima)

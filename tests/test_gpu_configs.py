@@ -918,13 +918,16 @@ def test_lsd_offsets_long_gaps_vs_oracle(torch, monkeypatch, cap):
     eng.close()
 
 
-def test_lsd_fused_offsets_dense_vs_oracle(torch):
+@pytest.mark.parametrize("lsd_hot", ["0", "1"])
+def test_lsd_fused_offsets_dense_vs_oracle(torch, monkeypatch, lsd_hot):
     """The LSD plan's last pass writing the bucket offsets itself (round 6: OUT_FINAL_GAPS + k_bound_last / k_bound_scan /
     k_bound_apply + k_sweep_tail), taken when a batch has >= 2 messages per bucket (config 3's shape; sparser batches keep
     k_offsets_gaps).  n_act 8.5M (24-bit keys: 8 + 8 + 8-bit digits), batches of 18-20M messages: uniform, Zipf-hot (one key
     with millions of messages), a few keys with millions of empty buckets between and around them, the unresolved bucket,
     keys only in the low half, and the digit stream (OUT_PAIR_DIG) feeding each later histogram.  Order and offsets == the
-    oracle's stable bucketing (ActivationData.cs:483-514).  (The sparse form: test_lsd_offsets_long_gaps_vs_oracle.)"""
+    oracle's stable bucketing (ActivationData.cs:483-514).  (The sparse form: test_lsd_offsets_long_gaps_vs_oracle.)  Batches
+    of one shape come in pairs: with the LSD hot-key path on (ORL_LSD_HOT=1 at context creation: opt-in) the
+    second takes it on the key the first picked (ORL_Q_HOT_BATCHES)."""
     t = torch
     n_act = 8_500_000
     n = 2 * (n_act + 2) + 1000
@@ -935,12 +938,18 @@ def test_lsd_fused_offsets_dense_vs_oracle(torch):
         r = np.minimum(rng.zipf(1.1, k), n_act) - 1
         return ((r.astype(np.uint64) * np.uint64(2654435761)) % np.uint64(n_act)).astype(np.uint32)
 
+    few = np.array([3, 4, 4_000_000, 4_000_001, 8_400_000], np.uint32)
+    unres = lambda: np.where(rng.random(n) < 0.3, np.uint32(L.NO_ACT), zipf(n)).astype(np.uint32)  # noqa: E731
+    # consecutive batches of one shape: the second runs the hot-key path (round 6) on the key the first one picked —
+    # Zipf's top key (keys above and below it), one of a few keys, the unresolved bucket (the largest key)
     batches = [rng.integers(0, n_act, n, dtype=np.int64).astype(np.uint32),
-               zipf(n),
-               rng.choice(np.array([3, 4, 4_000_000, 4_000_001, 8_400_000], np.uint32), n),
-               np.where(rng.random(n) < 0.3, np.uint32(L.NO_ACT), zipf(n)).astype(np.uint32),
+               zipf(n), zipf(n),
+               rng.choice(few, n), rng.choice(few, n),
+               unres(), unres(),
                rng.integers(0, n_act // 2, n, dtype=np.int64).astype(np.uint32)]
+    monkeypatch.setenv("ORL_LSD_HOT", lsd_hot)  # read at context creation
     eng = GrainDirectoryEngine(n_act=n_act, dir_capacity=1024, max_batch=n, device=0)
+    monkeypatch.delenv("ORL_LSD_HOT")
     W.setup_engine(eng, W.default_cluster())
     off = t.empty(n_act + 2, dtype=t.int32, device="cuda")
     order = t.empty(n, dtype=t.int32, device="cuda")
@@ -953,6 +962,10 @@ def test_lsd_fused_offsets_dense_vs_oracle(torch):
         eo, ef = o.bucket(a, n_act)
         np.testing.assert_array_equal(_u32(order), eo, err_msg=f"batch {k} order")
         np.testing.assert_array_equal(_u32(off), ef, err_msg=f"batch {k} offsets")
+    if lsd_hot == "1":
+        assert eng.query(L.Q_HOT_BATCHES) >= 3  # the second batch of each pair ran the hot-key path
+    else:
+        assert eng.query(L.Q_HOT_BATCHES) == 0
     eng.close()
 
 
