@@ -2978,8 +2978,17 @@ __device__ __forceinline__ void seg_chunks(const void* __restrict__ in, uint32_t
 // bucket to ONE workgroup).  direct (solo, no hot-key path): the bucket's per-key totals are written as the final bucket
 // offsets (bstart[b] + the exclusive prefix inside the bucket), so no offsets scan follows.  pick_word (direct, a batch
 // large enough for the hot-key pick): each bucket also folds its most frequent key of [0, nkeys) into *pick_word.
+// k_seg_count_scan at 7 workgroups per CU (round 6): left alone it took 79 VGPRs and 106 SGPRs (6 per CU); held to 72 VGPRs
+// (1-4 spilled) and 94 SGPRs: config 2 1.897 -> 1.890 ms, the hot rank's route + stage 4 at 8 ranks 1.178 -> 1.155 ms
+// (profiles/r06v_seg_count_scan_occupancy_ab.txt).  ORL_SEGCS_MINW=1 and an empty ORL_SEGCS_ATTR restore it (lab A/B).
+#ifndef ORL_SEGCS_MINW
+#define ORL_SEGCS_MINW 7
+#endif
+#ifndef ORL_SEGCS_ATTR
+#define ORL_SEGCS_ATTR __attribute__((amdgpu_num_sgpr(96)))
+#endif
 template <int LB, int IN>
-__global__ __launch_bounds__(256) void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
+__global__ __launch_bounds__(256, ORL_SEGCS_MINW) ORL_SEGCS_ATTR void k_seg_count_scan(const void* __restrict__ in, uint32_t n_total, uint32_t n_act,
                                                         uint32_t nbk, uint32_t nb, uint32_t seg,
                                                         const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ sstart,
                                                         uint32_t* __restrict__ seg_hist, uint32_t* __restrict__ counts,
