@@ -2556,6 +2556,79 @@ __global__ __launch_bounds__(256) void k_bound_apply(const uint32_t* __restrict_
     }
 }
 
+// The same two kernels with the chunk's FL / M rows staged through LDS (round 6): lane = tile reads a column of the
+// [ntiles][bins] matrices, 1 KB between lanes (64 lines per load instruction); here a 64-tile x 16-digit block is loaded
+// row-wise (16 B per thread, 64 B per tile row) and read column-wise from LDS.  bins a multiple of 16.
+constexpr uint32_t kBoundCols = 16;
+__device__ __forceinline__ void bound_stage(const uint32_t* __restrict__ A, uint32_t ntiles, uint32_t bins, uint32_t d0,
+                                            uint32_t fill, uint32_t (*sA)[kScanRows + 1]) {
+    const uint32_t tl = threadIdx.x >> 2, k4 = (threadIdx.x & 3u) * 4u;
+    const uint32_t t = blockIdx.x * kScanRows + tl;
+    uint4 v = make_uint4(fill, fill, fill, fill);
+    if (t < ntiles) v = *reinterpret_cast<const uint4*>(A + (size_t)t * bins + d0 + k4);
+    sA[k4][tl] = v.x;
+    sA[k4 + 1][tl] = v.y;
+    sA[k4 + 2][tl] = v.z;
+    sA[k4 + 3][tl] = v.w;
+}
+
+__global__ __launch_bounds__(256) void k_bound_last_t(const uint32_t* __restrict__ FL, uint32_t ntiles, uint32_t bins,
+                                                      uint32_t* __restrict__ S) {
+    __shared__ uint32_t sF[kBoundCols][kScanRows + 1];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    for (uint32_t d0 = 0; d0 < bins; d0 += kBoundCols) {
+        bound_stage(FL, ntiles, bins, d0, kFlEmpty, sF);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kBoundCols / kWaves; ++k) {
+            const uint32_t c = w * (kBoundCols / kWaves) + k;
+            const uint32_t v = sF[c][lane];
+            const uint64_t m = __ballot(fl_has(v));
+            const uint32_t hl = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+            const uint32_t l = (uint32_t)__shfl((int)(v >> 16), (int)hl, 64);
+            if (lane == 0) S[(size_t)blockIdx.x * bins + d0 + c] = m ? l : kFlNone;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bound_apply_t(const uint32_t* __restrict__ FL, const uint32_t* __restrict__ M,
+                                                       const uint32_t* __restrict__ P, uint32_t ntiles, uint32_t bins,
+                                                       uint32_t shift, uint32_t nb, uint32_t* __restrict__ offsets,
+                                                       uint32_t* __restrict__ q, uint32_t cap) {
+    __shared__ uint32_t sF[kBoundCols][kScanRows + 1];
+    __shared__ uint32_t sM[kBoundCols][kScanRows + 1];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t below = lanes_below();
+    for (uint32_t d0 = 0; d0 < bins; d0 += kBoundCols) {
+        bound_stage(FL, ntiles, bins, d0, kFlEmpty, sF);
+        bound_stage(M, ntiles, bins, d0, 0u, sM);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kBoundCols / kWaves; ++k) {
+            const uint32_t c = w * (kBoundCols / kWaves) + k, d = d0 + c;
+            const uint32_t v = sF[c][lane], mv = sM[c][lane];
+            const uint32_t pv = P[(size_t)blockIdx.x * bins + d];
+            const bool has = fl_has(v);
+            const uint64_t lower = __ballot(has) & below;
+            const uint32_t src = lower ? 63u - (uint32_t)__builtin_clzll(lower) : lane;
+            const uint32_t pl = (uint32_t)__shfl((int)(v >> 16), (int)src, 64);
+            const uint32_t prev = lower ? pl : pv;
+            uint32_t lo = 0, len = 0;
+            if (has) {
+                const uint32_t first = v & 0xFFFFu;
+                const uint32_t from = prev == kFlNone ? 0u : prev + 1u;  // the first bucket of the digit not started yet
+                if (first >= from) {
+                    lo = (d << shift) + from;
+                    len = lo < nb ? min(first - from + 1u, nb - lo) : 0u;
+                }
+            }
+            write_gap(offsets, lo, len, mv, q, cap);
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Stage 4, two-level path (keys of <= 22 bits; BucketPlan in orl_internal.h).  After the MSD pass the
 // messages are grouped by bucket b = key >> lb (stable), so each bucket is a contiguous range
@@ -5694,6 +5767,15 @@ bool offsets_sufmin() {
 }
 
 
+// The fused offsets' bound kernels with LDS-staged rows (k_bound_*_t); ORL_BOUND_STAGED=0: column loads (A/B).
+bool bound_staged() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_BOUND_STAGED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // The digit stream's histogram, one wave per tile (k_hist_dig8_wave); ORL_DIG8_WAVE=0: one workgroup per tile (A/B).
 bool dig8_wave() {
     static const bool on = [] {
@@ -5830,10 +5912,16 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     if (gaps) {  // the buckets the last pass could not see from inside a tile (k_bound_last), then the digits' tails
         const int lp = plan.passes - 1;
         const uint32_t bins = 1u << plan.bits[lp], nch = ceil_div(ntiles, kScanRows);
-        hipLaunchKernelGGL(k_bound_last, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
+        const bool bt = bins % kBoundCols == 0 && bound_staged();
+        if (bt) hipLaunchKernelGGL(k_bound_last_t, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
+        else hipLaunchKernelGGL(k_bound_last, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
         hipLaunchKernelGGL(k_bound_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.sorted_keys + (size_t)ntiles * bins);
-        hipLaunchKernelGGL(k_bound_apply, dim3(nch), dim3(256), 0, st, s.sorted_keys, s.tile_hist, s.col_sums, ntiles, bins,
-                           (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
+        if (bt)
+            hipLaunchKernelGGL(k_bound_apply_t, dim3(nch), dim3(256), 0, st, s.sorted_keys, s.tile_hist, s.col_sums, ntiles, bins,
+                               (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
+        else
+            hipLaunchKernelGGL(k_bound_apply, dim3(nch), dim3(256), 0, st, s.sorted_keys, s.tile_hist, s.col_sums, ntiles, bins,
+                               (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
         hipLaunchKernelGGL(k_sweep_tail, dim3(bins), dim3(256), 0, st, s.col_tot, s.sorted_keys + (size_t)ntiles * bins,
                            (uint32_t)plan.bits[lp], (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap, nullptr);
         if (lhot) {  // the offsets above the hot key + hc, then its run into the gap the last pass left
