@@ -1454,6 +1454,10 @@ __global__ __launch_bounds__(256) void k_col_sum(const uint16_t* __restrict__ C,
 // serialised plan cost more than the launch.)
 // hot_rows (stage 4's hot-key path): one more block scans the hot column's chunk sums (hot_rows[nrows + c]) in place
 // and writes their total to T[bins].
+#ifndef ORL_COL_SCAN_COLS
+#define ORL_COL_SCAN_COLS 4
+#endif
+constexpr uint32_t kColScanCols = ORL_COL_SCAN_COLS, kColScanGroups = 256 / kColScanCols;
 __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
                                                   uint32_t* __restrict__ T, uint32_t* __restrict__ hot_rows, uint32_t nrows) {
     __shared__ uint32_t part[16][17];
@@ -1473,22 +1477,29 @@ __global__ __launch_bounds__(256) void k_col_scan(uint32_t* __restrict__ S, uint
         if (threadIdx.x == 0) T[bins] = total;
         return;
     }
-    const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
-    const uint32_t d = blockIdx.x * 16 + col;
-    const uint32_t per = (nchunks + 15) / 16;
-    const uint32_t c0 = grp * per, c1 = min(c0 + per, nchunks);
+    // kColScanCols columns per block, 256 / kColScanCols threads per column each owning a contiguous run of chunks, its
+    // loads unrolled (round 6: 16 columns x 16 threads left 16 workgroups walking 64 strided loads each, 25 us per scan
+    // at config 3; profiles/r06z_col_scan_ab.txt)
+    __shared__ uint32_t gpart[kColScanGroups][kColScanCols + 1];
+    const uint32_t col = threadIdx.x % kColScanCols, grp = threadIdx.x / kColScanCols;
+    const uint32_t d = blockIdx.x * kColScanCols + col;
+    const uint32_t per = (nchunks + kColScanGroups - 1) / kColScanGroups;
+    const uint32_t c0 = min(grp * per, nchunks), c1 = min(c0 + per, nchunks);
     uint32_t acc = 0;
-    if (d < bins)
+    if (d < bins) {
+#pragma unroll 8
         for (uint32_t c = c0; c < c1; ++c) acc += S[(size_t)c * bins + d];
-    part[grp][col] = acc;
+    }
+    gpart[grp][col] = acc;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
-    for (uint32_t g = 0; g < 16; ++g) {
-        const uint32_t v = part[g][col];
+    for (uint32_t g = 0; g < kColScanGroups; ++g) {
+        const uint32_t v = gpart[g][col];
         if (g < grp) pre += v;
         tot += v;
     }
     if (d < bins) {
+#pragma unroll 8
         for (uint32_t c = c0; c < c1; ++c) {
             const uint32_t v = S[(size_t)c * bins + d];
             S[(size_t)c * bins + d] = pre;
@@ -2482,24 +2493,27 @@ __global__ __launch_bounds__(256) void k_bound_last(const uint32_t* __restrict__
     }
 }
 
-// 16 columns per block, 16 threads per column each owning a contiguous run of chunks (k_col_scan's shape).
+// k_col_scan's shape: kColScanCols columns per block, 256 / kColScanCols threads per column each owning a contiguous run
+// of chunks.
 __global__ __launch_bounds__(256) void k_bound_scan(uint32_t* __restrict__ S, uint32_t nchunks, uint32_t bins,
                                                     uint32_t* __restrict__ gmax) {
-    __shared__ uint32_t part[16][17];
-    const uint32_t col = threadIdx.x & 15u, grp = threadIdx.x >> 4;
-    const uint32_t d = blockIdx.x * 16 + col;
-    const uint32_t per = (nchunks + 15) / 16;
-    const uint32_t c0 = grp * per, c1 = min(c0 + per, nchunks);
+    __shared__ uint32_t part[kColScanGroups][kColScanCols + 1];
+    const uint32_t col = threadIdx.x % kColScanCols, grp = threadIdx.x / kColScanCols;
+    const uint32_t d = blockIdx.x * kColScanCols + col;
+    const uint32_t per = (nchunks + kColScanGroups - 1) / kColScanGroups;
+    const uint32_t c0 = min(grp * per, nchunks), c1 = min(c0 + per, nchunks);
     uint32_t last = kFlNone;
-    if (d < bins)
+    if (d < bins) {
+#pragma unroll 8
         for (uint32_t c = c0; c < c1; ++c) {
             const uint32_t v = S[(size_t)c * bins + d];
             if (v != kFlNone) last = v;
         }
+    }
     part[grp][col] = last;
     __syncthreads();
     uint32_t run = kFlNone, all = kFlNone;
-    for (uint32_t g = 0; g < 16; ++g) {
+    for (uint32_t g = 0; g < kColScanGroups; ++g) {
         const uint32_t v = part[g][col];
         if (v != kFlNone) {
             if (g < grp) run = v;
@@ -2507,6 +2521,7 @@ __global__ __launch_bounds__(256) void k_bound_scan(uint32_t* __restrict__ S, ui
         }
     }
     if (d < bins) {
+#pragma unroll 8
         for (uint32_t c = c0; c < c1; ++c) {
             const uint32_t v = S[(size_t)c * bins + d];
             S[(size_t)c * bins + d] = run;
@@ -5609,8 +5624,8 @@ void col_scan(uint32_t* M, uint32_t ntiles, uint32_t bins, uint32_t row_step, co
     const uint32_t hy = hot_rows ? 1u : 0u;  // the hot column's extra grid row / block
     if (!self_sums || hot_rows || nch > kSelfScanChunks)
         hipLaunchKernelGGL(k_col_sum, dim3(nch, cb + hy), dim3(256), 0, st, C, ntiles, bins, s.col_sums, hot_rows);
-    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, 16) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot, hot_rows,
-                       ntiles);
+    hipLaunchKernelGGL(k_col_scan, dim3(ceil_div(bins, kColScanCols) + hy), dim3(256), 0, st, s.col_sums, nch, bins, s.col_tot,
+                       hot_rows, ntiles);
     const bool plan = plan_n > 0;
     hipLaunchKernelGGL(k_col_apply, dim3(nch + (plan ? 1u : 0u), ceil_div(bins, kApplyCols) + hy), dim3(256), 0, st, C, M, ntiles,
                        bins, s.col_sums, s.col_tot, row_step, hot_rows, plan_n, plan_seg, plan ? s.bstart : nullptr,
@@ -5915,7 +5930,8 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const bool bt = bins % kBoundCols == 0 && bound_staged();
         if (bt) hipLaunchKernelGGL(k_bound_last_t, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
         else hipLaunchKernelGGL(k_bound_last, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
-        hipLaunchKernelGGL(k_bound_scan, dim3(ceil_div(bins, 16)), dim3(256), 0, st, s.col_sums, nch, bins, s.sorted_keys + (size_t)ntiles * bins);
+        hipLaunchKernelGGL(k_bound_scan, dim3(ceil_div(bins, kColScanCols)), dim3(256), 0, st, s.col_sums, nch, bins,
+                           s.sorted_keys + (size_t)ntiles * bins);
         if (bt)
             hipLaunchKernelGGL(k_bound_apply_t, dim3(nch), dim3(256), 0, st, s.sorted_keys, s.tile_hist, s.col_sums, ntiles, bins,
                                (uint32_t)plan.shift[lp], nb, d_offsets, s.gap_q, s.gap_cap);
