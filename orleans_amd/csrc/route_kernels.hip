@@ -1368,9 +1368,12 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 // atomic to its wave's private 256-bin row in LDS, and the wave stores its tile's row — no workgroup barrier, a quarter of
 // the workgroups (the per-tile form spent its time in launch, zeroing and barriers: 0.15 ms per 256M for 256 MB read).
 // n_dev as k_hist_pairs.  bins <= 256.
+// Q: 16-B loads per lane (the tile is 64 x 16 x Q digits: 4096 for Q = 4, 3072 for the 12-item passes).
+template <uint32_t Q = 4>
 __global__ __launch_bounds__(256) void k_hist_dig8_wave(const uint8_t* __restrict__ dig, uint32_t n, uint32_t bins,
                                                         uint32_t ntiles, uint16_t* __restrict__ tile_cnt,
                                                         const uint32_t* __restrict__ n_dev) {
+    constexpr uint32_t PL = 16u * Q;  // digits per lane
     if (n_dev) n = min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(n_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), n);
     __shared__ uint32_t hist[kWaves][256];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -1379,27 +1382,27 @@ __global__ __launch_bounds__(256) void k_hist_dig8_wave(const uint8_t* __restric
     uint32_t* h = hist[w];
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) h[lane + 64u * q] = 0;
-    const uint32_t e0 = tile * kTile + lane * 64u;
-    uint32_t v[16];
-    if (e0 + 64u <= n) {
+    const uint32_t e0 = tile * (64u * PL) + lane * PL;
+    uint32_t v[4 * Q];
+    if (e0 + PL <= n) {
         const uint4* p = reinterpret_cast<const uint4*>(dig + e0);
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
+        for (uint32_t q = 0; q < Q; ++q) {
             const uint4 x = ld_s4(p + q);
             v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
         }
     } else {
 #pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) v[q] = 0;
-        for (uint32_t i = 0; e0 + i < n && i < 64u; ++i) v[i >> 2] |= (uint32_t)dig[e0 + i] << (8u * (i & 3u));
+        for (uint32_t q = 0; q < 4 * Q; ++q) v[q] = 0;
+        for (uint32_t i = 0; e0 + i < n && i < PL; ++i) v[i >> 2] |= (uint32_t)dig[e0 + i] << (8u * (i & 3u));
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the zeroed row before the wave's adds
-    const uint32_t m = e0 < n ? min(64u, n - e0) : 0u;
+    const uint32_t m = e0 < n ? min(PL, n - e0) : 0u;
     if (m) {
         uint32_t cur = v[0] & 0xFFu, len = 1;
 #pragma unroll
-        for (uint32_t i = 1; i < 64; ++i) {
+        for (uint32_t i = 1; i < PL; ++i) {
             if (i < m) {
                 const uint32_t b = (v[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
                 if (b == cur) {
@@ -5506,11 +5509,22 @@ uint32_t route_items(uint64_t n, uint32_t max_items, uint32_t min_wg = 0) {
     return items;
 }
 
+// The LSD plan's later passes in 3072-element tiles (round 6): their LDS image is 24 KB instead of 32, so 6 workgroups fit a
+// CU instead of 4 (the first pass keeps 4096: its rows are the route kernel's).  ORL_LSD_TILE12=0: 4096 (A/B).
+constexpr uint32_t kItems12 = 12;
+bool lsd_tile12() {
+    static const bool on = [] {
+        const char* e = getenv("ORL_LSD_TILE12");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int BITS>
 void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint32_t n_act, uint32_t shift, const uint32_t* toff,
                       uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                       const uint32_t* hot_words, const uint32_t* hot_rows, uint32_t* hot_idx, uint32_t* offsets, uint32_t nb,
-                      uint32_t* gap_q, uint32_t gap_cap, uint32_t dsel, const uint32_t* lsd_hot) {
+                      uint32_t* gap_q, uint32_t gap_cap, uint32_t dsel, const uint32_t* lsd_hot, uint32_t items) {
     const dim3 g(ntiles), b(256);
 #define ORL_RP3(I, O, IT, R) hipLaunchKernelGGL((k_radix_pass<BITS, I, O, IT, R>), g, b, 0, st, kin, n, n_act, shift, toff,    \
                                                 row_step, ntiles, pout, order, keys, hot_words, hot_rows, hot_idx, offsets, nb,   \
@@ -5530,9 +5544,11 @@ void launch_pass_bits(int rm, int in, int out, const void* kin, uint32_t n, uint
     } else if (out == OUT_PAIR || out == OUT_LSD_PAIR) {
         ORL_RP(IN_PAIR, OUT_PAIR, kItems);
     } else if (out == OUT_PAIR_DIG) {
-        ORL_RP(IN_PAIR, OUT_PAIR_DIG, kItems);
+        if (items == kItems12) ORL_RP(IN_PAIR, OUT_PAIR_DIG, kItems12);
+        else ORL_RP(IN_PAIR, OUT_PAIR_DIG, kItems);
     } else if (out == OUT_FINAL_GAPS) {
-        ORL_RP(IN_PAIR, OUT_FINAL_GAPS, kItems);
+        if (items == kItems12) ORL_RP(IN_PAIR, OUT_FINAL_GAPS, kItems12);
+        else ORL_RP(IN_PAIR, OUT_FINAL_GAPS, kItems);
     } else {
         ORL_RP(IN_PAIR, OUT_FINAL, kItems);
     }
@@ -5544,10 +5560,10 @@ void launch_pass(int rm, int bits, int in, int out, const void* kin, uint32_t n,
                  uint32_t row_step, uint32_t ntiles, uint2* pout, uint32_t* order, uint32_t* keys, hipStream_t st,
                  const uint32_t* hot_words = nullptr, const uint32_t* hot_rows = nullptr, uint32_t* hot_idx = nullptr,
                  uint32_t* offsets = nullptr, uint32_t nb = 0, uint32_t* gap_q = nullptr, uint32_t gap_cap = 0,
-                 uint32_t dsel = 0, const uint32_t* lsd_hot = nullptr) {
+                 uint32_t dsel = 0, const uint32_t* lsd_hot = nullptr, uint32_t items = kItems) {
     switch (bits) {
 #define ORL_CASE(B) case B: launch_pass_bits<B>(rm, in, out, kin, n, n_act, shift, toff, row_step, ntiles, pout, order, keys, st, \
-                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap, dsel, lsd_hot); break;
+                                                hot_words, hot_rows, hot_idx, offsets, nb, gap_q, gap_cap, dsel, lsd_hot, items); break;
         ORL_CASE(1) ORL_CASE(2) ORL_CASE(3) ORL_CASE(4) ORL_CASE(5) ORL_CASE(6)
         ORL_CASE(7) ORL_CASE(8) ORL_CASE(9) ORL_CASE(10) ORL_CASE(11)
 #undef ORL_CASE
@@ -5895,13 +5911,22 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
     // writes sorted_keys / the FL rows there
     uint8_t* dig = reinterpret_cast<uint8_t*>(s.sorted_keys);
     bool have_dig = false;
+    // the later passes in 3072-element tiles when each of them gets its digit stream and writes the offsets itself
+    bool t12 = lsd_tile12() && gaps && lsd_digits() && dig8_wave() && plan.passes >= 2;
+    for (int p = 1; p < plan.passes; ++p) t12 = t12 && plan.bits[p] <= 8;
+    const uint32_t ntiles12 = ceil_div(n, kRouteThreads * kItems12);
+    const uint32_t ntl = t12 ? ntiles12 : ntiles;  // the later passes' tiles
     for (int p = 0; p < plan.passes; ++p) {
         const uint32_t bins = 1u << plan.bits[p];
         const uint32_t row_step = (p == 0) ? row_step0 : 1u;
-        const uint32_t nrows = (p == 0) ? nrows0 : ntiles;
+        const uint32_t ntp = p == 0 ? ntiles : ntl;
+        const uint32_t nrows = (p == 0) ? nrows0 : ntl;
         const uint32_t* n_dev = (p > 0 && lhot) ? s.lsd_hot + 2 : nullptr;
-        if (p > 0 && have_dig && bins >= 2 && bins <= 256 && dig8_wave())
-            hipLaunchKernelGGL(k_hist_dig8_wave, dim3(ceil_div(ntiles, kWaves)), dim3(256), 0, st, dig, n, bins, ntiles,
+        if (p > 0 && t12)
+            hipLaunchKernelGGL(k_hist_dig8_wave<3>, dim3(ceil_div(ntl, kWaves)), dim3(256), 0, st, dig, n, bins, ntl, s.tile_cnt,
+                               n_dev);
+        else if (p > 0 && have_dig && bins >= 2 && bins <= 256 && dig8_wave())
+            hipLaunchKernelGGL(k_hist_dig8_wave<4>, dim3(ceil_div(ntiles, kWaves)), dim3(256), 0, st, dig, n, bins, ntiles,
                                s.tile_cnt, n_dev);
         else if (p > 0 && have_dig)
             hipLaunchKernelGGL((k_hist_pairs<false, true>), dim3(ntiles), dim3(256), 0, st, dig, n, n_act, 0u, bins, s.tile_cnt,
@@ -5919,13 +5944,14 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t dsel = wdig ? (uint32_t)plan.shift[p + 1] | ((uint32_t)plan.bits[p + 1] << 8) : 0u;
         const bool hp = p == 0 && lhot;  // the first pass writes the hot key's indices to its run (idx_a: free in stage 4)
         launch_pass(host_rm(s.device), plan.bits[p], p == 0 ? IN_ACT : IN_PAIR, out, kin, n, n_act, (uint32_t)plan.shift[p],
-                    s.tile_hist, row_step, ntiles, pbuf[p & 1], d_order, wdig ? reinterpret_cast<uint32_t*>(dig) : s.sorted_keys,
+                    s.tile_hist, row_step, ntp, pbuf[p & 1], d_order, wdig ? reinterpret_cast<uint32_t*>(dig) : s.sorted_keys,
                     st, hp ? hw : nullptr, hp ? s.hot_rows : nullptr, hp ? s.idx_a : nullptr, d_offsets, nb, s.gap_q, s.gap_cap,
-                    dsel, (p > 0 && lhot) ? s.lsd_hot : nullptr);
+                    dsel, (p > 0 && lhot) ? s.lsd_hot : nullptr, (p > 0 && t12) ? kItems12 : kItems);
         have_dig = wdig;
     }
     if (gaps) {  // the buckets the last pass could not see from inside a tile (k_bound_last), then the digits' tails
         const int lp = plan.passes - 1;
+        const uint32_t ntiles = ntl;  // the last pass's tiles
         const uint32_t bins = 1u << plan.bits[lp], nch = ceil_div(ntiles, kScanRows);
         const bool bt = bins % kBoundCols == 0 && bound_staged();
         if (bt) hipLaunchKernelGGL(k_bound_last_t, dim3(nch), dim3(256), 0, st, s.sorted_keys, ntiles, bins, s.col_sums);
