@@ -1369,57 +1369,70 @@ __global__ __launch_bounds__(256) void k_hist_pairs(const void* __restrict__ in,
 // the workgroups (the per-tile form spent its time in launch, zeroing and barriers: 0.15 ms per 256M for 256 MB read).
 // n_dev as k_hist_pairs.  bins <= 256.
 // Q: 16-B loads per lane (the tile is 64 x 16 x Q digits: 4096 for Q = 4, 3072 for the 12-item passes).
-template <uint32_t Q = 4>
+// TW: tiles per wave (2 measured no faster: 133 vs 131 us per pass at config 3, profiles/r06tw_config3_kernel_stats.txt —
+// the wave's serial run-length loop and its LDS adds, not the load round trip, bound it).
+template <uint32_t Q = 4, uint32_t TW = 1>
 __global__ __launch_bounds__(256) void k_hist_dig8_wave(const uint8_t* __restrict__ dig, uint32_t n, uint32_t bins,
                                                         uint32_t ntiles, uint16_t* __restrict__ tile_cnt,
                                                         const uint32_t* __restrict__ n_dev) {
+    // TW tiles per wave, all their loads issued first (one memory round trip per TW tiles)
     constexpr uint32_t PL = 16u * Q;  // digits per lane
     if (n_dev) n = min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(n_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), n);
     __shared__ uint32_t hist[kWaves][256];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x * kWaves + w;
-    if (tile >= ntiles) return;  // whole waves: no barrier below
+    const uint32_t tile0 = (blockIdx.x * kWaves + w) * TW;
+    if (tile0 >= ntiles) return;  // whole waves: no barrier below
     uint32_t* h = hist[w];
+    uint32_t v[TW][4 * Q];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) h[lane + 64u * q] = 0;
-    const uint32_t e0 = tile * (64u * PL) + lane * PL;
-    uint32_t v[4 * Q];
-    if (e0 + PL <= n) {
-        const uint4* p = reinterpret_cast<const uint4*>(dig + e0);
+    for (uint32_t tw = 0; tw < TW; ++tw) {
+        const uint32_t e0 = (tile0 + tw) * (64u * PL) + lane * PL;
+        if (e0 + PL <= n) {
+            const uint4* p = reinterpret_cast<const uint4*>(dig + e0);
 #pragma unroll
-        for (uint32_t q = 0; q < Q; ++q) {
-            const uint4 x = ld_s4(p + q);
-            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+            for (uint32_t q = 0; q < Q; ++q) {
+                const uint4 x = ld_s4(p + q);
+                v[tw][4 * q] = x.x; v[tw][4 * q + 1] = x.y; v[tw][4 * q + 2] = x.z; v[tw][4 * q + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < 4 * Q; ++q) v[tw][q] = 0;
+            for (uint32_t i = 0; e0 + i < n && i < PL; ++i) v[tw][i >> 2] |= (uint32_t)dig[e0 + i] << (8u * (i & 3u));
         }
-    } else {
-#pragma unroll
-        for (uint32_t q = 0; q < 4 * Q; ++q) v[q] = 0;
-        for (uint32_t i = 0; e0 + i < n && i < PL; ++i) v[i >> 2] |= (uint32_t)dig[e0 + i] << (8u * (i & 3u));
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the zeroed row before the wave's adds
-    const uint32_t m = e0 < n ? min(PL, n - e0) : 0u;
-    if (m) {
-        uint32_t cur = v[0] & 0xFFu, len = 1;
 #pragma unroll
-        for (uint32_t i = 1; i < PL; ++i) {
-            if (i < m) {
-                const uint32_t b = (v[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
-                if (b == cur) {
-                    ++len;
-                } else {
-                    atomicAdd(&h[cur], len);
-                    cur = b;
-                    len = 1;
+    for (uint32_t tw = 0; tw < TW; ++tw) {
+        const uint32_t tile = tile0 + tw;
+        if (tile >= ntiles) break;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) h[lane + 64u * q] = 0;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the zeroed row before the wave's adds
+        const uint32_t e0 = tile * (64u * PL) + lane * PL;
+        const uint32_t m = e0 < n ? min(PL, n - e0) : 0u;
+        if (m) {
+            uint32_t cur = v[tw][0] & 0xFFu, len = 1;
+#pragma unroll
+            for (uint32_t i = 1; i < PL; ++i) {
+                if (i < m) {
+                    const uint32_t b = (v[tw][i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+                    if (b == cur) {
+                        ++len;
+                    } else {
+                        atomicAdd(&h[cur], len);
+                        cur = b;
+                        len = 1;
+                    }
                 }
             }
+            atomicAdd(&h[cur], len);
         }
-        atomicAdd(&h[cur], len);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t* r2 = reinterpret_cast<uint32_t*>(tile_cnt + (size_t)tile * bins);
+        for (uint32_t b = lane; b < bins / 2u; b += 64u) r2[b] = h[2u * b] | (h[2u * b + 1u] << 16);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row read out before the next tile zeroes it
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint32_t* r2 = reinterpret_cast<uint32_t*>(tile_cnt + (size_t)tile * bins);
-    for (uint32_t b = lane; b < bins / 2u; b += 64u) r2[b] = h[2u * b] | (h[2u * b + 1u] << 16);
 }
 
 // Column scan of the [ntiles][bins] count matrix, in chunks of kScanRows tiles.
@@ -5923,10 +5936,10 @@ int bucket_after_route(const uint32_t* d_act, uint32_t n, uint32_t n_act, uint32
         const uint32_t nrows = (p == 0) ? nrows0 : ntl;
         const uint32_t* n_dev = (p > 0 && lhot) ? s.lsd_hot + 2 : nullptr;
         if (p > 0 && t12)
-            hipLaunchKernelGGL(k_hist_dig8_wave<3>, dim3(ceil_div(ntl, kWaves)), dim3(256), 0, st, dig, n, bins, ntl, s.tile_cnt,
-                               n_dev);
+            hipLaunchKernelGGL((k_hist_dig8_wave<3, 1>), dim3(ceil_div(ntl, kWaves)), dim3(256), 0, st, dig, n, bins, ntl,
+                               s.tile_cnt, n_dev);
         else if (p > 0 && have_dig && bins >= 2 && bins <= 256 && dig8_wave())
-            hipLaunchKernelGGL(k_hist_dig8_wave<4>, dim3(ceil_div(ntiles, kWaves)), dim3(256), 0, st, dig, n, bins, ntiles,
+            hipLaunchKernelGGL((k_hist_dig8_wave<4, 1>), dim3(ceil_div(ntiles, kWaves)), dim3(256), 0, st, dig, n, bins, ntiles,
                                s.tile_cnt, n_dev);
         else if (p > 0 && have_dig)
             hipLaunchKernelGGL((k_hist_pairs<false, true>), dim3(ntiles), dim3(256), 0, st, dig, n, n_act, 0u, bins, s.tile_cnt,
